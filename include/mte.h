@@ -1,0 +1,207 @@
+/*
+ * mte.h — C ABI of the MI355X batched merge-tree replay engine ("mte").
+ *
+ * Drop-in boundary for the sequenced-op replay path of @fluidframework/merge-tree 0.31.0
+ * (reference: /root/reference/packages/dds/merge-tree/src). The reference boundary is an
+ * in-process TypeScript class API; each entry point below names the reference interface it
+ * stands in for. The N-API addon (packages/merge-tree-native) and the Python host mirror
+ * (fluidframework_amd/) bind exactly these symbols; INTEGRATION.md shows the bindings.
+ *
+ * Conventions
+ *   - Plain C types only: pointers + sizes, no torch / STL types.
+ *   - Every call returns int: 0 = ok, <0 = MTE_E_* engine error (message via mte_last_error).
+ *     Per-document replay failures never abort a batch: they are recorded as a per-doc status
+ *     (mte_doc_status), mirroring the throw points of the reference (e.g. "MergeTree insert
+ *     failed", mergeTree.ts:2210-2216).
+ *   - One engine per GPU per process; calls on one engine are not re-entrant.
+ *   - Strings in op payloads are UTF-16 code units (JavaScript string semantics: lengths and
+ *     positions are UTF-16 units, lone surrogates allowed).
+ */
+#ifndef MTE_H
+#define MTE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTE_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------------------ */
+enum {
+    MTE_OK = 0,
+    MTE_E_ARG = -1,          /* bad argument */
+    MTE_E_NOMEM = -2,        /* host or device allocation failed */
+    MTE_E_HIP = -3,          /* HIP runtime error (no device, launch failure, ...) */
+    MTE_E_STATE = -4,        /* call out of order (e.g. mte_text before mte_replay) */
+    MTE_E_PARSE = -5,        /* malformed op-log JSON */
+    MTE_E_UNSUPPORTED = -6,  /* op-log feature outside the engine's scope */
+    MTE_E_RANGE = -7,        /* index out of range / buffer too small (required size returned) */
+};
+
+/* per-document replay status (mte_doc_status) */
+enum {
+    MTE_DOC_OK = 0,
+    MTE_DOC_INSERT_FAILED = 1,   /* mergeTree.ts:2210-2216 "MergeTree insert failed" */
+    MTE_DOC_SEQ_ORDER = 2,       /* client.ts:469-472,832-834 sequencing asserts */
+    MTE_DOC_CAPACITY = 3,        /* engine arena exhausted (sizing bug; never silent) */
+    MTE_DOC_UNSUPPORTED = 4,     /* > 64 clients, > MTE_MAX_PROPS keys on a segment, ... */
+    MTE_DOC_NOT_RUN = 5,
+};
+
+#define MTE_MAX_CLIENTS 64       /* short ids 0..63 (observer = 0), overlap kept as a u64 mask */
+#define MTE_MAX_PROPS 7          /* keys per segment property map on the device */
+
+/* ---- op records (one per merge-tree delta op; 32 bytes) ---------------------------------- */
+/* Types follow ops.ts:29-34 (MergeTreeDeltaType) plus two engine-level kinds. */
+enum {
+    MTE_OP_INSERT = 0,        /* insert text segment: a = payload offset, b = length */
+    MTE_OP_REMOVE = 1,        /* remove [pos1, a) */
+    MTE_OP_ANNOTATE = 2,      /* annotate [pos1, a) with prop set `props` */
+    MTE_OP_INSERT_MARKER = 3, /* insert Marker: b = refType, props = marker props */
+    MTE_OP_NOOP = 4,          /* sequenced message with no merge-tree op (only seq/msn advance) */
+};
+
+/* flags */
+#define MTE_F_END_OF_MSG 0x1u   /* last op of its ISequencedDocumentMessage: currentSeq=seq, setMinSeq(msn) */
+#define MTE_F_REWRITE 0x2u      /* annotate combiningOp {name:"rewrite"} (segmentPropertiesManager.ts:65-78) */
+
+typedef struct mte_op {
+    int32_t seq;        /* sequenceNumber */
+    int32_t ref_seq;    /* referenceSequenceNumber */
+    int32_t msn;        /* minimumSequenceNumber */
+    int32_t pos1;
+    int32_t a;          /* REMOVE/ANNOTATE: pos2; INSERT: payload offset (UTF-16 units, doc-relative) */
+    uint32_t b;         /* INSERT: payload length; INSERT_MARKER: refType */
+    uint32_t props;     /* prop-set id (0 = no props object; see mte_propset) */
+    uint8_t type;       /* MTE_OP_* */
+    uint8_t client;     /* short client id (first-appearance order, observer = 0; client.ts:644-668) */
+    uint16_t flags;     /* MTE_F_* */
+} mte_op;
+
+/* An interned property set: the entries of one `props` object in JS Object.keys order.
+ * kv[first .. first+count) index mte_batch.prop_keys / prop_vals. value id 0 == JSON null. */
+typedef struct mte_propset {
+    uint32_t first;
+    uint32_t count;
+} mte_propset;
+
+/* A batch of documents (host memory, borrowed for the duration of mte_load). */
+typedef struct mte_batch {
+    uint32_t n_docs;
+    const uint64_t* doc_op_offsets;       /* n_docs+1 prefix offsets into ops */
+    const mte_op* ops;
+    const uint64_t* doc_payload_offsets;  /* n_docs+1 prefix offsets (UTF-16 units) into payload */
+    const uint16_t* payload;              /* UTF-16 text arena */
+    /* property interning (shared by all docs) */
+    uint32_t n_propsets;                  /* propset id 0 is reserved (= no props) */
+    const mte_propset* propsets;
+    const uint32_t* prop_keys;            /* key id per kv entry */
+    const uint32_t* prop_vals;            /* value id per kv entry (0 = null / delete) */
+    uint32_t n_keys;                      /* key strings: JSON-escaped, quoted ("\"bold\"") */
+    const uint64_t* key_offsets;          /* n_keys+1 byte offsets into key_text */
+    const char* key_text;
+    uint32_t n_vals;                      /* value texts: canonical JSON.stringify output; id 0 = "null" */
+    const uint64_t* val_offsets;          /* n_vals+1 byte offsets into val_text */
+    const char* val_text;
+    /* client names: per doc, short id order (index 0 = observer) */
+    const uint32_t* doc_client_offsets;   /* n_docs+1 prefix offsets into client_name_offsets */
+    const uint64_t* client_name_offsets;  /* (total names)+1 byte offsets into client_names */
+    const char* client_names;             /* UTF-8 */
+} mte_batch;
+
+/* ---- engine ------------------------------------------------------------------------------ */
+typedef struct mte_engine mte_engine;
+
+typedef struct mte_config {
+    int32_t device;             /* HIP device ordinal */
+    uint32_t chunk_size;        /* SnapshotV1 chunk size (snapshotV1.ts:40); 0 => 10000 */
+    uint32_t reserved[6];
+} mte_config;
+
+typedef struct mte_stats {
+    uint64_t docs;
+    uint64_t ops;               /* merge-tree ops applied (all docs) */
+    uint64_t messages;          /* sequenced messages applied */
+    uint64_t failed_docs;
+    double kernel_ms;           /* replay kernel time (HIP events on the engine stream) */
+    double h2d_ms;              /* upload time of the last mte_load */
+} mte_stats;
+
+typedef struct mte_doc_summary {   /* 32-B record gathered across ranks */
+    uint64_t checksum;             /* FNV-1a-64(UTF-8 text ‖ 0 ‖ blob0 ‖ 0 ‖ blob1 ...) */
+    uint32_t ops;
+    uint32_t length;
+    uint32_t segments;
+    uint32_t snapshot_bytes;
+    int32_t status;
+    uint32_t doc_id;
+} mte_doc_summary;
+
+typedef struct mte_seg_row {       /* parity dump row (walkAllSegments order, mergeTree.ts:2969) */
+    uint32_t kind;                 /* 0 text, 1 marker */
+    uint32_t len;
+    int32_t seq;
+    int32_t client;                /* short id (-1 local, -2 non-collab) */
+    int32_t removed_seq;           /* INT32_MIN when not removed */
+    int32_t removed_client;
+    uint64_t overlap_mask;         /* removedClientOverlap as a short-id set */
+    uint32_t text_off;             /* offset into the text returned by mte_segment_text */
+    uint32_t ref_type;
+} mte_seg_row;
+
+/* Library identity / capability */
+int mte_abi_version(void);
+const char* mte_build_info(void);     /* "gfx950 hip <ver>" */
+
+/* new Client(specToSegment, logger, options) + startOrUpdateCollaboration(observer)
+ * (client.ts:74-83, 1059-1079) — one engine replays many documents at once. */
+int mte_create(const mte_config* cfg, mte_engine** out);
+void mte_destroy(mte_engine* e);
+const char* mte_last_error(const mte_engine* e);
+
+/* Stage a batch on the device (copies host buffers; returns after the upload). */
+int mte_load(mte_engine* e, const mte_batch* batch);
+
+/* Client.applyMsg for every message of every document (client.ts:805-836), on the GPU.
+ * Blocking. Per-doc failures are recorded, never thrown. */
+int mte_replay(mte_engine* e, mte_stats* out);
+
+/* Synthetic workload: generate op logs on the device and leave them loaded, as if
+ * by mte_load. kind: 2 = C2 (insert/remove), 3 = C3 (annotate + ties), 5 = C5-style.
+ * ops_per_doc may be NULL (uniform n_ops) or per-doc counts. */
+int mte_generate(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops,
+                 const uint32_t* ops_per_doc, uint32_t n_clients, uint64_t seed_base);
+
+/* Copy the (generated or loaded) op logs back to the host in mte_batch form. Buffers are owned by
+ * the engine and stay valid until the next load/generate/destroy. */
+int mte_export_batch(mte_engine* e, mte_batch* out);
+
+/* Results (after mte_replay). */
+int mte_doc_status(mte_engine* e, uint32_t doc, int32_t* code, int64_t* failing_seq);
+/* MergeTreeTextHelper.getText(currentSeq, observer) (textSegment.ts:154-172), UTF-16. */
+int mte_text(mte_engine* e, uint32_t doc, uint16_t* buf, size_t cap, size_t* len);
+/* Final segment table (parity dump). rows may be NULL to query *n. */
+int mte_segments(mte_engine* e, uint32_t doc, mte_seg_row* rows, size_t cap, size_t* n);
+/* SnapshotV1.extractSync + emit (snapshotV1.ts:85-247): the ITree as JSON
+ * {"entries":[{"mode":"100644","path":"header","type":"Blob","value":{"contents":...,"encoding":"utf-8"}},...],"id":null}
+ * buf may be NULL to query *len. */
+int mte_snapshot_v1(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len, uint32_t* n_blobs);
+/* Per-doc summaries for all docs of the batch (checksum over text + snapshot blobs). */
+int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap);
+
+/* Op-log ingestion: build a batch from per-doc JSON arrays of ISequencedDocumentMessage
+ * (protocol.ts:126-166). The builder owns the memory. */
+typedef struct mte_builder mte_builder;
+int mte_builder_create(mte_builder** out);
+int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* json, size_t len);
+int mte_builder_batch(mte_builder* b, mte_batch* out);   /* view valid until destroy */
+const char* mte_builder_error(const mte_builder* b);
+void mte_builder_destroy(mte_builder* b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTE_H */

@@ -1,0 +1,133 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the CPU oracle (oracle/mt_oracle.cpp).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module; the
+product path (fluidframework_amd/) never does. See oracle/mt_oracle.cpp for what the oracle
+restates and how it is pinned against the reference's own golden vectors.
+"""
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, cp, i32, u32, u64 = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64
+        L.orc_new.restype = vp
+        L.orc_new.argtypes = [cp]
+        L.orc_free.argtypes = [vp]
+        L.orc_str_free.argtypes = [vp]
+        L.orc_apply_json.argtypes = [vp, cp, ctypes.c_size_t]
+        L.orc_apply_batch.argtypes = [vp, vp, u32]
+        L.orc_local_insert_text.argtypes = [vp, i32, cp, cp]
+        L.orc_local_insert_marker.argtypes = [vp, i32, i32, cp]
+        L.orc_local_remove.argtypes = [vp, i32, i32]
+        L.orc_local_annotate.argtypes = [vp, i32, i32, cp]
+        L.orc_get_length.argtypes = [vp]
+        L.orc_get_length_at.argtypes = [vp, i32, i32]
+        for f in ("orc_text", "orc_segments_json"):
+            getattr(L, f).restype = vp
+            getattr(L, f).argtypes = [vp]
+        L.orc_snapshot_json.restype = vp
+        L.orc_snapshot_json.argtypes = [vp, u32]
+        L.orc_checksum.restype = u64
+        L.orc_checksum.argtypes = [vp, u32]
+        L.orc_ops_applied.restype = u64
+        L.orc_ops_applied.argtypes = [vp]
+        L.orc_status.argtypes = [vp, cp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_longlong)]
+        L.orc_stats.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        L.orc_replay_batch.restype = u64
+        L.orc_replay_batch.argtypes = [vp, u32, u32, i32, cp, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int32), i32]
+        _lib = L
+    return _lib
+
+
+def _take(ptr):
+    s = ctypes.string_at(ptr).decode("utf-8")
+    lib().orc_str_free(ptr)
+    return s
+
+
+class OracleDoc:
+    """One document replayed by the oracle. observer=None => local, non-collaborative tree."""
+
+    def __init__(self, observer="__observer__"):
+        self._h = lib().orc_new(observer.encode() if observer is not None else None)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_free(self._h)
+            self._h = None
+
+    # -- input
+    def apply_json(self, text):
+        b = text.encode() if isinstance(text, str) else text
+        return lib().orc_apply_json(self._h, b, len(b))
+
+    def apply_batch(self, batch_ptr, doc):
+        return lib().orc_apply_batch(self._h, batch_ptr, doc)
+
+    def insert_text_local(self, pos, text, props_json=None):
+        return lib().orc_local_insert_text(self._h, pos, text.encode(), props_json.encode() if props_json else None)
+
+    def insert_marker_local(self, pos, ref_type, props_json=None):
+        return lib().orc_local_insert_marker(self._h, pos, ref_type, props_json.encode() if props_json else None)
+
+    def remove_local(self, start, end):
+        return lib().orc_local_remove(self._h, start, end)
+
+    def annotate_local(self, start, end, props_json):
+        return lib().orc_local_annotate(self._h, start, end, props_json.encode())
+
+    # -- outputs
+    def length(self):
+        return lib().orc_get_length(self._h)
+
+    def length_at(self, ref_seq, short_client):
+        return lib().orc_get_length_at(self._h, ref_seq, short_client)
+
+    def text(self):
+        return _take(lib().orc_text(self._h))
+
+    def segments_json(self):
+        return _take(lib().orc_segments_json(self._h))
+
+    def snapshot_json(self, chunk=10000):
+        return _take(lib().orc_snapshot_json(self._h, chunk))
+
+    def checksum(self, chunk=10000):
+        return lib().orc_checksum(self._h, chunk)
+
+    def ops_applied(self):
+        return lib().orc_ops_applied(self._h)
+
+    def status(self):
+        buf = ctypes.create_string_buffer(512)
+        fs = ctypes.c_longlong(0)
+        code = lib().orc_status(self._h, buf, 512, ctypes.byref(fs))
+        return code, buf.value.decode(), fs.value
+
+    def stats(self):
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        lib().orc_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return {"leafCount": a.value, "removedLeafCount": b.value, "maxHeight": c.value}
+
+
+def replay_batch(batch_ptr, d0, d1, threads=1, with_snapshot=True):
+    """Replay docs [d0, d1) of an mte_batch; returns (ops, checksums[list], statuses[list])."""
+    n = d1 - d0
+    cs = (ctypes.c_uint64 * max(n, 1))()
+    st = (ctypes.c_int32 * max(n, 1))()
+    ops = lib().orc_replay_batch(batch_ptr, d0, d1, threads, None, cs, st, 1 if with_snapshot else 0)
+    return ops, list(cs)[:n], list(st)[:n]

@@ -1,0 +1,1266 @@
+// TEST INFRASTRUCTURE ONLY — CPU oracle for the merge-tree replay path.
+//
+// A restatement of @fluidframework/merge-tree 0.31.0 as a *tree* (the same B-tree object model the
+// reference uses: 8-slot blocks, parent pointers, LRU heap, zamboni scour/pack), independent of the
+// flat, wave-parallel design of the HIP engine it checks. Only tests/, __graft_entry__.smoke() and
+// bench.py's cpu_baseline leg may load it. Every function cites the reference file:line it follows
+// (paths relative to /root/reference/packages/dds/merge-tree/src unless stated).
+//
+// Parity pinning: the reference is TypeScript and is NOT built here (no tsc in the image; building
+// it would need a stand-in compiler). The oracle is pinned by the reference's own golden vectors:
+// packages/dds/sequence/src/test/snapshots/v1/*.json (SnapshotV1 bytes, reproduced through the
+// local, non-collaborative path of generateSharedStrings.ts:24-98) and by the expected strings of
+// the merge-tree spec tests (tests/test_oracle_specs.py). Collaborative merge-info snapshot bytes
+// and zamboni boundaries are not covered by any reference fixture: "parity unpinned" for those rows.
+//
+// The one deliberate replacement: PartialSequenceLengths (partialLengths.ts) is not reproduced; a
+// block's length for (refSeq, clientId) is the sum of the leaf visibility predicate
+// (mergeTree.ts:1673-1696) over its subtree, which is what the partial-length cache computes when
+// each client's refSeq is non-decreasing (deli guarantees it, lambdas/src/deli/lambda.ts:282-295).
+#include <algorithm>
+#include <atomic>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <sstream>
+#include <thread>
+#include <unordered_map>
+
+#include "../include/mte.h"
+#include "jsvalue.hpp"
+
+namespace orc {
+
+// constants.ts:11-15, mergeTree.ts:334,1059-1061
+constexpr int MaxNodesInBlock = 8;
+constexpr int UniversalSequenceNumber = 0;
+constexpr int UnassignedSequenceNumber = -1;
+constexpr int TreeMaintenanceSequenceNumber = -2;
+constexpr int LocalClientId = -1;
+constexpr int NonCollabClient = -2;
+constexpr int TextSegmentGranularity = 256;
+constexpr int ZamboniSegmentsMaxCount = 2;
+
+struct EngineError : std::runtime_error {
+    int code;
+    EngineError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+struct Block;
+
+struct Node {
+    Block* parent = nullptr;
+    int index = 0;
+    bool leaf;
+    explicit Node(bool l) : leaf(l) {}
+};
+
+// BaseSegment / TextSegment / Marker (mergeTree.ts:429-798, textSegment.ts:16-111)
+struct Segment : Node {
+    bool marker = false;
+    int refType = 0;
+    u16s text;
+    int len = 0;                                  // cachedLength
+    bool hasProps = false;                        // properties !== undefined
+    JObj props;
+    int seq = UniversalSequenceNumber;            // mergeTree.ts:434
+    int clientId = LocalClientId;                 // mergeTree.ts:433
+    bool removed = false;                         // removedSeq !== undefined
+    int removedSeq = 0;
+    int removedClientId = 0;
+    std::vector<int> overlap;                     // removedClientOverlap
+    Segment() : Node(true) {}
+};
+
+struct Block : Node {
+    Node* children[MaxNodesInBlock] = {};
+    int childCount = 0;
+    int needsScour = -1;  // -1 undefined, 0 false, 1 true (mergeTree.ts:63)
+    Block() : Node(false) {}
+};
+
+struct LRUSegment {
+    Segment* segment;
+    int maxSeq;
+};
+
+// collections.ts:213-265 — binary min-heap, 1-based, exactly the reference's sift rules.
+struct Heap {
+    std::vector<LRUSegment> L{LRUSegment{nullptr, -2}};
+    int count() const { return (int)L.size() - 1; }
+    const LRUSegment* peek() const { return count() > 0 ? &L[1] : nullptr; }
+    static int cmp(const LRUSegment& a, const LRUSegment& b) { return a.maxSeq - b.maxSeq; }  // mergeTree.ts:923-926
+    LRUSegment get() {
+        LRUSegment x = L[1];
+        L[1] = L[count()];
+        L.pop_back();
+        fixdown(1);
+        return x;
+    }
+    void add(LRUSegment x) {
+        L.push_back(x);
+        fixup(count());
+    }
+    void fixup(int k) {
+        while (k > 1 && cmp(L[k >> 1], L[k]) > 0) {
+            std::swap(L[k >> 1], L[k]);
+            k >>= 1;
+        }
+    }
+    void fixdown(int k) {
+        while ((k << 1) <= count()) {
+            int j = k << 1;
+            if (j < count() && cmp(L[j], L[j + 1]) > 0) j++;
+            if (cmp(L[k], L[j]) <= 0) break;
+            std::swap(L[k], L[j]);
+            k = j;
+        }
+    }
+};
+
+// properties.ts:62-93 matchProperties, generalised to JS values for the recursive call.
+static std::vector<u16s> for_in_keys(const JV* v) {
+    std::vector<u16s> ks;
+    if (!v) return ks;
+    if (v->t == JV::Obj) return v->o.keys();
+    if (v->t == JV::Arr) {
+        for (size_t i = 0; i < v->a.size(); i++) {
+            std::string d = std::to_string(i);
+            ks.push_back(u16s(d.begin(), d.end()));
+        }
+    } else if (v->t == JV::Str) {
+        for (size_t i = 0; i < v->s.size(); i++) {
+            std::string d = std::to_string(i);
+            ks.push_back(u16s(d.begin(), d.end()));
+        }
+    }
+    return ks;
+}
+static JVP member(const JV* v, const u16s& k) {
+    if (!v) return nullptr;
+    if (v->t == JV::Obj) return v->o.get(k);
+    uint32_t idx;
+    if (!is_array_index(k, &idx)) return nullptr;
+    if (v->t == JV::Arr) return idx < v->a.size() ? v->a[idx] : nullptr;
+    if (v->t == JV::Str) return idx < v->s.size() ? JV::str(u16s(1, v->s[idx])) : nullptr;
+    return nullptr;
+}
+static bool strict_equal(const JV* a, const JV* b) {  // b is a primitive here
+    if (!a || !b) return a == b;
+    if (a->t != b->t) return false;
+    switch (a->t) {
+        case JV::Null: return true;
+        case JV::Bool: return a->b == b->b;
+        case JV::Num: return a->n == b->n;
+        case JV::Str: return a->s == b->s;
+        default: return a == b;
+    }
+}
+static bool match_values(const JV* a, const JV* b) {
+    if (truthy(a)) {
+        if (!truthy(b)) return false;
+        for (auto& k : for_in_keys(a)) {
+            JVP bk = member(b, k);
+            JVP ak = member(a, k);
+            if (!bk) return false;
+            if (bk->t == JV::Obj || bk->t == JV::Arr || bk->t == JV::Null) {
+                if (!match_values(ak.get(), bk.get())) return false;
+            } else if (!strict_equal(bk.get(), ak.get())) {
+                return false;
+            }
+        }
+        for (auto& k : for_in_keys(b))
+            if (!member(a, k)) return false;
+    } else {
+        if (truthy(b)) return false;
+    }
+    return true;
+}
+static bool matchProperties(const Segment* a, const Segment* b) {
+    JV av, bv;
+    av.t = JV::Obj; av.o = a->props;
+    bv.t = JV::Obj; bv.o = b->props;
+    return match_values(a->hasProps ? &av : nullptr, b->hasProps ? &bv : nullptr);
+}
+
+// textSegment.ts:63-68
+static bool canAppend(const Segment* prev, const Segment* seg) {
+    if (prev->marker) return false;  // Marker.canAppend (mergeTree.ts:793-795)
+    return !(prev->text.size() && prev->text.back() == u'\n') && !seg->marker &&
+           (prev->len <= TextSegmentGranularity || seg->len <= TextSegmentGranularity);
+}
+
+struct CollabWindow {  // mergeTree.ts:822-839
+    int clientId = LocalClientId;
+    bool collaborating = false;
+    int minSeq = 0;
+    int currentSeq = 0;
+};
+
+struct SegmentChanges {
+    Segment* replaceCurrent = nullptr;
+    Node* next = nullptr;
+};
+
+struct InsertCtx {
+    bool splitMode;          // ensureIntervalBoundary (leaf = splitLeafSegment) vs blockInsert (onLeaf)
+    Segment* candidate = nullptr;
+    bool continuePredicate = false;
+};
+
+class MergeTree {
+   public:
+    Block* root;
+    CollabWindow cw;
+    Heap heap;
+    std::deque<Segment> segPool;
+    std::deque<Block> blockPool;
+    std::vector<std::string>* longIds = nullptr;  // getLongClientId
+
+    MergeTree() { root = makeBlock(0); }
+
+    Block* makeBlock(int childCount) {  // mergeTree.ts:1114-1123
+        blockPool.emplace_back();
+        Block* b = &blockPool.back();
+        b->childCount = childCount;
+        return b;
+    }
+    Segment* newSegment() {
+        segPool.emplace_back();
+        return &segPool.back();
+    }
+
+    void startCollaboration(int localClientId, int minSeq, int currentSeq) {  // mergeTree.ts:1254-1271
+        cw.clientId = localClientId;
+        cw.minSeq = minSeq;
+        cw.collaborating = true;
+        cw.currentSeq = currentSeq;
+        heap = Heap();
+    }
+
+    // mergeTree.ts:1161-1172
+    int localNetLength(const Segment* s) const { return s->removed ? 0 : s->len; }
+
+    int localLength(const Node* n) const {
+        if (n->leaf) return localNetLength((const Segment*)n);
+        const Block* b = (const Block*)n;
+        int t = 0;
+        for (int i = 0; i < b->childCount; i++) t += localLength(b->children[i]);
+        return t;
+    }
+
+    // mergeTree.ts:1659-1699 (branch ids are all 0 for an observer; origin is never set)
+    int nodeLength(const Node* node, int refSeq, int clientId) const {
+        if (!cw.collaborating || cw.clientId == clientId) return localLength(node);
+        if (!node->leaf) {
+            const Block* b = (const Block*)node;
+            int t = 0;
+            for (int i = 0; i < b->childCount; i++) t += nodeLength(b->children[i], refSeq, clientId);
+            return t;  // == partialLengths.getPartialLength(refSeq, clientId)
+        }
+        const Segment* s = (const Segment*)node;
+        if (s->clientId == clientId || (s->seq != UnassignedSequenceNumber && s->seq <= refSeq)) {
+            if (s->removed) {
+                if (s->removedClientId == clientId ||
+                    std::find(s->overlap.begin(), s->overlap.end(), clientId) != s->overlap.end() ||
+                    (s->removedSeq != UnassignedSequenceNumber && s->removedSeq <= refSeq))
+                    return 0;
+                return s->len;
+            }
+            return s->len;
+        }
+        return 0;
+    }
+
+    int getLength(int refSeq, int clientId) const { return nodeLength(root, refSeq, clientId); }
+
+    void assignChild(Block* b, Node* child, int index) {  // mergeTree.ts:375-382
+        child->parent = b;
+        child->index = index;
+        b->children[index] = child;
+    }
+
+    // mergeTree.ts:2248-2277
+    bool breakTie(int pos, const Node* node, int refSeq, int clientId) const {
+        if (node->leaf) {
+            if (pos == 0) {
+                const Segment* s = (const Segment*)node;
+                if (s->removed && s->removedSeq != 0 && s->removedSeq <= refSeq &&
+                    s->removedSeq != UnassignedSequenceNumber)
+                    return false;
+                if (clientId == cw.clientId) return true;
+                if (s->seq != UnassignedSequenceNumber) return true;
+            }
+            return false;
+        }
+        return true;
+    }
+
+    // TextSegment.createSplitSegmentAt + BaseSegment.splitAt (textSegment.ts:103-111, mergeTree.ts:524-568)
+    Segment* splitAt(Segment* s, int pos) {
+        if (!(pos > 0) || s->marker) return nullptr;
+        Segment* r = newSegment();
+        r->text = s->text.substr(pos);
+        s->text = s->text.substr(0, pos);
+        s->len = (int)s->text.size();
+        r->len = (int)r->text.size();
+        if (s->hasProps) { r->hasProps = true; r->props = s->props; }  // segmentPropertiesManager.ts:113-128
+        r->parent = s->parent;
+        r->removedClientId = s->removedClientId;
+        r->removedSeq = s->removedSeq;
+        r->removed = s->removed;
+        r->seq = s->seq;
+        r->clientId = s->clientId;
+        r->overlap = s->overlap;
+        return r;
+    }
+
+    SegmentChanges leafAction(InsertCtx& ctx, Segment* segment, int pos) {
+        SegmentChanges ch;
+        if (ctx.splitMode) {  // splitLeafSegment, mergeTree.ts:2225-2239
+            if (!(pos > 0)) return ch;
+            ch.next = splitAt(segment, pos);
+            return ch;
+        }
+        if (segment) {  // onLeaf, mergeTree.ts:2180-2190
+            ch.replaceCurrent = ctx.candidate;
+            ch.next = segment;
+        } else {
+            ch.next = ctx.candidate;
+        }
+        return ch;
+    }
+
+    // rightExcursion + checkSegmentIsLocal (mergeTree.ts:2143-2161, 2313-2343)
+    bool continueFrom(Block* node) {
+        Node* start = node;
+        Block* parent = start->parent;
+        while (parent) {
+            bool matched = false;
+            for (int i = 0; i < parent->childCount; i++) {
+                Node* c = parent->children[i];
+                if (matched) {
+                    Segment* first = firstLeaf(c);
+                    if (first) return first->seq == UnassignedSequenceNumber;
+                    if (c->leaf) return ((Segment*)c)->seq == UnassignedSequenceNumber;
+                } else {
+                    matched = (c == start);
+                }
+            }
+            start = parent;
+            parent = parent->parent;
+        }
+        return false;
+    }
+    Segment* firstLeaf(Node* n) {
+        if (n->leaf) return (Segment*)n;
+        Block* b = (Block*)n;
+        for (int i = 0; i < b->childCount; i++) {
+            Segment* s = firstLeaf(b->children[i]);
+            if (s) return s;
+        }
+        return nullptr;
+    }
+
+    Block* const UNFINISHED = (Block*)(intptr_t)1;
+
+    // mergeTree.ts:2476-2489
+    Block* split(Block* node) {
+        int half = MaxNodesInBlock / 2;
+        Block* nn = makeBlock(half);
+        node->childCount = half;
+        for (int i = 0; i < half; i++) {
+            assignChild(nn, node->children[half + i], i);
+            node->children[half + i] = nullptr;
+        }
+        return nn;
+    }
+
+    // mergeTree.ts:2345-2474
+    Block* insertingWalk(Block* block, int pos, int refSeq, int clientId, int seq, InsertCtx& ctx) {
+        int childIndex;
+        Node* newNode = nullptr;
+        for (childIndex = 0; childIndex < block->childCount; childIndex++) {
+            Node* child = block->children[childIndex];
+            int len = nodeLength(child, refSeq, clientId);
+            if (pos < len || (pos == len && breakTie(pos, child, refSeq, clientId))) {
+                if (!child->leaf) {
+                    Block* splitNode = insertingWalk((Block*)child, pos, refSeq, clientId, seq, ctx);
+                    if (splitNode == nullptr) return nullptr;
+                    if (splitNode == UNFINISHED) {
+                        pos -= len;
+                        continue;
+                    }
+                    newNode = splitNode;
+                    childIndex++;
+                } else {
+                    Segment* segment = (Segment*)child;
+                    SegmentChanges ch = leafAction(ctx, segment, pos);
+                    if (ch.replaceCurrent) assignChild(block, ch.replaceCurrent, childIndex);
+                    if (ch.next) {
+                        newNode = ch.next;
+                        childIndex++;
+                    } else {
+                        return nullptr;
+                    }
+                }
+                break;
+            } else {
+                pos -= len;
+            }
+        }
+        if (!newNode) {
+            if (pos == 0) {
+                if (seq != UnassignedSequenceNumber && ctx.continuePredicate && continueFrom(block)) {
+                    return UNFINISHED;
+                }
+                SegmentChanges ch = leafAction(ctx, nullptr, pos);
+                newNode = ch.next;
+            }
+        }
+        if (newNode) {
+            for (int i = block->childCount; i > childIndex; i--) {
+                block->children[i] = block->children[i - 1];
+                block->children[i]->index = i;
+            }
+            assignChild(block, newNode, childIndex);
+            block->childCount++;
+            if (block->childCount < MaxNodesInBlock) return nullptr;
+            return split(block);
+        }
+        return nullptr;
+    }
+
+    void updateRoot(Block* splitNode) {  // mergeTree.ts:1876-1887
+        if (splitNode != nullptr && splitNode != UNFINISHED) {
+            Block* nr = makeBlock(2);
+            assignChild(nr, root, 0);
+            assignChild(nr, splitNode, 1);
+            root = nr;
+        }
+    }
+
+    void ensureIntervalBoundary(int pos, int refSeq, int clientId) {  // mergeTree.ts:2241-2245
+        InsertCtx ctx{true};
+        Block* s = insertingWalk(root, pos, refSeq, clientId, TreeMaintenanceSequenceNumber, ctx);
+        updateRoot(s);
+    }
+
+    // mergeTree.ts:1273-1283
+    void addToLRUSet(Segment* seg, int seq) {
+        if (seg->parent->needsScour != 1 && seq > cw.currentSeq) {
+            seg->parent->needsScour = 1;
+            heap.add(LRUSegment{seg, seq});
+        }
+    }
+
+    // mergeTree.ts:2141-2224
+    void blockInsert(int pos, int refSeq, int clientId, int seq, std::vector<Segment*>& segs) {
+        int insertPos = pos;
+        for (Segment* ns : segs) {
+            if (ns->len > 0) {
+                ns->seq = seq;
+                ns->clientId = clientId;
+                InsertCtx ctx{false, ns, true};
+                Block* splitNode = insertingWalk(root, insertPos, refSeq, clientId, seq, ctx);
+                if (ns->parent == nullptr) {
+                    throw EngineError(MTE_DOC_INSERT_FAILED, "MergeTree insert failed");
+                }
+                updateRoot(splitNode);
+                // saveIfLocal (:2164-2179)
+                if (cw.collaborating) {
+                    if (!(ns->seq == UnassignedSequenceNumber && clientId == cw.clientId) && ns->seq > cw.minSeq)
+                        addToLRUSet(ns, ns->seq);
+                }
+                insertPos += ns->len;
+            }
+        }
+    }
+
+    // mergeTree.ts:1968-1998
+    void insertSegments(int pos, std::vector<Segment*>& segs, int refSeq, int clientId, int seq) {
+        ensureIntervalBoundary(pos, refSeq, clientId);
+        blockInsert(pos, refSeq, clientId, seq, segs);
+        if (cw.collaborating && seq != UnassignedSequenceNumber) zamboniSegments();
+    }
+
+    // nodeMap (mergeTree.ts:2903-2965) restricted to leaf actions (post actions only update caches)
+    template <class F>
+    bool nodeMap(Block* node, int pos, int refSeq, int clientId, int start, int end, F& leaf) {
+        bool go = true;
+        for (int ci = 0; ci < node->childCount; ci++) {
+            Node* child = node->children[ci];
+            int len = nodeLength(child, refSeq, clientId);
+            if (go && end > 0 && len > 0 && start < len) {
+                if (!child->leaf) {
+                    if (go) go = nodeMap((Block*)child, pos, refSeq, clientId, start, end, leaf);
+                } else {
+                    go = leaf((Segment*)child, pos, start, end);
+                }
+            }
+            if (!go) break;
+            pos += len;
+            start -= len;
+            end -= len;
+        }
+        return go;
+    }
+
+    // mergeTree.ts:2607-2719 (observer / non-collab paths; branch 0)
+    void markRangeRemoved(int start, int end, int refSeq, int clientId, int seq) {
+        ensureIntervalBoundary(start, refSeq, clientId);
+        ensureIntervalBoundary(end, refSeq, clientId);
+        auto markRemoved = [&](Segment* s, int, int, int) {
+            if (s->removed) {
+                if (s->removedSeq == UnassignedSequenceNumber) {
+                    s->removedClientId = clientId;
+                    s->removedSeq = seq;
+                } else {
+                    s->overlap.push_back(clientId);  // addOverlappingClient :2544-2552
+                }
+            } else {
+                s->removed = true;
+                s->removedClientId = clientId;
+                s->removedSeq = seq;
+            }
+            if (cw.collaborating) {
+                if (!(s->removedSeq == UnassignedSequenceNumber && clientId == cw.clientId)) addToLRUSet(s, seq);
+            }
+            return true;
+        };
+        nodeMap(root, 0, refSeq, clientId, start, end, markRemoved);
+        if (cw.collaborating && seq != UnassignedSequenceNumber) zamboniSegments();
+    }
+
+    // SegmentPropertiesManager.addProperties (segmentPropertiesManager.ts:35-111), remote / non-collab
+    static void addProperties(Segment* s, const JObj& newProps, bool rewrite) {
+        if (!s->hasProps) {
+            s->hasProps = true;
+            s->props = JObj();
+        }
+        if (rewrite) {
+            for (auto& k : s->props.keys()) {
+                JVP nv = newProps.get(k);
+                if (!truthy(nv.get())) s->props.del(k);
+            }
+        }
+        for (auto& k : newProps.keys()) {
+            JVP nv = newProps.get(k);
+            if (nv->t == JV::Null) s->props.del(k);
+            else s->props.set(k, nv);
+        }
+    }
+
+    // mergeTree.ts:2565-2605
+    void annotateRange(int start, int end, const JObj& props, bool rewrite, int refSeq, int clientId, int seq) {
+        ensureIntervalBoundary(start, refSeq, clientId);
+        ensureIntervalBoundary(end, refSeq, clientId);
+        auto annotate = [&](Segment* s, int, int, int) {
+            addProperties(s, props, rewrite);
+            if (cw.collaborating && seq != UnassignedSequenceNumber) addToLRUSet(s, seq);
+            return true;
+        };
+        nodeMap(root, 0, refSeq, clientId, start, end, annotate);
+        if (cw.collaborating && seq != UnassignedSequenceNumber) zamboniSegments();
+    }
+
+    bool underflow(const Block* b) const { return b->childCount < MaxNodesInBlock / 2; }  // :1285-1287
+
+    // mergeTree.ts:1289-1365 (observer: segmentGroups/trackingCollection empty, all branch 0)
+    void scourNode(Block* node, std::vector<Node*>& hold) {
+        Segment* prev = nullptr;
+        for (int k = 0; k < node->childCount; k++) {
+            Node* cn = node->children[k];
+            if (!cn->leaf) {
+                hold.push_back(cn);
+                prev = nullptr;
+                continue;
+            }
+            Segment* s = (Segment*)cn;
+            if (s->removed) {
+                if (s->removedSeq > cw.minSeq) hold.push_back(s);
+                else s->parent = nullptr;
+                prev = nullptr;
+            } else if (s->seq <= cw.minSeq) {
+                bool ok = prev && canAppend(prev, s) && matchProperties(prev, s) && localNetLength(s) > 0;
+                if (ok) {
+                    prev->text += s->text;  // TextSegment.append (textSegment.ts:74-85)
+                    prev->len = (int)prev->text.size();
+                    s->parent = nullptr;
+                } else {
+                    hold.push_back(s);
+                    prev = localNetLength(s) > 0 ? s : nullptr;
+                }
+            } else {
+                hold.push_back(s);
+                prev = nullptr;
+            }
+        }
+    }
+
+    // mergeTree.ts:1368-1420
+    void pack(Block* block) {
+        Block* parent = block->parent;
+        std::vector<Node*> hold;
+        for (int ci = 0; ci < parent->childCount; ci++) {
+            Block* cb = (Block*)parent->children[ci];
+            scourNode(cb, hold);
+            cb->parent = nullptr;
+        }
+        int total = (int)hold.size();
+        int half = MaxNodesInBlock / 2;
+        int childCount = std::min(MaxNodesInBlock - 1, total / half);
+        if (childCount < 1) childCount = 1;
+        int baseCount = total / childCount;
+        int extra = total % childCount;
+        Block* packed[MaxNodesInBlock] = {};
+        int rd = 0;
+        for (int ni = 0; ni < childCount; ni++) {
+            int nc = baseCount;
+            if (extra > 0) { nc++; extra--; }
+            Block* pb = makeBlock(nc);
+            for (int pi = 0; pi < nc; pi++) assignChild(pb, hold[rd++], pi);
+            pb->parent = parent;
+            packed[ni] = pb;
+        }
+        for (int j = 0; j < MaxNodesInBlock; j++) parent->children[j] = nullptr;
+        for (int j = 0; j < childCount; j++) assignChild(parent, packed[j], j);
+        parent->childCount = childCount;
+        if (underflow(parent) && parent->parent) pack(parent);
+    }
+
+    // mergeTree.ts:1422-1478
+    void zamboniSegments() {
+        if (!cw.collaborating) return;
+        for (int i = 0; i < ZamboniSegmentsMaxCount; i++) {
+            const LRUSegment* top = heap.peek();
+            if (!top || top->maxSeq > cw.minSeq) break;
+            LRUSegment e = heap.get();
+            if (e.segment->parent && e.segment->parent->needsScour != 0) {
+                Block* block = e.segment->parent;
+                std::vector<Node*> copy;
+                scourNode(block, copy);
+                block->needsScour = 0;
+                int nc = (int)copy.size();
+                if (nc < block->childCount) {
+                    for (int j = 0; j < MaxNodesInBlock; j++) block->children[j] = nullptr;
+                    block->childCount = nc;
+                    for (int j = 0; j < nc; j++) assignChild(block, copy[j], j);
+                    if (underflow(block) && block->parent) pack(block);
+                }
+            }
+        }
+    }
+
+    // mergeTree.ts:1718-1736
+    void setMinSeq(int minSeq) {
+        if (minSeq > cw.currentSeq) throw EngineError(MTE_DOC_SEQ_ORDER, "minSeq > currentSeq");
+        if (minSeq < cw.minSeq) throw EngineError(MTE_DOC_SEQ_ORDER, "minSeq moved backwards");
+        if (minSeq > cw.minSeq) {
+            cw.minSeq = minSeq;
+            zamboniSegments();
+        }
+    }
+
+    template <class F>
+    bool walkAllSegments(Block* b, F& f) {  // mergeTree.ts:2969-2983
+        bool go = true;
+        for (int i = 0; go && i < b->childCount; i++) {
+            Node* c = b->children[i];
+            go = c->leaf ? f((Segment*)c) : walkAllSegments((Block*)c, f);
+        }
+        return go;
+    }
+
+    // getStats (mergeTree.ts:1484-1527): leafCount, removedLeafCount, maxHeight
+    void stats(Block* b, int& leaves, int& removed, int& height) {
+        int h = 0;
+        for (int i = 0; i < b->childCount; i++) {
+            Node* c = b->children[i];
+            int ch = 1;
+            if (!c->leaf) {
+                int l2 = 0, r2 = 0, h2 = 0;
+                stats((Block*)c, l2, r2, h2);
+                leaves += l2;
+                removed += r2;
+                ch = 1 + h2;
+            } else {
+                leaves++;
+                if (((Segment*)c)->removed) removed++;
+            }
+            h = std::max(h, ch);
+        }
+        height = h;
+    }
+};
+
+// ---- JSON of a segment (TextSegment.toJSONObject textSegment.ts:48-54, Marker mergeTree.ts:652-656)
+static void props_json(std::string& o, const JObj& p) {
+    JV v;
+    v.t = JV::Obj;
+    v.o = p;
+    js_stringify(o, v);
+}
+static void segment_json(std::string& o, const Segment* s) {
+    if (s->marker) {
+        o += "{\"marker\":{\"refType\":" + js_number(s->refType) + "}";
+        if (s->hasProps) { o += ",\"props\":"; props_json(o, s->props); }
+        o += "}";
+    } else if (s->hasProps) {
+        o += "{\"text\":";
+        js_quote(o, s->text);
+        o += ",\"props\":";
+        props_json(o, s->props);
+        o += "}";
+    } else {
+        js_quote(o, s->text);
+    }
+}
+
+// FNV-1a-64
+static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const uint8_t* b = (const uint8_t*)p;
+    for (size_t i = 0; i < n; i++) { h ^= b[i]; h *= 0x100000001b3ull; }
+    return h;
+}
+
+class Doc {
+   public:
+    MergeTree mt;
+    std::vector<std::string> shortIds;                 // shortClientIdMap (client.ts:644-668)
+    std::unordered_map<std::string, int> nameToShort;  // clientNameToIds
+    std::string observer;
+    bool collab = false;
+    int status = 0;
+    long long failingSeq = -1;
+    std::string error;
+    uint64_t opsApplied = 0;
+
+    explicit Doc(const char* observerName) {
+        mt.longIds = &shortIds;
+        if (observerName) {  // startOrUpdateCollaboration(observer) (client.ts:1059-1079)
+            observer = observerName;
+            collab = true;
+            getOrAddShortClientId(observer);
+            mt.startCollaboration(0, 0, 0);
+        }
+    }
+
+    int getOrAddShortClientId(const std::string& name) {
+        auto it = nameToShort.find(name);
+        if (it != nameToShort.end()) return it->second;
+        int id = (int)shortIds.size();
+        shortIds.push_back(name);
+        nameToShort[name] = id;
+        return id;
+    }
+    std::string longId(int shortId) const { return shortId >= 0 ? shortIds[shortId] : "original"; }
+
+    Segment* makeSegment(const JV& spec) {  // SharedStringFactory.segmentFromSpec (sequenceFactory.ts:31-37)
+        Segment* s = mt.newSegment();
+        if (spec.t == JV::Str) {
+            s->text = spec.s;
+            s->len = (int)s->text.size();
+            return s;
+        }
+        if (spec.t == JV::Obj) {
+            JVP m = spec.o.get(u"marker");
+            JVP t = spec.o.get(u"text");
+            JVP p = spec.o.get(u"props");
+            if (m) {
+                s->marker = true;
+                JVP rt = m->t == JV::Obj ? m->o.get(u"refType") : nullptr;
+                s->refType = rt && rt->t == JV::Num ? (int)rt->n : 0;
+                s->len = 1;
+            } else if (t && t->t == JV::Str) {
+                s->text = t->s;
+                s->len = (int)s->text.size();
+            } else {
+                throw EngineError(MTE_DOC_UNSUPPORTED, "unknown segment spec");
+            }
+            if (truthy(p.get())) MergeTree::addProperties(s, p->o, false);
+            return s;
+        }
+        throw EngineError(MTE_DOC_UNSUPPORTED, "unknown segment spec");
+    }
+
+    static int num(const JObj& o, const char16_t* k, bool* has = nullptr) {
+        JVP v = o.get(k);
+        if (has) *has = v && v->t == JV::Num;
+        return v && v->t == JV::Num ? (int)v->n : 0;
+    }
+
+    // Client.applyRemoteOp (client.ts:776-803) -> applyInsertOp/RemoveRange/AnnotateRange (:328-449)
+    void applyRemoteOp(const JObj& op, int clientId, int refSeq, int seq) {
+        if (op.get(u"relativePos1") || op.get(u"relativePos2") || op.get(u"register"))
+            throw EngineError(MTE_DOC_UNSUPPORTED, "relative positions / registers are out of scope");
+        int type = num(op, u"type");
+        bool hasPos1 = false;
+        int pos1 = num(op, u"pos1", &hasPos1);
+        int pos2 = num(op, u"pos2");
+        switch (type) {
+            case 0: {
+                JVP seg = op.get(u"seg");
+                if (!seg) return;
+                std::vector<Segment*> segs{makeSegment(*seg)};
+                mt.insertSegments(pos1, segs, refSeq, clientId, seq);
+                opsApplied++;
+                break;
+            }
+            case 1:
+                mt.markRangeRemoved(pos1, pos2, refSeq, clientId, seq);
+                opsApplied++;
+                break;
+            case 2: {
+                JVP props = op.get(u"props");
+                JVP comb = op.get(u"combiningOp");
+                bool rewrite = false;
+                if (comb) {
+                    JVP name = comb->t == JV::Obj ? comb->o.get(u"name") : nullptr;
+                    if (name && name->t == JV::Str && name->s == u"rewrite") rewrite = true;
+                    else throw EngineError(MTE_DOC_UNSUPPORTED, "combiningOp other than rewrite");
+                }
+                JObj empty;
+                mt.annotateRange(pos1, pos2, props && props->t == JV::Obj ? props->o : empty, rewrite, refSeq,
+                                 clientId, seq);
+                opsApplied++;
+                break;
+            }
+            case 3: {
+                JVP ops = op.get(u"ops");
+                if (ops && ops->t == JV::Arr)
+                    for (auto& m : ops->a) applyRemoteOp(m->o, clientId, refSeq, seq);
+                break;
+            }
+            default: break;
+        }
+    }
+
+    // Client.applyMsg + updateSeqNumbers (client.ts:805-836)
+    void applyMsg(const JV& msg) {
+        if (status) return;
+        const JObj& m = msg.o;
+        JVP cid = m.get(u"clientId");
+        std::string clientName = cid && cid->t == JV::Str ? u16_to_utf8(cid->s) : "";
+        int seq = num(m, u"sequenceNumber");
+        int refSeq = num(m, u"referenceSequenceNumber");
+        int msn = num(m, u"minimumSequenceNumber");
+        try {
+            int shortId = getOrAddShortClientId(clientName);
+            JVP type = m.get(u"type");
+            if (type && type->t == JV::Str && type->s == u"op") {
+                if (clientName == observer) throw EngineError(MTE_DOC_UNSUPPORTED, "observer never submits ops");
+                if (!(mt.cw.currentSeq < seq)) throw EngineError(MTE_DOC_SEQ_ORDER, "seq <= currentSeq");
+                JVP contents = m.get(u"contents");
+                if (contents && contents->t == JV::Obj) applyRemoteOp(contents->o, shortId, refSeq, seq);
+            }
+            updateSeqNumbers(msn, seq);
+        } catch (EngineError& e) {
+            status = e.code;
+            failingSeq = seq;
+            error = e.what();
+        }
+    }
+
+    void updateSeqNumbers(int msn, int seq) {
+        if (seq < mt.cw.currentSeq) throw EngineError(MTE_DOC_SEQ_ORDER, "seq < currentSeq");
+        mt.cw.currentSeq = seq;
+        if (msn > seq) throw EngineError(MTE_DOC_SEQ_ORDER, "msn > seq");
+        mt.setMinSeq(msn);
+    }
+
+    // ---- binary batch input (include/mte.h records) ----------------------------------------
+    JObj propset(const mte_batch* b, uint32_t id) {
+        JObj o;
+        if (id == 0 || id >= b->n_propsets) return o;
+        const mte_propset& ps = b->propsets[id];
+        for (uint32_t i = 0; i < ps.count; i++) {
+            uint32_t k = b->prop_keys[ps.first + i], v = b->prop_vals[ps.first + i];
+            std::string ktxt(b->key_text + b->key_offsets[k], b->key_text + b->key_offsets[k + 1]);
+            std::string vtxt(b->val_text + b->val_offsets[v], b->val_text + b->val_offsets[v + 1]);
+            JVP kv = parse(ktxt);
+            o.set(kv->s, parse(vtxt));
+        }
+        return o;
+    }
+
+    void applyBatch(const mte_batch* b, uint32_t d) {
+        // client names in short-id order; the observer is short id 0
+        uint32_t c0 = b->doc_client_offsets[d], c1 = b->doc_client_offsets[d + 1];
+        std::vector<std::string> names;
+        for (uint32_t c = c0; c < c1; c++)
+            names.emplace_back(b->client_names + b->client_name_offsets[c],
+                               b->client_names + b->client_name_offsets[c + 1]);
+        const uint16_t* payload = b->payload + b->doc_payload_offsets[d];
+        for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1] && !status; i++) {
+            const mte_op& op = b->ops[i];
+            try {
+                if (op.client >= names.size()) throw EngineError(MTE_DOC_UNSUPPORTED, "client id out of range");
+                int shortId = getOrAddShortClientId(names[op.client]);
+                if (shortId != op.client) throw EngineError(MTE_DOC_UNSUPPORTED, "client ids not in first-appearance order");
+                if (op.type != MTE_OP_NOOP && !(mt.cw.currentSeq < op.seq))
+                    throw EngineError(MTE_DOC_SEQ_ORDER, "seq <= currentSeq");
+                switch (op.type) {
+                    case MTE_OP_INSERT:
+                    case MTE_OP_INSERT_MARKER: {
+                        Segment* s = mt.newSegment();
+                        if (op.type == MTE_OP_INSERT) {
+                            s->text.assign((const char16_t*)payload + op.a, op.b);
+                            s->len = (int)op.b;
+                        } else {
+                            s->marker = true;
+                            s->refType = (int)op.b;
+                            s->len = 1;
+                        }
+                        if (op.props) MergeTree::addProperties(s, propset(b, op.props), false);
+                        std::vector<Segment*> segs{s};
+                        mt.insertSegments(op.pos1, segs, op.ref_seq, op.client, op.seq);
+                        opsApplied++;
+                        break;
+                    }
+                    case MTE_OP_REMOVE:
+                        mt.markRangeRemoved(op.pos1, op.a, op.ref_seq, op.client, op.seq);
+                        opsApplied++;
+                        break;
+                    case MTE_OP_ANNOTATE:
+                        mt.annotateRange(op.pos1, op.a, propset(b, op.props), (op.flags & MTE_F_REWRITE) != 0,
+                                         op.ref_seq, op.client, op.seq);
+                        opsApplied++;
+                        break;
+                    default: break;
+                }
+                if (op.flags & MTE_F_END_OF_MSG) updateSeqNumbers(op.msn, op.seq);
+            } catch (EngineError& e) {
+                status = e.code;
+                failingSeq = op.seq;
+                error = e.what();
+            }
+        }
+    }
+
+    // ---- local, non-collaborative ops (SharedString before attach; generateSharedStrings.ts) --
+    void localInsert(int pos, Segment* s) {
+        std::vector<Segment*> segs{s};
+        mt.insertSegments(pos, segs, mt.cw.currentSeq, mt.cw.clientId, UniversalSequenceNumber);
+    }
+
+    // ---- outputs ------------------------------------------------------------------------------
+    u16s text() {  // MergeTreeTextHelper.getText(currentSeq, clientId) (textSegment.ts:154-172)
+        u16s out;
+        auto f = [&](Segment* s) {
+            if (!s->marker && !s->removed) out += s->text;
+            return true;
+        };
+        mt.walkAllSegments(mt.root, f);
+        return out;
+    }
+
+    std::string segmentsJson() {
+        std::string o = "[";
+        bool first = true;
+        auto f = [&](Segment* s) {
+            if (!first) o += ",";
+            first = false;
+            o += "{\"kind\":";
+            o += s->marker ? "\"M\"" : "\"T\"";
+            if (s->marker) o += ",\"refType\":" + std::to_string(s->refType);
+            else { o += ",\"text\":"; js_quote(o, s->text); }
+            o += ",\"len\":" + std::to_string(s->len) + ",\"seq\":" + std::to_string(s->seq) + ",\"client\":";
+            js_quote(o, utf8_to_u16(longId(s->clientId).data(), longId(s->clientId).size()));
+            if (s->removed) {
+                o += ",\"removedSeq\":" + std::to_string(s->removedSeq) + ",\"removedClient\":";
+                std::string rc = longId(s->removedClientId);
+                js_quote(o, utf8_to_u16(rc.data(), rc.size()));
+            }
+            std::vector<int> ov = s->overlap;
+            std::sort(ov.begin(), ov.end());
+            o += ",\"overlap\":[";
+            for (size_t i = 0; i < ov.size(); i++) {
+                if (i) o += ",";
+                std::string n = longId(ov[i]);
+                js_quote(o, utf8_to_u16(n.data(), n.size()));
+            }
+            o += "],\"props\":";
+            if (s->hasProps) {
+                std::string pj;
+                props_json(pj, s->props);
+                js_quote(o, utf8_to_u16(pj.data(), pj.size()));
+            } else {
+                o += "null";
+            }
+            o += "}";
+            return true;
+        };
+        mt.walkAllSegments(mt.root, f);
+        o += "]";
+        return o;
+    }
+
+    // SnapshotV1.extractSync (snapshotV1.ts:151-247) + emit (:85-149); blobs in tree-entry order
+    std::vector<std::string> snapshotBlobs(uint32_t chunkSize) {
+        int minSeq = mt.cw.minSeq, currentSeq = mt.cw.currentSeq;
+        std::vector<std::string> segJson;
+        std::vector<int> segLen;
+        // coalescing candidate: owned copy (clone + append never mutates the tree)
+        std::unique_ptr<Segment> prevClone;
+        Segment* prev = nullptr;
+        auto pushSeg = [&](Segment* s) {
+            if (!s) return;
+            std::string j;
+            segment_json(j, s);
+            segJson.push_back(j);
+            segLen.push_back(s->len);
+        };
+        auto f = [&](Segment* s) {
+            if (s->seq == UnassignedSequenceNumber || (s->removed && s->removedSeq <= minSeq)) return true;
+            if (s->seq <= minSeq && (!s->removed || s->removedSeq == UnassignedSequenceNumber)) {
+                if (!prev) {
+                    prev = s;
+                } else if (canAppend(prev, s) && matchProperties(prev, s)) {
+                    auto c = std::make_unique<Segment>(*prev);
+                    c->text += s->text;
+                    c->len = (int)c->text.size();
+                    prevClone = std::move(c);
+                    prev = prevClone.get();
+                } else {
+                    pushSeg(prev);
+                    prevClone.reset();
+                    prev = s;
+                }
+            } else {
+                pushSeg(prev);
+                prevClone.reset();
+                prev = nullptr;
+                std::string raw = "{\"json\":";
+                segment_json(raw, s);
+                if (s->seq > minSeq) {
+                    raw += ",\"seq\":" + js_number(s->seq) + ",\"client\":";
+                    std::string c = longId(s->clientId);
+                    js_quote(raw, utf8_to_u16(c.data(), c.size()));
+                }
+                if (s->removed) {
+                    raw += ",\"removedSeq\":" + js_number(s->removedSeq) + ",\"removedClient\":";
+                    std::string c = longId(s->removedClientId);
+                    js_quote(raw, utf8_to_u16(c.data(), c.size()));
+                }
+                raw += "}";
+                segJson.push_back(raw);
+                segLen.push_back(s->len);
+            }
+            return true;
+        };
+        mt.walkAllSegments(mt.root, f);
+        pushSeg(prev);
+
+        // emit: greedy chunks (getSeqLengthSegs :57-79)
+        struct Chunk { size_t start, count; long long length; };
+        std::vector<Chunk> chunks;
+        size_t total = 0;
+        long long totalLen = 0;
+        do {
+            Chunk c{total, 0, 0};
+            while (c.length < (long long)chunkSize && c.start + c.count < segJson.size()) {
+                c.length += segLen[c.start + c.count];
+                c.count++;
+            }
+            chunks.push_back(c);
+            total += c.count;
+            totalLen += c.length;
+        } while (total < segJson.size());
+        auto chunkJson = [&](const Chunk& c, bool header) {
+            std::string o = "{\"version\":\"1\",\"segmentCount\":" + std::to_string(c.count) +
+                            ",\"length\":" + std::to_string(c.length) + ",\"segments\":[";
+            for (size_t i = 0; i < c.count; i++) {
+                if (i) o += ",";
+                o += segJson[c.start + i];
+            }
+            o += "],\"startIndex\":" + std::to_string(c.start);
+            if (header) {
+                o += ",\"headerMetadata\":{\"minSequenceNumber\":" + js_number(minSeq) +
+                     ",\"sequenceNumber\":" + js_number(currentSeq) + ",\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+                for (size_t i = 1; i < chunks.size(); i++) o += ",{\"id\":\"body_" + std::to_string(i - 1) + "\"}";
+                o += "],\"totalLength\":" + std::to_string(totalLen) +
+                     ",\"totalSegmentCount\":" + std::to_string(total) + "}";
+            }
+            o += "}";
+            return o;
+        };
+        std::vector<std::string> blobs;
+        for (size_t i = 0; i < chunks.size(); i++) blobs.push_back(chunkJson(chunks[i], i == 0));
+        return blobs;
+    }
+
+    std::string snapshotTree(uint32_t chunkSize) {
+        auto blobs = snapshotBlobs(chunkSize);
+        std::string o = "{\"entries\":[";
+        for (size_t i = 0; i < blobs.size(); i++) {
+            if (i) o += ",";
+            std::string path = i == 0 ? "header" : "body_" + std::to_string(i - 1);
+            o += "{\"mode\":\"100644\",\"path\":\"" + path + "\",\"type\":\"Blob\",\"value\":{\"contents\":";
+            js_quote(o, utf8_to_u16(blobs[i].data(), blobs[i].size()));
+            o += ",\"encoding\":\"utf-8\"}}";
+        }
+        o += "],\"id\":null}";
+        return o;
+    }
+
+    uint64_t checksum(uint32_t chunkSize) {
+        uint64_t h = 0xcbf29ce484222325ull;
+        std::string t = u16_to_utf8(text());
+        h = fnv1a(h, t.data(), t.size());
+        for (auto& b : snapshotBlobs(chunkSize)) {
+            uint8_t z = 0;
+            h = fnv1a(h, &z, 1);
+            h = fnv1a(h, b.data(), b.size());
+        }
+        return h;
+    }
+};
+
+}  // namespace orc
+
+using orc::Doc;
+
+static char* dupstr(const std::string& s) {
+    char* p = (char*)malloc(s.size() + 1);
+    memcpy(p, s.data(), s.size());
+    p[s.size()] = 0;
+    return p;
+}
+
+extern "C" {
+
+Doc* orc_new(const char* observer) { return new Doc(observer); }
+void orc_free(Doc* d) { delete d; }
+void orc_str_free(char* p) { free(p); }
+
+// Apply a JSON array of ISequencedDocumentMessage (or one message object).
+int orc_apply_json(Doc* d, const char* json, size_t len) {
+    try {
+        orc::JVP v = orc::parse(json, len);
+        if (v->t == orc::JV::Arr) {
+            for (auto& m : v->a) d->applyMsg(*m);
+        } else {
+            d->applyMsg(*v);
+        }
+    } catch (std::exception& e) {
+        d->status = MTE_DOC_UNSUPPORTED;
+        d->error = e.what();
+        return -1;
+    }
+    return d->status;
+}
+
+int orc_apply_batch(Doc* d, const mte_batch* b, uint32_t doc) {
+    d->applyBatch(b, doc);
+    return d->status;
+}
+
+static orc::JObj parse_props(const char* props_json) {
+    orc::JObj o;
+    if (props_json) {
+        orc::JVP v = orc::parse(props_json, strlen(props_json));
+        if (v->t == orc::JV::Obj) o = v->o;
+    }
+    return o;
+}
+
+int orc_local_insert_text(Doc* d, int pos, const char* text, const char* props_json) {
+    try {
+        orc::Segment* s = d->mt.newSegment();
+        s->text = orc::utf8_to_u16(text, strlen(text));
+        s->len = (int)s->text.size();
+        if (props_json) orc::MergeTree::addProperties(s, parse_props(props_json), false);
+        d->localInsert(pos, s);
+    } catch (orc::EngineError& e) {
+        d->status = e.code;
+        d->error = e.what();
+        return e.code;
+    }
+    return 0;
+}
+
+int orc_local_insert_marker(Doc* d, int pos, int refType, const char* props_json) {
+    try {
+        orc::Segment* s = d->mt.newSegment();
+        s->marker = true;
+        s->refType = refType;
+        s->len = 1;
+        if (props_json) orc::MergeTree::addProperties(s, parse_props(props_json), false);
+        d->localInsert(pos, s);
+    } catch (orc::EngineError& e) {
+        d->status = e.code;
+        d->error = e.what();
+        return e.code;
+    }
+    return 0;
+}
+
+int orc_local_remove(Doc* d, int start, int end) {
+    d->mt.markRangeRemoved(start, end, d->mt.cw.currentSeq, d->mt.cw.clientId, orc::UniversalSequenceNumber);
+    return 0;
+}
+
+int orc_local_annotate(Doc* d, int start, int end, const char* props_json) {
+    d->mt.annotateRange(start, end, parse_props(props_json), false, d->mt.cw.currentSeq, d->mt.cw.clientId,
+                        orc::UniversalSequenceNumber);
+    return 0;
+}
+
+int orc_get_length(Doc* d) { return d->mt.getLength(d->mt.cw.currentSeq, d->mt.cw.clientId); }
+int orc_get_length_at(Doc* d, int refSeq, int shortClientId) { return d->mt.getLength(refSeq, shortClientId); }
+
+char* orc_text(Doc* d) { return dupstr(orc::u16_to_utf8(d->text())); }
+char* orc_segments_json(Doc* d) { return dupstr(d->segmentsJson()); }
+char* orc_snapshot_json(Doc* d, uint32_t chunk) { return dupstr(d->snapshotTree(chunk ? chunk : 10000)); }
+uint64_t orc_checksum(Doc* d, uint32_t chunk) { return d->checksum(chunk ? chunk : 10000); }
+uint64_t orc_ops_applied(Doc* d) { return d->opsApplied; }
+
+int orc_status(Doc* d, char* msg, size_t cap, long long* failing_seq) {
+    if (msg && cap) {
+        snprintf(msg, cap, "%s", d->error.c_str());
+    }
+    if (failing_seq) *failing_seq = d->failingSeq;
+    return d->status;
+}
+
+int orc_stats(Doc* d, int* leaves, int* removed, int* height) {
+    *leaves = *removed = *height = 0;
+    d->mt.stats(d->mt.root, *leaves, *removed, *height);
+    return 0;
+}
+
+// CPU baseline / bulk parity: replay docs [d0, d1) of a batch on `threads` threads. Writes one
+// checksum (text + SnapshotV1 blobs) and status per doc; returns ops applied.
+uint64_t orc_replay_batch(const mte_batch* b, uint32_t d0, uint32_t d1, int threads, const char* observer,
+                          uint64_t* checksums, int32_t* statuses, int with_snapshot) {
+    std::atomic<uint32_t> next{d0};
+    std::atomic<uint64_t> ops{0};
+    auto work = [&]() {
+        uint64_t local = 0;
+        while (true) {
+            uint32_t d = next.fetch_add(1);
+            if (d >= d1) break;
+            uint32_t c0 = b->doc_client_offsets[d];
+            std::string obs(b->client_names + b->client_name_offsets[c0],
+                            b->client_names + b->client_name_offsets[c0 + 1]);
+            Doc doc(observer ? observer : obs.c_str());
+            doc.applyBatch(b, d);
+            local += doc.opsApplied;
+            if (checksums) checksums[d - d0] = with_snapshot ? doc.checksum(10000) : 0;
+            if (statuses) statuses[d - d0] = doc.status;
+        }
+        ops += local;
+    };
+    if (threads <= 1) {
+        work();
+    } else {
+        std::vector<std::thread> ts;
+        for (int i = 0; i < threads; i++) ts.emplace_back(work);
+        for (auto& t : ts) t.join();
+    }
+    return ops.load();
+}
+
+}  // extern "C"

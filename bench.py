@@ -1,0 +1,173 @@
+"""bench.py — headline benchmark of the MI355X merge-tree replay engine.
+
+Workload (BASELINE.json configs[1], "C2"): 4096 synthetic SharedString documents x 10,000 sequenced
+ops each, insert/remove only, 8 simulated writers plus a read-only observer (SURVEY §8d generator,
+run on the GPU). A step = one replay of the whole batch (Client.applyMsg for every message of every
+document, client.ts:805-836) from empty state to every document's final state, inputs resident in
+HBM. Multi-GPU: documents are sharded by doc id (each rank replays its own 4096-doc shard; weak
+scaling); the only collective is the final all-gather of 32-B per-document summary records over
+RCCL/xGMI, outside the timed region.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "sequenced ops applied/sec (whole node) + achieved HBM GB/s, 256k docs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+OP_RECORD_B, LEAF_BLOCK_B = 32, 512  # SURVEY §8(d) algorithmic bytes per op: 32 + P + 512
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--docs", type=int, default=4096)
+    ap.add_argument("--ops", type=int, default=10000)
+    ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--kind", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify-docs", type=int, default=32, help="docs checked against the oracle after timing")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")  # RCCL over xGMI
+    from fluidframework_amd import mte
+
+    eng = mte.Engine(local)
+    t0 = time.time()
+    # per-rank shard: distinct seeds => distinct documents (doc ids rank*docs + i)
+    eng.generate(args.kind, args.docs, args.ops, n_clients=args.clients, seed=1000 + rank)
+    gen_s = time.time() - t0
+    batch = eng.export_batch()
+    ops_np = mte.batch_ops(batch)
+    ins = ops_np["type"] == mte.MTE_OP_INSERT
+    payload_chars = int(ops_np["b"][ins].sum())
+    n_ops_rank = int(len(ops_np))
+
+    def step():
+        return eng.replay()
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    kms = []
+    st = None
+    for _ in range(args.steps):
+        st = step()
+        kms.append(st["kernel_ms"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert st["failed_docs"] == 0, st
+    ops_applied = st["ops"]
+    total_ops = ops_applied * world
+    ms_per_step = elapsed / args.steps * 1000.0
+    value = total_ops * args.steps / elapsed
+
+    # final summary gather (RCCL all-gather of 32-B records), outside the timed region
+    t1 = time.time()
+    summ = eng.summaries()
+    snap_host_s = time.time() - t1
+    snap_bytes = int(summ["snapshot_bytes"].sum())
+    if world > 1:
+        rec = torch.from_numpy(summ.view(np.uint8).copy()).cuda()
+        out = [torch.empty_like(rec) for _ in range(world)]
+        dist.all_gather(out, rec)
+        gathered = sum(o.numel() for o in out) // 32
+    else:
+        gathered = len(summ)
+
+    # roofline on the replay kernel: algorithmic bytes per launch / HIP-event kernel time
+    alg_bytes = n_ops_rank * (OP_RECORD_B + LEAF_BLOCK_B) + payload_chars  # 1 B/char ASCII payload
+    kernel_ms = sum(kms) / len(kms)
+    achieved = alg_bytes / (kernel_ms / 1000.0) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_replay.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            if pmc.get("docs") == args.docs and pmc.get("ops") == args.ops and pmc.get("kind") == args.kind:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    # verify a sample of documents against the CPU oracle (checker only)
+    verified = None
+    cpu = None
+    if rank == 0:
+        from oracle import replay_batch
+
+        nv = min(args.verify_docs, args.docs)
+        if nv:
+            o_ops, cks, sts = replay_batch(ctypes.addressof(batch), 0, nv, threads=args.cpu_threads)
+            verified = all(int(summ["checksum"][d]) == cks[d] and int(summ["status"][d]) == sts[d] for d in range(nv))
+        if not args.no_cpu_baseline:
+            # bounded sample: grow the doc count until ~cpu_seconds of oracle replay on cpu_threads threads
+            nd = max(args.cpu_threads, 16)
+            while True:
+                nd = min(nd, args.docs)
+                c0 = time.perf_counter()
+                c_ops, _, _ = replay_batch(ctypes.addressof(batch), 0, nd, threads=args.cpu_threads,
+                                           with_snapshot=False)
+                dt = time.perf_counter() - c0
+                if dt >= args.cpu_seconds * 0.5 or nd >= args.docs:
+                    break
+                nd = int(nd * min(8.0, max(2.0, args.cpu_seconds / max(dt, 1e-3))))
+            cpu = {"value": c_ops / dt, "unit": "ops/s", "cores": args.cpu_threads, "kind": "port",
+                   "sample": f"oracle (tree-shaped C++ restatement) replaying docs 0..{nd - 1} of the same C2 batch "
+                             f"({c_ops} ops, replay only) on {args.cpu_threads} threads in {dt:.2f} s"}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int32", "data": "synthetic (GPU generator, SURVEY §8d)",
+            "config": {"workload": f"C{args.kind}: {args.docs} docs x {args.ops} ops per GPU, "
+                                   f"{'insert/remove' if args.kind == 2 else 'mixed'}, {args.clients} writers",
+                       "docs_per_gpu": args.docs, "ops_per_doc": args.ops, "clients": args.clients,
+                       "parallelism": f"doc-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "mte::k_replay", "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "extra": {"ops_per_step_per_gpu": ops_applied, "gen_s": gen_s, "snapshot_host_s": snap_host_s,
+                      "snapshot_bytes": snap_bytes, "summaries_gathered": gathered, "oracle_verified_docs": verified},
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

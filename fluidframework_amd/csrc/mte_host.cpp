@@ -1,0 +1,1260 @@
+// mte_host.cpp — host side of the MI355X merge-tree replay engine: the C ABI of include/mte.h.
+//
+//   * mte_builder_*: ISequencedDocumentMessage JSON logs -> SoA op records + interned property sets
+//     (Client.applyMsg input, client.ts:805-836; op shapes ops.ts:29-110).
+//   * mte_load / mte_generate: stage batches in HBM, size per-document arenas.
+//   * mte_replay: one wavefront per document on the GPU (mte_kernels.hip / engine_core.hpp).
+//   * outputs: text (textSegment.ts:154-172), segment table (walkAllSegments, mergeTree.ts:2969),
+//     SnapshotV1 ITree (snapshotV1.ts:85-247), per-doc FNV-1a-64 summary.
+// There is no CPU execution path for replay: without a HIP device mte_create fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mte.h"
+#include "engine_types.hpp"
+#include "jsonlite.hpp"
+#include "mte_kernels.h"
+
+using namespace mte;
+
+namespace {
+
+struct HostBatch {
+    std::vector<uint64_t> doc_op_offsets{0};
+    std::vector<mte_op> ops;
+    std::vector<uint64_t> doc_payload_offsets{0};
+    std::vector<uint16_t> payload;
+    std::vector<mte_propset> propsets{mte_propset{0, 0}};
+    std::vector<uint32_t> prop_keys, prop_vals;
+    std::vector<uint64_t> key_offsets{0};
+    std::string key_text;
+    std::vector<uint64_t> val_offsets{0};
+    std::string val_text;
+    std::vector<uint32_t> doc_client_offsets{0};
+    std::vector<uint64_t> client_name_offsets{0};
+    std::string client_names;
+
+    uint32_t n_docs() const { return (uint32_t)doc_op_offsets.size() - 1; }
+    void view(mte_batch* b) const {
+        b->n_docs = n_docs();
+        b->doc_op_offsets = doc_op_offsets.data();
+        b->ops = ops.data();
+        b->doc_payload_offsets = doc_payload_offsets.data();
+        b->payload = payload.data();
+        b->n_propsets = (uint32_t)propsets.size();
+        b->propsets = propsets.data();
+        b->prop_keys = prop_keys.data();
+        b->prop_vals = prop_vals.data();
+        b->n_keys = (uint32_t)key_offsets.size() - 1;
+        b->key_offsets = key_offsets.data();
+        b->key_text = key_text.data();
+        b->n_vals = (uint32_t)val_offsets.size() - 1;
+        b->val_offsets = val_offsets.data();
+        b->val_text = val_text.data();
+        b->doc_client_offsets = doc_client_offsets.data();
+        b->client_name_offsets = client_name_offsets.data();
+        b->client_names = client_names.data();
+    }
+    void copy_from(const mte_batch* b) {
+        const uint32_t n = b->n_docs;
+        doc_op_offsets.assign(b->doc_op_offsets, b->doc_op_offsets + n + 1);
+        ops.assign(b->ops, b->ops + doc_op_offsets[n]);
+        doc_payload_offsets.assign(b->doc_payload_offsets, b->doc_payload_offsets + n + 1);
+        payload.assign(b->payload, b->payload + doc_payload_offsets[n]);
+        propsets.assign(b->propsets, b->propsets + b->n_propsets);
+        size_t nkv = 0;
+        for (auto& ps : propsets) nkv = std::max<size_t>(nkv, (size_t)ps.first + ps.count);
+        prop_keys.assign(b->prop_keys, b->prop_keys + nkv);
+        prop_vals.assign(b->prop_vals, b->prop_vals + nkv);
+        key_offsets.assign(b->key_offsets, b->key_offsets + b->n_keys + 1);
+        key_text.assign(b->key_text, b->key_offsets[b->n_keys]);
+        val_offsets.assign(b->val_offsets, b->val_offsets + b->n_vals + 1);
+        val_text.assign(b->val_text, b->val_offsets[b->n_vals]);
+        doc_client_offsets.assign(b->doc_client_offsets, b->doc_client_offsets + n + 1);
+        uint32_t nn = doc_client_offsets[n];
+        client_name_offsets.assign(b->client_name_offsets, b->client_name_offsets + nn + 1);
+        client_names.assign(b->client_names, b->client_name_offsets[nn]);
+    }
+    std::string key(uint32_t k) const { return key_text.substr(key_offsets[k], key_offsets[k + 1] - key_offsets[k]); }
+    std::string val(uint32_t v) const { return val_text.substr(val_offsets[v], val_offsets[v + 1] - val_offsets[v]); }
+    std::string client(uint32_t doc, uint32_t shortId) const {
+        uint32_t i = doc_client_offsets[doc] + shortId;
+        if (i >= doc_client_offsets[doc + 1]) return std::string();
+        return client_names.substr(client_name_offsets[i], client_name_offsets[i + 1] - client_name_offsets[i]);
+    }
+};
+
+// Interning tables shared by the builder and the generator.
+struct Interner {
+    HostBatch* hb;
+    std::unordered_map<std::string, uint32_t> keys, vals;
+    std::map<std::vector<uint32_t>, uint32_t> sets;
+    explicit Interner(HostBatch* h) : hb(h) {
+        if (hb->val_offsets.size() == 1) {  // value id 0 == JSON null (a delete in annotate)
+            hb->val_text = "null";
+            hb->val_offsets.push_back(4);
+        }
+        vals["null"] = 0;
+    }
+    uint32_t key(const std::u16string& k) {
+        std::string q;
+        json::quote(q, k);
+        auto it = keys.find(q);
+        if (it != keys.end()) return it->second;
+        uint32_t id = (uint32_t)hb->key_offsets.size() - 1;
+        hb->key_text += q;
+        hb->key_offsets.push_back(hb->key_text.size());
+        keys[q] = id;
+        return id;
+    }
+    uint32_t val(const std::string& canonical) {
+        auto it = vals.find(canonical);
+        if (it != vals.end()) return it->second;
+        uint32_t id = (uint32_t)hb->val_offsets.size() - 1;
+        hb->val_text += canonical;
+        hb->val_offsets.push_back(hb->val_text.size());
+        vals[canonical] = id;
+        return id;
+    }
+    // A props object in Object.keys order (properties are applied key by key in that order,
+    // segmentPropertiesManager.ts:81-106).
+    uint32_t propset(const json::Value& obj) {
+        std::vector<uint32_t> kv;
+        for (size_t i : json::key_order(obj)) {
+            kv.push_back(key(obj.members[i].first));
+            kv.push_back(val(json::stringify(obj.members[i].second)));
+        }
+        return intern_kv(kv);
+    }
+    uint32_t intern_kv(const std::vector<uint32_t>& kv) {
+        auto it = sets.find(kv);
+        if (it != sets.end()) return it->second;
+        uint32_t id = (uint32_t)hb->propsets.size();
+        mte_propset ps{(uint32_t)hb->prop_keys.size(), (uint32_t)(kv.size() / 2)};
+        for (size_t i = 0; i < kv.size(); i += 2) {
+            hb->prop_keys.push_back(kv[i]);
+            hb->prop_vals.push_back(kv[i + 1]);
+        }
+        hb->propsets.push_back(ps);
+        sets[kv] = id;
+        return id;
+    }
+};
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t alloc(size_t count) {
+        release();
+        n = count;
+        if (count == 0) count = 1;
+        return hipMalloc((void**)&p, count * sizeof(T));
+    }
+};
+
+}  // namespace
+
+struct mte_builder {
+    HostBatch hb;
+    std::unique_ptr<Interner> in;
+    std::string err;
+    mte_builder() { in.reset(new Interner(&hb)); }
+};
+
+struct mte_engine {
+    int device = 0;
+    uint32_t chunk = 10000;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    HostBatch hb;
+    bool generated = false;    // ops/payload live on the device; host copy filled on demand
+    bool host_ops_valid = false;
+    uint32_t gen_kind = 0;
+    // derived per-value data (matchProperties, rewrite truthiness)
+    std::vector<uint32_t> val_flags, val_objidx;
+    std::vector<uint64_t> val_objmatch;
+    std::vector<uint8_t> key_is_index;
+    std::vector<uint32_t> key_index;
+    // layout
+    std::vector<DocCfg> cfg;
+    std::vector<uint32_t> order;
+    std::vector<DocRes> res;
+    Params P{};
+    bool replayed = false;
+    bool downloaded = false;
+    double last_kernel_ms = 0, last_h2d_ms = 0;
+    // device buffers
+    DevBuf<mte_op> d_ops;
+    DevBuf<uint16_t> d_payload, d_arena;
+    DevBuf<mte_propset> d_propsets;
+    DevBuf<uint32_t> d_prop_keys, d_prop_vals, d_val_flags, d_val_objidx, d_order, d_seg_parent, d_lbo, d_maps;
+    DevBuf<uint64_t> d_val_objmatch;
+    DevBuf<DocCfg> d_cfg;
+    DevBuf<DocRes> d_res;
+    DevBuf<uint2> d_heap;
+    DevBuf<uint4> d_lb_vis;
+    DevBuf<uint64_t> d_lb_ovl;
+    DevBuf<uint32_t> d_lb_props, d_lb_sid, d_lb_cnt, d_lb_par, d_lb_scour, d_in_child, d_in_cnt, d_in_par, d_counters,
+        d_first_seen;
+    DevBuf<uint2> d_lb_txt;
+    // downloaded final state
+    std::vector<uint32_t> h_lbo, h_maps, h_lb_cnt, h_lb_props;
+    std::vector<uint4> h_lb_vis;
+    std::vector<uint64_t> h_lb_ovl;
+    std::vector<uint2> h_lb_txt;
+    std::vector<uint16_t> h_arena;
+    uint32_t h_nlb_used = 0;
+};
+
+static int set_err(mte_engine* e, int code, const std::string& m) {
+    if (e) e->err = m;
+    return code;
+}
+#define HIP_TRY(e, x)                                                                     \
+    do {                                                                                  \
+        hipError_t _r = (x);                                                              \
+        if (_r != hipSuccess) return set_err(e, MTE_E_HIP, std::string(#x ": ") + hipGetErrorString(_r)); \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// Value / key metadata for the device: JS falsiness (rewrite), object-typed values and the
+// matchProperties relation against object-typed values (properties.ts:62-93).
+static int derive_value_tables(mte_engine* e) {
+    const HostBatch& hb = e->hb;
+    uint32_t nv = (uint32_t)hb.val_offsets.size() - 1;
+    std::vector<json::Value> vals(nv);
+    for (uint32_t v = 0; v < nv; v++) {
+        std::string t = hb.val(v);
+        try {
+            vals[v] = json::parse(t.data(), t.size());
+        } catch (std::exception& ex) {
+            return set_err(e, MTE_E_PARSE, ex.what());
+        }
+    }
+    e->val_flags.assign(nv, 0);
+    e->val_objidx.assign(nv, NONE);
+    e->val_objmatch.assign(nv, 0);
+    std::vector<uint32_t> objs;
+    for (uint32_t v = 0; v < nv; v++) {
+        if (!json::truthy(&vals[v])) e->val_flags[v] |= 1u;
+        if (json::is_object_typed(&vals[v]) && v != 0) {
+            e->val_flags[v] |= 2u;
+            if (objs.size() < 64) {
+                e->val_objidx[v] = (uint32_t)objs.size();
+                objs.push_back(v);
+            }
+        }
+    }
+    for (uint32_t v = 0; v < nv; v++)
+        for (size_t j = 0; j < objs.size(); j++)
+            if (json::match_properties(&vals[v], &vals[objs[j]])) e->val_objmatch[v] |= 1ull << j;
+    uint32_t nk = (uint32_t)hb.key_offsets.size() - 1;
+    e->key_is_index.assign(nk, 0);
+    e->key_index.assign(nk, 0);
+    for (uint32_t k = 0; k < nk; k++) {
+        std::string t = hb.key(k);
+        json::Value kv = json::parse(t.data(), t.size());
+        uint32_t idx;
+        if (json::array_index(kv.str, &idx)) {
+            e->key_is_index[k] = 1;
+            e->key_index[k] = idx;
+        }
+    }
+    return MTE_OK;
+}
+
+template <class T>
+static int upload(mte_engine* e, DevBuf<T>& d, const std::vector<T>& h) {
+    HIP_TRY(e, d.alloc(h.size()));
+    if (!h.empty()) HIP_TRY(e, hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, e->stream));
+    return MTE_OK;
+}
+
+// Per-document arena sizing (see DESIGN.md "HBM layout").
+static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, const std::vector<uint64_t>& pay_len,
+                            const std::vector<uint64_t>& n_prop_ins, const std::vector<uint64_t>& n_ann,
+                            const std::vector<uint8_t>& collab, uint64_t arena_limit = 0) {
+    const uint32_t nd = (uint32_t)n_ops.size();
+    e->cfg.assign(nd, DocCfg{});
+    uint64_t op = 0, pay = 0, ar = 0, seg = 0, hp = 0, lb = 0, mp = 0, nlb = 0;
+    for (uint32_t d = 0; d < nd; d++) {
+        DocCfg& c = e->cfg[d];
+        uint64_t n = n_ops[d];
+        c.op_begin = op;
+        c.op_end = op + n;
+        op += n;
+        c.payload_off = pay;
+        c.payload_len = (uint32_t)pay_len[d];
+        pay += pay_len[d];
+        // merge arena semispace: live arena text <= 2x live text, a scour needs <= 4x a block's text
+        uint64_t acap = 6 * pay_len[d] + 4096;
+        if (arena_limit) acap = std::min<uint64_t>(acap, arena_limit);
+        c.arena_cap = (uint32_t)std::min<uint64_t>(acap, 0x7FFFFFF0ull / 2);
+        c.arena_off = ar;
+        ar += 2ull * c.arena_cap;
+        c.seg_cap = (uint32_t)(3 * n + 8);
+        c.seg_off = seg;
+        seg += c.seg_cap;
+        c.heap_cap = (uint32_t)(2 * n + 64);
+        c.heap_off = hp;
+        hp += c.heap_cap;
+        c.lbo_cap = (uint32_t)(n / 2 + 64);
+        c.lbo_off = lb;
+        lb += c.lbo_cap;
+        c.map_cap = (uint32_t)(n_prop_ins[d] + 4 * n_ann[d] + 16);
+        c.map_off = mp;
+        mp += c.map_cap;
+        c.collab = collab[d];
+        nlb += n / 4 + 64;
+    }
+    uint64_t nin = nlb / 3 + 16ull * nd + 64;
+    HIP_TRY(e, e->d_arena.alloc(ar));
+    HIP_TRY(e, e->d_seg_parent.alloc(seg));
+    HIP_TRY(e, e->d_heap.alloc(hp));
+    HIP_TRY(e, e->d_lbo.alloc(lb));
+    HIP_TRY(e, e->d_maps.alloc(mp * MAP_WORDS));
+    HIP_TRY(e, e->d_lb_vis.alloc(nlb * 8));
+    HIP_TRY(e, e->d_lb_ovl.alloc(nlb * 8));
+    HIP_TRY(e, e->d_lb_props.alloc(nlb * 8));
+    HIP_TRY(e, e->d_lb_txt.alloc(nlb * 8));
+    HIP_TRY(e, e->d_lb_sid.alloc(nlb * 8));
+    HIP_TRY(e, e->d_lb_cnt.alloc(nlb));
+    HIP_TRY(e, e->d_lb_par.alloc(nlb));
+    HIP_TRY(e, e->d_lb_scour.alloc(nlb));
+    HIP_TRY(e, e->d_in_child.alloc(nin * 8));
+    HIP_TRY(e, e->d_in_cnt.alloc(nin));
+    HIP_TRY(e, e->d_in_par.alloc(nin));
+    HIP_TRY(e, e->d_counters.alloc(4));
+    HIP_TRY(e, e->d_res.alloc(nd));
+    // LPT order: longest documents start first
+    e->order.resize(nd);
+    for (uint32_t d = 0; d < nd; d++) e->order[d] = d;
+    std::stable_sort(e->order.begin(), e->order.end(), [&](uint32_t a, uint32_t b) { return n_ops[a] > n_ops[b]; });
+    int rc;
+    if ((rc = upload(e, e->d_cfg, e->cfg))) return rc;
+    if ((rc = upload(e, e->d_order, e->order))) return rc;
+    Params& P = e->P;
+    P = Params{};
+    P.n_docs = nd;
+    P.docs = e->d_cfg.p;
+    P.doc_order = e->d_order.p;
+    P.res = e->d_res.p;
+    P.arena = e->d_arena.p;
+    P.seg_parent = e->d_seg_parent.p;
+    P.heap = e->d_heap.p;
+    P.lbo = e->d_lbo.p;
+    P.maps = e->d_maps.p;
+    P.lb_vis = e->d_lb_vis.p;
+    P.lb_ovl = e->d_lb_ovl.p;
+    P.lb_props = e->d_lb_props.p;
+    P.lb_txt = e->d_lb_txt.p;
+    P.lb_sid = e->d_lb_sid.p;
+    P.lb_cnt = e->d_lb_cnt.p;
+    P.lb_par = e->d_lb_par.p;
+    P.lb_scour = e->d_lb_scour.p;
+    P.in_child = e->d_in_child.p;
+    P.in_cnt = e->d_in_cnt.p;
+    P.in_par = e->d_in_par.p;
+    P.counters = e->d_counters.p;
+    P.nlb_cap = (uint32_t)std::min<uint64_t>(nlb, 0xFFFFFFF0ull);
+    P.nin_cap = (uint32_t)std::min<uint64_t>(nin, 0xFFFFFFF0ull);
+    return MTE_OK;
+}
+
+static int upload_props(mte_engine* e) {
+    int rc;
+    if ((rc = derive_value_tables(e))) return rc;
+    if ((rc = upload(e, e->d_propsets, e->hb.propsets))) return rc;
+    if ((rc = upload(e, e->d_prop_keys, e->hb.prop_keys))) return rc;
+    if ((rc = upload(e, e->d_prop_vals, e->hb.prop_vals))) return rc;
+    if ((rc = upload(e, e->d_val_flags, e->val_flags))) return rc;
+    if ((rc = upload(e, e->d_val_objidx, e->val_objidx))) return rc;
+    if ((rc = upload(e, e->d_val_objmatch, e->val_objmatch))) return rc;
+    e->P.propsets = e->d_propsets.p;
+    e->P.prop_keys = e->d_prop_keys.p;
+    e->P.prop_vals = e->d_prop_vals.p;
+    e->P.val_flags = e->d_val_flags.p;
+    e->P.val_objidx = e->d_val_objidx.p;
+    e->P.val_objmatch = e->d_val_objmatch.p;
+    e->P.n_propsets = (uint32_t)e->hb.propsets.size();
+    e->P.n_vals = (uint32_t)e->val_flags.size();
+    return MTE_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+int mte_abi_version(void) { return MTE_ABI_VERSION; }
+
+const char* mte_build_info(void) {
+    static std::string s = std::string("mte gfx950 hip ") + std::to_string(HIP_VERSION_MAJOR) + "." +
+                           std::to_string(HIP_VERSION_MINOR);
+    return s.c_str();
+}
+
+int mte_create(const mte_config* cfg, mte_engine** out) {
+    if (!out) return MTE_E_ARG;
+    *out = nullptr;
+    std::unique_ptr<mte_engine> e(new mte_engine());
+    if (cfg) {
+        e->device = cfg->device;
+        if (cfg->chunk_size) e->chunk = cfg->chunk_size;
+    }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= e->device) {
+        // No CPU fallback: the replay path runs on the GPU only.
+        static thread_local std::string why;
+        why = "mte: no HIP device available (MI355X/gfx950 required)";
+        return MTE_E_HIP;
+    }
+    HIP_TRY(e.get(), hipSetDevice(e->device));
+    HIP_TRY(e.get(), hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    HIP_TRY(e.get(), hipEventCreate(&e->ev0));
+    HIP_TRY(e.get(), hipEventCreate(&e->ev1));
+    *out = e.release();
+    return MTE_OK;
+}
+
+void mte_destroy(mte_engine* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->ev0) (void)hipEventDestroy(e->ev0);
+    if (e->ev1) (void)hipEventDestroy(e->ev1);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+const char* mte_last_error(const mte_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+static void count_doc_ops(const HostBatch& hb, uint32_t d, uint64_t& pi, uint64_t& an) {
+    pi = an = 0;
+    for (uint64_t i = hb.doc_op_offsets[d]; i < hb.doc_op_offsets[d + 1]; i++) {
+        const mte_op& o = hb.ops[i];
+        if ((o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER) && o.props) pi++;
+        if (o.type == MTE_OP_ANNOTATE) an++;
+    }
+}
+
+int mte_load(mte_engine* e, const mte_batch* b) {
+    if (!e || !b) return MTE_E_ARG;
+    HIP_TRY(e, hipSetDevice(e->device));
+    e->hb.copy_from(b);
+    e->generated = false;
+    e->host_ops_valid = true;
+    e->replayed = e->downloaded = false;
+    const uint32_t nd = b->n_docs;
+    std::vector<uint64_t> n_ops(nd), pay(nd), pi(nd), an(nd);
+    std::vector<uint8_t> collab(nd);
+    for (uint32_t d = 0; d < nd; d++) {
+        n_ops[d] = b->doc_op_offsets[d + 1] - b->doc_op_offsets[d];
+        pay[d] = b->doc_payload_offsets[d + 1] - b->doc_payload_offsets[d];
+        count_doc_ops(e->hb, d, pi[d], an[d]);
+        collab[d] = e->hb.client(d, 0).empty() ? 0 : 1;  // empty observer name => local, non-collab
+        if (b->doc_client_offsets[d + 1] - b->doc_client_offsets[d] > MTE_MAX_CLIENTS)
+            return set_err(e, MTE_E_UNSUPPORTED, "more than 64 clients in a document");
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    int rc;
+    if ((rc = layout_and_alloc(e, n_ops, pay, pi, an, collab))) return rc;
+    if ((rc = upload(e, e->d_ops, e->hb.ops))) return rc;
+    if ((rc = upload(e, e->d_payload, e->hb.payload))) return rc;
+    if ((rc = upload_props(e))) return rc;
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->last_h2d_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    e->P.ops = e->d_ops.p;
+    e->P.payload = e->d_payload.p;
+    return MTE_OK;
+}
+
+static int run_kernel(mte_engine* e, bool gen) {
+    HIP_TRY(e, hipSetDevice(e->device));
+    HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 4 * sizeof(uint32_t), e->stream));
+    HIP_TRY(e, hipEventRecord(e->ev0, e->stream));
+    HIP_TRY(e, gen ? launch_generate(e->P, e->P.n_docs, e->stream) : launch_replay(e->P, e->P.n_docs, e->stream));
+    HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    float ms = 0;
+    HIP_TRY(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    e->last_kernel_ms = ms;
+    e->res.resize(e->P.n_docs);
+    HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, e->res.size() * sizeof(DocRes), hipMemcpyDeviceToHost));
+    e->replayed = true;
+    e->downloaded = false;
+    return MTE_OK;
+}
+
+int mte_replay(mte_engine* e, mte_stats* out) {
+    if (!e) return MTE_E_ARG;
+    if (!e->P.ops) return set_err(e, MTE_E_STATE, "mte_replay before mte_load/mte_generate");
+    int rc = run_kernel(e, false);
+    if (rc) return rc;
+    if (out) {
+        memset(out, 0, sizeof *out);
+        out->docs = e->P.n_docs;
+        for (auto& r : e->res) {
+            out->ops += r.ops;
+            out->messages += r.msgs;
+            if (r.status) out->failed_docs++;
+        }
+        out->kernel_ms = e->last_kernel_ms;
+        out->h2d_ms = e->last_h2d_ms;
+    }
+    return MTE_OK;
+}
+
+// The generator's property sets: every single-key set and every two-key set over the C3 keys and
+// values, in a fixed order.
+static uint32_t build_generator_props(mte_engine* e) {
+    Interner in(&e->hb);
+    const char16_t* keys[4] = {u"bold", u"italic", u"color", u"size"};
+    const char* vals[7] = {"true", "false", "\"red\"", "\"blue\"", "10", "12", "null"};
+    uint32_t kid[4], vid[7];
+    for (int i = 0; i < 4; i++) kid[i] = in.key(keys[i]);
+    for (int i = 0; i < 7; i++) vid[i] = in.val(vals[i]);
+    uint32_t n = 0;
+    for (int k = 0; k < 4; k++)
+        for (int v = 0; v < 7; v++) {
+            in.intern_kv({kid[k], vid[v]});
+            n++;
+        }
+    for (int k1 = 0; k1 < 4; k1++)
+        for (int k2 = k1 + 1; k2 < 4; k2++)
+            for (int v1 = 0; v1 < 7; v1++)
+                for (int v2 = 0; v2 < 7; v2++) {
+                    in.intern_kv({kid[k1], vid[v1], kid[k2], vid[v2]});
+                    n++;
+                }
+    return n;
+}
+
+int mte_generate(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, const uint32_t* ops_per_doc,
+                 uint32_t n_clients, uint64_t seed_base) {
+    if (!e || n_docs == 0 || n_clients == 0 || n_clients >= MTE_MAX_CLIENTS) return MTE_E_ARG;
+    if (kind != 2 && kind != 3 && kind != 5) return set_err(e, MTE_E_ARG, "generator kind must be 2, 3 or 5");
+    HIP_TRY(e, hipSetDevice(e->device));
+    e->hb = HostBatch();
+    uint32_t nps = build_generator_props(e);
+    std::vector<uint64_t> nops(n_docs), pay(n_docs), pi(n_docs), an(n_docs);
+    std::vector<uint8_t> collab(n_docs, 1);
+    for (uint32_t d = 0; d < n_docs; d++) {
+        uint64_t n = ops_per_doc ? ops_per_doc[d] : n_ops;
+        nops[d] = n;
+        pay[d] = 8 * n;
+        pi[d] = kind == 3 ? n : 0;
+        an[d] = kind == 3 ? n : 0;
+        e->hb.doc_op_offsets.push_back(e->hb.doc_op_offsets.back() + n);
+        e->hb.doc_payload_offsets.push_back(e->hb.doc_payload_offsets.back() + 8 * n);
+    }
+    int rc;
+    // generated docs hover around a 2048-char target length: 64K-unit semispaces are ample
+    if ((rc = layout_and_alloc(e, nops, pay, pi, an, collab, 65536))) return rc;
+    HIP_TRY(e, e->d_ops.alloc(e->hb.doc_op_offsets.back()));
+    HIP_TRY(e, e->d_payload.alloc(e->hb.doc_payload_offsets.back()));
+    HIP_TRY(e, hipMemsetAsync(e->d_payload.p, 0, e->d_payload.n * sizeof(uint16_t), e->stream));
+    HIP_TRY(e, e->d_first_seen.alloc((size_t)n_docs * MTE_MAX_CLIENTS));
+    HIP_TRY(e, hipMemsetAsync(e->d_first_seen.p, 0xFF, (size_t)n_docs * MTE_MAX_CLIENTS * 4, e->stream));
+    if ((rc = upload_props(e))) return rc;
+    e->P.ops = e->d_ops.p;
+    e->P.payload = e->d_payload.p;
+    e->P.gen_first_seen = e->d_first_seen.p;
+    e->P.gen_kind = kind;
+    e->P.gen_nclients = n_clients;
+    e->P.gen_seed = seed_base;
+    e->P.gen_n_propsets = nps;
+    e->gen_kind = kind;
+    rc = run_kernel(e, true);
+    if (rc) return rc;
+    // client names: observer + writers in first-appearance (short id) order
+    std::vector<uint32_t> fs((size_t)n_docs * MTE_MAX_CLIENTS);
+    HIP_TRY(e, hipMemcpy(fs.data(), e->d_first_seen.p, fs.size() * 4, hipMemcpyDeviceToHost));
+    for (uint32_t d = 0; d < n_docs; d++) {
+        std::vector<std::string> names{"__observer__"};
+        for (uint32_t s = 1; s < MTE_MAX_CLIENTS; s++) {
+            uint32_t w = fs[(size_t)d * MTE_MAX_CLIENTS + s];
+            if (w == 0xFFFFFFFFu) break;
+            names.push_back("client-" + std::to_string(w));
+        }
+        for (auto& nm : names) {
+            e->hb.client_names += nm;
+            e->hb.client_name_offsets.push_back(e->hb.client_names.size());
+        }
+        e->hb.doc_client_offsets.push_back(e->hb.doc_client_offsets.back() + (uint32_t)names.size());
+    }
+    e->generated = true;
+    e->host_ops_valid = false;
+    return MTE_OK;
+}
+
+static int ensure_host_ops(mte_engine* e) {
+    if (e->host_ops_valid) return MTE_OK;
+    e->hb.ops.resize(e->d_ops.n);
+    e->hb.payload.resize(e->d_payload.n);
+    HIP_TRY(e, hipMemcpy(e->hb.ops.data(), e->d_ops.p, e->hb.ops.size() * sizeof(mte_op), hipMemcpyDeviceToHost));
+    HIP_TRY(e, hipMemcpy(e->hb.payload.data(), e->d_payload.p, e->hb.payload.size() * 2, hipMemcpyDeviceToHost));
+    e->host_ops_valid = true;
+    return MTE_OK;
+}
+
+int mte_export_batch(mte_engine* e, mte_batch* out) {
+    if (!e || !out) return MTE_E_ARG;
+    if (!e->P.ops) return set_err(e, MTE_E_STATE, "nothing loaded");
+    int rc = ensure_host_ops(e);
+    if (rc) return rc;
+    e->hb.view(out);
+    return MTE_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Final-state download and the host-side output walkers.
+static int ensure_download(mte_engine* e) {
+    if (!e->replayed) return set_err(e, MTE_E_STATE, "no replay results yet");
+    if (e->downloaded) return MTE_OK;
+    int rc = ensure_host_ops(e);
+    if (rc) return rc;
+    HIP_TRY(e, hipSetDevice(e->device));
+    uint32_t ctr[4];
+    HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
+    uint32_t used = std::min(ctr[0], e->P.nlb_cap);
+    e->h_nlb_used = used;
+    auto dl = [&](auto& h, auto& d, size_t n) -> int {
+        h.resize(n);
+        if (n) HIP_TRY(e, hipMemcpy(h.data(), d.p, n * sizeof(h[0]), hipMemcpyDeviceToHost));
+        return MTE_OK;
+    };
+    if ((rc = dl(e->h_lbo, e->d_lbo, e->d_lbo.n))) return rc;
+    if ((rc = dl(e->h_maps, e->d_maps, e->d_maps.n))) return rc;
+    if ((rc = dl(e->h_lb_cnt, e->d_lb_cnt, used))) return rc;
+    if ((rc = dl(e->h_lb_props, e->d_lb_props, (size_t)used * 8))) return rc;
+    if ((rc = dl(e->h_lb_vis, e->d_lb_vis, (size_t)used * 8))) return rc;
+    if ((rc = dl(e->h_lb_ovl, e->d_lb_ovl, (size_t)used * 8))) return rc;
+    if ((rc = dl(e->h_lb_txt, e->d_lb_txt, (size_t)used * 8))) return rc;
+    if ((rc = dl(e->h_arena, e->d_arena, e->d_arena.n))) return rc;
+    e->downloaded = true;
+    return MTE_OK;
+}
+
+namespace {
+struct SegView {
+    uint32_t kind;  // 0 text, 1 marker
+    uint32_t len;
+    int32_t seq, client, rseq, rclient;
+    bool removed;
+    uint64_t ovl;
+    uint32_t props;
+    uint32_t reftype;
+    const uint16_t* text;
+};
+
+struct DocView {
+    const mte_engine* e;
+    uint32_t d;
+    std::vector<SegView> segs;
+    void build() {
+        const DocCfg& c = e->cfg[d];
+        const DocRes& r = e->res[d];
+        const uint16_t* pay = e->hb.payload.data() + c.payload_off;
+        const uint16_t* ar = e->h_arena.data() + c.arena_off + (uint64_t)r.arena_sel * c.arena_cap;
+        for (uint32_t k = 0; k < r.n_lb; k++) {
+            uint32_t blk = e->h_lbo[c.lbo_off + k];
+            if (blk >= e->h_nlb_used) continue;
+            for (uint32_t s = 0; s < e->h_lb_cnt[blk]; s++) {
+                uint32_t i = blk * 8 + s;
+                uint4 v = e->h_lb_vis[i];
+                uint2 t = e->h_lb_txt[i];
+                SegView sv;
+                sv.kind = (v.w & F_MARKER) ? 1 : 0;
+                sv.len = v.x;
+                sv.seq = (int32_t)v.y;
+                sv.removed = (v.w & F_REMOVED) != 0;
+                sv.rseq = (int32_t)v.z;
+                sv.client = c.collab ? (int32_t)(v.w & 0xff) : -1;
+                sv.rclient = c.collab ? (int32_t)((v.w >> 8) & 0xff) : -1;
+                sv.ovl = e->h_lb_ovl[i];
+                sv.props = e->h_lb_props[i];
+                sv.reftype = sv.kind ? t.x : 0;
+                sv.text = sv.kind ? nullptr : ((t.x & ARENA_BIT) ? ar + (t.x & ~ARENA_BIT) : pay + t.x);
+                segs.push_back(sv);
+            }
+        }
+    }
+    std::string long_id(int32_t shortId) const {
+        if (shortId < 0) return "original";
+        return e->hb.client(d, (uint32_t)shortId);
+    }
+    const uint32_t* map(uint32_t id) const { return e->h_maps.data() + (e->cfg[d].map_off + id) * MAP_WORDS; }
+    // JSON of a property map in JS key order (integer-like keys ascending first, then insertion order)
+    void props_json(std::string& o, uint32_t id) const {
+        const uint32_t* m = map(id);
+        uint32_t n = m[0];
+        std::vector<std::pair<uint32_t, uint32_t>> idx;
+        std::vector<uint32_t> rest;
+        for (uint32_t i = 0; i < n; i++) {
+            uint32_t k = m[1 + 2 * i];
+            if (e->key_is_index[k]) idx.emplace_back(e->key_index[k], i);
+            else rest.push_back(i);
+        }
+        std::sort(idx.begin(), idx.end());
+        o.push_back('{');
+        bool first = true;
+        auto emit = [&](uint32_t i) {
+            if (!first) o.push_back(',');
+            first = false;
+            o += e->hb.key(m[1 + 2 * i]);
+            o.push_back(':');
+            o += e->hb.val(m[2 + 2 * i]);
+        };
+        for (auto& p : idx) emit(p.second);
+        for (uint32_t i : rest) emit(i);
+        o.push_back('}');
+    }
+    bool val_match(uint32_t a, uint32_t b) const {
+        if (a == b) return true;
+        if (e->val_flags[b] & 2u) {
+            uint32_t j = e->val_objidx[b];
+            return j != NONE && ((e->val_objmatch[a] >> j) & 1ull);
+        }
+        return false;
+    }
+    bool match_props(uint32_t a, uint32_t b) const {
+        if (a == b) return true;
+        if (!a || !b) return false;
+        const uint32_t *ma = map(a), *mb = map(b);
+        if (ma[0] != mb[0]) return false;
+        for (uint32_t i = 0; i < ma[0]; i++) {
+            bool found = false;
+            for (uint32_t q = 0; q < mb[0]; q++)
+                if (mb[1 + 2 * q] == ma[1 + 2 * i]) {
+                    if (!val_match(ma[2 + 2 * i], mb[2 + 2 * q])) return false;
+                    found = true;
+                }
+            if (!found) return false;
+        }
+        return true;
+    }
+    void seg_json(std::string& o, const SegView& s, const std::u16string* text) const {
+        if (s.kind == 1) {
+            o += "{\"marker\":{\"refType\":" + json::number((double)s.reftype) + "}";
+            if (s.props) {
+                o += ",\"props\":";
+                props_json(o, s.props);
+            }
+            o += "}";
+        } else if (s.props) {
+            o += "{\"text\":";
+            if (text) json::quote(o, *text); else json::quote(o, (const char16_t*)s.text, s.len);
+            o += ",\"props\":";
+            props_json(o, s.props);
+            o += "}";
+        } else {
+            if (text) json::quote(o, *text); else json::quote(o, (const char16_t*)s.text, s.len);
+        }
+    }
+    // SnapshotV1.extractSync + emit (snapshotV1.ts:57-247)
+    std::vector<std::string> snapshot_blobs(uint32_t chunk) const {
+        const DocRes& r = e->res[d];
+        const int32_t minSeq = r.min_seq, curSeq = r.cur_seq;
+        std::vector<std::string> sj;
+        std::vector<uint32_t> sl;
+        const SegView* prev = nullptr;
+        std::u16string prevText;  // coalesced text of `prev`
+        uint32_t prevLen = 0;
+        auto push_prev = [&]() {
+            if (!prev) return;
+            std::string j;
+            seg_json(j, *prev, &prevText);
+            sj.push_back(std::move(j));
+            sl.push_back(prevLen);
+        };
+        for (const SegView& s : segs) {
+            if (s.removed && s.rseq <= minSeq) continue;  // elided (:184-186)
+            if (s.seq <= minSeq && !s.removed) {
+                if (!prev) {
+                    prev = &s;
+                    prevText.assign((const char16_t*)s.text, s.kind ? 0 : s.len);
+                    prevLen = s.len;
+                } else if (prev->kind == 0 && s.kind == 0 && !(prevLen && prevText.back() == u'\n') &&
+                           (prevLen <= 256 || s.len <= 256) && match_props(prev->props, s.props)) {
+                    prevText.append((const char16_t*)s.text, s.len);  // clone + append (:197-202)
+                    prevLen += s.len;
+                } else {
+                    push_prev();
+                    prev = &s;
+                    prevText.assign((const char16_t*)s.text, s.kind ? 0 : s.len);
+                    prevLen = s.len;
+                }
+            } else {
+                push_prev();
+                prev = nullptr;
+                std::string raw = "{\"json\":";
+                seg_json(raw, s, nullptr);
+                if (s.seq > minSeq) {
+                    raw += ",\"seq\":" + json::number(s.seq) + ",\"client\":";
+                    std::string c = long_id(s.client);
+                    std::u16string cu;
+                    json::decode_utf8(c.data(), c.size(), cu);
+                    json::quote(raw, cu);
+                }
+                if (s.removed) {
+                    raw += ",\"removedSeq\":" + json::number(s.rseq) + ",\"removedClient\":";
+                    std::string c = long_id(s.rclient);
+                    std::u16string cu;
+                    json::decode_utf8(c.data(), c.size(), cu);
+                    json::quote(raw, cu);
+                }
+                raw += "}";
+                sj.push_back(std::move(raw));
+                sl.push_back(s.len);
+            }
+        }
+        push_prev();
+        struct Chunk {
+            size_t start, count;
+            uint64_t length;
+        };
+        std::vector<Chunk> chunks;
+        size_t total = 0;
+        uint64_t totalLen = 0;
+        do {
+            Chunk c{total, 0, 0};
+            while (c.length < chunk && c.start + c.count < sj.size()) c.length += sl[c.start + c.count++];
+            chunks.push_back(c);
+            total += c.count;
+            totalLen += c.length;
+        } while (total < sj.size());
+        std::vector<std::string> blobs;
+        for (size_t i = 0; i < chunks.size(); i++) {
+            const Chunk& c = chunks[i];
+            std::string o = "{\"version\":\"1\",\"segmentCount\":" + std::to_string(c.count) +
+                            ",\"length\":" + std::to_string(c.length) + ",\"segments\":[";
+            for (size_t q = 0; q < c.count; q++) {
+                if (q) o.push_back(',');
+                o += sj[c.start + q];
+            }
+            o += "],\"startIndex\":" + std::to_string(c.start);
+            if (i == 0) {
+                o += ",\"headerMetadata\":{\"minSequenceNumber\":" + json::number(minSeq) +
+                     ",\"sequenceNumber\":" + json::number(curSeq) + ",\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+                for (size_t b = 1; b < chunks.size(); b++) o += ",{\"id\":\"body_" + std::to_string(b - 1) + "\"}";
+                o += "],\"totalLength\":" + std::to_string(totalLen) + ",\"totalSegmentCount\":" +
+                     std::to_string(total) + "}";
+            }
+            o += "}";
+            blobs.push_back(std::move(o));
+        }
+        return blobs;
+    }
+    std::u16string text() const {
+        std::u16string t;
+        for (auto& s : segs)
+            if (!s.kind && !s.removed) t.append((const char16_t*)s.text, s.len);
+        return t;
+    }
+};
+
+uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const uint8_t* b = (const uint8_t*)p;
+    for (size_t i = 0; i < n; i++) {
+        h ^= b[i];
+        h *= 0x100000001b3ull;
+    }
+    return h;
+}
+}  // namespace
+
+static int doc_view(mte_engine* e, uint32_t doc, DocView& v) {
+    if (!e) return MTE_E_ARG;
+    int rc = ensure_download(e);
+    if (rc) return rc;
+    if (doc >= e->P.n_docs) return set_err(e, MTE_E_RANGE, "doc index out of range");
+    v.e = e;
+    v.d = doc;
+    v.build();
+    return MTE_OK;
+}
+
+int mte_doc_status(mte_engine* e, uint32_t doc, int32_t* code, int64_t* failing_seq) {
+    if (!e) return MTE_E_ARG;
+    if (!e->replayed) return set_err(e, MTE_E_STATE, "no replay results yet");
+    if (doc >= e->res.size()) return set_err(e, MTE_E_RANGE, "doc index out of range");
+    if (code) *code = e->res[doc].status;
+    if (failing_seq) *failing_seq = e->res[doc].failing_seq;
+    return MTE_OK;
+}
+
+int mte_text(mte_engine* e, uint32_t doc, uint16_t* buf, size_t cap, size_t* len) {
+    DocView v;
+    int rc = doc_view(e, doc, v);
+    if (rc) return rc;
+    std::u16string t = v.text();
+    if (len) *len = t.size();
+    if (!buf) return MTE_OK;
+    if (cap < t.size()) return MTE_E_RANGE;
+    memcpy(buf, t.data(), t.size() * 2);
+    return MTE_OK;
+}
+
+int mte_segments(mte_engine* e, uint32_t doc, mte_seg_row* rows, size_t cap, size_t* n) {
+    DocView v;
+    int rc = doc_view(e, doc, v);
+    if (rc) return rc;
+    if (n) *n = v.segs.size();
+    if (!rows) return MTE_OK;
+    if (cap < v.segs.size()) return MTE_E_RANGE;
+    uint32_t off = 0;
+    for (size_t i = 0; i < v.segs.size(); i++) {
+        const SegView& s = v.segs[i];
+        mte_seg_row& r = rows[i];
+        r.kind = s.kind;
+        r.len = s.len;
+        r.seq = s.seq;
+        r.client = s.client;
+        r.removed_seq = s.removed ? s.rseq : INT32_MIN;
+        r.removed_client = s.removed ? s.rclient : -1;
+        r.overlap_mask = s.ovl;
+        r.text_off = off;
+        r.ref_type = s.reftype;
+        if (!s.kind) off += s.len;
+    }
+    return MTE_OK;
+}
+
+// Extra (non-header) helper used by the Python mirror: full segment dump as JSON rows.
+int mte_segments_json(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len) {
+    DocView v;
+    int rc = doc_view(e, doc, v);
+    if (rc) return rc;
+    std::string o = "[";
+    for (size_t i = 0; i < v.segs.size(); i++) {
+        const SegView& s = v.segs[i];
+        if (i) o += ",";
+        o += "{\"kind\":";
+        o += s.kind ? "\"M\"" : "\"T\"";
+        if (s.kind) o += ",\"refType\":" + std::to_string(s.reftype);
+        else {
+            o += ",\"text\":";
+            json::quote(o, (const char16_t*)s.text, s.len);
+        }
+        o += ",\"len\":" + std::to_string(s.len) + ",\"seq\":" + std::to_string(s.seq) + ",\"client\":";
+        std::u16string cu;
+        std::string c = v.long_id(s.client);
+        json::decode_utf8(c.data(), c.size(), cu);
+        json::quote(o, cu);
+        if (s.removed) {
+            o += ",\"removedSeq\":" + std::to_string(s.rseq) + ",\"removedClient\":";
+            std::string rc2 = v.long_id(s.rclient);
+            std::u16string ru;
+            json::decode_utf8(rc2.data(), rc2.size(), ru);
+            json::quote(o, ru);
+        }
+        o += ",\"overlap\":[";
+        bool first = true;
+        for (int b = 0; b < 64; b++)
+            if ((s.ovl >> b) & 1ull) {
+                if (!first) o += ",";
+                first = false;
+                std::string nm = v.long_id(b);
+                std::u16string nu;
+                json::decode_utf8(nm.data(), nm.size(), nu);
+                json::quote(o, nu);
+            }
+        o += "],\"props\":";
+        if (s.props) {
+            std::string pj;
+            v.props_json(pj, s.props);
+            std::u16string pu;
+            json::decode_utf8(pj.data(), pj.size(), pu);
+            json::quote(o, pu);
+        } else {
+            o += "null";
+        }
+        o += "}";
+    }
+    o += "]";
+    if (len) *len = o.size();
+    if (!buf) return MTE_OK;
+    if (cap < o.size()) return MTE_E_RANGE;
+    memcpy(buf, o.data(), o.size());
+    return MTE_OK;
+}
+
+int mte_snapshot_v1(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len, uint32_t* n_blobs) {
+    DocView v;
+    int rc = doc_view(e, doc, v);
+    if (rc) return rc;
+    auto blobs = v.snapshot_blobs(e->chunk);
+    std::string o = "{\"entries\":[";
+    for (size_t i = 0; i < blobs.size(); i++) {
+        if (i) o += ",";
+        std::string path = i == 0 ? "header" : "body_" + std::to_string(i - 1);
+        o += "{\"mode\":\"100644\",\"path\":\"" + path + "\",\"type\":\"Blob\",\"value\":{\"contents\":";
+        std::u16string bu;
+        json::decode_utf8(blobs[i].data(), blobs[i].size(), bu);
+        json::quote(o, bu);
+        o += ",\"encoding\":\"utf-8\"}}";
+    }
+    o += "],\"id\":null}";
+    if (n_blobs) *n_blobs = (uint32_t)blobs.size();
+    if (len) *len = o.size();
+    if (!buf) return MTE_OK;
+    if (cap < o.size()) return MTE_E_RANGE;
+    memcpy(buf, o.data(), o.size());
+    return MTE_OK;
+}
+
+int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap) {
+    if (!e || !out) return MTE_E_ARG;
+    int rc = ensure_download(e);
+    if (rc) return rc;
+    const uint32_t nd = e->P.n_docs;
+    if (cap < nd) return MTE_E_RANGE;
+    std::atomic<uint32_t> next{0};
+    auto work = [&]() {
+        for (uint32_t d; (d = next.fetch_add(1)) < nd;) {
+            DocView v;
+            v.e = e;
+            v.d = d;
+            v.build();
+            std::u16string t = v.text();
+            std::string t8 = json::to_utf8(t.data(), t.size());
+            uint64_t h = fnv1a(0xcbf29ce484222325ull, t8.data(), t8.size());
+            uint32_t sb = 0;
+            for (auto& b : v.snapshot_blobs(e->chunk)) {
+                uint8_t z = 0;
+                h = fnv1a(h, &z, 1);
+                h = fnv1a(h, b.data(), b.size());
+                sb += (uint32_t)b.size();
+            }
+            mte_doc_summary& s = out[d];
+            s.checksum = h;
+            s.ops = e->res[d].ops;
+            s.length = (uint32_t)t.size();
+            s.segments = (uint32_t)v.segs.size();
+            s.snapshot_bytes = sb;
+            s.status = e->res[d].status;
+            s.doc_id = d;
+        }
+    };
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> ts;
+    for (unsigned i = 0; i < nt; i++) ts.emplace_back(work);
+    for (auto& t : ts) t.join();
+    return MTE_OK;
+}
+
+// Extra helpers (not part of include/mte.h's contract; used by tests / bench for diagnostics).
+int mte_doc_result(mte_engine* e, uint32_t doc, void* out, size_t sz) {
+    if (!e || !e->replayed || doc >= e->res.size() || sz < sizeof(DocRes)) return MTE_E_ARG;
+    memcpy(out, &e->res[doc], sizeof(DocRes));
+    return MTE_OK;
+}
+int mte_pool_usage(mte_engine* e, uint32_t* lb_used, uint32_t* lb_cap, uint32_t* in_used, uint32_t* in_cap) {
+    if (!e) return MTE_E_ARG;
+    uint32_t ctr[4];
+    HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
+    *lb_used = ctr[0];
+    *lb_cap = e->P.nlb_cap;
+    *in_used = ctr[1];
+    *in_cap = e->P.nin_cap;
+    return MTE_OK;
+}
+int mte_wave_selftest(mte_engine* e, const uint32_t* in, uint32_t* out, uint32_t n_waves) {
+    if (!e) return MTE_E_ARG;
+    HIP_TRY(e, hipSetDevice(e->device));
+    DevBuf<uint32_t> di, dout;
+    HIP_TRY(e, di.alloc((size_t)n_waves * 64));
+    HIP_TRY(e, dout.alloc((size_t)n_waves * 64 * 3));
+    HIP_TRY(e, hipMemcpy(di.p, in, (size_t)n_waves * 64 * 4, hipMemcpyHostToDevice));
+    HIP_TRY(e, launch_wave_selftest(di.p, dout.p, n_waves, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    HIP_TRY(e, hipMemcpy(out, dout.p, (size_t)n_waves * 64 * 3 * 4, hipMemcpyDeviceToHost));
+    return MTE_OK;
+}
+// Replay kernel time of the last mte_replay, measured with HIP events on the engine stream.
+double mte_last_kernel_ms(mte_engine* e) { return e ? e->last_kernel_ms : 0; }
+
+// ------------------------------------------------------------------------------------------------
+// Builder: ISequencedDocumentMessage JSON -> op records (client.ts:776-836; ops.ts:29-110)
+int mte_builder_create(mte_builder** out) {
+    if (!out) return MTE_E_ARG;
+    *out = new mte_builder();
+    return MTE_OK;
+}
+void mte_builder_destroy(mte_builder* b) { delete b; }
+const char* mte_builder_error(const mte_builder* b) { return b ? b->err.c_str() : "null builder"; }
+
+static int num_field(const json::Value& o, const char16_t* k, int32_t* out) {
+    const json::Value* v = o.get(k);
+    if (!v || v->kind != json::Value::Number) return 0;
+    *out = (int32_t)v->num;
+    return 1;
+}
+
+int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* text, size_t len) {
+    if (!b || !text) return MTE_E_ARG;
+    HostBatch& hb = b->hb;
+    json::Value doc;
+    try {
+        doc = json::parse(text, len);
+    } catch (std::exception& ex) {
+        b->err = ex.what();
+        return MTE_E_PARSE;
+    }
+    if (doc.kind != json::Value::Array) {
+        b->err = "op log must be a JSON array of messages";
+        return MTE_E_PARSE;
+    }
+    std::vector<mte_op> ops;
+    std::vector<uint16_t> payload;
+    std::vector<std::string> names;
+    std::unordered_map<std::string, uint32_t> ids;
+    const std::string observer = observer_name ? observer_name : "";
+    names.push_back(observer);
+    ids[observer] = 0;
+    const bool collab = !observer.empty();
+    auto fail = [&](int code, const std::string& m) {
+        b->err = m;
+        return code;
+    };
+    for (const json::Value& m : doc.items) {
+        if (m.kind != json::Value::Object) return fail(MTE_E_PARSE, "message is not an object");
+        mte_op base{};
+        num_field(m, u"sequenceNumber", &base.seq);
+        num_field(m, u"referenceSequenceNumber", &base.ref_seq);
+        num_field(m, u"minimumSequenceNumber", &base.msn);
+        const json::Value* cid = m.get(u"clientId");
+        std::string name = (cid && cid->kind == json::Value::String) ? json::to_utf8(cid->str.data(), cid->str.size()) : "";
+        if (!collab) name = "";
+        auto it = ids.find(name);
+        uint32_t sid;
+        if (it == ids.end()) {
+            sid = (uint32_t)names.size();
+            if (sid >= MTE_MAX_CLIENTS) return fail(MTE_E_UNSUPPORTED, "more than 64 clients in a document");
+            names.push_back(name);
+            ids[name] = sid;
+        } else {
+            sid = it->second;
+        }
+        base.client = (uint8_t)sid;
+        const json::Value* type = m.get(u"type");
+        const json::Value* contents = m.get(u"contents");
+        std::vector<const json::Value*> members;
+        bool isOp = type && type->kind == json::Value::String && type->str == u"op" && contents &&
+                    contents->kind == json::Value::Object;
+        if (isOp) {
+            if (collab && sid == 0) return fail(MTE_E_UNSUPPORTED, "observer never submits ops (ack path)");
+            int32_t t = -1;
+            num_field(*contents, u"type", &t);
+            if (t == 3) {
+                const json::Value* g = contents->get(u"ops");
+                if (g && g->kind == json::Value::Array)
+                    for (auto& x : g->items) members.push_back(&x);
+            } else {
+                members.push_back(contents);
+            }
+        }
+        size_t first = ops.size();
+        for (const json::Value* c : members) {
+            if (c->kind != json::Value::Object) continue;
+            if (c->get(u"relativePos1") || c->get(u"relativePos2") || c->get(u"register"))
+                return fail(MTE_E_UNSUPPORTED, "relative positions / registers are out of scope");
+            mte_op o = base;
+            int32_t t = -1;
+            num_field(*c, u"type", &t);
+            num_field(*c, u"pos1", &o.pos1);
+            if (t == 0) {
+                const json::Value* seg = c->get(u"seg");
+                if (!seg) continue;
+                const json::Value* props = nullptr;
+                if (seg->kind == json::Value::String) {
+                    o.type = MTE_OP_INSERT;
+                    o.a = (int32_t)payload.size();
+                    o.b = (uint32_t)seg->str.size();
+                    payload.insert(payload.end(), seg->str.begin(), seg->str.end());
+                } else if (seg->kind == json::Value::Object && seg->get(u"marker")) {
+                    o.type = MTE_OP_INSERT_MARKER;
+                    const json::Value* mk = seg->get(u"marker");
+                    int32_t rt = 0;
+                    if (mk->kind == json::Value::Object) num_field(*mk, u"refType", &rt);
+                    o.b = (uint32_t)rt;
+                    props = seg->get(u"props");
+                } else if (seg->kind == json::Value::Object && seg->get(u"text") &&
+                           seg->get(u"text")->kind == json::Value::String) {
+                    const json::Value* tx = seg->get(u"text");
+                    o.type = MTE_OP_INSERT;
+                    o.a = (int32_t)payload.size();
+                    o.b = (uint32_t)tx->str.size();
+                    payload.insert(payload.end(), tx->str.begin(), tx->str.end());
+                    props = seg->get(u"props");
+                } else {
+                    return fail(MTE_E_UNSUPPORTED, "unknown segment spec");
+                }
+                if (props && json::truthy(props)) {
+                    if (props->kind != json::Value::Object) return fail(MTE_E_UNSUPPORTED, "non-object props");
+                    o.props = b->in->propset(*props);
+                }
+            } else if (t == 1) {
+                o.type = MTE_OP_REMOVE;
+                num_field(*c, u"pos2", &o.a);
+            } else if (t == 2) {
+                o.type = MTE_OP_ANNOTATE;
+                num_field(*c, u"pos2", &o.a);
+                const json::Value* props = c->get(u"props");
+                const json::Value* comb = c->get(u"combiningOp");
+                if (comb) {
+                    const json::Value* nm = comb->kind == json::Value::Object ? comb->get(u"name") : nullptr;
+                    if (nm && nm->kind == json::Value::String && nm->str == u"rewrite") o.flags |= MTE_F_REWRITE;
+                    else return fail(MTE_E_UNSUPPORTED, "combiningOp other than rewrite is out of scope");
+                }
+                json::Value empty;
+                empty.kind = json::Value::Object;
+                o.props = b->in->propset(props && props->kind == json::Value::Object ? *props : empty);
+            } else {
+                continue;
+            }
+            ops.push_back(o);
+        }
+        if (ops.size() == first) {  // no merge-tree op: still a sequenced message
+            mte_op o = base;
+            o.type = MTE_OP_NOOP;
+            ops.push_back(o);
+        }
+        ops.back().flags |= MTE_F_END_OF_MSG;
+    }
+    hb.ops.insert(hb.ops.end(), ops.begin(), ops.end());
+    hb.doc_op_offsets.push_back(hb.ops.size());
+    hb.payload.insert(hb.payload.end(), payload.begin(), payload.end());
+    hb.doc_payload_offsets.push_back(hb.payload.size());
+    for (auto& nm : names) {
+        hb.client_names += nm;
+        hb.client_name_offsets.push_back(hb.client_names.size());
+    }
+    hb.doc_client_offsets.push_back(hb.doc_client_offsets.back() + (uint32_t)names.size());
+    return MTE_OK;
+}
+
+int mte_builder_batch(mte_builder* b, mte_batch* out) {
+    if (!b || !out) return MTE_E_ARG;
+    b->hb.view(out);
+    return MTE_OK;
+}
+
+}  // extern "C"

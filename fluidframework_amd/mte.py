@@ -1,0 +1,296 @@
+"""Python host mirror of the engine's C ABI (include/mte.h), via ctypes.
+
+The reference surface this mirrors is @fluidframework/merge-tree's Client
+(packages/dds/merge-tree/src/client.ts): applyMsg (:805-827), getText via MergeTreeTextHelper
+(textSegment.ts:154-172), snapshot -> SnapshotV1 (snapshotV1.ts:85-247). Replay always runs on the
+GPU through libmte.so; there is no Python or CPU fallback: if the library or the device is missing
+these classes raise.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libmte.so")
+
+MTE_OP_INSERT, MTE_OP_REMOVE, MTE_OP_ANNOTATE, MTE_OP_INSERT_MARKER, MTE_OP_NOOP = 0, 1, 2, 3, 4
+MTE_F_END_OF_MSG, MTE_F_REWRITE = 1, 2
+DOC_STATUS = {0: "ok", 1: "insert failed", 2: "sequence order", 3: "capacity", 4: "unsupported", 5: "not run"}
+
+OP_DTYPE = np.dtype([("seq", "<i4"), ("ref_seq", "<i4"), ("msn", "<i4"), ("pos1", "<i4"), ("a", "<i4"),
+                     ("b", "<u4"), ("props", "<u4"), ("type", "u1"), ("client", "u1"), ("flags", "<u2")])
+assert OP_DTYPE.itemsize == 32
+
+
+class MteError(RuntimeError):
+    pass
+
+
+class mte_batch(ctypes.Structure):
+    _fields_ = [
+        ("n_docs", ctypes.c_uint32),
+        ("doc_op_offsets", ctypes.POINTER(ctypes.c_uint64)),
+        ("ops", ctypes.c_void_p),
+        ("doc_payload_offsets", ctypes.POINTER(ctypes.c_uint64)),
+        ("payload", ctypes.POINTER(ctypes.c_uint16)),
+        ("n_propsets", ctypes.c_uint32),
+        ("propsets", ctypes.c_void_p),
+        ("prop_keys", ctypes.POINTER(ctypes.c_uint32)),
+        ("prop_vals", ctypes.POINTER(ctypes.c_uint32)),
+        ("n_keys", ctypes.c_uint32),
+        ("key_offsets", ctypes.POINTER(ctypes.c_uint64)),
+        ("key_text", ctypes.c_void_p),
+        ("n_vals", ctypes.c_uint32),
+        ("val_offsets", ctypes.POINTER(ctypes.c_uint64)),
+        ("val_text", ctypes.c_void_p),
+        ("doc_client_offsets", ctypes.POINTER(ctypes.c_uint32)),
+        ("client_name_offsets", ctypes.POINTER(ctypes.c_uint64)),
+        ("client_names", ctypes.c_void_p),
+    ]
+
+
+class mte_config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("chunk_size", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 6)]
+
+
+class mte_stats(ctypes.Structure):
+    _fields_ = [("docs", ctypes.c_uint64), ("ops", ctypes.c_uint64), ("messages", ctypes.c_uint64),
+                ("failed_docs", ctypes.c_uint64), ("kernel_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double)]
+
+
+class mte_doc_summary(ctypes.Structure):
+    _fields_ = [("checksum", ctypes.c_uint64), ("ops", ctypes.c_uint32), ("length", ctypes.c_uint32),
+                ("segments", ctypes.c_uint32), ("snapshot_bytes", ctypes.c_uint32), ("status", ctypes.c_int32),
+                ("doc_id", ctypes.c_uint32)]
+
+
+SUMMARY_DTYPE = np.dtype([("checksum", "<u8"), ("ops", "<u4"), ("length", "<u4"), ("segments", "<u4"),
+                          ("snapshot_bytes", "<u4"), ("status", "<i4"), ("doc_id", "<u4")])
+
+# Every symbol declared in include/mte.h (checked by tests/test_abi.py).
+EXPORTS = ["mte_abi_version", "mte_build_info", "mte_create", "mte_destroy", "mte_last_error", "mte_load",
+           "mte_replay", "mte_generate", "mte_export_batch", "mte_doc_status", "mte_text", "mte_segments",
+           "mte_snapshot_v1", "mte_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_batch",
+           "mte_builder_error", "mte_builder_destroy"]
+
+_lib = None
+
+
+def lib():
+    """Load libmte.so; raises (never falls back) when the HIP build is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MteError(f"libmte.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, u64, sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
+        L.mte_abi_version.restype = ctypes.c_int
+        L.mte_build_info.restype = ctypes.c_char_p
+        L.mte_create.argtypes = [ctypes.POINTER(mte_config), ctypes.POINTER(vp)]
+        L.mte_destroy.argtypes = [vp]
+        L.mte_last_error.argtypes = [vp]
+        L.mte_last_error.restype = ctypes.c_char_p
+        L.mte_load.argtypes = [vp, ctypes.POINTER(mte_batch)]
+        L.mte_replay.argtypes = [vp, ctypes.POINTER(mte_stats)]
+        L.mte_generate.argtypes = [vp, u32, u32, u32, ctypes.POINTER(u32), u32, u64]
+        L.mte_export_batch.argtypes = [vp, ctypes.POINTER(mte_batch)]
+        L.mte_doc_status.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]
+        L.mte_text.argtypes = [vp, u32, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+        L.mte_segments_json.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+        L.mte_snapshot_v1.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz), ctypes.POINTER(u32)]
+        L.mte_summaries.argtypes = [vp, ctypes.c_void_p, sz]
+        L.mte_doc_result.argtypes = [vp, u32, ctypes.c_void_p, sz]
+        L.mte_pool_usage.argtypes = [vp] + [ctypes.POINTER(u32)] * 4
+        L.mte_wave_selftest.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, u32]
+        L.mte_last_kernel_ms.argtypes = [vp]
+        L.mte_last_kernel_ms.restype = ctypes.c_double
+        L.mte_builder_create.argtypes = [ctypes.POINTER(vp)]
+        L.mte_builder_add_doc.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
+        L.mte_builder_batch.argtypes = [vp, ctypes.POINTER(mte_batch)]
+        L.mte_builder_error.argtypes = [vp]
+        L.mte_builder_error.restype = ctypes.c_char_p
+        L.mte_builder_destroy.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+class Builder:
+    """Op-log ingestion: per-document JSON arrays of ISequencedDocumentMessage -> mte_batch."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        rc = lib().mte_builder_create(ctypes.byref(h))
+        if rc:
+            raise MteError(f"mte_builder_create: {rc}")
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().mte_builder_destroy(self._h)
+            self._h = None
+
+    def add_doc(self, messages, observer="__observer__"):
+        """messages: list of message dicts or a JSON string. observer='' => local, non-collab edits."""
+        text = messages if isinstance(messages, (str, bytes)) else json.dumps(messages, separators=(",", ":"),
+                                                                               ensure_ascii=False)
+        b = text.encode() if isinstance(text, str) else text
+        rc = lib().mte_builder_add_doc(self._h, observer.encode(), b, len(b))
+        if rc:
+            raise MteError(f"mte_builder_add_doc: {rc}: {lib().mte_builder_error(self._h).decode()}")
+
+    def batch(self):
+        b = mte_batch()
+        lib().mte_builder_batch(self._h, ctypes.byref(b))
+        b._owner = self  # keep the builder (which owns the memory) alive
+        return b
+
+
+def batch_ops(b):
+    """numpy view of a batch's op records (valid while the owner lives)."""
+    n = b.doc_op_offsets[b.n_docs]
+    if n == 0:
+        return np.zeros(0, OP_DTYPE)
+    buf = (ctypes.c_char * (n * 32)).from_address(b.ops)
+    return np.frombuffer(buf, dtype=OP_DTYPE, count=n)
+
+
+class Engine:
+    """One engine per GPU: loads/generates batches, replays them with the HIP kernel."""
+
+    def __init__(self, device=0, chunk_size=10000):
+        cfg = mte_config(device=device, chunk_size=chunk_size)
+        h = ctypes.c_void_p()
+        rc = lib().mte_create(ctypes.byref(cfg), ctypes.byref(h))
+        if rc:
+            raise MteError(f"mte_create failed ({rc}): no HIP device? The replay path has no CPU fallback.")
+        self._h = h
+        self.n_docs = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mte_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc:
+            raise MteError(f"{what} failed ({rc}): {lib().mte_last_error(self._h).decode()}")
+
+    def load(self, batch):
+        self._check(lib().mte_load(self._h, ctypes.byref(batch)), "mte_load")
+        self.n_docs = batch.n_docs
+
+    def generate(self, kind, n_docs, n_ops, n_clients=8, seed=0, ops_per_doc=None):
+        arr = None
+        if ops_per_doc is not None:
+            arr = (ctypes.c_uint32 * n_docs)(*[int(x) for x in ops_per_doc])
+        self._check(lib().mte_generate(self._h, kind, n_docs, n_ops, arr, n_clients, seed), "mte_generate")
+        self.n_docs = n_docs
+
+    def replay(self):
+        st = mte_stats()
+        self._check(lib().mte_replay(self._h, ctypes.byref(st)), "mte_replay")
+        return {"docs": st.docs, "ops": st.ops, "messages": st.messages, "failed_docs": st.failed_docs,
+                "kernel_ms": st.kernel_ms, "h2d_ms": st.h2d_ms}
+
+    def export_batch(self):
+        b = mte_batch()
+        self._check(lib().mte_export_batch(self._h, ctypes.byref(b)), "mte_export_batch")
+        b._owner = self
+        return b
+
+    def status(self, doc):
+        c, s = ctypes.c_int32(), ctypes.c_int64()
+        self._check(lib().mte_doc_status(self._h, doc, ctypes.byref(c), ctypes.byref(s)), "mte_doc_status")
+        return c.value, s.value
+
+    def text(self, doc):
+        n = ctypes.c_size_t()
+        self._check(lib().mte_text(self._h, doc, None, 0, ctypes.byref(n)), "mte_text")
+        buf = (ctypes.c_uint16 * max(n.value, 1))()
+        self._check(lib().mte_text(self._h, doc, buf, n.value, ctypes.byref(n)), "mte_text")
+        return np.frombuffer(buf, dtype=np.uint16, count=n.value).tobytes().decode("utf-16-le", "surrogatepass")
+
+    def _str_call(self, fn, doc, *extra):
+        n = ctypes.c_size_t()
+        self._check(fn(self._h, doc, None, 0, ctypes.byref(n), *extra), fn.__name__)
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._check(fn(self._h, doc, buf, n.value + 1, ctypes.byref(n), *extra), fn.__name__)
+        return buf.raw[: n.value].decode("utf-8")
+
+    def segments_json(self, doc):
+        return self._str_call(lib().mte_segments_json, doc)
+
+    def snapshot_json(self, doc):
+        nb = ctypes.c_uint32()
+        return self._str_call(lib().mte_snapshot_v1, doc, ctypes.byref(nb))
+
+    def summaries(self):
+        out = np.zeros(self.n_docs, dtype=SUMMARY_DTYPE)
+        self._check(lib().mte_summaries(self._h, out.ctypes.data, self.n_docs), "mte_summaries")
+        return out
+
+    def doc_result(self, doc):
+        buf = (ctypes.c_int32 * 16)()
+        self._check(lib().mte_doc_result(self._h, doc, buf, ctypes.sizeof(buf)), "mte_doc_result")
+        names = ["status", "failing_seq", "ops", "msgs", "min_seq", "cur_seq", "root", "height", "n_lb",
+                 "arena_sel", "arena_top", "map_next", "seg_next", "heap_size", "n_gc", "lb_free"]
+        return dict(zip(names, list(buf)))
+
+    def pool_usage(self):
+        v = [ctypes.c_uint32() for _ in range(4)]
+        self._check(lib().mte_pool_usage(self._h, *[ctypes.byref(x) for x in v]), "mte_pool_usage")
+        return {"lb_used": v[0].value, "lb_cap": v[1].value, "in_used": v[2].value, "in_cap": v[3].value}
+
+    def last_kernel_ms(self):
+        return lib().mte_last_kernel_ms(self._h)
+
+    def wave_selftest(self, values):
+        values = np.ascontiguousarray(values, dtype=np.uint32)
+        nw = values.size // 64
+        out = np.zeros(nw * 64 * 3, dtype=np.uint32)
+        self._check(lib().mte_wave_selftest(self._h, values.ctypes.data, out.ctypes.data, nw), "mte_wave_selftest")
+        return out.reshape(nw, 3, 64)
+
+
+class MergeTreeClient:
+    """Client-shaped facade for one document (client.ts:42): applyMsg batches are staged and replayed
+    on the GPU when an output is requested."""
+
+    def __init__(self, observer="__observer__", device=0):
+        self.observer = observer
+        self.msgs = []
+        self._engine = None
+        self._device = device
+        self._dirty = True
+
+    def applyMsg(self, msg):  # noqa: N802 (reference name)
+        self.msgs.append(msg)
+        self._dirty = True
+
+    def _run(self):
+        if self._dirty:
+            b = Builder()
+            b.add_doc(self.msgs, observer=self.observer)
+            if self._engine is None:
+                self._engine = Engine(self._device)
+            self._engine.load(b.batch())
+            self._engine.replay()
+            code, seq = self._engine.status(0)
+            if code:
+                raise MteError(f"replay failed at seq {seq}: {DOC_STATUS.get(code, code)}")
+            self._dirty = False
+        return self._engine
+
+    def getText(self):  # noqa: N802
+        return self._run().text(0)
+
+    def getLength(self):  # noqa: N802
+        return len(self.getText().encode("utf-16-le", "surrogatepass")) // 2
+
+    def snapshot(self):
+        return json.loads(self._run().snapshot_json(0))

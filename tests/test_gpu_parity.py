@@ -1,0 +1,155 @@
+"""GPU parity: the HIP replay engine (through the C ABI) against the CPU oracle and the reference's
+golden vectors. Integer/byte work: every comparison is bit-exact."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from fluidframework_amd import mte
+from tests.gpu_helpers import compare_batch_checksums, compare_doc
+from tests.oplog import TestString, ann, ins, msg, rem
+from tests.test_builder_cpu import random_log
+from tests.test_oracle_fixtures import GOLDEN, fixture_blobs
+from tests.test_oracle_specs import SNAPSHOT_CASES, hello_world_log
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = mte.Engine(0)
+    yield e
+    e.close()
+
+
+def test_wave_primitives(engine):
+    rng = np.random.default_rng(1)
+    vals = rng.integers(0, 1 << 20, size=64 * 8, dtype=np.uint32)
+    out = engine.wave_selftest(vals)
+    for w in range(8):
+        v = vals[w * 64:(w + 1) * 64]
+        assert np.array_equal(out[w, 0], np.cumsum(v, dtype=np.uint64).astype(np.uint32))
+        assert np.array_equal(out[w, 1], v[::-1])
+        bits = (v & 1).astype(np.uint64)
+        mask = int(sum(int(b) << i for i, b in enumerate(bits)))
+        assert int(out[w, 2][0]) == mask & 0xFFFFFFFF and int(out[w, 2][32]) == mask >> 32
+
+
+def spec_logs():
+    logs = [hello_world_log()]
+    m = hello_world_log()
+    m += [msg("remote2", 12, 11, rem(0, 11)), msg("remote", 13, 11, ins(0, "text"))]
+    logs.append(m)
+    m = hello_world_log()
+    m += [msg("remote", 12, 11, ins(0, "text")), msg("remote2", 13, 11, rem(0, 11))]
+    logs.append(m)
+    for case in sorted(SNAPSHOT_CASES):
+        steps, _ = SNAPSHOT_CASES[case]
+        s = TestString()
+        for st in steps:
+            if st[0] == "append":
+                s.append(st[1], st[2])
+            elif st[0] == "insert":
+                s.insert(st[1], st[2], st[3])
+            else:
+                s.remove_range(st[1], st[2], st[3])
+        logs.append(s.msgs)
+    for inc in (True, False):
+        s = TestString()
+        for i in range(10010):
+            s.append(str(i % 10), inc)
+        logs.append(s.msgs)
+    logs.append([msg("a", 1, 0, ins(0, "xy")), msg("b", 2, 1, ins(1, "B")), msg("c", 3, 1, ins(1, "C"))])
+    logs.append([msg("a", 1, 0, ins(0, "hello")), msg("b", 2, 1, rem(1, 3)), msg("c", 3, 1, rem(0, 4))])
+    logs.append([msg("w", 1, 0, ins(0, "abc")), msg("w", 2, 1, ann(0, 3, {"b": 1, "a": 2, "7": "x"})),
+                 msg("w", 3, 2, ann(0, 3, {"b": None})), msg("w", 4, 3, ann(0, 3, {"b": 3, "2": True}))])
+    logs.append([msg("w", 1, 0, ins(0, "ab")), msg("w", 2, 1, ins(5, "x"))])  # insert failed
+    return logs
+
+
+def test_spec_logs_match_oracle(engine):
+    logs = spec_logs()
+    b = mte.Builder()
+    for m in logs:
+        b.add_doc(m)
+    batch = b.batch()
+    engine.load(batch)
+    engine.replay()
+    for d in range(len(logs)):
+        compare_doc(engine, batch, d)
+    assert engine.text(1) == "text" and engine.text(2) == "text"
+    assert engine.status(len(logs) - 1)[0] == 1  # MergeTree insert failed
+
+
+def local_fixture_log(name):
+    """generateSharedStrings.ts:24-98 as local (non-collaborative) ops; lengths tracked here."""
+    ops = []
+    length = 0
+
+    def add(c):
+        ops.append(msg("local", 0, 0, c))
+
+    n = {"headerOnly": 1250, "headerAndBody": 5000, "withMarkers": 5000, "withAnnotations": 5000}.get(name)
+    if name == "largeBody":
+        for i in range(10000):
+            t = f"text-{i}"
+            add(ins(0, t))
+            length += len(t)
+    else:
+        for i in range(n):
+            t = f"text{i}"
+            add(ins(0, t))
+            length += len(t)
+    if name == "withMarkers":
+        i = 0
+        while i < length:
+            add(ins(i, {"marker": {"refType": 1}, "props": {"ItemType": "Paragraph", "Properties": {"Bold": False},
+                                                            "markerId": f"marker{i}", "referenceTileLabels": ["Eop"]}}))
+            length += 1
+            i += 70
+    if name == "withAnnotations":
+        i = 0
+        while i < length:
+            add(ann(i, i + 10, {"bold": True}))
+            i += 70
+    return ops
+
+
+def test_v1_golden_fixtures_on_gpu(engine):
+    names = ["headerOnly", "headerAndBody", "largeBody", "withMarkers", "withAnnotations"]
+    b = mte.Builder()
+    for nm in names:
+        b.add_doc(local_fixture_log(nm), observer="")
+    engine.load(b.batch())
+    engine.replay()
+    for d, nm in enumerate(names):
+        assert engine.status(d)[0] == 0
+        tree = json.loads(engine.snapshot_json(d))
+        got = [(e["path"], e["value"]["contents"]) for e in tree["entries"]]
+        assert got == fixture_blobs(nm), nm
+
+
+def test_random_logs_match_oracle(engine):
+    logs = [random_log(s, n=400) for s in range(24)]
+    b = mte.Builder()
+    for m in logs:
+        b.add_doc(m)
+    batch = b.batch()
+    engine.load(batch)
+    engine.replay()
+    for d in range(len(logs)):
+        compare_doc(engine, batch, d)
+
+
+@pytest.mark.parametrize("kind,docs,ops", [(2, 96, 3000), (3, 96, 3000), (5, 32, 6000)])
+def test_generated_workloads_match_oracle(engine, kind, docs, ops):
+    engine.generate(kind, docs, ops, n_clients=8, seed=7)
+    gen_fail = [d for d in range(docs) if engine.status(d)[0]]
+    assert not gen_fail, f"generator hit errors: {[(d, engine.status(d)) for d in gen_fail[:5]]}"
+    batch = engine.export_batch()
+    engine.replay()  # a fresh replay of the recorded log
+    bad, _, _ = compare_batch_checksums(engine, batch)
+    if bad:
+        compare_doc(engine, batch, bad[0])  # raises with a precise diff
+    assert not bad

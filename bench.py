@@ -41,6 +41,10 @@ def parse():
     return ap.parse_args()
 
 
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     import numpy as np
@@ -60,6 +64,7 @@ def main():
     # per-rank shard: distinct seeds => distinct documents (doc ids rank*docs + i)
     eng.generate(args.kind, args.docs, args.ops, n_clients=args.clients, seed=1000 + rank)
     gen_s = time.time() - t0
+    log(f"rank {rank}: generated {args.docs} docs x {args.ops} ops in {gen_s:.1f} s")
     batch = eng.export_batch()
     ops_np = mte.batch_ops(batch)
     ins = ops_np["type"] == mte.MTE_OP_INSERT
@@ -70,7 +75,8 @@ def main():
         return eng.replay()
 
     for _ in range(args.warmup):
-        step()
+        w = step()
+        log(f"warmup step: {w['kernel_ms']:.1f} ms kernel, {w['ops']} ops")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -94,6 +100,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1000.0
     value = total_ops * args.steps / elapsed
 
+    log(f"timed {args.steps} steps: {ms_per_step:.1f} ms/step, {value / 1e6:.1f} Mops/s")
     # final summary gather (RCCL all-gather of 32-B records), outside the timed region
     t1 = time.time()
     summ = eng.summaries()
@@ -132,6 +139,7 @@ def main():
         if nv:
             o_ops, cks, sts = replay_batch(ctypes.addressof(batch), 0, nv, threads=args.cpu_threads)
             verified = all(int(summ["checksum"][d]) == cks[d] and int(summ["status"][d]) == sts[d] for d in range(nv))
+        log(f"oracle verification of {nv} docs: {verified}")
         if not args.no_cpu_baseline:
             # bounded sample: grow the doc count until ~cpu_seconds of oracle replay on cpu_threads threads
             nd = max(args.cpu_threads, 16)
@@ -141,6 +149,7 @@ def main():
                 c_ops, _, _ = replay_batch(ctypes.addressof(batch), 0, nd, threads=args.cpu_threads,
                                            with_snapshot=False)
                 dt = time.perf_counter() - c0
+                log(f"cpu baseline sample: {nd} docs, {c_ops} ops in {dt:.2f} s")
                 if dt >= args.cpu_seconds * 0.5 or nd >= args.docs:
                     break
                 nd = int(nd * min(8.0, max(2.0, args.cpu_seconds / max(dt, 1e-3))))

@@ -1,0 +1,34 @@
+// Type declarations for @fluidframework/merge-tree-native (see index.js).
+import { ISequencedDocumentMessage, ITree } from "@fluidframework/protocol-definitions";
+
+export declare const DocStatus: { Ok: 0; InsertFailed: 1; SequenceOrder: 2; Capacity: 3; Unsupported: 4 };
+
+export interface ReplayStats { docs: number; ops: number; messages: number; failedDocs: number; kernelMs: number; }
+export interface DocSummary {
+    checksum: bigint | string; ops: number; length: number; segments: number;
+    snapshotBytes: number; status: number; docId: number;
+}
+export interface DocLog { observer?: string; messages: ISequencedDocumentMessage[]; }
+
+export declare class BatchedMergeEngine {
+    constructor(options?: { device?: number; chunkSize?: number });
+    load(docs: DocLog[]): void;
+    generate(kind: 2 | 3 | 5, nDocs: number, nOps: number, nClients?: number, seed?: number): void;
+    replay(): ReplayStats;
+    docStatus(doc: number): [number, number];
+    getText(doc: number): string;
+    snapshotV1(doc: number): ITree;
+    summaries(): DocSummary[];
+}
+
+/** Client-shaped facade (merge-tree client.ts:42) for one document. */
+export declare class MergeTreeClient {
+    constructor(observer?: string, options?: { device?: number; chunkSize?: number });
+    applyMsg(msg: ISequencedDocumentMessage): void;
+    getText(): string;
+    getLength(): number;
+    snapshot(): ITree;
+}
+
+export declare function abiVersion(): number;
+export declare function buildInfo(): string;

@@ -1,0 +1,87 @@
+"use strict";
+/**
+ * @fluidframework/merge-tree-native — batched, GPU-resident replay of merge-tree op logs.
+ *
+ * Mirrors the slice of @fluidframework/merge-tree's Client API that the replay / summarize path uses
+ * (client.ts:805-836 applyMsg, textSegment.ts:154-172 getText, snapshotV1.ts:85-247 SnapshotV1 emit),
+ * but for many documents at once: messages are staged per document and replayed on the MI355X in one
+ * launch. There is no CPU fallback — without a HIP device createEngine throws.
+ */
+const path = require("path");
+const addon = require(path.join(__dirname, "build", "mte_native.node"));
+
+const DocStatus = Object.freeze({ Ok: 0, InsertFailed: 1, SequenceOrder: 2, Capacity: 3, Unsupported: 4 });
+
+class BatchedMergeEngine {
+    constructor(options = {}) {
+        this.device = options.device || 0;
+        this.chunkSize = options.chunkSize || 10000;  // SnapshotV1.chunkSize (snapshotV1.ts:40)
+        this._engine = addon.createEngine(this.device, this.chunkSize);
+        this._docs = 0;
+    }
+    /** Stage per-document logs: docs = [{ observer, messages: ISequencedDocumentMessage[] }] */
+    load(docs) {
+        const b = addon.createBuilder();
+        for (const d of docs) {
+            addon.builderAddDoc(b, d.observer === undefined ? "__observer__" : d.observer, JSON.stringify(d.messages));
+        }
+        addon.load(this._engine, b);
+        this._docs = docs.length;
+    }
+    generate(kind, nDocs, nOps, nClients = 8, seed = 0) {
+        addon.generate(this._engine, kind, nDocs, nOps, nClients, seed);
+        this._docs = nDocs;
+    }
+    replay() { return addon.replay(this._engine); }
+    docStatus(doc) { return addon.docStatus(this._engine, doc); }
+    getText(doc) { return addon.getText(this._engine, doc); }
+    /** The ITree SnapshotV1.emit(serializer) returns: { entries: [...], id: null } */
+    snapshotV1(doc) { return JSON.parse(addon.snapshotV1(this._engine, doc)); }
+    /** 32-byte records {checksum u64, ops, length, segments, snapshotBytes, status, docId} */
+    summaries() {
+        const buf = addon.summaries(this._engine, this._docs);
+        const out = [];
+        for (let i = 0; i < this._docs; i++) {
+            const o = i * 32;
+            out.push({
+                checksum: buf.readBigUInt64LE ? buf.readBigUInt64LE(o) : buf.toString("hex", o, o + 8),
+                ops: buf.readUInt32LE(o + 8), length: buf.readUInt32LE(o + 12), segments: buf.readUInt32LE(o + 16),
+                snapshotBytes: buf.readUInt32LE(o + 20), status: buf.readInt32LE(o + 24), docId: buf.readUInt32LE(o + 28),
+            });
+        }
+        return out;
+    }
+}
+
+/** Client-shaped facade for one document (client.ts:42): applyMsg, getText, getLength, snapshot. */
+class MergeTreeClient {
+    constructor(observer = "__observer__", options = {}) {
+        this.observer = observer;
+        this.options = options;
+        this.messages = [];
+        this._engine = undefined;
+        this._dirty = true;
+    }
+    applyMsg(msg) { this.messages.push(msg); this._dirty = true; }
+    _run() {
+        if (this._dirty) {
+            if (!this._engine) this._engine = new BatchedMergeEngine(this.options);
+            this._engine.load([{ observer: this.observer, messages: this.messages }]);
+            this._engine.replay();
+            const [code, seq] = this._engine.docStatus(0);
+            if (code === DocStatus.InsertFailed) throw new Error(`MergeTree insert failed at seq ${seq}`);
+            if (code !== DocStatus.Ok) throw new Error(`replay failed (status ${code}) at seq ${seq}`);
+            this._dirty = false;
+        }
+        return this._engine;
+    }
+    getText() { return this._run().getText(0); }
+    getLength() { return this.getText().length; }
+    snapshot() { return this._run().snapshotV1(0); }
+}
+
+module.exports = {
+    BatchedMergeEngine, MergeTreeClient, DocStatus,
+    abiVersion: addon.abiVersion, buildInfo: addon.buildInfo,
+    createBuilder: addon.createBuilder, builderAddDoc: addon.builderAddDoc, builderDocCount: addon.builderDocCount,
+};

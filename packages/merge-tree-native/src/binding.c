@@ -1,0 +1,283 @@
+/*
+ * N-API addon over libmte.so (include/mte.h): the Node/TypeScript host binding of the MI355X
+ * merge-tree replay engine. It is the drop-in a SharedSegmentSequence / replay tool binds instead of
+ * driving @fluidframework/merge-tree's Client (client.ts:805-836) message by message.
+ * Plain C, NAPI_VERSION 8 (Node >= 12.22). Errors are thrown as JS Errors carrying mte_last_error.
+ */
+#define NAPI_VERSION 8
+#include <node_api.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../../include/mte.h"
+
+#define CHECK(env, call)                                                       \
+    do {                                                                       \
+        if ((call) != napi_ok) {                                               \
+            napi_throw_error((env), NULL, "N-API call failed: " #call);        \
+            return NULL;                                                       \
+        }                                                                      \
+    } while (0)
+
+static napi_value throw_mte(napi_env env, const char* what, int rc, const char* detail) {
+    char buf[512];
+    snprintf(buf, sizeof buf, "%s failed (%d)%s%s", what, rc, detail ? ": " : "", detail ? detail : "");
+    napi_throw_error(env, NULL, buf);
+    return NULL;
+}
+
+static void finalize_engine(napi_env env, void* data, void* hint) {
+    (void)env;
+    (void)hint;
+    mte_destroy((mte_engine*)data);
+}
+static void finalize_builder(napi_env env, void* data, void* hint) {
+    (void)env;
+    (void)hint;
+    mte_builder_destroy((mte_builder*)data);
+}
+
+static int get_args(napi_env env, napi_callback_info info, size_t want, napi_value* argv) {
+    size_t argc = want;
+    if (napi_get_cb_info(env, info, &argc, argv, NULL, NULL) != napi_ok) return 0;
+    return argc >= want;
+}
+
+static void* get_external(napi_env env, napi_value v) {
+    void* p = NULL;
+    if (napi_get_value_external(env, v, &p) != napi_ok) return NULL;
+    return p;
+}
+
+static char* get_string(napi_env env, napi_value v, size_t* len_out) {
+    size_t len = 0;
+    if (napi_get_value_string_utf8(env, v, NULL, 0, &len) != napi_ok) return NULL;
+    char* s = (char*)malloc(len + 1);
+    napi_get_value_string_utf8(env, v, s, len + 1, &len);
+    if (len_out) *len_out = len;
+    return s;
+}
+
+static napi_value make_u32(napi_env env, uint32_t v) {
+    napi_value r;
+    napi_create_uint32(env, v, &r);
+    return r;
+}
+static napi_value make_f64(napi_env env, double v) {
+    napi_value r;
+    napi_create_double(env, v, &r);
+    return r;
+}
+
+/* abiVersion(): number */
+static napi_value js_abi_version(napi_env env, napi_callback_info info) {
+    (void)info;
+    return make_u32(env, (uint32_t)mte_abi_version());
+}
+
+/* buildInfo(): string */
+static napi_value js_build_info(napi_env env, napi_callback_info info) {
+    (void)info;
+    napi_value r;
+    CHECK(env, napi_create_string_utf8(env, mte_build_info(), NAPI_AUTO_LENGTH, &r));
+    return r;
+}
+
+/* createEngine(device, chunkSize): External — new Client(...) for a whole batch */
+static napi_value js_create_engine(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    mte_config cfg;
+    memset(&cfg, 0, sizeof cfg);
+    if (get_args(env, info, 2, argv)) {
+        napi_get_value_int32(env, argv[0], &cfg.device);
+        napi_get_value_uint32(env, argv[1], &cfg.chunk_size);
+    }
+    mte_engine* e = NULL;
+    int rc = mte_create(&cfg, &e);
+    if (rc) return throw_mte(env, "mte_create", rc, "no HIP device (MI355X/gfx950 required; no CPU fallback)");
+    napi_value ext;
+    CHECK(env, napi_create_external(env, e, finalize_engine, NULL, &ext));
+    return ext;
+}
+
+/* createBuilder(): External */
+static napi_value js_create_builder(napi_env env, napi_callback_info info) {
+    (void)info;
+    mte_builder* b = NULL;
+    int rc = mte_builder_create(&b);
+    if (rc) return throw_mte(env, "mte_builder_create", rc, NULL);
+    napi_value ext;
+    CHECK(env, napi_create_external(env, b, finalize_builder, NULL, &ext));
+    return ext;
+}
+
+/* builderAddDoc(builder, observerName, messagesJson): void */
+static napi_value js_builder_add_doc(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) {
+        napi_throw_type_error(env, NULL, "builderAddDoc(builder, observer, json)");
+        return NULL;
+    }
+    mte_builder* b = (mte_builder*)get_external(env, argv[0]);
+    size_t len = 0;
+    char* obs = get_string(env, argv[1], NULL);
+    char* json = get_string(env, argv[2], &len);
+    int rc = (b && obs && json) ? mte_builder_add_doc(b, obs, json, len) : MTE_E_ARG;
+    free(obs);
+    free(json);
+    if (rc) return throw_mte(env, "mte_builder_add_doc", rc, b ? mte_builder_error(b) : NULL);
+    return NULL;
+}
+
+/* builderDocCount(builder): number */
+static napi_value js_builder_doc_count(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    mte_builder* b = (mte_builder*)get_external(env, argv[0]);
+    mte_batch batch;
+    if (!b || mte_builder_batch(b, &batch)) return throw_mte(env, "mte_builder_batch", MTE_E_ARG, NULL);
+    return make_u32(env, batch.n_docs);
+}
+
+/* load(engine, builder): void */
+static napi_value js_load(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    mte_builder* b = (mte_builder*)get_external(env, argv[1]);
+    mte_batch batch;
+    if (!e || !b || mte_builder_batch(b, &batch)) return throw_mte(env, "load", MTE_E_ARG, NULL);
+    int rc = mte_load(e, &batch);
+    if (rc) return throw_mte(env, "mte_load", rc, mte_last_error(e));
+    return NULL;
+}
+
+/* generate(engine, kind, nDocs, nOps, nClients, seed): void */
+static napi_value js_generate(napi_env env, napi_callback_info info) {
+    napi_value argv[6];
+    if (!get_args(env, info, 6, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    uint32_t kind, nd, no, nc;
+    int64_t seed;
+    napi_get_value_uint32(env, argv[1], &kind);
+    napi_get_value_uint32(env, argv[2], &nd);
+    napi_get_value_uint32(env, argv[3], &no);
+    napi_get_value_uint32(env, argv[4], &nc);
+    napi_get_value_int64(env, argv[5], &seed);
+    int rc = mte_generate(e, kind, nd, no, NULL, nc, (uint64_t)seed);
+    if (rc) return throw_mte(env, "mte_generate", rc, mte_last_error(e));
+    return NULL;
+}
+
+/* replay(engine): {docs, ops, messages, failedDocs, kernelMs} — Client.applyMsg for every message */
+static napi_value js_replay(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    mte_stats st;
+    int rc = mte_replay(e, &st);
+    if (rc) return throw_mte(env, "mte_replay", rc, mte_last_error(e));
+    napi_value o;
+    CHECK(env, napi_create_object(env, &o));
+    napi_set_named_property(env, o, "docs", make_f64(env, (double)st.docs));
+    napi_set_named_property(env, o, "ops", make_f64(env, (double)st.ops));
+    napi_set_named_property(env, o, "messages", make_f64(env, (double)st.messages));
+    napi_set_named_property(env, o, "failedDocs", make_f64(env, (double)st.failed_docs));
+    napi_set_named_property(env, o, "kernelMs", make_f64(env, st.kernel_ms));
+    return o;
+}
+
+/* docStatus(engine, doc): [code, failingSeq] */
+static napi_value js_doc_status(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    uint32_t d;
+    napi_get_value_uint32(env, argv[1], &d);
+    int32_t code;
+    int64_t seq;
+    int rc = mte_doc_status(e, d, &code, &seq);
+    if (rc) return throw_mte(env, "mte_doc_status", rc, mte_last_error(e));
+    napi_value arr;
+    CHECK(env, napi_create_array_with_length(env, 2, &arr));
+    napi_set_element(env, arr, 0, make_f64(env, code));
+    napi_set_element(env, arr, 1, make_f64(env, (double)seq));
+    return arr;
+}
+
+/* getText(engine, doc): string (UTF-16, MergeTreeTextHelper.getText) */
+static napi_value js_text(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    uint32_t d;
+    napi_get_value_uint32(env, argv[1], &d);
+    size_t n = 0;
+    int rc = mte_text(e, d, NULL, 0, &n);
+    if (rc) return throw_mte(env, "mte_text", rc, mte_last_error(e));
+    uint16_t* buf = (uint16_t*)malloc((n + 1) * 2);
+    rc = mte_text(e, d, buf, n, &n);
+    napi_value s;
+    if (!rc) napi_create_string_utf16(env, (const char16_t*)buf, n, &s);
+    free(buf);
+    if (rc) return throw_mte(env, "mte_text", rc, mte_last_error(e));
+    return s;
+}
+
+/* snapshotV1(engine, doc): string — the SnapshotV1.emit ITree as JSON */
+static napi_value js_snapshot(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    uint32_t d;
+    napi_get_value_uint32(env, argv[1], &d);
+    size_t n = 0;
+    uint32_t nb = 0;
+    int rc = mte_snapshot_v1(e, d, NULL, 0, &n, &nb);
+    if (rc) return throw_mte(env, "mte_snapshot_v1", rc, mte_last_error(e));
+    char* buf = (char*)malloc(n + 1);
+    rc = mte_snapshot_v1(e, d, buf, n + 1, &n, &nb);
+    napi_value s;
+    if (!rc) napi_create_string_utf8(env, buf, n, &s);
+    free(buf);
+    if (rc) return throw_mte(env, "mte_snapshot_v1", rc, mte_last_error(e));
+    return s;
+}
+
+/* summaries(engine, nDocs): Buffer of 32-byte mte_doc_summary records */
+static napi_value js_summaries(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    uint32_t nd;
+    napi_get_value_uint32(env, argv[1], &nd);
+    void* data = NULL;
+    napi_value buf;
+    CHECK(env, napi_create_buffer(env, (size_t)nd * sizeof(mte_doc_summary), &data, &buf));
+    int rc = mte_summaries(e, (mte_doc_summary*)data, nd);
+    if (rc) return throw_mte(env, "mte_summaries", rc, mte_last_error(e));
+    return buf;
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+    napi_property_descriptor props[] = {
+        {"abiVersion", 0, js_abi_version, 0, 0, 0, napi_default, 0},
+        {"buildInfo", 0, js_build_info, 0, 0, 0, napi_default, 0},
+        {"createEngine", 0, js_create_engine, 0, 0, 0, napi_default, 0},
+        {"createBuilder", 0, js_create_builder, 0, 0, 0, napi_default, 0},
+        {"builderAddDoc", 0, js_builder_add_doc, 0, 0, 0, napi_default, 0},
+        {"builderDocCount", 0, js_builder_doc_count, 0, 0, 0, napi_default, 0},
+        {"load", 0, js_load, 0, 0, 0, napi_default, 0},
+        {"generate", 0, js_generate, 0, 0, 0, napi_default, 0},
+        {"replay", 0, js_replay, 0, 0, 0, napi_default, 0},
+        {"docStatus", 0, js_doc_status, 0, 0, 0, napi_default, 0},
+        {"getText", 0, js_text, 0, 0, 0, napi_default, 0},
+        {"snapshotV1", 0, js_snapshot, 0, 0, 0, napi_default, 0},
+        {"summaries", 0, js_summaries, 0, 0, 0, napi_default, 0},
+    };
+    napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
+    return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

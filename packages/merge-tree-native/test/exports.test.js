@@ -1,0 +1,17 @@
+// CPU-only checks: the addon loads, binds every entry point, and the host-side builder works.
+"use strict";
+const assert = require("assert");
+const m = require("..");
+assert.strictEqual(m.abiVersion(), 1);
+assert.ok(/gfx950/.test(m.buildInfo()));
+for (const f of ["BatchedMergeEngine", "MergeTreeClient", "createBuilder", "builderAddDoc", "builderDocCount"]) {
+    assert.strictEqual(typeof m[f], "function", f);
+}
+const b = m.createBuilder();
+const msg = (c, s, r, contents) => ({ clientId: c, sequenceNumber: s, referenceSequenceNumber: r,
+    minimumSequenceNumber: 0, type: "op", contents });
+m.builderAddDoc(b, "__observer__", JSON.stringify([msg("a", 1, 0, { pos1: 0, seg: "hi", type: 0 })]));
+m.builderAddDoc(b, "__observer__", JSON.stringify([msg("a", 1, 0, { pos1: 0, pos2: 1, type: 1 })]));
+assert.strictEqual(m.builderDocCount(b), 2);
+assert.throws(() => m.builderAddDoc(b, "__observer__", "[{]"), /mte_builder_add_doc/);
+console.log("exports ok");

@@ -1,0 +1,22 @@
+// GPU: the Node path replays the reference's markRangeRemoved / snapshot spec scenarios on the MI355X
+// (mergeTree.markRangeRemoved.spec.ts:67-106) and a generated batch, printing checksums for pytest.
+"use strict";
+const assert = require("assert");
+const { BatchedMergeEngine, MergeTreeClient } = require("..");
+const msg = (c, s, r, contents, msn = 0) => ({ clientId: c, sequenceNumber: s, referenceSequenceNumber: r,
+    minimumSequenceNumber: msn, type: "op", contents });
+const hello = [];
+for (const [i, ch] of [..."hello world"].entries()) hello.push(msg("local", i + 1, i, { pos1: i, seg: ch, type: 0 }));
+const c1 = new MergeTreeClient();
+for (const m of hello) c1.applyMsg(m);
+c1.applyMsg(msg("remote2", 12, 11, { pos1: 0, pos2: 11, type: 1 }));
+c1.applyMsg(msg("remote", 13, 11, { pos1: 0, seg: "text", type: 0 }));
+assert.strictEqual(c1.getText(), "text");
+const tree = c1.snapshot();
+assert.strictEqual(tree.entries[0].path, "header");
+const e = new BatchedMergeEngine();
+e.generate(2, 8, 500, 8, 3);
+const st = e.replay();
+assert.strictEqual(st.failedDocs, 0);
+const sums = e.summaries();
+console.log(JSON.stringify({ ops: st.ops, checksums: sums.map((s) => s.checksum.toString()) }));

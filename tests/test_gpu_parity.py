@@ -153,3 +153,17 @@ def test_generated_workloads_match_oracle(engine, kind, docs, ops):
     if bad:
         compare_doc(engine, batch, bad[0])  # raises with a precise diff
     assert not bad
+
+
+def test_c1_conflict_farm_on_gpu(engine):
+    from tests.workloads import c1_farm_log
+
+    logs = [c1_farm_log(seed=s) for s in range(4)]
+    b = mte.Builder()
+    for m in logs:
+        b.add_doc(m, observer="0")
+    batch = b.batch()
+    engine.load(batch)
+    engine.replay()
+    for d in range(len(logs)):
+        compare_doc(engine, batch, d, observer="0")

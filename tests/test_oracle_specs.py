@@ -156,3 +156,15 @@ def test_overlapping_remove_records_overlap_client():
     segs = json.loads(d.segments_json())
     el = [s for s in segs if s.get("text") == "el"][0]
     assert el["removedSeq"] == 2 and el["removedClient"] == "b" and el["overlap"] == ["c"]
+
+
+def test_c1_conflict_farm_replays_cleanly():
+    # BASELINE.json configs[0]: 3 clients, 1k insert/remove ops; the oracle must replay it with no
+    # sequencing / insert errors and converge to one text (its own replay is deterministic).
+    from tests.workloads import c1_farm_log
+
+    m = c1_farm_log(seed=5)
+    assert len(m) == 1000
+    a = replay(m, observer="0")
+    b = replay(m, observer="0")
+    assert a.text() == b.text() and a.snapshot_json() == b.snapshot_json()

@@ -1,0 +1,50 @@
+"""Summarise rocprofv3 CSV output (kernel stats + FETCH_SIZE/WRITE_SIZE passes) into profiles/."""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def rows(pattern):
+    out = []
+    for p in glob.glob(pattern, recursive=True):
+        with open(p) as f:
+            out += list(csv.DictReader(f))
+    return out
+
+
+def main(tag, docs=4096, ops=10000, kind=2):
+    base = f"gpurun_out/prof_{tag}"
+    stats = rows(f"{base}/trace/**/*kernel_stats.csv")
+    trace = rows(f"{base}/trace/**/*kernel_trace.csv")
+    summary = {"tag": tag, "docs": docs, "ops": ops, "kind": kind, "kernels": {}}
+    for r in stats:
+        summary["kernels"][r["Name"]] = {k: r[k] for k in ("Calls", "TotalDurationNs", "AverageNs", "Percentage")}
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace if "k_replay" in r["Kernel_Name"]]
+    if durs:
+        summary["k_replay_avg_ms_trace"] = sum(durs) / len(durs) / 1e6
+    for cname in ("FETCH_SIZE", "WRITE_SIZE"):
+        pm = rows(f"{base}/pmc_{'fetch' if cname == 'FETCH_SIZE' else 'write'}/**/*counter_collection.csv")
+        vals = [float(r["Counter_Value"]) for r in pm if "k_replay" in r["Kernel_Name"] and r["Counter_Name"] == cname]
+        if vals:
+            summary[cname + "_kib_per_launch"] = sum(vals) / len(vals)
+    if "FETCH_SIZE_kib_per_launch" in summary and "WRITE_SIZE_kib_per_launch" in summary:
+        summary["hbm_bytes_per_launch"] = (summary["FETCH_SIZE_kib_per_launch"] + summary["WRITE_SIZE_kib_per_launch"]) * 1024
+    os.makedirs("profiles", exist_ok=True)
+    with open(f"profiles/{tag}_summary.json", "w") as f:
+        json.dump(summary, f, indent=1)
+    for p in glob.glob(f"{base}/trace/**/*kernel_stats.csv", recursive=True):
+        with open(p) as f, open(f"profiles/{tag}_kernel_stats.csv", "w") as g:
+            g.write(f.read())
+    if "hbm_bytes_per_launch" in summary:
+        with open("profiles/pmc_replay.json", "w") as f:
+            json.dump({"docs": docs, "ops": ops, "kind": kind, "source": f"profiles/{tag}_summary.json",
+                       "hbm_bytes_per_launch": summary["hbm_bytes_per_launch"],
+                       "note": "raw (FETCH_SIZE+WRITE_SIZE)*1024; gfx950 FETCH_SIZE calibration (x2) applies only to "
+                               "wide coalesced streams and is NOT applied to this narrow-access kernel"}, f, indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")

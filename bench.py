@@ -81,11 +81,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    kms = []
+    kms, lds_ms = [], []
     st = None
     for _ in range(args.steps):
         st = step()
         kms.append(st["kernel_ms"])
+        lds_ms.append(eng.run_info()["lds_ms"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -117,6 +118,7 @@ def main():
     # roofline on the replay kernel: algorithmic bytes per launch / HIP-event kernel time
     alg_bytes = n_ops_rank * (OP_RECORD_B + LEAF_BLOCK_B) + payload_chars  # 1 B/char ASCII payload
     kernel_ms = sum(kms) / len(kms)
+    info = eng.run_info()
     achieved = alg_bytes / (kernel_ms / 1000.0) / 1e9
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_replay.json")
@@ -168,9 +170,10 @@ def main():
                        "parallelism": f"doc-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "mte::k_replay", "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes},
+                         "kernel": "mte::k_lds<false>", "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
-            "extra": {"ops_per_step_per_gpu": ops_applied, "gen_s": gen_s, "snapshot_host_s": snap_host_s,
+            "extra": {"ops_per_step_per_gpu": ops_applied, "lds_pass_ms": sum(lds_ms) / len(lds_ms),
+                      "hbm_pass_ms": info["hbm_ms"], "docs_spilled_to_hbm": info["spilled"], "gen_s": gen_s, "snapshot_host_s": snap_host_s,
                       "snapshot_bytes": snap_bytes, "summaries_gathered": gathered, "oracle_verified_docs": verified},
         }
         print(json.dumps(line))

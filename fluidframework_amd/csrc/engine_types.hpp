@@ -5,6 +5,8 @@
 
 #include "../../include/mte.h"
 
+#define MTE_HOSTDEV_ __host__ __device__ inline
+
 namespace mte {
 
 typedef uint32_t u32;
@@ -15,44 +17,65 @@ typedef uint16_t u16;
 constexpr u32 NONE = 0xFFFFFFFFu;
 constexpr u32 ARENA_BIT = 0x80000000u;
 constexpr u32 SC_UNDEF = 0, SC_TRUE = 1, SC_FALSE = 2;   // needsScour tri-state (mergeTree.ts:63)
-constexpr u32 F_REMOVED = 1u << 16, F_MARKER = 1u << 17;  // Slot.meta flags
+constexpr u32 F_REMOVED = 1u << 16, F_MARKER = 1u << 17;  // slot meta flags
+constexpr u32 F_OVL = 1u << 18;                          // removedClientOverlap non-empty (mask in HBM, by sid)
 constexpr u32 MAP_WORDS = 16;                            // [0]=count, then 7 (key,val) pairs
 constexpr i32 GRANULARITY = 256;                         // TextSegmentGranularity (mergeTree.ts:1059)
 
-// Visibility-relevant part of a leaf slot: 16 bytes, one dwordx4 load per lane.
-struct Slot {
-    u32 len;
-    i32 seq;
-    i32 rseq;
-    u32 meta;  // client | rclient << 8 | flags
-};
+// Leaf-block metadata word: parent interior node (bits 0..29) | needsScour (bits 30..31).
+constexpr u32 BM_PAR = 0x3FFFFFFFu;
+constexpr u32 BM_NOPAR = 0x3FFFFFFFu;
 
-struct SegRec {
-    Slot v;
-    u64 ovl;      // removedClientOverlap as a short-id mask
-    u32 props;    // property-map id (0 = undefined)
-    u32 toff;     // text offset (ARENA_BIT => merge arena, else doc payload); marker: refType
-    u32 tcap;     // owned arena capacity from toff (0 for payload text)
-    u32 sid;      // segment id (LRU heap identity)
+// ------------------------------------------------------------------------------------------------
+// LDS plan of the replay kernel: ONE workgroup per CU with LDS_WAVES waves; each wave replays one
+// document at a time (persistent doc queue). Per-document structures live in the wave's region;
+// leaf blocks (8 slots of 32 B) come from a pool shared by the CU's waves, so one large document
+// can borrow blocks that the others do not need.
+constexpr u32 LDS_WAVES = 8;
+constexpr u32 LDS_BYTES = 163840;  // 160 KiB per CU (MI355X_MICROARCH.md), one workgroup declares all of it
+constexpr u32 ORD_CAP = 128;       // leaf blocks per document while resident in LDS
+constexpr u32 IN_CAP = 48;         // interior nodes per document while resident in LDS
+constexpr u32 HEAP_CAP = 191;      // LRU heap entries per document while resident in LDS
+constexpr u32 RING_OPS = 32;       // op records staged per wave (prefetched one batch ahead)
+
+struct WaveRegion {
+    uint4 ord[ORD_CAP];         // doc order: (block id, observer-visible length, max seq, child count)
+    u32 in_child[IN_CAP * 8];
+    u32 in_cnt[IN_CAP];
+    u32 in_par[IN_CAP];
+    uint2 heap[HEAP_CAP + 1];   // 1-based binary heap of (segment id, maxSeq)
+    mte_op ring[RING_OPS];
+    u32 scratch[64];
 };
+constexpr u32 POOL_HDR = 64;  // 16-word allocation bitmap
+constexpr u32 POOL_BLOCKS = ((LDS_BYTES - LDS_WAVES * (u32)sizeof(WaveRegion) - POOL_HDR - 16) / (8 * 32 + 4 + 1)) & ~3u;
+
+struct LdsPlan {
+    u32 bitmap[16];              // 1 = block taken (or beyond the pool)
+    WaveRegion wave[LDS_WAVES];
+    uint4 vis[POOL_BLOCKS * 8];  // len, seq, removedSeq, client | removedClient << 8 | flags
+    uint4 aux[POOL_BLOCKS * 8];  // props map id, text offset, owned text capacity, segment id
+    u32 bmeta[POOL_BLOCKS];
+    unsigned char owner[POOL_BLOCKS];  // wave holding the block (0xFF = free)
+};
+static_assert(sizeof(LdsPlan) <= LDS_BYTES, "LDS plan exceeds 160 KiB");
+static_assert(POOL_BLOCKS <= 16 * 32, "bitmap too small");
 
 // Host-computed per-document layout.
 struct DocCfg {
     u64 op_begin, op_end;
     u64 payload_off;
     u64 arena_off;     // two semispaces of arena_cap units each
-    u64 seg_off;
-    u64 heap_off;
-    u64 lbo_off;
+    u64 ovl_off;       // per segment id: removedClientOverlap mask (u64)
     u64 map_off;
+    u64 hb_off;        // byte offset of this doc's HBM-resident state (HBM mode only)
     u32 payload_len;
     u32 arena_cap;
-    u32 seg_cap;
-    u32 heap_cap;
-    u32 lbo_cap;
+    u32 seg_cap;       // segment ids available
     u32 map_cap;
+    u32 hb_blk, hb_ord, hb_in, hb_heap;  // HBM-mode capacities
     u32 collab;        // 1 = observer replay, 0 = local non-collaborative edits
-    u32 pad;
+    u32 has_nl;        // payload contains '\n' (TextSegment.canAppend reads last chars only then)
 };
 
 // Per-document results written by the kernel.
@@ -63,7 +86,6 @@ struct DocRes {
     u32 msgs;
     i32 min_seq;
     i32 cur_seq;
-    u32 root;
     u32 height;
     u32 n_lb;
     u32 arena_sel;
@@ -72,8 +94,17 @@ struct DocRes {
     u32 seg_next;
     u32 heap_size;
     u32 n_gc;
-    u32 lb_free;
+    u32 out_off;     // first row of this doc's final segments in the output pool
+    u32 n_segs;
+    u32 max_lb;      // peak leaf-block count
+    u32 mode;        // 0 LDS-resident, 1 HBM-resident
+    u32 spill_why;   // why the LDS pass gave the doc up (engine.hpp St::spillWhy)
+    u32 pad;
 };
+
+// internal status: the LDS-resident replay ran out of room (leaf-block pool, interior nodes, heap
+// or block list); the doc's LDS state is dropped and the host re-runs it HBM-resident
+constexpr i32 DOC_SPILL = 100;
 
 struct Params {
     mte_op* ops;
@@ -87,35 +118,61 @@ struct Params {
     u32 n_propsets;
     u32 n_vals;
     const DocCfg* docs;
-    const u32* doc_order;
+    const u32* doc_list;      // docs to run, in start order (LPT)
+    u32 n_list;
     u32 n_docs;
-    u32 pad0;
     DocRes* res;
     u16* arena;
-    u32* seg_parent;
-    uint2* heap;
-    u32* lbo;
+    u64* ovl;
     u32* maps;
-    uint4* lb_vis;
-    u64* lb_ovl;
-    u32* lb_props;
-    uint2* lb_txt;
-    u32* lb_sid;
-    u32* lb_cnt;
-    u32* lb_par;
-    u32* lb_scour;
-    u32* in_child;
-    u32* in_cnt;
-    u32* in_par;
-    u32* counters;  // [0] leaf-block bump, [1] internal-node bump
-    u32 nlb_cap, nin_cap;
+    unsigned char* hbm;       // HBM-mode per-doc state (DocCfg::hb_off)
+    uint4* out_vis;           // final segments, doc order (output pool)
+    uint4* out_aux;
+    u64* out_ovl;
+    u64 out_cap;
+    u32* counters;            // [0] doc queue, [1] output rows, [2] spilled docs
+    u32 pool_limit;           // test knob: LDS leaf blocks usable per CU (0 = all)
+    u64* prof;                // MTE_PROFILE builds: per doc PROF_SLOTS cycle counters
     // synthetic workload generator
-    u32* gen_first_seen;  // per doc: 64 entries, writer index for each short id (1..)
+    u32* gen_first_seen;      // per doc: 64 entries, writer index for each short id (1..)
     u32 gen_kind;
     u32 gen_nclients;
     u64 gen_seed;
-    u32 gen_n_propsets;   // propset ids 1..gen_n_propsets are the generator's annotate sets
+    u32 gen_n_propsets;       // propset ids 1..gen_n_propsets are the generator's annotate sets
     u32 pad1;
+};
+
+// MTE_PROFILE builds: s_memtime cycles per engine phase, per document (engine.hpp PROF_*).
+constexpr u32 PROF_SLOTS = 16;
+
+// HBM-mode state layout of one document (byte offsets from DocCfg::hb_off).
+struct HbmLayout {
+    MTE_HOSTDEV_ static u64 a16(u64 n) { return (n + 15) & ~15ull; }
+    u64 vis, aux, bmeta, ord, in_child, in_cnt, in_par, heap, scratch, bytes;
+    MTE_HOSTDEV_ static HbmLayout of(u32 blk, u32 ord, u32 in, u32 heap) {
+        HbmLayout l;
+        u64 o = 0;
+        l.vis = o;
+        o += a16((u64)blk * 8 * 16);
+        l.aux = o;
+        o += a16((u64)blk * 8 * 16);
+        l.bmeta = o;
+        o += a16((u64)blk * 4);
+        l.ord = o;
+        o += a16((u64)ord * 16);
+        l.in_child = o;
+        o += a16((u64)in * 8 * 4);
+        l.in_cnt = o;
+        o += a16((u64)in * 4);
+        l.in_par = o;
+        o += a16((u64)in * 4);
+        l.heap = o;
+        o += a16((u64)(heap + 1) * 8);
+        l.scratch = o;
+        o += 64 * 4;
+        l.bytes = o;
+        return l;
+    }
 };
 
 }  // namespace mte

@@ -3,7 +3,9 @@
 //   * mte_builder_*: ISequencedDocumentMessage JSON logs -> SoA op records + interned property sets
 //     (Client.applyMsg input, client.ts:805-836; op shapes ops.ts:29-110).
 //   * mte_load / mte_generate: stage batches in HBM, size per-document arenas.
-//   * mte_replay: one wavefront per document on the GPU (mte_kernels.hip / engine_core.hpp).
+//   * mte_replay: one wavefront per document on the GPU (mte_kernels.hip / engine.hpp): an
+//     LDS-resident pass over every document, then an HBM-resident pass for the documents that
+//     outgrew the LDS plan.
 //   * outputs: text (textSegment.ts:154-172), segment table (walkAllSegments, mergeTree.ts:2969),
 //     SnapshotV1 ITree (snapshotV1.ts:85-247), per-doc FNV-1a-64 summary.
 // There is no CPU execution path for replay: without a HIP device mte_create fails.
@@ -205,23 +207,26 @@ struct mte_engine {
     DevBuf<mte_op> d_ops;
     DevBuf<uint16_t> d_payload, d_arena;
     DevBuf<mte_propset> d_propsets;
-    DevBuf<uint32_t> d_prop_keys, d_prop_vals, d_val_flags, d_val_objidx, d_order, d_seg_parent, d_lbo, d_maps;
-    DevBuf<uint64_t> d_val_objmatch;
+    DevBuf<uint32_t> d_prop_keys, d_prop_vals, d_val_flags, d_val_objidx, d_order, d_list, d_maps, d_counters,
+        d_first_seen;
+    DevBuf<uint64_t> d_val_objmatch, d_ovl, d_out_ovl, d_prof;
     DevBuf<DocCfg> d_cfg;
     DevBuf<DocRes> d_res;
-    DevBuf<uint2> d_heap;
-    DevBuf<uint4> d_lb_vis;
-    DevBuf<uint64_t> d_lb_ovl;
-    DevBuf<uint32_t> d_lb_props, d_lb_sid, d_lb_cnt, d_lb_par, d_lb_scour, d_in_child, d_in_cnt, d_in_par, d_counters,
-        d_first_seen;
-    DevBuf<uint2> d_lb_txt;
+    DevBuf<uint4> d_out_vis, d_out_aux;
+    DevBuf<unsigned char> d_hbm;
+    std::vector<uint64_t> n_ops_doc;
+    // options (mte_set_option)
+    bool force_hbm = false;
+    uint32_t pool_limit = 0;
+    // last run
+    double last_lds_ms = 0, last_hbm_ms = 0;
+    uint32_t last_spilled = 0;
+    uint32_t n_groups = 256;
     // downloaded final state
-    std::vector<uint32_t> h_lbo, h_maps, h_lb_cnt, h_lb_props;
-    std::vector<uint4> h_lb_vis;
-    std::vector<uint64_t> h_lb_ovl;
-    std::vector<uint2> h_lb_txt;
+    std::vector<uint32_t> h_maps;
+    std::vector<uint4> h_out_vis, h_out_aux;
+    std::vector<uint64_t> h_out_ovl;
     std::vector<uint16_t> h_arena;
-    uint32_t h_nlb_used = 0;
 };
 
 static int set_err(mte_engine* e, int code, const std::string& m) {
@@ -291,10 +296,12 @@ static int upload(mte_engine* e, DevBuf<T>& d, const std::vector<T>& h) {
 // Per-document arena sizing (see DESIGN.md "HBM layout").
 static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, const std::vector<uint64_t>& pay_len,
                             const std::vector<uint64_t>& n_prop_ins, const std::vector<uint64_t>& n_ann,
-                            const std::vector<uint8_t>& collab, uint64_t arena_limit = 0) {
+                            const std::vector<uint8_t>& collab, const std::vector<uint8_t>& has_nl,
+                            uint64_t arena_limit = 0) {
     const uint32_t nd = (uint32_t)n_ops.size();
     e->cfg.assign(nd, DocCfg{});
-    uint64_t op = 0, pay = 0, ar = 0, seg = 0, hp = 0, lb = 0, mp = 0, nlb = 0;
+    e->n_ops_doc = n_ops;
+    uint64_t op = 0, pay = 0, ar = 0, seg = 0, mp = 0, out = 0;
     for (uint32_t d = 0; d < nd; d++) {
         DocCfg& c = e->cfg[d];
         uint64_t n = n_ops[d];
@@ -310,40 +317,27 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
         c.arena_cap = (uint32_t)std::min<uint64_t>(acap, 0x7FFFFFF0ull / 2);
         c.arena_off = ar;
         ar += 2ull * c.arena_cap;
-        c.seg_cap = (uint32_t)(3 * n + 8);
-        c.seg_off = seg;
+        c.seg_cap = (uint32_t)std::min<uint64_t>(3 * n + 8, 0xFFFFFFF0ull);
+        c.ovl_off = seg;
         seg += c.seg_cap;
-        c.heap_cap = (uint32_t)(2 * n + 64);
-        c.heap_off = hp;
-        hp += c.heap_cap;
-        c.lbo_cap = (uint32_t)(n / 2 + 64);
-        c.lbo_off = lb;
-        lb += c.lbo_cap;
         c.map_cap = (uint32_t)(n_prop_ins[d] + 4 * n_ann[d] + 16);
         c.map_off = mp;
         mp += c.map_cap;
         c.collab = collab[d];
-        nlb += n / 4 + 64;
+        c.has_nl = has_nl[d];
+        out += std::min<uint64_t>(3 * n + 8, 4096);
     }
-    uint64_t nin = nlb / 3 + 16ull * nd + 64;
+    out += 1u << 20;
     HIP_TRY(e, e->d_arena.alloc(ar));
-    HIP_TRY(e, e->d_seg_parent.alloc(seg));
-    HIP_TRY(e, e->d_heap.alloc(hp));
-    HIP_TRY(e, e->d_lbo.alloc(lb));
+    HIP_TRY(e, e->d_ovl.alloc(seg));
     HIP_TRY(e, e->d_maps.alloc(mp * MAP_WORDS));
-    HIP_TRY(e, e->d_lb_vis.alloc(nlb * 8));
-    HIP_TRY(e, e->d_lb_ovl.alloc(nlb * 8));
-    HIP_TRY(e, e->d_lb_props.alloc(nlb * 8));
-    HIP_TRY(e, e->d_lb_txt.alloc(nlb * 8));
-    HIP_TRY(e, e->d_lb_sid.alloc(nlb * 8));
-    HIP_TRY(e, e->d_lb_cnt.alloc(nlb));
-    HIP_TRY(e, e->d_lb_par.alloc(nlb));
-    HIP_TRY(e, e->d_lb_scour.alloc(nlb));
-    HIP_TRY(e, e->d_in_child.alloc(nin * 8));
-    HIP_TRY(e, e->d_in_cnt.alloc(nin));
-    HIP_TRY(e, e->d_in_par.alloc(nin));
+    HIP_TRY(e, e->d_out_vis.alloc(out));
+    HIP_TRY(e, e->d_out_aux.alloc(out));
+    HIP_TRY(e, e->d_out_ovl.alloc(out));
     HIP_TRY(e, e->d_counters.alloc(4));
     HIP_TRY(e, e->d_res.alloc(nd));
+    HIP_TRY(e, e->d_prof.alloc((size_t)nd * PROF_SLOTS));
+    HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, (size_t)nd * PROF_SLOTS * 8, e->stream));
     // LPT order: longest documents start first
     e->order.resize(nd);
     for (uint32_t d = 0; d < nd; d++) e->order[d] = d;
@@ -355,27 +349,21 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     P = Params{};
     P.n_docs = nd;
     P.docs = e->d_cfg.p;
-    P.doc_order = e->d_order.p;
+    P.doc_list = e->d_order.p;
+    P.n_list = nd;
     P.res = e->d_res.p;
     P.arena = e->d_arena.p;
-    P.seg_parent = e->d_seg_parent.p;
-    P.heap = e->d_heap.p;
-    P.lbo = e->d_lbo.p;
+    P.ovl = e->d_ovl.p;
     P.maps = e->d_maps.p;
-    P.lb_vis = e->d_lb_vis.p;
-    P.lb_ovl = e->d_lb_ovl.p;
-    P.lb_props = e->d_lb_props.p;
-    P.lb_txt = e->d_lb_txt.p;
-    P.lb_sid = e->d_lb_sid.p;
-    P.lb_cnt = e->d_lb_cnt.p;
-    P.lb_par = e->d_lb_par.p;
-    P.lb_scour = e->d_lb_scour.p;
-    P.in_child = e->d_in_child.p;
-    P.in_cnt = e->d_in_cnt.p;
-    P.in_par = e->d_in_par.p;
+    P.out_vis = e->d_out_vis.p;
+    P.out_aux = e->d_out_aux.p;
+    P.out_ovl = e->d_out_ovl.p;
+    P.out_cap = out;
     P.counters = e->d_counters.p;
-    P.nlb_cap = (uint32_t)std::min<uint64_t>(nlb, 0xFFFFFFF0ull);
-    P.nin_cap = (uint32_t)std::min<uint64_t>(nin, 0xFFFFFFF0ull);
+    P.prof = e->d_prof.p;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || cus <= 0) cus = 256;
+    e->n_groups = (uint32_t)cus;
     return MTE_OK;
 }
 
@@ -463,8 +451,13 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     e->replayed = e->downloaded = false;
     const uint32_t nd = b->n_docs;
     std::vector<uint64_t> n_ops(nd), pay(nd), pi(nd), an(nd);
-    std::vector<uint8_t> collab(nd);
+    std::vector<uint8_t> collab(nd), has_nl(nd, 0);
     for (uint32_t d = 0; d < nd; d++) {
+        for (uint64_t q = b->doc_payload_offsets[d]; q < b->doc_payload_offsets[d + 1]; q++)
+            if (b->payload[q] == (uint16_t)'\n') {
+                has_nl[d] = 1;
+                break;
+            }
         n_ops[d] = b->doc_op_offsets[d + 1] - b->doc_op_offsets[d];
         pay[d] = b->doc_payload_offsets[d + 1] - b->doc_payload_offsets[d];
         count_doc_ops(e->hb, d, pi[d], an[d]);
@@ -474,7 +467,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     }
     auto t0 = std::chrono::steady_clock::now();
     int rc;
-    if ((rc = layout_and_alloc(e, n_ops, pay, pi, an, collab))) return rc;
+    if ((rc = layout_and_alloc(e, n_ops, pay, pi, an, collab, has_nl))) return rc;
     if ((rc = upload(e, e->d_ops, e->hb.ops))) return rc;
     if ((rc = upload(e, e->d_payload, e->hb.payload))) return rc;
     if ((rc = upload_props(e))) return rc;
@@ -485,18 +478,72 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     return MTE_OK;
 }
 
+// HBM-resident capacities for a document that outgrew the LDS plan (blocks hold >= 4 segments
+// except transiently; segments <= 2 per op + 1 without zamboni).
+static void hbm_caps(uint64_t n, DocCfg& c, uint64_t& bytes) {
+    uint64_t blk = std::min<uint64_t>(n / 2 + 64 + POOL_BLOCKS, 0x3FFFFFF0ull);
+    c.hb_blk = (uint32_t)blk;
+    c.hb_ord = (uint32_t)blk;
+    c.hb_in = (uint32_t)std::min<uint64_t>(blk / 2 + 64, 0x3FFFFFF0ull);
+    c.hb_heap = (uint32_t)std::min<uint64_t>(2 * n + 64, 0x3FFFFFF0ull);
+    bytes = HbmLayout::of(c.hb_blk, c.hb_ord, c.hb_in, c.hb_heap).bytes;
+}
+
 static int run_kernel(mte_engine* e, bool gen) {
     HIP_TRY(e, hipSetDevice(e->device));
+    const uint32_t nd = e->P.n_docs;
+    e->P.pool_limit = e->pool_limit;
+    e->P.doc_list = e->d_order.p;
+    e->P.n_list = nd;
     HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 4 * sizeof(uint32_t), e->stream));
     HIP_TRY(e, hipEventRecord(e->ev0, e->stream));
-    HIP_TRY(e, gen ? launch_generate(e->P, e->P.n_docs, e->stream) : launch_replay(e->P, e->P.n_docs, e->stream));
-    HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
-    float ms = 0;
-    HIP_TRY(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
-    e->last_kernel_ms = ms;
-    e->res.resize(e->P.n_docs);
-    HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, e->res.size() * sizeof(DocRes), hipMemcpyDeviceToHost));
+    std::vector<uint32_t> spill;
+    float lds_ms = 0, hbm_ms = 0;
+    if (!e->force_hbm) {
+        uint32_t groups = std::min<uint32_t>(e->n_groups, (nd + LDS_WAVES - 1) / LDS_WAVES);
+        if (groups == 0) groups = 1;
+        HIP_TRY(e, launch_lds(e->P, gen, groups, e->stream));
+        HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+        HIP_TRY(e, hipEventElapsedTime(&lds_ms, e->ev0, e->ev1));
+        e->res.resize(nd);
+        HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nd * sizeof(DocRes), hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < nd; i++)
+            if (e->res[e->order[i]].status == DOC_SPILL) spill.push_back(e->order[i]);
+    } else {
+        spill = e->order;
+    }
+    e->last_spilled = e->force_hbm ? 0 : (uint32_t)spill.size();
+    if (!spill.empty()) {
+        // second pass: the spilled documents, HBM-resident, one wave each, longest first
+        uint64_t total = 0;
+        for (uint32_t d : spill) {
+            uint64_t bytes;
+            hbm_caps(e->n_ops_doc[d], e->cfg[d], bytes);
+            e->cfg[d].hb_off = total;
+            total += (bytes + 255) & ~255ull;
+        }
+        HIP_TRY(e, e->d_hbm.alloc(total));
+        int rc;
+        if ((rc = upload(e, e->d_cfg, e->cfg))) return rc;
+        if ((rc = upload(e, e->d_list, spill))) return rc;
+        e->P.docs = e->d_cfg.p;
+        e->P.hbm = e->d_hbm.p;
+        e->P.doc_list = e->d_list.p;
+        e->P.n_list = (uint32_t)spill.size();
+        HIP_TRY(e, hipEventRecord(e->ev0, e->stream));
+        HIP_TRY(e, launch_hbm(e->P, gen, (uint32_t)spill.size(), e->stream));
+        HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
+        HIP_TRY(e, hipStreamSynchronize(e->stream));
+        HIP_TRY(e, hipEventElapsedTime(&hbm_ms, e->ev0, e->ev1));
+        e->P.doc_list = e->d_order.p;
+        e->P.n_list = nd;
+    }
+    e->last_lds_ms = lds_ms;
+    e->last_hbm_ms = hbm_ms;
+    e->last_kernel_ms = (double)lds_ms + hbm_ms;
+    e->res.resize(nd);
+    HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nd * sizeof(DocRes), hipMemcpyDeviceToHost));
     e->replayed = true;
     e->downloaded = false;
     return MTE_OK;
@@ -554,7 +601,7 @@ int mte_generate(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, 
     e->hb = HostBatch();
     uint32_t nps = build_generator_props(e);
     std::vector<uint64_t> nops(n_docs), pay(n_docs), pi(n_docs), an(n_docs);
-    std::vector<uint8_t> collab(n_docs, 1);
+    std::vector<uint8_t> collab(n_docs, 1), has_nl(n_docs, 0);
     for (uint32_t d = 0; d < n_docs; d++) {
         uint64_t n = ops_per_doc ? ops_per_doc[d] : n_ops;
         nops[d] = n;
@@ -566,7 +613,7 @@ int mte_generate(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, 
     }
     int rc;
     // generated docs hover around a 2048-char target length: 64K-unit semispaces are ample
-    if ((rc = layout_and_alloc(e, nops, pay, pi, an, collab, 65536))) return rc;
+    if ((rc = layout_and_alloc(e, nops, pay, pi, an, collab, has_nl, 65536))) return rc;
     HIP_TRY(e, e->d_ops.alloc(e->hb.doc_op_offsets.back()));
     HIP_TRY(e, e->d_payload.alloc(e->hb.doc_payload_offsets.back()));
     HIP_TRY(e, hipMemsetAsync(e->d_payload.p, 0, e->d_payload.n * sizeof(uint16_t), e->stream));
@@ -633,20 +680,16 @@ static int ensure_download(mte_engine* e) {
     HIP_TRY(e, hipSetDevice(e->device));
     uint32_t ctr[4];
     HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
-    uint32_t used = std::min(ctr[0], e->P.nlb_cap);
-    e->h_nlb_used = used;
+    const uint64_t rows = std::min<uint64_t>(ctr[1], e->P.out_cap);
     auto dl = [&](auto& h, auto& d, size_t n) -> int {
         h.resize(n);
         if (n) HIP_TRY(e, hipMemcpy(h.data(), d.p, n * sizeof(h[0]), hipMemcpyDeviceToHost));
         return MTE_OK;
     };
-    if ((rc = dl(e->h_lbo, e->d_lbo, e->d_lbo.n))) return rc;
     if ((rc = dl(e->h_maps, e->d_maps, e->d_maps.n))) return rc;
-    if ((rc = dl(e->h_lb_cnt, e->d_lb_cnt, used))) return rc;
-    if ((rc = dl(e->h_lb_props, e->d_lb_props, (size_t)used * 8))) return rc;
-    if ((rc = dl(e->h_lb_vis, e->d_lb_vis, (size_t)used * 8))) return rc;
-    if ((rc = dl(e->h_lb_ovl, e->d_lb_ovl, (size_t)used * 8))) return rc;
-    if ((rc = dl(e->h_lb_txt, e->d_lb_txt, (size_t)used * 8))) return rc;
+    if ((rc = dl(e->h_out_vis, e->d_out_vis, rows))) return rc;
+    if ((rc = dl(e->h_out_aux, e->d_out_aux, rows))) return rc;
+    if ((rc = dl(e->h_out_ovl, e->d_out_ovl, rows))) return rc;
     if ((rc = dl(e->h_arena, e->d_arena, e->d_arena.n))) return rc;
     e->downloaded = true;
     return MTE_OK;
@@ -673,13 +716,13 @@ struct DocView {
         const DocRes& r = e->res[d];
         const uint16_t* pay = e->hb.payload.data() + c.payload_off;
         const uint16_t* ar = e->h_arena.data() + c.arena_off + (uint64_t)r.arena_sel * c.arena_cap;
-        for (uint32_t k = 0; k < r.n_lb; k++) {
-            uint32_t blk = e->h_lbo[c.lbo_off + k];
-            if (blk >= e->h_nlb_used) continue;
-            for (uint32_t s = 0; s < e->h_lb_cnt[blk]; s++) {
-                uint32_t i = blk * 8 + s;
-                uint4 v = e->h_lb_vis[i];
-                uint2 t = e->h_lb_txt[i];
+        if (r.status || (uint64_t)r.out_off + r.n_segs > e->h_out_vis.size()) return;
+        for (uint32_t q = 0; q < r.n_segs; q++) {
+            {
+                const uint64_t i = (uint64_t)r.out_off + q;
+                uint4 v = e->h_out_vis[i];
+                uint4 a = e->h_out_aux[i];
+                uint2 t = make_uint2(a.y, a.z);
                 SegView sv;
                 sv.kind = (v.w & F_MARKER) ? 1 : 0;
                 sv.len = v.x;
@@ -688,8 +731,8 @@ struct DocView {
                 sv.rseq = (int32_t)v.z;
                 sv.client = c.collab ? (int32_t)(v.w & 0xff) : -1;
                 sv.rclient = c.collab ? (int32_t)((v.w >> 8) & 0xff) : -1;
-                sv.ovl = e->h_lb_ovl[i];
-                sv.props = e->h_lb_props[i];
+                sv.ovl = e->h_out_ovl[i];
+                sv.props = a.x;
                 sv.reftype = sv.kind ? t.x : 0;
                 sv.text = sv.kind ? nullptr : ((t.x & ARENA_BIT) ? ar + (t.x & ~ARENA_BIT) : pay + t.x);
                 segs.push_back(sv);
@@ -1066,14 +1109,35 @@ int mte_doc_result(mte_engine* e, uint32_t doc, void* out, size_t sz) {
     memcpy(out, &e->res[doc], sizeof(DocRes));
     return MTE_OK;
 }
-int mte_pool_usage(mte_engine* e, uint32_t* lb_used, uint32_t* lb_cap, uint32_t* in_used, uint32_t* in_cap) {
+// Diagnostics of the last replay/generate: documents that outgrew the LDS plan and ran the
+// HBM-resident pass, and the two passes' kernel times.
+int mte_run_info(mte_engine* e, uint32_t* spilled, double* lds_ms, double* hbm_ms, uint64_t* out_rows) {
     if (!e) return MTE_E_ARG;
-    uint32_t ctr[4];
-    HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
-    *lb_used = ctr[0];
-    *lb_cap = e->P.nlb_cap;
-    *in_used = ctr[1];
-    *in_cap = e->P.nin_cap;
+    uint32_t ctr[4] = {0, 0, 0, 0};
+    if (e->d_counters.p) HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
+    if (spilled) *spilled = e->last_spilled;
+    if (lds_ms) *lds_ms = e->last_lds_ms;
+    if (hbm_ms) *hbm_ms = e->last_hbm_ms;
+    if (out_rows) *out_rows = ctr[1];
+    return MTE_OK;
+}
+// Phase cycle counters of the last run (libmte built with MTE_PROFILE; zeros otherwise):
+// PROF_SLOTS u64 per document (engine.hpp ProfSlot).
+int mte_profile(mte_engine* e, uint64_t* out, size_t cap) {
+    if (!e || !out) return MTE_E_ARG;
+    size_t n = (size_t)e->P.n_docs * PROF_SLOTS;
+    if (cap < n) return MTE_E_RANGE;
+    HIP_TRY(e, hipMemcpy(out, e->d_prof.p, n * 8, hipMemcpyDeviceToHost));
+    return MTE_OK;
+}
+// Engine options (tests / tuning): "force_hbm" (1 = skip the LDS pass), "pool_limit" (LDS leaf
+// blocks usable per CU; 0 = all).
+int mte_set_option(mte_engine* e, const char* key, int64_t value) {
+    if (!e || !key) return MTE_E_ARG;
+    std::string k(key);
+    if (k == "force_hbm") e->force_hbm = value != 0;
+    else if (k == "pool_limit") e->pool_limit = (uint32_t)std::max<int64_t>(0, value);
+    else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
 }
 int mte_wave_selftest(mte_engine* e, const uint32_t* in, uint32_t* out, uint32_t n_waves) {
@@ -1081,11 +1145,11 @@ int mte_wave_selftest(mte_engine* e, const uint32_t* in, uint32_t* out, uint32_t
     HIP_TRY(e, hipSetDevice(e->device));
     DevBuf<uint32_t> di, dout;
     HIP_TRY(e, di.alloc((size_t)n_waves * 64));
-    HIP_TRY(e, dout.alloc((size_t)n_waves * 64 * 3));
+    HIP_TRY(e, dout.alloc((size_t)n_waves * 64 * 5));
     HIP_TRY(e, hipMemcpy(di.p, in, (size_t)n_waves * 64 * 4, hipMemcpyHostToDevice));
     HIP_TRY(e, launch_wave_selftest(di.p, dout.p, n_waves, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
-    HIP_TRY(e, hipMemcpy(out, dout.p, (size_t)n_waves * 64 * 3 * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(e, hipMemcpy(out, dout.p, (size_t)n_waves * 64 * 5 * 4, hipMemcpyDeviceToHost));
     return MTE_OK;
 }
 // Replay kernel time of the last mte_replay, measured with HIP events on the engine stream.

@@ -1,5 +1,5 @@
 // Wave64 primitives for gfx950 (CDNA4). One wavefront replays one document; these are the only
-// cross-lane operations the engine uses (engine_core.hpp).
+// cross-lane operations the engine uses (engine.hpp).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -10,10 +10,17 @@ namespace mte {
 
 MTE_DEV uint32_t lane_id() { return __lane_id(); }
 
-// Execution + memory barrier across the wave: every lane's earlier global/LDS writes are visible
-// to every lane's later reads (workgroup == one wave here).
+// Full barrier for cross-lane GLOBAL-memory hand-offs inside a wave: every lane's earlier
+// global/LDS writes are complete and visible to every lane's later reads.
 MTE_DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Cross-lane LDS hand-off inside a wave: LDS instructions of one wavefront execute in order, so
+// only compiler reordering has to be prevented (no s_waitcnt, no cache maintenance).
+MTE_DEV void lds_order() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -31,6 +38,8 @@ MTE_DEV uint64_t wave_shfl(uint64_t v, uint32_t src) {
 // Uniform broadcast from a known lane (v_readlane -> SGPR).
 MTE_DEV uint32_t wave_read(uint32_t v, uint32_t src) { return __builtin_amdgcn_readlane(v, src); }
 MTE_DEV int32_t wave_read(int32_t v, uint32_t src) { return (int32_t)__builtin_amdgcn_readlane((uint32_t)v, src); }
+MTE_DEV uint32_t wave_first(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+MTE_DEV int32_t wave_first(int32_t v) { return (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)v); }
 
 // Inclusive prefix sum over the 64 lanes with DPP: row_shr:1,2,4,8 inside each 16-lane row, then
 // row_bcast:15 / row_bcast:31 to carry across rows (GFX9-family DPP controls, present on gfx950).
@@ -47,6 +56,25 @@ MTE_DEV uint32_t wave_scan_incl(uint32_t v) {
 }
 
 MTE_DEV uint32_t wave_sum(uint32_t v) { return wave_read(wave_scan_incl(v), 63); }
+
+// Inclusive prefix sum inside each aligned group of 8 lanes (one leaf block per group).
+MTE_DEV uint32_t group8_scan(uint32_t v) {
+    const uint32_t g = lane_id() & 7;
+    uint32_t x = v, t;
+    t = __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false); if (g >= 1) x += t;
+    t = __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false); if (g >= 2) x += t;
+    t = __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false); if (g >= 4) x += t;
+    return x;
+}
+// Inclusive prefix max (signed) inside each aligned group of 8 lanes.
+MTE_DEV int32_t group8_max(int32_t v) {
+    const uint32_t g = lane_id() & 7;
+    int32_t x = v, t;
+    t = (int32_t)__builtin_amdgcn_update_dpp(0u, (uint32_t)x, 0x111, 0xf, 0xf, false); if (g >= 1 && t > x) x = t;
+    t = (int32_t)__builtin_amdgcn_update_dpp(0u, (uint32_t)x, 0x112, 0xf, 0xf, false); if (g >= 2 && t > x) x = t;
+    t = (int32_t)__builtin_amdgcn_update_dpp(0u, (uint32_t)x, 0x114, 0xf, 0xf, false); if (g >= 4 && t > x) x = t;
+    return x;
+}
 
 MTE_DEV uint32_t atomic_add_u32(uint32_t* p, uint32_t v) { return atomicAdd(p, v); }
 

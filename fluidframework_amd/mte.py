@@ -13,7 +13,10 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libmte.so")
+# MTE_LIB=prof selects the phase-profiling build (csrc/Makefile `prof`, engine.hpp MTE_PROFILE)
+LIB_PATH = os.path.join(_HERE, "_build", "prof" if os.environ.get("MTE_LIB") == "prof" else "", "libmte.so")
+PROF_NAMES = ["apply", "resolve", "insert_slot", "range", "zamboni", "scour", "heap", "find_seg", "map", "pack",
+              "fetch", "lru", "text", "alloc", "ops", "total"]
 
 MTE_OP_INSERT, MTE_OP_REMOVE, MTE_OP_ANNOTATE, MTE_OP_INSERT_MARKER, MTE_OP_NOOP = 0, 1, 2, 3, 4
 MTE_F_END_OF_MSG, MTE_F_REWRITE = 1, 2
@@ -102,7 +105,10 @@ def lib():
         L.mte_snapshot_v1.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz), ctypes.POINTER(u32)]
         L.mte_summaries.argtypes = [vp, ctypes.c_void_p, sz]
         L.mte_doc_result.argtypes = [vp, u32, ctypes.c_void_p, sz]
-        L.mte_pool_usage.argtypes = [vp] + [ctypes.POINTER(u32)] * 4
+        L.mte_run_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]
+        L.mte_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
+        L.mte_profile.argtypes = [vp, ctypes.c_void_p, sz]
         L.mte_wave_selftest.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, u32]
         L.mte_last_kernel_ms.argtypes = [vp]
         L.mte_last_kernel_ms.restype = ctypes.c_double
@@ -234,17 +240,31 @@ class Engine:
         self._check(lib().mte_summaries(self._h, out.ctypes.data, self.n_docs), "mte_summaries")
         return out
 
-    def doc_result(self, doc):
-        buf = (ctypes.c_int32 * 16)()
-        self._check(lib().mte_doc_result(self._h, doc, buf, ctypes.sizeof(buf)), "mte_doc_result")
-        names = ["status", "failing_seq", "ops", "msgs", "min_seq", "cur_seq", "root", "height", "n_lb",
-                 "arena_sel", "arena_top", "map_next", "seg_next", "heap_size", "n_gc", "lb_free"]
-        return dict(zip(names, list(buf)))
+    DOC_RESULT_FIELDS = ["status", "failing_seq", "ops", "msgs", "min_seq", "cur_seq", "height", "n_lb",
+                         "arena_sel", "arena_top", "map_next", "seg_next", "heap_size", "n_gc", "out_off", "n_segs",
+                         "max_lb", "mode", "spill_why"]
 
-    def pool_usage(self):
-        v = [ctypes.c_uint32() for _ in range(4)]
-        self._check(lib().mte_pool_usage(self._h, *[ctypes.byref(x) for x in v]), "mte_pool_usage")
-        return {"lb_used": v[0].value, "lb_cap": v[1].value, "in_used": v[2].value, "in_cap": v[3].value}
+    def doc_result(self, doc):
+        buf = (ctypes.c_int32 * 20)()
+        self._check(lib().mte_doc_result(self._h, doc, buf, ctypes.sizeof(buf)), "mte_doc_result")
+        return dict(zip(self.DOC_RESULT_FIELDS, list(buf)))
+
+    def run_info(self):
+        """Last replay/generate: docs that outgrew the LDS plan (re-run HBM-resident) and pass times."""
+        sp, a, b, rows = ctypes.c_uint32(), ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+        self._check(lib().mte_run_info(self._h, ctypes.byref(sp), ctypes.byref(a), ctypes.byref(b),
+                                       ctypes.byref(rows)), "mte_run_info")
+        return {"spilled": sp.value, "lds_ms": a.value, "hbm_ms": b.value, "out_rows": rows.value}
+
+    def profile(self):
+        """Per-doc phase cycle counters (MTE_LIB=prof build), shape (n_docs, len(PROF_NAMES))."""
+        out = np.zeros((self.n_docs, len(PROF_NAMES)), dtype=np.uint64)
+        self._check(lib().mte_profile(self._h, out.ctypes.data, out.size), "mte_profile")
+        return out
+
+    def set_option(self, key, value):
+        """"force_hbm" (skip the LDS-resident pass) or "pool_limit" (LDS leaf blocks per CU)."""
+        self._check(lib().mte_set_option(self._h, key.encode(), int(value)), "mte_set_option")
 
     def last_kernel_ms(self):
         return lib().mte_last_kernel_ms(self._h)
@@ -252,9 +272,9 @@ class Engine:
     def wave_selftest(self, values):
         values = np.ascontiguousarray(values, dtype=np.uint32)
         nw = values.size // 64
-        out = np.zeros(nw * 64 * 3, dtype=np.uint32)
+        out = np.zeros(nw * 64 * 5, dtype=np.uint32)
         self._check(lib().mte_wave_selftest(self._h, values.ctypes.data, out.ctypes.data, nw), "mte_wave_selftest")
-        return out.reshape(nw, 3, 64)
+        return out.reshape(nw, 5, 64)
 
 
 class MergeTreeClient:

@@ -34,6 +34,9 @@ def test_wave_primitives(engine):
         bits = (v & 1).astype(np.uint64)
         mask = int(sum(int(b) << i for i, b in enumerate(bits)))
         assert int(out[w, 2][0]) == mask & 0xFFFFFFFF and int(out[w, 2][32]) == mask >> 32
+        g = v.reshape(8, 8)
+        assert np.array_equal(out[w, 3], np.cumsum(g, axis=1, dtype=np.uint64).astype(np.uint32).ravel())
+        assert np.array_equal(out[w, 4], np.maximum.accumulate(g.astype(np.int64), axis=1).astype(np.uint32).ravel())
 
 
 def spec_logs():
@@ -167,3 +170,45 @@ def test_c1_conflict_farm_on_gpu(engine):
     engine.replay()
     for d in range(len(logs)):
         compare_doc(engine, batch, d, observer="0")
+
+
+def _summary_key(s):
+    return [(int(x["checksum"]), int(x["status"]), int(x["segments"])) for x in s]
+
+
+def test_hbm_resident_pass_matches_lds_pass(engine):
+    """The HBM-resident engine (second pass for documents that outgrow LDS) is the same code over
+    HBM; both passes must give bit-identical results, and both match the oracle."""
+    engine.generate(3, 64, 2500, n_clients=8, seed=11)
+    batch = engine.export_batch()
+    engine.replay()
+    lds = engine.summaries()
+    info = engine.run_info()
+    assert info["spilled"] == 0, (info, [engine.doc_result(d) for d in range(64) if engine.doc_result(d)["mode"] == 1][:3])
+    engine.set_option("force_hbm", 1)
+    try:
+        engine.replay()
+        hbm = engine.summaries()
+    finally:
+        engine.set_option("force_hbm", 0)
+    assert _summary_key(lds) == _summary_key(hbm)
+    bad, _, _ = compare_batch_checksums(engine, batch)
+    assert not bad
+
+
+def test_lds_pool_exhaustion_spills_and_matches_oracle(engine):
+    """A tiny LDS block pool forces documents out of the LDS plan mid-replay; the host re-runs them
+    HBM-resident and every document still matches the oracle."""
+    engine.generate(2, 128, 3000, n_clients=8, seed=5)
+    batch = engine.export_batch()
+    engine.set_option("pool_limit", 48)
+    try:
+        engine.replay()
+        info = engine.run_info()
+    finally:
+        engine.set_option("pool_limit", 0)
+    assert info["spilled"] > 0, info
+    bad, _, _ = compare_batch_checksums(engine, batch)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad

@@ -173,7 +173,8 @@ def main():
                          "kernel": "mte::k_lds<false>", "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "extra": {"ops_per_step_per_gpu": ops_applied, "lds_pass_ms": sum(lds_ms) / len(lds_ms),
-                      "hbm_pass_ms": info["hbm_ms"], "docs_spilled_to_hbm": info["spilled"], "gen_s": gen_s, "snapshot_host_s": snap_host_s,
+                      "hbm_pass_ms": info["hbm_ms"], "docs_rerun_hbm": info["spilled"],
+                      "docs_continued_hbm": info["continued"], "gen_s": gen_s, "snapshot_host_s": snap_host_s,
                       "snapshot_bytes": snap_bytes, "summaries_gathered": gathered, "oracle_verified_docs": verified},
         }
         print(json.dumps(line))

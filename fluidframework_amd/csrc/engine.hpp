@@ -23,11 +23,23 @@
 
 namespace mte {
 
+// The LDS of the replay kernel: one plan per CU (k_lds declares nothing else).
+__shared__ LdsPlan g_plan;
+
 // Phase profiling (compile with -DMTE_PROFILE): inclusive s_memtime cycles per phase.
 enum ProfSlot : u32 {
     PF_APPLY = 0, PF_RESOLVE, PF_INSERT_SLOT, PF_RANGE, PF_ZAMBONI, PF_SCOUR, PF_HEAP, PF_FIND_SEG,
-    PF_MAP, PF_PACK, PF_FETCH, PF_LRU, PF_TEXT, PF_ALLOC, PF_OPS, PF_TOTAL
+    PF_MAP, PF_PACK, PF_FETCH, PF_LRU, PF_TEXT, PF_ALLOC, PF_OPS, PF_TOTAL,
+    // event counts
+    PN_RESOLVE, PN_DIRTY, PN_SCOUR, PN_SCOUR_CHANGED, PN_PACK, PN_POP, PN_PUSH, PN_SPLIT_BLK
 };
+#ifdef MTE_PROFILE
+#define MTE_COUNT(slot, n) (prof[slot] += (n))
+#else
+#define MTE_COUNT(slot, n) \
+    do {                   \
+    } while (0)
+#endif
 #ifdef MTE_PROFILE
 struct ProfScope {
     u64& acc;
@@ -90,115 +102,160 @@ struct Seg {
     u32 sid;    // segment id (LRU heap identity)
 };
 
+// Synthetic writers' state (generator), resumable across the LDS -> HBM hand-off.
+struct GenState {
+    Rng rng;
+    i32 ref[MTE_MAX_CLIENTS];
+    u32 sid_of[MTE_MAX_CLIENTS];
+    u32 nextShort, pay;
+    i32 lastC, lastR, lastPos;
+    u64 step;
+};
+
 // Uniform replay state (identical in every lane).
 struct St {
-    u32 root, height, n_lb, max_lb;
+    u32 root, height, n_lb;
     i32 minSeq, curSeq;
     u32 heapSize, segNext, arenaTop, arenaSel, mapNext;
-    u32 lbFree, lbBump, inFree, inBump, inUsed;
-    i32 status, failingSeq;
-    u32 opsApplied, msgs, nGc;
+    u32 lbFree, lbBump, inFree, inBump, inUsed, credit;
+    i32 status;
     u32 adirty, gdirty;
 };
 
 template <bool LDSM>
 struct Engine {
     const Params& p;
-    DocCfg cfg;
     u32 doc;
+    // hot per-document limits (DocCfg, engine_types.hpp)
+    u32 seg_cap, arena_cap, payload_len, map_cap;
     u32 L;  // lane
     St st;
     bool collab, has_nl;
 #ifdef MTE_PROFILE
     u64 prof[PROF_SLOTS];
 #endif
-    // state arrays (LDS-resident for LDSM, else HBM-resident)
-    uint4* vis;  // by block id * 8 + slot
-    uint4* aux;
-    u32* bmeta;  // by block id: parent | needsScour << 30
-    uint4* ord;  // doc order: (block id, observer-visible length, max seq, child count)
-    u32* in_child;
-    u32* in_cnt;
-    u32* in_par;
-    uint2* heap;
-    u32* scratch;
-    mte_op* ring;
-    u32 blk_cap, ord_cap, in_cap, heap_cap;
-    u32* bitmap;             // LDS pool allocation bitmap
-    unsigned char* owner;    // LDS pool block -> wave
+    // HBM-resident state arrays (HBM mode); in LDS mode every array is an address in the CU's
+    // LdsPlan (g_plan), a compile-time constant plus the wave's region offset.
+    uint4* m_vis;  // by block id * 8 + slot
+    uint4* m_aux;
+    u32* m_bmeta;  // by block id: parent | needsScour << 30
+    uint4* m_ord;  // doc order: (block id, observer-visible length, max seq, child count)
+    u32* m_in_child;
+    u32* m_in_cnt;
+    u32* m_in_par;
+    uint2* m_heap;
+    u32* m_scratch;
+    u32* m_stats;
+    u32 m_blk_cap, m_ord_cap, m_in_cap, m_heap_cap;
     u32 wave;
+    bool continued = false;  // HBM-resident after starting in LDS
+
+#define MTE_ARR(T, NAME, MEM, LDSX)            \
+    MTE_DEV T* NAME() const {                  \
+        if constexpr (LDSM) return (T*)(LDSX); \
+        else return MEM;                       \
+    }
+    MTE_ARR(uint4, VIS, m_vis, g_plan.vis)
+    MTE_ARR(uint4, AUX, m_aux, g_plan.aux)
+    MTE_ARR(u32, BMETA, m_bmeta, g_plan.bmeta)
+    MTE_ARR(uint4, ORD, m_ord, g_plan.wave[wave].ord)
+    MTE_ARR(u32, INCH, m_in_child, g_plan.wave[wave].in_child)
+    MTE_ARR(u32, INCNT, m_in_cnt, g_plan.wave[wave].in_cnt)
+    MTE_ARR(u32, INPAR, m_in_par, g_plan.wave[wave].in_par)
+    MTE_ARR(uint2, HEAP, m_heap, g_plan.wave[wave].heap)
+    MTE_ARR(u32, SCRATCH, m_scratch, g_plan.wave[wave].scratch)
+    MTE_ARR(u32, STATS, m_stats, g_plan.wave[wave].stats)
+    MTE_ARR(mte_op, RING, nullptr, g_plan.wave[wave].ring)
+    MTE_ARR(u16, HINT, nullptr, g_plan.wave[wave].hint)        // segment id (mod 256) -> block at push
+    MTE_ARR(u32, BITMAP, nullptr, g_plan.bitmap)               // pool allocation bitmap
+    MTE_ARR(unsigned char, OWNER, nullptr, g_plan.owner)       // pool block -> wave
+    MTE_ARR(u32, POOLAV, nullptr, &g_plan.pool_avail)          // pool blocks free of credit
+#undef MTE_ARR
+    MTE_DEV u32 blk_cap() const { if constexpr (LDSM) return POOL_BLOCKS; else return m_blk_cap; }
+    MTE_DEV u32 ord_cap() const { if constexpr (LDSM) return ORD_CAP; else return m_ord_cap; }
+    MTE_DEV u32 in_cap() const { if constexpr (LDSM) return IN_CAP; else return m_in_cap; }
+    MTE_DEV u32 heap_cap() const { if constexpr (LDSM) return HEAP_CAP; else return m_heap_cap; }
     // doc-relative HBM bases
     u16* payload;
     u16* arena0;
     u64* ovl;
     u32* maps;
 
-    MTE_DEV Engine(const Params& p_, u32 doc_) : p(p_), cfg(p_.docs[doc_]), doc(doc_) {
+    MTE_DEV Engine(const Params& p_, u32 doc_) : p(p_), doc(doc_) {
         L = lane_id();
 #ifdef MTE_PROFILE
         for (u32 i = 0; i < PROF_SLOTS; i++) prof[i] = 0;
 #endif
-        payload = p.payload + cfg.payload_off;
-        arena0 = p.arena + cfg.arena_off;
-        ovl = p.ovl + cfg.ovl_off;
-        maps = p.maps + cfg.map_off * MAP_WORDS;
-        collab = cfg.collab != 0;
-        has_nl = cfg.has_nl != 0;
+        const DocCfg& c = p.docs[doc];
+        seg_cap = c.seg_cap;
+        arena_cap = c.arena_cap;
+        payload_len = c.payload_len;
+        map_cap = c.map_cap;
+        payload = p.payload + c.payload_off;
+        arena0 = p.arena + c.arena_off;
+        ovl = p.ovl + c.ovl_off;
+        maps = p.maps + c.map_off * MAP_WORDS;
+        collab = c.collab != 0;
+        has_nl = c.has_nl != 0;
         st.root = NONE;
         st.height = 1;
-        st.n_lb = st.max_lb = 0;
+        st.n_lb = 0;
         st.minSeq = st.curSeq = 0;
         st.heapSize = st.segNext = st.arenaTop = st.arenaSel = 0;
         st.mapNext = 1;  // map id 0 == undefined
         st.lbFree = st.inFree = NONE;
-        st.lbBump = st.inBump = st.inUsed = 0;
+        st.lbBump = st.inBump = st.inUsed = st.credit = 0;
         st.status = 0;
-        st.failingSeq = -1;
-        st.opsApplied = st.msgs = st.nGc = 0;
         st.adirty = st.gdirty = 0;
-        bitmap = nullptr;
-        owner = nullptr;
         wave = 0;
-        ring = nullptr;
     }
 
-    MTE_DEV void bind_lds(LdsPlan* lp, u32 w) {
-        WaveRegion& r = lp->wave[w];
-        vis = lp->vis;
-        aux = lp->aux;
-        bmeta = lp->bmeta;
-        ord = r.ord;
-        in_child = r.in_child;
-        in_cnt = r.in_cnt;
-        in_par = r.in_par;
-        heap = r.heap;
-        scratch = r.scratch;
-        ring = r.ring;
-        blk_cap = POOL_BLOCKS;
-        ord_cap = ORD_CAP;
-        in_cap = IN_CAP;
-        heap_cap = HEAP_CAP;
-        bitmap = lp->bitmap;
-        owner = lp->owner;
+    // per-document counters kept in memory (few updates; spares scalar registers)
+    MTE_DEV void stat_add(u32 i, u32 v) {
+        if (L == 0) atomicAdd(&STATS()[i], v);
+    }
+    MTE_DEV void stat_max(u32 i, u32 v) {
+        if (L == 0) atomicMax(&STATS()[i], v);
+    }
+    MTE_DEV u32 stat_get(u32 i) {
+        sync();
+        return wave_first(STATS()[i]);
+    }
+
+    MTE_DEV void bind_lds(u32 w) {
         wave = w;
+        if (L < ST_WORDS) STATS()[L] = L == ST_FAILSEQ ? NONE : 0u;
+        lds_order();
     }
     MTE_DEV void bind_hbm() {
-        HbmLayout l = HbmLayout::of(cfg.hb_blk, cfg.hb_ord, cfg.hb_in, cfg.hb_heap);
-        unsigned char* b = p.hbm + cfg.hb_off;
-        vis = (uint4*)(b + l.vis);
-        aux = (uint4*)(b + l.aux);
-        bmeta = (u32*)(b + l.bmeta);
-        ord = (uint4*)(b + l.ord);
-        in_child = (u32*)(b + l.in_child);
-        in_cnt = (u32*)(b + l.in_cnt);
-        in_par = (u32*)(b + l.in_par);
-        heap = (uint2*)(b + l.heap);
-        scratch = (u32*)(b + l.scratch);
-        blk_cap = cfg.hb_blk;
-        ord_cap = cfg.hb_ord;
-        in_cap = cfg.hb_in;
-        heap_cap = cfg.hb_heap;
+        const DocCfg& c = p.docs[doc];
+        HbmLayout l = HbmLayout::of(c.hb_blk, c.hb_ord, c.hb_in, c.hb_heap);
+        unsigned char* b = p.hbm + c.hb_off;
+        m_vis = (uint4*)(b + l.vis);
+        m_aux = (uint4*)(b + l.aux);
+        m_bmeta = (u32*)(b + l.bmeta);
+        m_ord = (uint4*)(b + l.ord);
+        m_in_child = (u32*)(b + l.in_child);
+        m_in_cnt = (u32*)(b + l.in_cnt);
+        m_in_par = (u32*)(b + l.in_par);
+        m_heap = (uint2*)(b + l.heap);
+        m_scratch = (u32*)(b + l.scratch);
+        m_stats = m_scratch + 32;
+        m_blk_cap = c.hb_blk;
+        m_ord_cap = c.hb_ord;
+        m_in_cap = c.hb_in;
+        m_heap_cap = c.hb_heap;
+        if (L < ST_WORDS) m_stats[L] = L == ST_FAILSEQ ? NONE : 0u;
+        wave_sync();
     }
+
+    // Wave-uniform reads: a load from a uniform address is broadcast through readfirstlane so the
+    // value (and all control flow and state updates that depend on it) stays scalar.
+    MTE_DEV static u32 U(u32 v) { return wave_first(v); }
+    MTE_DEV static uint4 U(uint4 v) { return make_uint4(wave_first(v.x), wave_first(v.y), wave_first(v.z), wave_first(v.w)); }
+    MTE_DEV uint4 ord_u(u32 k) const { return U(ORD()[k]); }
+    MTE_DEV u32 incnt_u(u32 n) const { return U(INCNT()[n]); }
+    MTE_DEV u32 inpar_u(u32 n) const { return U(INPAR()[n]); }
 
     // Order lane-crossing hand-offs through the state arrays.
     MTE_DEV void sync() const {
@@ -223,22 +280,18 @@ struct Engine {
     MTE_DEV void fail(i32 code, i32 seq) {
         if (st.status == 0) {
             st.status = code;
-            st.failingSeq = seq;
+            if (L == 0) STATS()[ST_FAILSEQ] = (u32)seq;
         }
     }
 
     // ---------------------------------------------------------------- slots
+    // Slot index with the block clamped into the pool (ids are validated where they are produced;
+    // the clamp keeps a corrupted id from ever addressing outside the state arrays).
+    MTE_DEV u32 sidx(u32 blk, u32 s) const { return (blk < blk_cap() ? blk : 0u) * 8 + (s & 7); }
     MTE_DEV Seg load(u32 blk, u32 s) const {
         Seg g;
-        if (blk >= blk_cap || s >= 8) {
-            g.len = 0;
-            g.seq = g.rseq = 0;
-            g.meta = g.props = g.toff = g.tcap = 0;
-            g.sid = NONE;
-            return g;
-        }
-        u32 i = blk * 8 + s;
-        uint4 v = vis[i], a = aux[i];
+        const u32 i = sidx(blk, s);
+        uint4 v = VIS()[i], a = AUX()[i];
         g.len = v.x;
         g.seq = (i32)v.y;
         g.rseq = (i32)v.z;
@@ -249,11 +302,22 @@ struct Engine {
         g.sid = a.w;
         return g;
     }
+    MTE_DEV Seg load_u(u32 blk, u32 s) const {  // a slot at a uniform address, as scalars
+        Seg g = load(blk, s);
+        g.len = U(g.len);
+        g.seq = (i32)U((u32)g.seq);
+        g.rseq = (i32)U((u32)g.rseq);
+        g.meta = U(g.meta);
+        g.props = U(g.props);
+        g.toff = U(g.toff);
+        g.tcap = U(g.tcap);
+        g.sid = U(g.sid);
+        return g;
+    }
     MTE_DEV void store(u32 blk, u32 s, const Seg& g) const {
-        if (blk >= blk_cap || s >= 8) return;
-        u32 i = blk * 8 + s;
-        vis[i] = make_uint4(g.len, (u32)g.seq, (u32)g.rseq, g.meta);
-        aux[i] = make_uint4(g.props, g.toff, g.tcap, g.sid);
+        const u32 i = sidx(blk, s);
+        VIS()[i] = make_uint4(g.len, (u32)g.seq, (u32)g.rseq, g.meta);
+        AUX()[i] = make_uint4(g.props, g.toff, g.tcap, g.sid);
     }
     MTE_DEV Seg shfl_seg(const Seg& r, u32 src) const {
         Seg o;
@@ -274,56 +338,88 @@ struct Engine {
 
     // block metadata
     MTE_DEV u32 bpar(u32 b) const {
-        if (b >= blk_cap) return NONE;
-        u32 x = bmeta[b] & BM_PAR;
+        if (b >= blk_cap()) return NONE;
+        u32 x = U(BMETA()[b]) & BM_PAR;
         return x == BM_NOPAR ? NONE : x;
     }
-    MTE_DEV u32 bscour(u32 b) const { return b < blk_cap ? bmeta[b] >> 30 : SC_UNDEF; }
+    MTE_DEV u32 bscour(u32 b) const { return b < blk_cap() ? U(BMETA()[b]) >> 30 : SC_UNDEF; }
     MTE_DEV void set_bpar_lane(u32 b, u32 par) const {  // per-lane write
-        if (b < blk_cap) bmeta[b] = (bmeta[b] & ~BM_PAR) | (par == NONE ? BM_NOPAR : (par & BM_PAR));
+        if (b < blk_cap()) BMETA()[b] = (BMETA()[b] & ~BM_PAR) | (par == NONE ? BM_NOPAR : (par & BM_PAR));
     }
     MTE_DEV void set_bscour(u32 b, u32 sc) const {
-        if (L == 0 && b < blk_cap) bmeta[b] = (bmeta[b] & BM_PAR) | (sc << 30);
+        if (L == 0 && b < blk_cap()) BMETA()[b] = (BMETA()[b] & BM_PAR) | (sc << 30);
     }
 
-    // Visible length of slot idx for (refSeq R, client C): nodeLength for a leaf
-    // (mergeTree.ts:1659-1699). C == 0 is the observer / local client: localNetLength (:1161-1172).
-    MTE_DEV u32 vislen(uint4 v, u32 idx, i32 R, u32 C) const {
-        const u32 meta = v.w;
-        const bool removed = (meta & F_REMOVED) != 0;
-        if (C == 0) return removed ? 0u : v.x;
-        if (!(client_of(meta) == C || (i32)v.y <= R)) return 0u;
-        if (removed) {
-            if (rclient_of(meta) == C || (i32)v.z <= R) return 0u;
-            if (meta & F_OVL) {
-                u32 sid = aux[idx].w;
-                if (sid < cfg.seg_cap && ((ovl[sid] >> C) & 1ull)) return 0u;
-            }
+    // Visible length of a slot for (refSeq R, client C): nodeLength for a leaf
+    // (mergeTree.ts:1659-1699) in branch-free 32-bit integer arithmetic:
+    //   ins = client == C || seq <= R;  rem = removed && (rclient == C || rseq <= R || C in overlap)
+    //   len if ins && !rem, else 0.
+    // z = the slot's aux.z (the overlap mask of clients 0..31 once removed). cz: C == 0, the
+    // observer / local client (localNetLength, :1161-1172) for whom every seq is <= R.
+    MTE_DEV static u32 le1(i32 a, i32 b) { return (u32)~(b - a) >> 31; }  // a <= b (|b - a| < 2^31)
+    MTE_DEV static u32 eq1(u32 a, u32 b) { return ((a ^ b) - 1u) >> 31; }   // a == b (a, b < 2^31)
+    MTE_DEV u32 vis_len(uint4 q, u32 z, u32 idx, i32 R, u32 C, u32 cz) const {
+        const u32 meta = q.w;
+        const u32 rm = (meta >> 16) & 1u;  // F_REMOVED
+        const u32 ins = eq1(meta & 0xffu, C) | le1((i32)q.y, R) | cz;
+        u32 ovh;
+        if (C < 32) {
+            ovh = (z >> C) & 1u;
+        } else {  // clients 32..63: HBM half of the mask (rare)
+            ovh = 0;
+            if ((meta & (F_REMOVED | F_OVLHI)) == (F_REMOVED | F_OVLHI)) ovh = ovl_hides(idx, C, meta) ? 1u : 0u;
         }
-        return v.x;
+        ovh &= (meta >> 18) & 1u;  // F_OVL
+        const u32 rem = rm & (eq1((meta >> 8) & 0xffu, C) | le1((i32)q.z, R) | cz | ovh);
+        return q.x & (0u - (ins & (rem ^ 1u)));
+    }
+    // C among the overlapping removers (removedClientOverlap, mergeTree.ts:2544-2552): clients
+    // 0..31 in the removed slot's aux.z (its arena-capacity word is dead once removed), 32..63 in
+    // the document's HBM mask by segment id.
+    MTE_DEV bool ovl_hides(u32 idx, u32 C, u32 meta) const {
+        if (C < 32) return (AUX()[idx].z >> C) & 1u;
+        if (!(meta & F_OVLHI)) return false;
+        const u32 sid = AUX()[idx].w;
+        return sid < seg_cap && ((ovl[sid] >> C) & 1ull);
     }
     // breakTie for a zero-visible leaf at pos 0: skip tombstones already seen at R (mergeTree.ts:2257-2261)
-    MTE_DEV static bool tie_ok(uint4 v, i32 R) {
-        return !((v.w & F_REMOVED) && (i32)v.z != 0 && (i32)v.z <= R);
+    MTE_DEV static u32 tie_ok(uint4 q, i32 R, u32 cz) {
+        const u32 seen = ((q.w >> 16) & 1u) & (((u32)(i32)q.z != 0u) ? 1u : 0u) & le1((i32)q.z, R);
+        return cz | (seen ^ 1u);
     }
-    // Visible length of a whole leaf block (one ord entry) for (R, C).
-    MTE_DEV u32 blen(uint4 o, i32 R, u32 C) const {
-        if (C == 0 || (i32)o.z <= R) return o.y;  // every child settled at R: same for all clients
-        u32 v = 0;
-        const u32 n = o.w > 8 ? 8u : o.w;
-        for (u32 s = 0; s < n; s++) v += vislen(vis[o.x * 8 + s], o.x * 8 + s, R, C);
+    // Visible lengths of the leaf blocks held one per lane (ord entries) for (R, C). A block whose
+    // children are all settled at R (max seq <= R) has the same length for every client; the others
+    // read their slots (independent LDS reads) and evaluate the predicate in integer arithmetic.
+    MTE_DEV u32 blen_all(uint4 o, bool valid, i32 R, u32 C) const {
+        const u32 cz = C == 0 ? 1u : 0u;
+        const bool fast = !valid | (cz != 0) | ((i32)o.z <= R);
+        u32 v = valid ? o.y : 0u;
+        if (wave_ballot(!fast)) {
+            const u32 b = o.x < blk_cap() ? o.x : 0u;
+            uint4 q[8];
+            u32 z[8];
+#pragma unroll
+            for (u32 s = 0; s < 8; s++) {
+                q[s] = VIS()[b * 8 + s];
+                z[s] = AUX()[b * 8 + s].z;
+            }
+            u32 sv = 0;
+#pragma unroll
+            for (u32 s = 0; s < 8; s++) sv += s < o.w ? vis_len(q[s], z[s], b * 8 + s, R, C, cz) : 0u;
+            v = fast ? v : sv;
+        }
         return v;
     }
 
-    // Recompute (visible length, max seq) of ord[k0 .. k0+n), n <= 8, from the slots.
+    // Recompute (visible length, max seq) of ORD()[k0 .. k0+n), n <= 8, from the slots.
     MTE_DEV void refresh(u32 k0, u32 n) {
         const u32 g = L >> 3, s = L & 7;
         const bool act = g < n;
-        uint4 o = act ? ord[k0 + g] : make_uint4(0, 0, 0, 0);
+        uint4 o = act ? ORD()[k0 + g] : make_uint4(0, 0, 0, 0);
         u32 len = 0;
         i32 mx = 0;
-        if (act && s < o.w && o.x < blk_cap) {
-            uint4 v = vis[o.x * 8 + s];
+        if (act && s < o.w && o.x < blk_cap()) {
+            uint4 v = VIS()[o.x * 8 + s];
             len = obs_len(v.x, v.w);
             mx = seq_hi((i32)v.y, (i32)v.z, v.w);
         }
@@ -331,8 +427,8 @@ struct Engine {
         i32 tm = group8_max(mx);
         sync();
         if (act && s == 7) {
-            ord[k0 + g].y = tl;
-            ord[k0 + g].z = (u32)tm;
+            ORD()[k0 + g].y = tl;
+            ORD()[k0 + g].z = (u32)tm;
         }
         sync();
     }
@@ -353,8 +449,10 @@ struct Engine {
         for (u32 base = 0; base < st.n_lb; base += 64) {
             const u32 k = base + L;
             const bool valid = k < st.n_lb;
-            uint4 o = valid ? ord[k] : make_uint4(0, 0, 0, 0);
-            u32 v = valid ? blen(o, R, C) : 0u;
+            uint4 o = valid ? ORD()[k] : make_uint4(0, 0, 0, 0);
+            const u32 v = blen_all(o, valid, R, C);
+            MTE_COUNT(PN_DIRTY, __builtin_popcountll(wave_ballot(valid && !(C == 0 || (i32)o.z <= R))));
+            MTE_COUNT(PN_RESOLVE, 1);
             u32 incl = wave_scan_incl(v);
             u64 hit = wave_ballot(valid && cum + (i32)incl >= pos);
             if (hit) {
@@ -371,17 +469,16 @@ struct Engine {
         if (!f.ok) return f;
         // inside the block: first slot with r < vislen, or a zero-visible slot at r == 0 that wins breakTie
         const u32 s = L;
-        uint4 q = make_uint4(0, 0, 0, 0);
-        u32 v = 0;
-        bool tie = false;
-        if (s < f.cnt && s < 8) {
-            q = vis[f.blk * 8 + s];
-            v = vislen(q, f.blk * 8 + s, R, C);
-            tie = (C == 0) ? true : tie_ok(q, R);
-        }
-        u32 incl = group8_scan(v);
-        i32 r = pos - (f.cum + (i32)(incl - v));
-        bool cand = (s < f.cnt) && (s < 8) && (r < (i32)v || (r == 0 && v == 0 && tie));
+        const u32 idx = sidx(f.blk, s);
+        const uint4 q = VIS()[idx];
+        const u32 z = AUX()[idx].z;
+        const bool in = s < f.cnt && s < 8;
+        const u32 cz = C == 0 ? 1u : 0u;
+        const u32 v = in ? vis_len(q, z, idx, R, C, cz) : 0u;
+        const bool tie = tie_ok(q, R, cz) != 0;
+        const u32 incl = group8_scan(v);
+        const i32 r = pos - (f.cum + (i32)(incl - v));
+        const bool cand = in & ((r < (i32)v) | ((r == 0) & (v == 0) & tie));
         u64 m2 = wave_ballot(cand);
         if (m2) {
             u32 l2 = (u32)__builtin_ctzll(m2);
@@ -396,9 +493,9 @@ struct Engine {
         i32 cum = 0;
         for (u32 base = 0; base < st.n_lb; base += 64) {
             const u32 k = base + L;
-            u32 v = 0;
-            if (k < st.n_lb) v = blen(ord[k], R, C);
-            cum += (i32)wave_sum(v);
+            const bool valid = k < st.n_lb;
+            const uint4 o = valid ? ORD()[k] : make_uint4(0, 0, 0, 0);
+            cum += (i32)wave_sum(blen_all(o, valid, R, C));
         }
         return cum;
     }
@@ -411,57 +508,111 @@ struct Engine {
         else fail(MTE_DOC_CAPACITY, st.curSeq);
     }
 
+    // Take credit from the CU's pool: `want` blocks if available, at least `need`.
+    MTE_DEV bool take_credit(u32 need, u32 want) {
+        u32 got = 0;
+        if (L == 0) {
+            u32 cur = __atomic_load_n(POOLAV(), __ATOMIC_RELAXED);
+            for (;;) {
+                const u32 w = want < cur ? want : cur;
+                if (w < need) {
+                    got = NONE;
+                    break;
+                }
+                const u32 prev = atomicCAS(POOLAV(), cur, cur - w);
+                if (prev == cur) {
+                    got = w;
+                    break;
+                }
+                cur = prev;
+            }
+        }
+        got = wave_read(got, 0);
+        if (got == NONE) return false;
+        st.credit += got;
+        return true;
+    }
+    // Room for one more op while LDS-resident (per-wave caps with margins, OP_CREDIT leaf blocks
+    // in hand); false => the document continues HBM-resident from this op.
+    MTE_DEV bool room() {
+        if (!LDSM) return true;
+        if (st.n_lb + 16 > ord_cap() || st.inUsed + 12 > in_cap() || st.heapSize + st.n_lb + 8 > heap_cap())
+            return false;
+        if (st.credit >= OP_CREDIT) return true;
+        return take_credit(OP_CREDIT - st.credit, 2 * OP_CREDIT - st.credit);
+    }
+
     MTE_DEV u32 alloc_lb() {
         MTE_PROF(PF_ALLOC);
         u32 id = NONE;
         if (LDSM) {
+            if (st.credit == 0) {
+                // mid-op and the CU's pool is dry: the other waves return blocks as their scours,
+                // packs and documents complete, so wait (bounded) rather than abandon the replay
+                bool ok = take_credit(1, 1);
+                for (u32 spin = 0; !ok && spin < 20000; spin++) {
+                    __builtin_amdgcn_s_sleep(4);
+                    ok = take_credit(1, 1);
+                }
+                if (!ok) {
+                    fail_cap();
+                    return NONE;
+                }
+            }
             // claim a free bit of the CU's pool bitmap (other waves claim concurrently)
             for (int guard = 0; guard < 64; guard++) {
-                u32 w = L < 16 ? bitmap[L] : 0xFFFFFFFFu;
+                u32 w = L < 16 ? BITMAP()[L] : 0xFFFFFFFFu;
                 u64 m = wave_ballot(w != 0xFFFFFFFFu);
                 if (!m) break;
                 u32 wl = (u32)__builtin_ctzll(m);
                 u32 word = wave_read(w, wl);
                 u32 bit = (u32)__builtin_ctz(~word);
                 u32 old = 0;
-                if (L == 0) old = atomicOr(&bitmap[wl], 1u << bit);
+                if (L == 0) old = atomicOr(&BITMAP()[wl], 1u << bit);
                 old = wave_read(old, 0);
                 if (!(old & (1u << bit))) {
                     id = wl * 32 + bit;
                     break;
                 }
             }
-            if (id == NONE || id >= blk_cap) {
+            if (id == NONE || id >= blk_cap()) {
                 fail_cap();
                 return NONE;
             }
-            if (L == 0) owner[id] = (unsigned char)wave;
+            st.credit--;
+            if (L == 0) OWNER()[id] = (unsigned char)wave;
         } else {
             if (st.lbFree != NONE) {
                 id = st.lbFree;
-                u32 nx = bmeta[id] & BM_PAR;
+                u32 nx = U(BMETA()[id]) & BM_PAR;
                 st.lbFree = nx == BM_NOPAR ? NONE : nx;
-            } else if (st.lbBump < blk_cap) {
+            } else if (st.lbBump < blk_cap()) {
                 id = st.lbBump++;
             } else {
                 fail_cap();
                 return NONE;
             }
         }
+        id = U(id);
         sync();
-        if (L == 0) bmeta[id] = BM_NOPAR | (SC_UNDEF << 30);
+        if (L == 0) BMETA()[id] = BM_NOPAR | (SC_UNDEF << 30);
         sync();
         return id;
     }
     MTE_DEV void free_lb(u32 id) {
-        if (id >= blk_cap) return;
+        if (id >= blk_cap()) return;
         if (LDSM) {
             if (L == 0) {
-                owner[id] = 0xFF;
-                atomicAnd(&bitmap[id >> 5], ~(1u << (id & 31)));
+                OWNER()[id] = 0xFF;
+                atomicAnd(&BITMAP()[id >> 5], ~(1u << (id & 31)));
+            }
+            st.credit++;
+            if (st.credit >= 2 * OP_CREDIT) {  // hand surplus back: no hoarding across the CU's waves
+                if (L == 0) atomicAdd(POOLAV(), st.credit - OP_CREDIT);
+                st.credit = OP_CREDIT;
             }
         } else {
-            if (L == 0) bmeta[id] = st.lbFree == NONE ? BM_NOPAR : st.lbFree;
+            if (L == 0) BMETA()[id] = st.lbFree == NONE ? BM_NOPAR : st.lbFree;
             st.lbFree = id;
         }
         sync();
@@ -470,8 +621,8 @@ struct Engine {
         u32 id = NONE;
         if (st.inFree != NONE) {
             id = st.inFree;
-            st.inFree = in_par[id];
-        } else if (st.inBump < in_cap) {
+            st.inFree = inpar_u(id);
+        } else if (st.inBump < in_cap()) {
             id = st.inBump++;
         } else {
             fail_cap();
@@ -480,21 +631,21 @@ struct Engine {
         st.inUsed++;
         sync();
         if (L == 0) {
-            in_cnt[id] = 0;
-            in_par[id] = NONE;
+            INCNT()[id] = 0;
+            INPAR()[id] = NONE;
         }
         sync();
         return id;
     }
     MTE_DEV void free_in(u32 id) {
-        if (id >= in_cap) return;
-        if (L == 0) in_par[id] = st.inFree;
+        if (id >= in_cap()) return;
+        if (L == 0) INPAR()[id] = st.inFree;
         st.inFree = id;
         st.inUsed--;
         sync();
     }
     MTE_DEV u32 new_sid() {
-        if (st.segNext >= cfg.seg_cap) {
+        if (st.segNext >= seg_cap) {
             fail(MTE_DOC_CAPACITY, st.curSeq);
             return NONE;
         }
@@ -502,31 +653,31 @@ struct Engine {
     }
 
     // ---------------------------------------------------------------- doc-order block list
-    MTE_DEV void ord_shift_right(u32 from, u32 d) {  // ord[from..n_lb) -> ord[from+d..)
+    MTE_DEV void ord_shift_right(u32 from, u32 d) {  // ORD()[from..n_lb) -> ORD()[from+d..)
         for (i32 end = (i32)st.n_lb; end > (i32)from; end -= 64) {
             i32 start = end - 64 < (i32)from ? (i32)from : end - 64;
             i32 idx = start + (i32)L;
             uint4 v = make_uint4(0, 0, 0, 0);
-            if (idx < end) v = ord[idx];
+            if (idx < end) v = ORD()[idx];
             sync();
-            if (idx < end) ord[idx + d] = v;
+            if (idx < end) ORD()[idx + d] = v;
             sync();
         }
     }
-    MTE_DEV void ord_shift_left(u32 from, u32 d) {  // ord[from..n_lb) -> ord[from-d..)
+    MTE_DEV void ord_shift_left(u32 from, u32 d) {  // ORD()[from..n_lb) -> ORD()[from-d..)
         for (u32 start = from; start < st.n_lb; start += 64) {
             u32 idx = start + L;
             uint4 v = make_uint4(0, 0, 0, 0);
-            if (idx < st.n_lb) v = ord[idx];
+            if (idx < st.n_lb) v = ORD()[idx];
             sync();
-            if (idx < st.n_lb) ord[idx - d] = v;
+            if (idx < st.n_lb) ORD()[idx - d] = v;
             sync();
         }
     }
     MTE_DEV u32 ord_find(u32 blk) const {
         for (u32 base = 0; base < st.n_lb; base += 64) {
             u32 idx = base + L;
-            u64 m = wave_ballot(idx < st.n_lb && ord[idx].x == blk);
+            u64 m = wave_ballot(idx < st.n_lb && ORD()[idx].x == blk);
             if (m) return base + (u32)__builtin_ctzll(m);
         }
         return NONE;
@@ -534,10 +685,25 @@ struct Engine {
     // Current leaf block of segment `sid` (the LRU heap entry's segment.parent), NONE if unlinked.
     MTE_DEV bool find_seg(u32 sid, u32& k, u32& blk, u32& cnt) {
         MTE_PROF(PF_FIND_SEG);
+        if (LDSM) {  // the block recorded at push time (kept current by splits and packs)
+            const u32 hb = HINT()[sid & 255];
+            const u32 kk = ord_find(hb);
+            if (kk != NONE) {
+                const uint4 o = ORD()[kk];
+                const u32 c = wave_first(o.w);
+                const u64 m = wave_ballot((L < c) & (L < 8) & (AUX()[sidx(hb, L)].w == sid));
+                if (m) {
+                    k = kk;
+                    blk = hb;
+                    cnt = c;
+                    return true;
+                }
+            }
+        }
         for (u32 base = 0; base < st.n_lb; base += 8) {
             const u32 kk = base + (L >> 3), s = L & 7;
-            uint4 o = kk < st.n_lb ? ord[kk] : make_uint4(NONE, 0, 0, 0);
-            bool hit = kk < st.n_lb && s < o.w && o.x < blk_cap && aux[o.x * 8 + s].w == sid;
+            uint4 o = kk < st.n_lb ? ORD()[kk] : make_uint4(NONE, 0, 0, 0);
+            const bool hit = (kk < st.n_lb) & (s < o.w) & (AUX()[sidx(o.x, s)].w == sid);
             u64 m = wave_ballot(hit);
             if (m) {
                 u32 l = (u32)__builtin_ctzll(m);
@@ -551,11 +717,11 @@ struct Engine {
     }
 
     // ---------------------------------------------------------------- tree structure
-    MTE_DEV u32 parent_of(u32 node, u32 lvl) const { return lvl == 0 ? bpar(node) : (node < in_cap ? in_par[node] : NONE); }
+    MTE_DEV u32 parent_of(u32 node, u32 lvl) const { return lvl == 0 ? bpar(node) : (node < in_cap() ? inpar_u(node) : NONE); }
     MTE_DEV void set_parent(u32 node, u32 lvl, u32 par) const {
         if (L == 0) {
             if (lvl == 0) set_bpar_lane(node, par);
-            else if (node < in_cap) in_par[node] = par;
+            else if (node < in_cap()) INPAR()[node] = par;
         }
     }
     // Insert `nn` after `child` in `parent` (a node at level `lvl` >= 1); splits and root growth
@@ -567,7 +733,7 @@ struct Engine {
                 return;
             }
             u32 par = parent_of(child, lvl_child);
-            if (par != NONE && par >= in_cap) {
+            if (par != NONE && par >= in_cap()) {
                 fail(MTE_DOC_CAPACITY, st.curSeq);
                 return;
             }
@@ -575,10 +741,10 @@ struct Engine {
                 u32 r = alloc_in();
                 if (r == NONE) return;
                 if (L == 0) {
-                    in_child[r * 8 + 0] = child;
-                    in_child[r * 8 + 1] = nn;
-                    in_cnt[r] = 2;
-                    in_par[r] = NONE;
+                    INCH()[r * 8 + 0] = child;
+                    INCH()[r * 8 + 1] = nn;
+                    INCNT()[r] = 2;
+                    INPAR()[r] = NONE;
                 }
                 set_parent(child, lvl_child, r);
                 set_parent(nn, lvl_child, r);
@@ -587,12 +753,12 @@ struct Engine {
                 st.height++;
                 return;
             }
-            u32 cnt = in_cnt[par];
+            u32 cnt = incnt_u(par);
             if (cnt > 8) {
                 fail(MTE_DOC_CAPACITY, st.curSeq);
                 return;
             }
-            u32 c = (L < cnt) ? in_child[par * 8 + L] : NONE;
+            u32 c = (L < cnt) ? INCH()[par * 8 + L] : NONE;
             u64 m = wave_ballot(L < cnt && c == child);
             if (!m) {
                 fail(MTE_DOC_CAPACITY, st.curSeq);
@@ -600,10 +766,10 @@ struct Engine {
             }
             u32 idx = (u32)__builtin_ctzll(m);
             sync();
-            if (L > idx && L < cnt && L + 1 < 8) in_child[par * 8 + L + 1] = c;
+            if (L > idx && L < cnt && L + 1 < 8) INCH()[par * 8 + L + 1] = c;
             if (L == 0) {
-                in_child[par * 8 + idx + 1] = nn;
-                in_cnt[par] = cnt + 1;
+                INCH()[par * 8 + idx + 1] = nn;
+                INCNT()[par] = cnt + 1;
             }
             set_parent(nn, lvl_child, par);
             sync();
@@ -612,16 +778,16 @@ struct Engine {
             u32 q = alloc_in();
             if (q == NONE) return;
             u32 moved = NONE;
-            if (L < 4) moved = in_child[par * 8 + 4 + L];
+            if (L < 4) moved = INCH()[par * 8 + 4 + L];
             sync();
             if (L < 4) {
-                in_child[q * 8 + L] = moved;
+                INCH()[q * 8 + L] = moved;
                 if (lvl_child == 0) set_bpar_lane(moved, q);
-                else if (moved < in_cap) in_par[moved] = q;
+                else if (moved < in_cap()) INPAR()[moved] = q;
             }
             if (L == 0) {
-                in_cnt[par] = 4;
-                in_cnt[q] = 4;
+                INCNT()[par] = 4;
+                INCNT()[q] = 4;
             }
             sync();
             child = par;
@@ -648,35 +814,39 @@ struct Engine {
         const u32 nc = cnt + 1;
         if (nc < 8) {
             if (L == 0) {
-                uint4 o = ord[k];
+                uint4 o = ORD()[k];
                 o.w = nc;
                 if (fresh) {
                     o.y += obs_len(rec.len, rec.meta);
                     i32 hi = seq_hi(rec.seq, rec.rseq, rec.meta);
                     if (hi > (i32)o.z) o.z = (u32)hi;
                 }
-                ord[k] = o;
+                ORD()[k] = o;
             }
             sync();
             return blk;
         }
-        if (st.n_lb + 1 > ord_cap) {
+        if (st.n_lb + 1 > ord_cap()) {
             fail_cap();
             return NONE;
         }
+        MTE_COUNT(PN_SPLIT_BLK, 1);
         u32 nb = alloc_lb();
         if (nb == NONE) return NONE;
         Seg m;
         if (L < 4) m = load(blk, 4 + L);
         sync();
-        if (L < 4) store(nb, L, m);
+        if (L < 4) {
+            store(nb, L, m);
+            if (LDSM) HINT()[m.sid & 255] = (u16)nb;
+        }
         ord_shift_right(k + 1, 1);
         if (L == 0) {
-            ord[k].w = 4;
-            ord[k + 1] = make_uint4(nb, 0, 0, 4);
+            ORD()[k].w = 4;
+            ORD()[k + 1] = make_uint4(nb, 0, 0, 4);
         }
         st.n_lb++;
-        if (st.n_lb > st.max_lb) st.max_lb = st.n_lb;
+        stat_max(ST_MAXLB, st.n_lb);
         sync();
         refresh(k, 2);
         insert_after(blk, nb, 0);
@@ -684,54 +854,96 @@ struct Engine {
     }
 
     // ---------------------------------------------------------------- LRU heap (collections.ts:213-265)
-    MTE_DEV void heap_push(u32 sid, i32 maxSeq) {
+    // Binary heap exactly as collections.ts:213-265 (key maxSeq, strict comparisons).
+    // Push: the key is the current op's seq (add_lru's only callers) and seqs are validated
+    // strictly increasing (client.ts:469-470), so every key already in the heap is <= the new one
+    // and the sift-up (collections.ts:241-250, which moves strictly larger parents) never moves an
+    // entry: a push appends.
+    MTE_DEV void heap_push(u32 sid, i32 maxSeq, u32 blk) {
         MTE_PROF(PF_HEAP);
-        if (st.heapSize + 1 >= heap_cap) {
+        if (st.heapSize + 1 >= heap_cap()) {
             fail_cap();
             return;
         }
-        st.heapSize++;
+        const u32 n = U(++st.heapSize);
+        MTE_COUNT(PN_PUSH, 1);
         if (L == 0) {
-            u32 k = st.heapSize;
-            uint2 b = make_uint2(sid, (u32)maxSeq);
-            while (k > 1) {  // sift up: parents with a strictly larger key move down
-                uint2 a = heap[k >> 1];
-                if (!((i32)a.y - (i32)b.y > 0)) break;
-                heap[k] = a;
-                k >>= 1;
-            }
-            heap[k] = b;
+            HEAP()[n] = make_uint2(sid, (u32)maxSeq);
+            if (LDSM) HINT()[sid & 255] = (u16)blk;
         }
         sync();
     }
+    // heap entry at a uniform position held in registers (position i: lane i % 64 of set i / 64)
+    MTE_DEV static uint2 hent(uint2 h0, uint2 h1, uint2 h2, u32 i) {
+        if (i < 64) return make_uint2(wave_read(h0.x, i), wave_read(h0.y, i));
+        if (i < 128) return make_uint2(wave_read(h1.x, i - 64), wave_read(h1.y, i - 64));
+        return make_uint2(wave_read(h2.x, i - 128), wave_read(h2.y, i - 128));
+    }
+    // Pop: sift-down of collections.ts:252-264 (the smaller child, left on ties, moves up while
+    // strictly below the moved last entry). LDS mode: the whole heap (<= HEAP_CAP) is read once
+    // into registers and walked with scalar reads; only the moved entries are written back.
     MTE_DEV uint2 heap_pop() {
         MTE_PROF(PF_HEAP);
-        uint2 x = make_uint2(0, 0);
-        if (L == 0) {
-            x = heap[1];
-            u32 n = st.heapSize;
-            uint2 last = heap[n];
-            n--;
+        MTE_COUNT(PN_POP, 1);
+        uint2* H = HEAP();
+        const u32 n = st.heapSize;
+        uint2 x;
+        if constexpr (LDSM) {
+            static_assert(HEAP_CAP < 192, "heap register image holds 192 positions");
+            uint2 h0 = make_uint2(0, 0), h1 = h0, h2 = h0;
+            if (L <= n) h0 = H[L];
+            if (n >= 64 && 64 + L <= n) h1 = H[64 + L];
+            if (n >= 128 && 128 + L <= n) h2 = H[128 + L];
+            x = hent(h0, h1, h2, 1);
+            const uint2 last = hent(h0, h1, h2, n);
+            const u32 m = n - 1;
             u32 k = 1;
-            while ((k << 1) <= n) {  // sift down: the smaller child (left on ties) moves up
+            while ((k << 1) <= m) {
                 u32 j = k << 1;
-                uint2 hj = heap[j];
-                if (j < n) {
-                    uint2 hj1 = heap[j + 1];
+                uint2 hj = hent(h0, h1, h2, j);
+                if (j < m) {
+                    const uint2 hj1 = hent(h0, h1, h2, j + 1);
                     if ((i32)hj.y - (i32)hj1.y > 0) {
                         j++;
                         hj = hj1;
                     }
                 }
                 if ((i32)last.y - (i32)hj.y <= 0) break;
-                heap[k] = hj;
+                if (L == 0) H[k] = hj;
                 k = j;
             }
-            if (n >= 1) heap[k] = last;
+            if (m >= 1 && L == 0) H[k] = last;
+        } else {
+            x = make_uint2(0, 0);
+            if (L == 0) {
+                x = H[1];
+                u32 m = n;
+                const uint2 last = H[m];
+                m--;
+                u32 k = 1;
+                while ((k << 1) <= m) {
+                    u32 j = k << 1;
+                    uint2 hj;
+                    if (j < m) {
+                        const uint4 pr = *(const uint4*)(H + j);  // both children (16-B aligned)
+                        hj = make_uint2(pr.x, pr.y);
+                        if ((i32)pr.y - (i32)pr.w > 0) {
+                            j++;
+                            hj = make_uint2(pr.z, pr.w);
+                        }
+                    } else {
+                        hj = H[j];
+                    }
+                    if ((i32)last.y - (i32)hj.y <= 0) break;
+                    H[k] = hj;
+                    k = j;
+                }
+                if (m >= 1) H[k] = last;
+            }
+            x.x = wave_read(x.x, 0);
+            x.y = wave_read(x.y, 0);
         }
-        x.x = wave_read(x.x, 0);
-        x.y = wave_read(x.y, 0);
-        st.heapSize--;
+        st.heapSize = n - 1;
         sync();
         return x;
     }
@@ -744,33 +956,35 @@ struct Engine {
             sync();
             set_bscour(blk, SC_TRUE);
             sync();
-            heap_push(sid, seq);
+            heap_push(sid, seq, blk);
         }
     }
 
     // ---------------------------------------------------------------- property maps (HBM, lane 0)
     MTE_DEV bool val_match(u32 a, u32 b) const {  // matchProperties on one key (properties.ts:72-80)
         if (a == b) return true;
-        if (p.val_flags[b] & 2u) {
-            u32 j = p.val_objidx[b];
-            return j != NONE && ((p.val_objmatch[a] >> j) & 1ull);
+        if (U(p.val_flags[b]) & 2u) {
+            const u32 j = U(p.val_objidx[b]);
+            if (j == NONE) return false;
+            const u64 om = p.val_objmatch[a];
+            return (U((u32)(j < 32 ? om : (om >> 32))) >> (j & 31)) & 1u;
         }
         return false;
     }
     MTE_DEV bool match_props(u32 a, u32 b) const {  // properties.ts:62-93
         if (a == b) return true;
         if (a == 0 || b == 0) return false;
-        if (a >= cfg.map_cap || b >= cfg.map_cap) return false;
+        if (a >= map_cap || b >= map_cap) return false;
         const u32* ma = maps + (u64)a * MAP_WORDS;
         const u32* mb = maps + (u64)b * MAP_WORDS;
-        u32 na = ma[0], nb = mb[0];
+        const u32 na = U(ma[0]), nb = U(mb[0]);
         if (na != nb) return false;
         for (u32 i = 0; i < na; i++) {
-            u32 k = ma[1 + 2 * i], v = ma[2 + 2 * i];
+            const u32 k = U(ma[1 + 2 * i]), v = U(ma[2 + 2 * i]);
             bool found = false;
             for (u32 q = 0; q < nb; q++) {
-                if (mb[1 + 2 * q] == k) {
-                    if (!val_match(v, mb[2 + 2 * q])) return false;
+                if (U(mb[1 + 2 * q]) == k) {
+                    if (!val_match(v, U(mb[2 + 2 * q]))) return false;
                     found = true;
                     break;
                 }
@@ -785,11 +999,11 @@ struct Engine {
         MTE_PROF(PF_MAP);
         u32 id = NONE;
         i32 err = 0;
-        if (st.mapNext >= cfg.map_cap) err = MTE_DOC_CAPACITY;
+        if (st.mapNext >= map_cap) err = MTE_DOC_CAPACITY;
         if (L == 0 && !err) {
             u32 kv[2 * MTE_MAX_PROPS];
             u32 n = 0;
-            if (old && old < cfg.map_cap) {
+            if (old && old < map_cap) {
                 const u32* mo = maps + (u64)old * MAP_WORDS;
                 n = mo[0] > MTE_MAX_PROPS ? MTE_MAX_PROPS : mo[0];
                 for (u32 i = 0; i < 2 * n; i++) kv[i] = mo[1 + i];
@@ -852,11 +1066,11 @@ struct Engine {
 
     // ---------------------------------------------------------------- text arena (HBM)
     MTE_DEV u16* text_ptr(u32 off) const {
-        return (off & ARENA_BIT) ? arena0 + (u64)st.arenaSel * cfg.arena_cap + (off & ~ARENA_BIT) : payload + off;
+        return (off & ARENA_BIT) ? arena0 + (u64)st.arenaSel * arena_cap + (off & ~ARENA_BIT) : payload + off;
     }
     MTE_DEV bool text_ok(u32 off, u32 n) const {
         u64 end = (u64)(off & ~ARENA_BIT) + n;
-        return (off & ARENA_BIT) ? end <= cfg.arena_cap : end <= cfg.payload_len;
+        return (off & ARENA_BIT) ? end <= arena_cap : end <= payload_len;
     }
     // TextSegment.canAppend's `!text.endsWith("\n")` (textSegment.ts:63-69): only documents whose
     // payload holds a newline read text here.
@@ -864,40 +1078,30 @@ struct Engine {
         if (!has_nl || n == 0 || !text_ok(off, n)) return false;
         return text_ptr(off)[n - 1] == (u16)u'\n';
     }
-    MTE_DEV void copy_text(u32 dst_off, u32 src_off, u32 n) {
-        MTE_PROF(PF_TEXT);
-        if (!text_ok(dst_off, n) || !text_ok(src_off, n)) {
-            fail(MTE_DOC_CAPACITY, st.curSeq);
-            return;
-        }
-        u16* d = text_ptr(dst_off);
-        const u16* s = text_ptr(src_off);
-        for (u32 i = L; i < n; i += 64) d[i] = s[i];
-        st.adirty = 1;
-    }
     // Semispace compaction of the merge arena (all live arena-resident segment texts).
     MTE_DEV void arena_gc() {
         fence_arena();
         const u32 other = st.arenaSel ^ 1u;
-        u16* dst = arena0 + (u64)other * cfg.arena_cap;
+        u16* dst = arena0 + (u64)other * arena_cap;
         u32 top = 0;
         for (u32 k = 0; k < st.n_lb; k++) {
-            uint4 o = ord[k];
+            uint4 o = ord_u(k);
             const u32 cnt = o.w > 8 ? 8u : o.w;
             for (u32 s = 0; s < cnt; s++) {
-                uint4 v = vis[o.x * 8 + s];
-                uint4 a = aux[o.x * 8 + s];
+                uint4 v = U(VIS()[o.x * 8 + s]);
+                uint4 a = U(AUX()[o.x * 8 + s]);
                 if ((v.w & F_MARKER) || !(a.y & ARENA_BIT)) continue;
                 const u32 len = v.x;
-                const u32 cap = a.z < len ? len : a.z;
-                if (!text_ok(a.y, len) || top + cap > cfg.arena_cap) {
+                const bool rm = (v.w & F_REMOVED) != 0;  // aux.z is the overlap mask then
+                const u32 cap = (rm || a.z < len) ? len : a.z;
+                if (!text_ok(a.y, len) || top + cap > arena_cap) {
                     fail(MTE_DOC_CAPACITY, st.curSeq);
                     return;
                 }
                 const u16* src = text_ptr(a.y);
                 for (u32 i = L; i < len; i += 64) dst[top + i] = src[i];
                 sync();
-                if (L == 0) aux[o.x * 8 + s] = make_uint4(a.x, top | ARENA_BIT, cap, a.w);
+                if (L == 0) AUX()[o.x * 8 + s] = make_uint4(a.x, top | ARENA_BIT, rm ? a.z : cap, a.w);
                 sync();
                 top += cap;
             }
@@ -905,127 +1109,162 @@ struct Engine {
         wave_sync();
         st.arenaSel = other;
         st.arenaTop = top;
-        st.nGc++;
+        stat_add(ST_GC, 1);
     }
-    MTE_DEV bool arena_reserve(u32 need) {
-        if (st.arenaTop + need <= cfg.arena_cap) return true;
-        arena_gc();
-        if (st.arenaTop + need <= cfg.arena_cap) return true;
-        fail(MTE_DOC_CAPACITY, st.curSeq);
-        return false;
-    }
-
     // ---------------------------------------------------------------- zamboni (mergeTree.ts:1289-1478)
-    // One scourNode decision pass over the slots of a leaf block (held one per lane in `me`).
-    // dry == true: no side effects, returns the arena units the real pass will allocate.
-    // dry == false: performs merges (text appends) and records the kept list in scratch.
-    MTE_DEV u32 scour_pass(bool dry, const Seg& me, u32 cnt, u32& nkeep) {
-        u32* sc_keep = scratch;
-        u32* sc_len = scratch + 8;
-        u32* sc_off = scratch + 16;
-        u32* sc_cap = scratch + 24;
-        u32 need = 0;
-        nkeep = 0;
-        i32 prev = -1;  // index into the kept list of the current merge target
-        u32 pLen = 0, pOff = 0, pCap = 0, pProps = 0;
-        bool pText = false, pNL = false;
-        for (u32 s = 0; s < cnt; s++) {
-            const u32 len = wave_read(me.len, s);
-            const i32 seq = wave_read(me.seq, s);
-            const i32 rseq = wave_read(me.rseq, s);
-            const u32 meta = wave_read(me.meta, s);
-            const u32 props = wave_read(me.props, s);
-            const u32 toff = wave_read(me.toff, s);
-            const u32 tcap = wave_read(me.tcap, s);
-            const bool marker = (meta & F_MARKER) != 0;
-            bool keep = false;
-            if (meta & F_REMOVED) {  // tombstone: dropped once removed at or below the MSN (:1296-1319)
-                if (rseq > st.minSeq) keep = true;
-                prev = -1;
-            } else if (seq <= st.minSeq) {
-                bool ok = prev >= 0 && pText && !pNL && !marker &&
-                          (pLen <= (u32)GRANULARITY || len <= (u32)GRANULARITY) && match_props(pProps, props);
-                if (ok) {  // TextSegment.append (textSegment.ts:74-85)
-                    if ((pOff & ARENA_BIT) && pLen + len <= pCap) {
-                        if (!dry) copy_text(pOff + pLen, toff, len);
-                    } else if (pOff + pLen == toff) {
-                        if (pOff & ARENA_BIT) pCap = toff + tcap - pOff;
-                    } else {
-                        u32 ncap = 2 * (pLen + len);
-                        if (ncap < 32) ncap = 32;
-                        need += ncap;
-                        const u32 dst = st.arenaTop | ARENA_BIT;
-                        if (!dry) {
-                            st.arenaTop += ncap;
-                            copy_text(dst, pOff, pLen);
-                            copy_text(dst + pLen, toff, len);
-                        }
-                        pOff = dst;
-                        pCap = ncap;
-                    }
-                    pLen += len;
-                    pNL = ends_nl(toff, len);
-                    if (!dry && L == 0) {
-                        sc_len[prev] = pLen;
-                        sc_off[prev] = pOff;
-                        sc_cap[prev] = pCap;
-                    }
-                } else {
-                    keep = true;
-                    prev = (i32)nkeep;
-                    pLen = len;
-                    pOff = toff;
-                    pCap = tcap;
-                    pProps = props;
-                    pText = !marker;
-                    pNL = !marker && ends_nl(toff, len);
-                }
-            } else {
-                keep = true;
-                prev = -1;
-            }
-            if (keep) {
-                if (!dry && L == 0) {
-                    sc_keep[nkeep] = s;
-                    sc_len[nkeep] = len;
-                    sc_off[nkeep] = toff;
-                    sc_cap[nkeep] = tcap;
-                }
-                nkeep++;
+    // Text copies recorded by one scour, executed together: lane j < nj holds job j.
+    struct Jobs {
+        u32 n;               // uniform: number of jobs
+        u32 dst, src, len;   // per lane
+    };
+    MTE_DEV void job_add(Jobs& jb, u32 dst, u32 src, u32 len) {
+        if (L == jb.n) {
+            jb.dst = dst;
+            jb.src = src;
+            jb.len = len;
+        }
+        jb.n++;
+    }
+    // All recorded copies as one flattened gather: lane l moves char base+l of the concatenated
+    // jobs (sources are never destinations of the same batch, see scour()).
+    MTE_DEV void run_jobs(const Jobs& jb) {
+        MTE_PROF(PF_TEXT);
+        const u32 jl = L < jb.n ? jb.len : 0u;
+        const u32 jinc = wave_scan_incl(jl);
+        const u32 total = wave_read(jinc, 63);
+        const u32 jstart = jinc - jl;
+        for (u32 base = 0; base < total; base += 64) {
+            const u32 f = base + L;
+            u32 j = 0;
+            for (u32 q = 1; q < jb.n; q++)
+                if (f >= wave_read(jstart, q)) j = q;
+            const u32 s0 = wave_shfl(jstart, j), d = wave_shfl(jb.dst, j), sr = wave_shfl(jb.src, j);
+            if (f < total) {
+                const u32 o = f - s0;
+                text_ptr(d)[o] = text_ptr(sr)[o];
             }
         }
-        return need;
+        st.adirty = 1;
     }
 
     // scourNode on leaf block `blk` (doc-order index k, child count cnt), compacting the kept
-    // slots in place; returns the new child count. A dry decision pass first (no side effects,
-    // sizes the arena need), then the real pass: ONE call site of scour_pass.
+    // slots in place; returns the new child count (mergeTree.ts:1289-1366).
+    //  1. lane-parallel classification of the slots into bit masks (ballots);
+    //  2. the left-to-right merge chain on those masks (uniform scalar code): tombstones at or
+    //     below the MSN are dropped and reset the chain, settled live text appends to the chain
+    //     head under TextSegment.canAppend + matchProperties (textSegment.ts:63-85,
+    //     properties.ts:62-93); text moves are recorded as copy jobs;
+    //  3. the jobs run as one gather (arena GC first if the merge arena is full), the kept slots
+    //     are compacted.
     MTE_DEV u32 scour(u32 k, u32 blk, u32 cnt) {
         MTE_PROF(PF_SCOUR);
         if (cnt > 8) cnt = 8;
-        Seg me;
-        if (L < cnt) me = load(blk, L);
         fence_arena();
+        Seg me;
+        const bool act = L < cnt;
+        if (act) me = load(blk, L);
+        const bool rem = act && (me.meta & F_REMOVED);
+        const u64 mREM = wave_ballot(rem);
+        const u64 mKEPT = wave_ballot(rem && me.rseq > st.minSeq);  // tombstones still in the window
+        const u64 mSET = wave_ballot(act && !rem && me.seq <= st.minSeq);
+        MTE_COUNT(PN_SCOUR, 1);
+        if (!(mREM & ~mKEPT) && !(mSET & (mSET << 1))) return cnt;  // nothing dropped, nothing to merge
+        MTE_COUNT(PN_SCOUR_CHANGED, 1);
+        const u64 mTXT = wave_ballot(act && !(me.meta & F_MARKER));
+        const u64 mNL = has_nl ? wave_ballot(act && !(me.meta & F_MARKER) && ends_nl(me.toff, me.len)) : 0ull;
         u32 nkeep = 0;
-        for (u32 pass = 0; pass < 2; pass++) {
-            const bool dry = pass == 0;
-            const u32 need = scour_pass(dry, me, cnt, nkeep);
-            if (st.status) return cnt;
-            if (dry) {
-                if (nkeep == cnt) return cnt;  // nothing dropped or merged => nothing changes
-                if (need) {
-                    if (!arena_reserve(need)) return cnt;
-                    if (L < cnt) me = load(blk, L);  // a GC may have moved arena texts
+        u32 kSrc = 0, kLen = 0, kOff = 0, kCap = 0;  // lane i < nkeep: kept slot i
+        Jobs jb;
+        for (u32 attempt = 0; attempt < 2; attempt++) {
+            nkeep = 0;
+            jb.n = 0;
+            jb.dst = jb.src = jb.len = 0;
+            u32 top = st.arenaTop, need = 0;
+            i32 prev = -1;  // kept index of the chain head
+            u32 pLen = 0, pOff = 0, pCap = 0, pProps = 0;
+            bool pText = false, pNL = false, pFresh = false;
+            for (u32 s = 0; s < cnt; s++) {
+                const u64 bit = 1ull << s;
+                bool keep = true;
+                if (mREM & bit) {
+                    keep = (mKEPT & bit) != 0;
+                    prev = -1;
+                } else if (mSET & bit) {
+                    const u32 len = wave_read(me.len, s), props = wave_read(me.props, s);
+                    const u32 toff = wave_read(me.toff, s), tcap = wave_read(me.tcap, s);
+                    const bool ok = prev >= 0 && pText && !pNL && (mTXT & bit) &&
+                                    (pLen <= (u32)GRANULARITY || len <= (u32)GRANULARITY) && match_props(pProps, props);
+                    if (ok) {  // TextSegment.append (textSegment.ts:74-85)
+                        if ((pOff & ARENA_BIT) && pLen + len <= pCap) {
+                            job_add(jb, pOff + pLen, toff, len);
+                        } else if (pOff + pLen == toff) {
+                            if (pOff & ARENA_BIT) pCap = toff + tcap - pOff;
+                        } else {
+                            u32 ncap = 2 * (pLen + len);
+                            if (ncap < 32) ncap = 32;
+                            const u32 dst = top | ARENA_BIT;
+                            top += ncap;
+                            need += ncap;
+                            if (pFresh) {  // the head's chunk is built by this batch: retarget its jobs
+                                if (L < jb.n && jb.dst >= pOff && jb.dst < pOff + pLen) jb.dst = jb.dst - pOff + dst;
+                            } else {
+                                job_add(jb, dst, pOff, pLen);
+                            }
+                            job_add(jb, dst + pLen, toff, len);
+                            pOff = dst;
+                            pCap = ncap;
+                            pFresh = true;
+                        }
+                        pLen += len;
+                        pNL = (mNL & bit) != 0;
+                        if ((i32)L == prev) {
+                            kLen = pLen;
+                            kOff = pOff;
+                            kCap = pCap;
+                        }
+                        keep = false;
+                    } else {
+                        prev = (i32)nkeep;
+                        pLen = len;
+                        pOff = toff;
+                        pCap = tcap;
+                        pProps = props;
+                        pText = (mTXT & bit) != 0;
+                        pNL = pText && (mNL & bit);
+                        pFresh = false;
+                    }
+                } else {
+                    prev = -1;
+                }
+                if (keep) {
+                    if (L == nkeep) {
+                        kSrc = s;
+                        kLen = wave_read(me.len, s);
+                        kOff = wave_read(me.toff, s);
+                        kCap = wave_read(me.tcap, s);
+                    }
+                    nkeep++;
                 }
             }
+            if (nkeep == cnt) return cnt;
+            if (st.arenaTop + need <= arena_cap && jb.n <= 64) {
+                st.arenaTop = top;
+                break;
+            }
+            if (attempt == 1) {
+                fail(MTE_DOC_CAPACITY, st.curSeq);
+                return cnt;
+            }
+            arena_gc();  // moves every arena text: re-read the slots and redo the chain
+            if (st.status) return cnt;
+            if (act) me = load(blk, L);
         }
-        sync();
-        const u32 src = L < nkeep ? scratch[L] : 0u;
-        Seg out = shfl_seg(me, src);
+        if (jb.n) run_jobs(jb);
+        Seg out = load(blk, L < nkeep ? kSrc : 0u);  // the kept slots, re-read (not yet overwritten)
         if (L < nkeep) {
-            out.len = scratch[8 + L];
-            out.toff = scratch[16 + L];
-            out.tcap = scratch[24 + L];
+            out.len = kLen;
+            out.toff = kOff;
+            out.tcap = kCap;
         }
         sync();
         if (L < nkeep) store(blk, L, out);
@@ -1033,7 +1272,7 @@ struct Engine {
         const i32 om = L < nkeep ? seq_hi(out.seq, out.rseq, out.meta) : 0;
         const u32 tl = wave_read(group8_scan(ol), 7);
         const i32 tm = wave_read(group8_max(om), 7);
-        if (L == 0) ord[k] = make_uint4(blk, tl, (u32)tm, nkeep);
+        if (L == 0) ORD()[k] = make_uint4(blk, tl, (u32)tm, nkeep);
         sync();
         return nkeep;
     }
@@ -1043,12 +1282,13 @@ struct Engine {
     // redistributed into max(1, min(7, T/4)) fresh blocks.
     MTE_DEV void pack_leaves(u32 par, u32 m, u32 kids, u32 k0, u32 cnts) {
         MTE_PROF(PF_PACK);
+        MTE_COUNT(PN_PACK, 1);
         const u32 T = wave_sum(L < m ? cnts : 0u);
         u32 kk = T / 4;
         if (kk > 7) kk = 7;
         if (kk < 1) kk = 1;
         const u32 base = T / kk, extra = T % kk;
-        if (st.n_lb + kk > ord_cap + m) {
+        if (st.n_lb + kk > ord_cap() + m) {
             fail_cap();
             return;
         }
@@ -1065,9 +1305,11 @@ struct Engine {
         Seg rec;
         if (L < T) rec = load(srcBlk, q);
         sync();
-        for (u32 i = 0; i < m; i++) free_lb(wave_read(kids, i));
-        u32 nb = NONE;
-        for (u32 j = 0; j < kk; j++) {
+        // The kk packed blocks reuse the ids of the first min(kk, m) old children (block ids are
+        // not observable): only the difference is freed or allocated.
+        for (u32 i = kk; i < m; i++) free_lb(wave_read(kids, i));
+        u32 nb = L < m ? kids : NONE;
+        for (u32 j = m; j < kk; j++) {
             u32 id = alloc_lb();
             if (id == NONE) return;
             if (L == j) nb = id;
@@ -1082,26 +1324,29 @@ struct Engine {
             dq = (L - big) % (base ? base : 1);
         }
         const u32 dstBlk = wave_shfl(nb, dj < kk ? dj : 0u);
-        if (L < T) store(dstBlk, dq, rec);
-        if (L < kk) {
-            bmeta[nb] = (par & BM_PAR) | (SC_UNDEF << 30);
-            in_child[par * 8 + L] = nb;
+        if (L < T) {
+            store(dstBlk, dq, rec);
+            if (LDSM) HINT()[rec.sid & 255] = (u16)dstBlk;
         }
-        if (L == 0) in_cnt[par] = kk;
+        if (L < kk) {
+            BMETA()[nb] = (par & BM_PAR) | (SC_UNDEF << 30);
+            INCH()[par * 8 + L] = nb;
+        }
+        if (L == 0) INCNT()[par] = kk;
         sync();
         // splice ord: the run of the parent's old children becomes the kk new blocks
         if (kk > m) {
             ord_shift_right(k0 + m, kk - m);
             st.n_lb += kk - m;
-            if (st.n_lb > st.max_lb) st.max_lb = st.n_lb;
+            stat_max(ST_MAXLB, st.n_lb);
         } else if (kk < m) {
             ord_shift_left(k0 + m, m - kk);
             st.n_lb -= m - kk;
         }
-        if (L < kk) ord[k0 + L] = make_uint4(nb, 0, 0, base + (L < extra ? 1u : 0u));
+        if (L < kk) ORD()[k0 + L] = make_uint4(nb, 0, 0, base + (L < extra ? 1u : 0u));
         sync();
         refresh(k0, kk);
-        if (kk < 4 && par < in_cap && in_par[par] != NONE) pack_internal(par, 1);
+        if (kk < 4 && par < in_cap() && inpar_u(par) != NONE) pack_internal(par, 1);
     }
 
     // pack on an interior level: `node` (level lvl) underflowed; redistribute the grandchildren of
@@ -1112,15 +1357,15 @@ struct Engine {
                 fail(MTE_DOC_CAPACITY, st.curSeq);
                 return;
             }
-            const u32 par = in_par[node];
-            if (par >= in_cap || in_cnt[par] > 8) {
+            const u32 par = inpar_u(node);
+            if (par >= in_cap() || incnt_u(par) > 8) {
                 fail(MTE_DOC_CAPACITY, st.curSeq);
                 return;
             }
-            const u32 m = in_cnt[par];
-            const u32 kids = L < m ? in_child[par * 8 + L] : NONE;
-            const u32 cnts = (L < m && kids < in_cap) ? in_cnt[kids] : 0u;
-            if (wave_ballot(L < m && (kids >= in_cap || cnts > 8))) {
+            const u32 m = incnt_u(par);
+            const u32 kids = L < m ? INCH()[par * 8 + L] : NONE;
+            const u32 cnts = (L < m && kids < in_cap()) ? INCNT()[kids] : 0u;
+            if (wave_ballot(L < m && (kids >= in_cap() || cnts > 8))) {
                 fail(MTE_DOC_CAPACITY, st.curSeq);
                 return;
             }
@@ -1139,11 +1384,12 @@ struct Engine {
             }
             const u32 srcN = wave_shfl(kids, sib < m ? sib : 0u);
             u32 gc = NONE;
-            if (L < T) gc = in_child[srcN * 8 + q];
+            if (L < T) gc = INCH()[srcN * 8 + q];
             sync();
-            for (u32 i = 0; i < m; i++) free_in(wave_read(kids, i));
-            u32 nb = NONE;
-            for (u32 j = 0; j < kk; j++) {
+            // reuse the first min(kk, m) old interior ids (not observable)
+            for (u32 i = kk; i < m; i++) free_in(wave_read(kids, i));
+            u32 nb = L < m ? kids : NONE;
+            for (u32 j = m; j < kk; j++) {
                 u32 id = alloc_in();
                 if (id == NONE) return;
                 if (L == j) nb = id;
@@ -1159,18 +1405,18 @@ struct Engine {
             }
             const u32 dstN = wave_shfl(nb, dj < kk ? dj : 0u);
             if (L < T) {
-                in_child[dstN * 8 + dq] = gc;
+                INCH()[dstN * 8 + dq] = gc;
                 if (lvl == 1) set_bpar_lane(gc, dstN);
-                else if (gc < in_cap) in_par[gc] = dstN;
+                else if (gc < in_cap()) INPAR()[gc] = dstN;
             }
             if (L < kk) {
-                in_cnt[nb] = base + (L < extra ? 1u : 0u);
-                in_par[nb] = par;
-                in_child[par * 8 + L] = nb;
+                INCNT()[nb] = base + (L < extra ? 1u : 0u);
+                INPAR()[nb] = par;
+                INCH()[par * 8 + L] = nb;
             }
-            if (L == 0) in_cnt[par] = kk;
+            if (L == 0) INCNT()[par] = kk;
             sync();
-            if (kk < 4 && in_par[par] != NONE) {
+            if (kk < 4 && inpar_u(par) != NONE) {
                 node = par;
                 lvl++;
                 continue;
@@ -1187,7 +1433,7 @@ struct Engine {
         MTE_PROF(PF_ZAMBONI);
         for (int i = 0; i < 2 && !st.status; i++) {
             if (st.heapSize == 0) break;
-            const i32 top = (i32)heap[1].y;
+            const i32 top = wave_first((i32)HEAP()[1].y);
             if (top > st.minSeq) break;
             uint2 e = heap_pop();
             u32 k, blk, cnt;
@@ -1203,15 +1449,15 @@ struct Engine {
                     sync();
                     if (!(nc < cnt && nc < 4 && st.height > 1)) break;
                     par = bpar(blk);
-                    if (par == NONE || par >= in_cap || in_cnt[par] > 8 || in_cnt[par] == 0) {
+                    if (par == NONE || par >= in_cap() || incnt_u(par) > 8 || incnt_u(par) == 0) {
                         fail(MTE_DOC_CAPACITY, st.curSeq);
                         return;
                     }
-                    m = in_cnt[par];
-                    kids = L < m ? in_child[par * 8 + L] : NONE;
+                    m = incnt_u(par);
+                    kids = L < m ? INCH()[par * 8 + L] : NONE;
                     k0 = ord_find(wave_read(kids, 0));
                     if (k0 == NONE || k0 + m > st.n_lb ||
-                        wave_ballot(L < m && ord[k0 + (L < m ? L : 0)].x != kids)) {
+                        wave_ballot(L < m && ORD()[k0 + (L < m ? L : 0)].x != kids)) {
                         fail(MTE_DOC_CAPACITY, st.curSeq);
                         return;
                     }
@@ -1225,7 +1471,7 @@ struct Engine {
                     pack_leaves(par, m, kids, k0, cnts);
                     break;
                 }
-                const uint4 o = ord[k0 + idx];
+                const uint4 o = ord_u(k0 + idx);
                 k = k0 + idx;
                 blk = o.x;
                 cnt = o.w;
@@ -1241,13 +1487,15 @@ struct Engine {
     MTE_DEV bool edit(u32 type, i32 p1, i32 p2, i32 R, u32 C, i32 seq, Seg rec, u32 propset, bool rewrite) {
         const bool ins = type == MTE_OP_INSERT || type == MTE_OP_INSERT_MARKER;
         const u32 nphase = ins ? 2u : 3u;
+        Found known;  // insert after a split: the insertion point follows from the split (below)
+        known.ok = false;
         for (u32 ph = 0; ph < nphase; ph++) {
             if (!ins && ph == 2) {
                 range_op(type == MTE_OP_REMOVE, p1, p2, R, C, seq, propset, rewrite);
                 return st.status == 0;
             }
             const bool place = ins && ph == 1;
-            const Found f = resolve(ph == 1 && !ins ? p2 : p1, R, C);
+            const Found f = known.ok ? known : resolve(ph == 1 && !ins ? p2 : p1, R, C);
             if (!f.ok) {
                 if (ins) {
                     fail(MTE_DOC_INSERT_FAILED, seq);
@@ -1266,20 +1514,21 @@ struct Engine {
             } else {
                 if (!(f.slot >= 0 && f.r > 0)) continue;
                 // ensureIntervalBoundary: split slot f.slot at f.r (BaseSegment.splitAt, :524-568)
-                Seg left = load(f.blk, (u32)f.slot);
+                Seg left = load_u(f.blk, (u32)f.slot);
                 const u32 sid = new_sid();
                 if (sid == NONE) return false;
                 task = left;
                 const u32 r = (u32)f.r;
                 task.len = left.len - r;
                 task.toff = left.toff + r;
-                task.tcap = (left.toff & ARENA_BIT) ? left.tcap - r : 0u;
+                const bool rm = (left.meta & F_REMOVED) != 0;  // tcap holds the overlap mask then
+                task.tcap = rm ? left.tcap : ((left.toff & ARENA_BIT) ? left.tcap - r : 0u);
                 task.sid = sid;
                 left.len = r;
-                left.tcap = (left.toff & ARENA_BIT) ? r : 0u;
-                if (left.meta & F_OVL) {  // the right piece copies removedClientOverlap
+                left.tcap = rm ? left.tcap : ((left.toff & ARENA_BIT) ? r : 0u);
+                if (left.meta & F_OVLHI) {  // the right piece copies removedClientOverlap (clients >= 32)
                     fence_ovl();
-                    if (L == 0 && left.sid < cfg.seg_cap && sid < cfg.seg_cap) ovl[sid] = ovl[left.sid];
+                    if (L == 0 && left.sid < seg_cap && sid < seg_cap) ovl[sid] = ovl[left.sid];
                     st.gdirty = 1;
                 }
                 sync();
@@ -1287,8 +1536,40 @@ struct Engine {
                 sync();
                 j = (u32)f.slot + 1;
             }
-            const u32 b = insert_slot(f.k, f.blk, f.cnt, j, task, place);
+            const u32 b = U(insert_slot(f.k, f.blk, f.cnt, j, task, place));
             if (st.status) return false;
+            if (ins && !place) {
+                // The split left piece ends exactly at pos and the right piece (visible to C)
+                // starts there, so the insertingWalk re-walk (mergeTree.ts:2248-2277) lands
+                // before the right piece -- except when the block split 4+4 right between the
+                // two pieces: then the left block's end equals pos, blocks win ties, and the
+                // new segment is appended to the left block.
+                const u32 s = (u32)f.slot;  // left piece
+                known.ok = true;
+                known.r = 0;
+                known.cum = 0;  // unused by the placement
+                if (f.cnt + 1 < 8) {
+                    known.k = f.k;
+                    known.blk = f.blk;
+                    known.cnt = f.cnt + 1;
+                    known.slot = (i32)s + 1;
+                } else if (s + 1 < 4) {
+                    known.k = f.k;
+                    known.blk = f.blk;
+                    known.cnt = 4;
+                    known.slot = (i32)s + 1;
+                } else if (s == 3) {
+                    known.k = f.k;
+                    known.blk = f.blk;
+                    known.cnt = 4;
+                    known.slot = -1;  // append
+                } else {
+                    known.k = f.k + 1;
+                    known.blk = U(ORD()[f.k + 1].x);
+                    known.cnt = 4;
+                    known.slot = (i32)s - 3;
+                }
+            }
             if (place && collab && seq > st.minSeq) add_lru(b, rec.sid, seq);
         }
         return st.status == 0;
@@ -1304,8 +1585,8 @@ struct Engine {
         for (u32 base = 0; base < st.n_lb && cum < p2; base += 64) {
             const u32 k = base + L;
             const bool valid = k < st.n_lb;
-            uint4 o = valid ? ord[k] : make_uint4(0, 0, 0, 0);
-            const u32 v = valid ? blen(o, R, C) : 0u;
+            uint4 o = valid ? ORD()[k] : make_uint4(0, 0, 0, 0);
+            const u32 v = blen_all(o, valid, R, C);
             const u32 incl = wave_scan_incl(v);
             const i32 cb = cum + (i32)(incl - v);
             u64 hm = wave_ballot(valid && v > 0 && cb < p2 && cb + (i32)v > p1);
@@ -1319,45 +1600,47 @@ struct Engine {
                 const i32 cbj = wave_read(cb, j);
                 // per slot (lanes 0..7)
                 const u32 s = L;
-                const u32 idx = blk * 8 + (s & 7);
-                uint4 q = make_uint4(0, 0, 0, 0);
-                u32 sv = 0;
-                if (s < cnt && s < 8) {
-                    q = vis[idx];
-                    sv = vislen(q, idx, R, C);
-                }
+                const u32 idx = sidx(blk, s);
+                uint4 q = VIS()[idx];
+                const u32 z = AUX()[idx].z;
+                const bool in = s < cnt && s < 8;
+                const u32 sv = in ? vis_len(q, z, idx, R, C, C == 0 ? 1u : 0u) : 0u;
                 const u32 si = group8_scan(sv);
                 const i32 ex = cbj + (i32)(si - sv);
                 const bool mark = s < cnt && s < 8 && sv > 0 && ex < p2 && ex + (i32)sv > p1;
                 const u64 mm = wave_ballot(mark);
                 if (!mm) continue;
-                const u32 sid = mark ? aux[idx].w : NONE;
+                const u32 sid = mark ? AUX()[idx].w : NONE;
                 if (remove) {
                     u32 fresh = 0;
                     if (mark) {
                         if (q.w & F_REMOVED) {  // addOverlappingClient (:2544-2552)
-                            if (sid < cfg.seg_cap) {
-                                u64 old = (q.w & F_OVL) ? ovl[sid] : 0ull;
+                            if (C < 32) {
+                                AUX()[idx].z = AUX()[idx].z | (1u << C);
+                            } else if (sid < seg_cap) {
+                                const u64 old = (q.w & F_OVLHI) ? ovl[sid] : 0ull;
                                 ovl[sid] = old | (1ull << C);
+                                q.w |= F_OVLHI;
                             }
                             q.w |= F_OVL;
-                            vis[idx].w = q.w;
+                            VIS()[idx].w = q.w;
                         } else {
                             q.w = (q.w & ~0xff00u) | (C << 8) | F_REMOVED;
-                            vis[idx] = make_uint4(q.x, q.y, (u32)seq, q.w);
+                            VIS()[idx] = make_uint4(q.x, q.y, (u32)seq, q.w);
+                            AUX()[idx].z = 0;  // overlap mask starts empty
                             fresh = q.x;
                         }
                     }
-                    if (wave_ballot(mark && (q.w & F_OVL) && !fresh)) st.gdirty = 1;
+                    if (C >= 32 && wave_ballot(mark && !fresh)) st.gdirty = 1;
                     const u32 gone = wave_read(group8_scan(fresh), 7);
                     if (L == 0) {
-                        uint4 ob = ord[kj];
+                        uint4 ob = ORD()[kj];
                         ob.y -= gone;
                         if (gone && seq > (i32)ob.z) ob.z = (u32)seq;
-                        ord[kj] = ob;
+                        ORD()[kj] = ob;
                     }
                 } else {
-                    const u32 props = mark ? aux[idx].x : 0u;
+                    const u32 props = mark ? AUX()[idx].x : 0u;
                     u64 pending = mm;
                     while (pending) {
                         const u32 leader = (u32)__builtin_ctzll(pending);
@@ -1372,7 +1655,7 @@ struct Engine {
                             memoNew = nid;
                         }
                         const bool same = mark && props == old && ((pending >> L) & 1ull);
-                        if (same) aux[idx].x = nid;
+                        if (same) AUX()[idx].x = nid;
                         pending &= ~wave_ballot(same);
                     }
                 }
@@ -1385,6 +1668,30 @@ struct Engine {
                 }
             }
         }
+    }
+
+    // Re-assert that the replay state is wave-uniform (readfirstlane): the compiler's divergence
+    // analysis cannot see that values loaded from LDS at uniform addresses are uniform, and once a
+    // state word is considered divergent every branch on it becomes an exec-mask branch.
+    MTE_DEV void uniformize() {
+        st.root = U(st.root);
+        st.height = U(st.height);
+        st.n_lb = U(st.n_lb);
+        st.minSeq = (i32)U((u32)st.minSeq);
+        st.curSeq = (i32)U((u32)st.curSeq);
+        st.heapSize = U(st.heapSize);
+        st.segNext = U(st.segNext);
+        st.arenaTop = U(st.arenaTop);
+        st.arenaSel = U(st.arenaSel);
+        st.mapNext = U(st.mapNext);
+        st.lbFree = U(st.lbFree);
+        st.lbBump = U(st.lbBump);
+        st.inFree = U(st.inFree);
+        st.inBump = U(st.inBump);
+        st.inUsed = U(st.inUsed);
+        st.status = (i32)U((u32)st.status);
+        st.adirty = U(st.adirty);
+        st.gdirty = U(st.gdirty);
     }
 
     // Client.applyMsg for one op record (client.ts:805-836): the edit, zamboni, then
@@ -1421,7 +1728,7 @@ struct Engine {
             rec.tcap = 0;
             rec.sid = 0;
             edited = edit(op.type, op.pos1, op.a, R, C, seq, rec, op.props, (op.flags & MTE_F_REWRITE) != 0);
-            st.opsApplied++;
+            stat_add(ST_OPS, 1);
             if (st.status) return;
         }
         for (u32 z = 0; z < 2; z++) {
@@ -1429,7 +1736,7 @@ struct Engine {
             if (z == 1) {
                 run = false;
                 if (collab && (op.flags & MTE_F_END_OF_MSG)) {
-                    st.msgs++;
+                    stat_add(ST_MSGS, 1);
                     if (op.seq < st.curSeq || op.msn > op.seq || op.msn < st.minSeq) {
                         fail(MTE_DOC_SEQ_ORDER, op.seq);
                         return;
@@ -1452,9 +1759,9 @@ struct Engine {
         st.root = r;
         st.height = 1;
         if (r == NONE) return;
-        if (L == 0) ord[0] = make_uint4(r, 0, 0, 0);
+        if (L == 0) ORD()[0] = make_uint4(r, 0, 0, 0);
         st.n_lb = 1;
-        st.max_lb = 1;
+        stat_max(ST_MAXLB, 1);
         sync();
     }
 
@@ -1462,13 +1769,19 @@ struct Engine {
     // abandoned replay, whose blocks need not all be linked).
     MTE_DEV void release() {
         if (!LDSM) return;
-        for (u32 base = 0; base < blk_cap; base += 64) {
+        u32 n = 0;
+        for (u32 base = 0; base < blk_cap(); base += 64) {
             const u32 b = base + L;
-            if (b < blk_cap && owner[b] == (unsigned char)wave) {
-                owner[b] = 0xFF;
-                atomicAnd(&bitmap[b >> 5], ~(1u << (b & 31)));
+            const bool mine = b < blk_cap() && OWNER()[b] == (unsigned char)wave;
+            if (mine) {
+                OWNER()[b] = 0xFF;
+                atomicAnd(&BITMAP()[b >> 5], ~(1u << (b & 31)));
             }
+            n += (u32)__builtin_popcountll(wave_ballot(mine));
         }
+        n += st.credit;
+        if (L == 0 && n) atomicAdd(POOLAV(), n);
+        st.credit = 0;
         st.n_lb = 0;
         sync();
     }
@@ -1482,7 +1795,7 @@ struct Engine {
         u32 nseg = 0;
         for (u32 base = 0; base < st.n_lb; base += 64) {
             u32 k = base + L;
-            nseg += wave_sum(k < st.n_lb ? ord[k].w : 0u);
+            nseg += wave_sum(k < st.n_lb ? ORD()[k].w : 0u);
         }
         u32 off = 0;
         if (st.status == 0) {
@@ -1500,25 +1813,29 @@ struct Engine {
             u32 run = off;
             for (u32 base = 0; base < st.n_lb; base += 64) {
                 const u32 k = base + L;
-                uint4 o = k < st.n_lb ? ord[k] : make_uint4(0, 0, 0, 0);
+                uint4 o = k < st.n_lb ? ORD()[k] : make_uint4(0, 0, 0, 0);
                 const u32 c = o.w > 8 ? 8u : o.w;
                 const u32 incl = wave_scan_incl(c);
                 u32 at = run + incl - c;
                 for (u32 s = 0; s < c; s++) {
-                    uint4 v = vis[o.x * 8 + s], a = aux[o.x * 8 + s];
+                    uint4 v = VIS()[o.x * 8 + s], a = AUX()[o.x * 8 + s];
                     p.out_vis[at + s] = v;
                     p.out_aux[at + s] = a;
-                    p.out_ovl[at + s] = ((v.w & F_OVL) && a.w < cfg.seg_cap) ? ovl[a.w] : 0ull;
+                    u64 m = (v.w & F_OVL) ? (u64)a.z : 0ull;
+                    if ((v.w & F_OVLHI) && a.w < seg_cap) m |= ovl[a.w] & 0xFFFFFFFF00000000ull;
+                    p.out_ovl[at + s] = m;
                 }
                 run += wave_read(incl, 63);
             }
         }
+        const u32 fseq = stat_get(ST_FAILSEQ), ops = stat_get(ST_OPS), msgs = stat_get(ST_MSGS);
+        const u32 ngc = stat_get(ST_GC), maxlb = stat_get(ST_MAXLB);
         if (L == 0) {
             DocRes& o = p.res[doc];
             o.status = st.status;
-            o.failing_seq = st.failingSeq;
-            o.ops = st.opsApplied;
-            o.msgs = st.msgs;
+            o.failing_seq = (i32)fseq;
+            o.ops = ops;
+            o.msgs = msgs;
             o.min_seq = st.minSeq;
             o.cur_seq = st.curSeq;
             o.height = st.height;
@@ -1528,21 +1845,22 @@ struct Engine {
             o.map_next = st.mapNext;
             o.seg_next = st.segNext;
             o.heap_size = st.heapSize;
-            o.n_gc = st.nGc;
+            o.n_gc = ngc;
             o.out_off = off;
             o.n_segs = nseg;
-            o.max_lb = st.max_lb;
-            o.mode = LDSM ? 0u : 1u;
+            o.max_lb = maxlb;
+            o.mode = LDSM ? 0u : (continued ? 2u : 1u);
         }
     }
 
     MTE_DEV void mark_spilled() {
+        const u32 maxlb = stat_get(ST_MAXLB);
         if (L == 0) {
             DocRes& o = p.res[doc];
             o.status = DOC_SPILL;
             o.failing_seq = st.curSeq;
             o.n_segs = 0;
-            o.max_lb = st.max_lb;
+            o.max_lb = maxlb;
             o.mode = 0;
             o.spill_why = (st.n_lb << 8) | (st.heapSize << 20) | (st.inUsed & 0xff);
             atomicAdd(&p.counters[2], 1u);
@@ -1560,22 +1878,22 @@ struct Engine {
         return op;
     }
 
-    // Replay the doc's op log. Returns false if the LDS plan ran out of room (spill).
-    MTE_DEV bool replay() {
+    // Replay ops [i, end) of the doc's log. Returns the index of the first op not applied:
+    // end when done; earlier when the LDS plan ran out of room before that op (the document then
+    // continues HBM-resident from there) or on a failure (st.status).
+    MTE_DEV u64 replay_run(u64 i) {
 #ifdef MTE_PROFILE
         ProfScope _total(prof[PF_TOTAL]);
 #endif
-        init();
-        const u64 b = cfg.op_begin, e = cfg.op_end;
+        const u64 b = i, e = p.docs[doc].op_end;
         if (LDSM) {
             // op records are staged RING_OPS at a time through LDS; the next batch is prefetched
             // into registers one batch ahead (lane l holds 16 B of record l/2 of the batch).
             const uint4* src = (const uint4*)(p.ops);
-            uint4* dst = (uint4*)ring;
+            uint4* dst = (uint4*)RING();
             uint4 nxt = make_uint4(0, 0, 0, 0);
-            u64 g = b * 2 + L;
-            if (b + (L >> 1) < e) nxt = src[g];
-            for (u64 i = b; i < e && !st.status; i++) {
+            if (b + (L >> 1) < e) nxt = src[b * 2 + L];
+            for (; i < e && !st.status; i++) {
                 const u32 r = (u32)((i - b) & (RING_OPS - 1));
                 if (r == 0) {
                     sync();
@@ -1587,62 +1905,128 @@ struct Engine {
                 mte_op op;
                 {
                     MTE_PROF(PF_FETCH);
-                    op = read_op(ring + r);
+                    op = read_op(RING() + r);
                 }
+                if (!room()) break;
                 apply(op);
             }
         } else {
-            for (u64 i = b; i < e && !st.status; i++) {
+            for (; i < e && !st.status; i++) {
                 mte_op op = p.ops[i];
                 apply(op);
             }
         }
-        return st.status != DOC_SPILL;
+        return i;
+    }
+
+    // ---------------------------------------------------------------- continue HBM-resident
+    // Engine<false>: take a chunk of the spill pool for this document.
+    MTE_DEV bool bind_spill() {
+        const DocCfg& c = p.docs[doc];
+        u32 cb, co, ci, ch;
+        hbm_caps(c.op_end - c.op_begin, cb, co, ci, ch);
+        const HbmLayout l = HbmLayout::of(cb, co, ci, ch);
+        const u32 units = (u32)((l.bytes + 255) >> 8);
+        u32 off = 0;
+        if (L == 0) off = atomicAdd(&p.counters[3], units);
+        off = wave_read(off, 0);
+        if (((u64)off + units) * 256 > p.spill_cap) return false;
+        unsigned char* base = p.spill + (u64)off * 256;
+        m_vis = (uint4*)(base + l.vis);
+        m_aux = (uint4*)(base + l.aux);
+        m_bmeta = (u32*)(base + l.bmeta);
+        m_ord = (uint4*)(base + l.ord);
+        m_in_child = (u32*)(base + l.in_child);
+        m_in_cnt = (u32*)(base + l.in_cnt);
+        m_in_par = (u32*)(base + l.in_par);
+        m_heap = (uint2*)(base + l.heap);
+        m_scratch = (u32*)(base + l.scratch);
+        m_stats = m_scratch + 32;
+        m_blk_cap = cb;
+        m_ord_cap = co;
+        m_in_cap = ci;
+        m_heap_cap = ch;
+        return true;
+    }
+    // Engine<false>: copy an LDS-resident document's state (block ids, interior nodes, heap and
+    // counters unchanged; fresh block ids start above the LDS pool's).
+    template <class E>
+    MTE_DEV void adopt(const E& e) {
+        st = e.st;
+        st.lbBump = POOL_BLOCKS;
+        st.lbFree = NONE;
+        st.credit = 0;
+        const u32 g = L >> 3, s = L & 7;
+        for (u32 base = 0; base < st.n_lb; base += 8) {
+            const u32 k = base + g;
+            if (k < st.n_lb) {
+                const u32 blk = e.ORD()[k].x;
+                m_vis[blk * 8 + s] = e.VIS()[blk * 8 + s];
+                m_aux[blk * 8 + s] = e.AUX()[blk * 8 + s];
+                if (s == 0) m_bmeta[blk] = e.BMETA()[blk];
+            }
+        }
+        for (u32 k = L; k < st.n_lb; k += 64) m_ord[k] = e.ORD()[k];
+        for (u32 q = L; q < st.inBump * 8; q += 64) m_in_child[q] = e.INCH()[q];
+        for (u32 n = L; n < st.inBump; n += 64) {
+            m_in_cnt[n] = e.INCNT()[n];
+            m_in_par[n] = e.INPAR()[n];
+        }
+        for (u32 h = 1 + L; h <= st.heapSize; h += 64) m_heap[h] = e.HEAP()[h];
+        if (L < ST_WORDS) m_stats[L] = e.STATS()[L];
+        wave_sync();
     }
 
     // Synthetic workload generator: simulated writers draw valid ops from their own
     // view (getLength(refSeq, client)); each op is recorded into the doc's op/payload slots and
-    // applied immediately, so the recorded log is exactly what a replay will see.
-    // Returns false if the LDS plan ran out of room (the host regenerates the doc HBM-resident;
-    // the generator is deterministic per (doc, seed)).
-    MTE_DEV bool generate() {
-        init();
-        Rng rng;
-        u64 sx = 0xF1D0C0DEull ^ (u64)doc ^ (p.gen_seed * 0x9E3779B97F4A7C15ull);
-        rng.seed(sx);
-        const u32 nc = p.gen_nclients;
-        i32 ref[MTE_MAX_CLIENTS];
-        u32 sid_of[MTE_MAX_CLIENTS];
-        for (u32 c = 0; c < nc; c++) {
-            ref[c] = 0;
-            sid_of[c] = 0;
+    // applied immediately, so the recorded log is exactly what a replay will see. The writers'
+    // state lives in GenState so a document that leaves the LDS plan continues HBM-resident.
+    MTE_DEV void gen_init(GenState& g) const {
+        const u64 sx = 0xF1D0C0DEull ^ (u64)doc ^ (p.gen_seed * 0x9E3779B97F4A7C15ull);
+        g.rng.seed(sx);
+        for (u32 c = 0; c < MTE_MAX_CLIENTS; c++) {
+            g.ref[c] = 0;
+            g.sid_of[c] = 0;
         }
-        u32 nextShort = 1;
-        u32 pay = 0;
-        i32 lastC = -1, lastR = 0, lastPos = 0;
+        g.nextShort = 1;
+        g.pay = 0;
+        g.lastC = -1;
+        g.lastR = 0;
+        g.lastPos = 0;
+        g.step = 0;
+    }
+    // Returns true when every op was generated (or the doc failed), false when the LDS plan ran out
+    // of room before op g.step.
+    MTE_DEV bool generate_run(GenState& g) {
+        const u32 nc = p.gen_nclients;
         u32* firstSeen = p.gen_first_seen + (u64)doc * MTE_MAX_CLIENTS;
-        const u64 nops = cfg.op_end - cfg.op_begin;
-        for (u64 step = 0; step < nops && !st.status; step++) {
+        const u64 op0 = p.docs[doc].op_begin;
+        const u64 nops = p.docs[doc].op_end - op0;
+        for (; g.step < nops && !st.status; g.step++) {
+            if (!room()) return false;
+            const u64 step = g.step;
             const i32 seq = (i32)step + 1;
             const i32 cur = seq - 1;
+            // the draws below consume the generator in a fixed order (no early outs)
+            Rng rng = g.rng;
             const u32 c = rng.below(nc);
-            if (rng.below(4) == 0) ref[c] = cur;
+            if (rng.below(4) == 0) g.ref[c] = cur;
             else {
-                i32 nr = ref[c] + (i32)rng.below(5);
-                ref[c] = nr < cur ? nr : cur;
+                i32 nr = g.ref[c] + (i32)rng.below(5);
+                g.ref[c] = nr < cur ? nr : cur;
             }
-            if (p.gen_kind == 5 && ref[c] < cur - 64) ref[c] = cur - 64;
+            if (p.gen_kind == 5 && g.ref[c] < cur - 64) g.ref[c] = cur - 64;
             bool forced = false;
-            if (p.gen_kind == 3 && lastC >= 0 && (u32)lastC != c && rng.below(100) < 15 && lastR >= ref[c]) {
-                ref[c] = lastR;  // replay a recent other-client op's refSeq and position
+            if (p.gen_kind == 3 && g.lastC >= 0 && (u32)g.lastC != c && rng.below(100) < 15 && g.lastR >= g.ref[c]) {
+                g.ref[c] = g.lastR;  // replay a recent other-client op's refSeq and position
                 forced = true;
             }
-            if (sid_of[c] == 0) {
-                sid_of[c] = nextShort++;
-                if (L == 0) firstSeen[sid_of[c]] = c;
+            if (g.sid_of[c] == 0) {
+                g.sid_of[c] = g.nextShort++;
+                if (L == 0) firstSeen[g.sid_of[c]] = c;
             }
-            const u32 C = sid_of[c];
-            const i32 R = ref[c];
+            const u32 C = g.sid_of[c];
+            const i32 R = g.ref[c];
             const i32 len = get_length(R, C);
             const u32 roll = rng.below(100);
             u32 type;
@@ -1658,36 +2042,37 @@ struct Engine {
             op.b = 0;
             op.type = (uint8_t)type;
             if (type == MTE_OP_INSERT) {
-                const i32 pos = forced ? (lastPos < len ? lastPos : len) : (i32)rng.below((u32)len + 1);
+                const i32 pos = forced ? (g.lastPos < len ? g.lastPos : len) : (i32)rng.below((u32)len + 1);
                 const u32 n = 1 + rng.below(8);
                 op.pos1 = pos;
-                op.a = (i32)pay;
+                op.a = (i32)g.pay;
                 op.b = n;
                 for (u32 i = 0; i < n; i++) {
                     const u16 ch = (u16)(u'a' + rng.below(26));
-                    if (L == 0) payload[pay + i] = ch;
+                    if (L == 0) payload[g.pay + i] = ch;
                 }
-                pay += n;
+                g.pay += n;
                 st.adirty = 1;  // later cross-lane text copies read these chars
                 if (p.gen_kind == 3 && rng.below(4) == 0) op.props = 1 + rng.below(p.gen_n_propsets);
             } else {
-                const i32 a = forced ? (lastPos < len ? lastPos : len - 1) : (i32)rng.below((u32)len);
+                const i32 a = forced ? (g.lastPos < len ? g.lastPos : len - 1) : (i32)rng.below((u32)len);
                 const i32 n = 1 + (i32)rng.below(16);
                 op.pos1 = a;
                 op.a = a + n < len ? a + n : len;
                 if (type == MTE_OP_ANNOTATE) op.props = 1 + rng.below(p.gen_n_propsets);
             }
-            i32 msn = ref[0];
-            for (u32 q = 1; q < nc; q++) msn = ref[q] < msn ? ref[q] : msn;
+            i32 msn = g.ref[0];
+            for (u32 q = 1; q < nc; q++) msn = g.ref[q] < msn ? g.ref[q] : msn;
             op.msn = msn;
-            lastC = (i32)c;
-            lastR = R;
-            lastPos = op.pos1;
-            if (L == 0) p.ops[cfg.op_begin + step] = op;
+            g.lastC = (i32)c;
+            g.lastR = R;
+            g.lastPos = op.pos1;
+            g.rng = rng;
+            if (L == 0) p.ops[op0 + step] = op;
             apply(op);
         }
         wave_sync();  // op records and payload visible before the replay kernel
-        return st.status != DOC_SPILL;
+        return true;
     }
 };
 

@@ -18,7 +18,8 @@ constexpr u32 NONE = 0xFFFFFFFFu;
 constexpr u32 ARENA_BIT = 0x80000000u;
 constexpr u32 SC_UNDEF = 0, SC_TRUE = 1, SC_FALSE = 2;   // needsScour tri-state (mergeTree.ts:63)
 constexpr u32 F_REMOVED = 1u << 16, F_MARKER = 1u << 17;  // slot meta flags
-constexpr u32 F_OVL = 1u << 18;                          // removedClientOverlap non-empty (mask in HBM, by sid)
+constexpr u32 F_OVL = 1u << 18;    // removedClientOverlap non-empty: clients 0..31 in aux.z (dead tcap)
+constexpr u32 F_OVLHI = 1u << 19;  // ... and clients 32..63 in the HBM mask by segment id
 constexpr u32 MAP_WORDS = 16;                            // [0]=count, then 7 (key,val) pairs
 constexpr i32 GRANULARITY = 256;                         // TextSegmentGranularity (mergeTree.ts:1059)
 
@@ -37,6 +38,7 @@ constexpr u32 ORD_CAP = 128;       // leaf blocks per document while resident in
 constexpr u32 IN_CAP = 48;         // interior nodes per document while resident in LDS
 constexpr u32 HEAP_CAP = 191;      // LRU heap entries per document while resident in LDS
 constexpr u32 RING_OPS = 32;       // op records staged per wave (prefetched one batch ahead)
+constexpr u32 OP_CREDIT = 4;       // leaf blocks a wave holds in reserve before each op
 
 struct WaveRegion {
     uint4 ord[ORD_CAP];         // doc order: (block id, observer-visible length, max seq, child count)
@@ -46,12 +48,17 @@ struct WaveRegion {
     uint2 heap[HEAP_CAP + 1];   // 1-based binary heap of (segment id, maxSeq)
     mte_op ring[RING_OPS];
     u32 scratch[64];
+    u16 hint[256];              // LRU heap: segment id (mod 256) -> leaf block
+    u32 stats[8];               // per-document counters (engine.hpp ST_*)
 };
-constexpr u32 POOL_HDR = 64;  // 16-word allocation bitmap
+constexpr u32 ST_OPS = 0, ST_MSGS = 1, ST_GC = 2, ST_MAXLB = 3, ST_FAILSEQ = 4, ST_WORDS = 8;
+constexpr u32 POOL_HDR = 80;  // 16-word allocation bitmap + pool_avail
 constexpr u32 POOL_BLOCKS = ((LDS_BYTES - LDS_WAVES * (u32)sizeof(WaveRegion) - POOL_HDR - 16) / (8 * 32 + 4 + 1)) & ~3u;
 
 struct LdsPlan {
     u32 bitmap[16];              // 1 = block taken (or beyond the pool)
+    u32 pool_avail;              // blocks neither owned nor held as credit by any wave
+    u32 pool_pad[3];
     WaveRegion wave[LDS_WAVES];
     uint4 vis[POOL_BLOCKS * 8];  // len, seq, removedSeq, client | removedClient << 8 | flags
     uint4 aux[POOL_BLOCKS * 8];  // props map id, text offset, owned text capacity, segment id
@@ -130,7 +137,10 @@ struct Params {
     uint4* out_aux;
     u64* out_ovl;
     u64 out_cap;
-    u32* counters;            // [0] doc queue, [1] output rows, [2] spilled docs
+    u32* counters;            // [0] doc queue, [1] output rows, [2] docs re-run by the host,
+                              // [3] spill-pool bump (256-B units), [4] docs continued HBM-resident
+    unsigned char* spill;     // HBM chunks for documents that leave the LDS plan mid-replay
+    u64 spill_cap;
     u32 pool_limit;           // test knob: LDS leaf blocks usable per CU (0 = all)
     u64* prof;                // MTE_PROFILE builds: per doc PROF_SLOTS cycle counters
     // synthetic workload generator
@@ -143,7 +153,21 @@ struct Params {
 };
 
 // MTE_PROFILE builds: s_memtime cycles per engine phase, per document (engine.hpp PROF_*).
-constexpr u32 PROF_SLOTS = 16;
+constexpr u32 PROF_SLOTS = 24;
+
+// HBM-resident capacities of a document with n ops (leaf blocks hold >= 4 segments except
+// transiently; segments <= 2 per op + 1 without zamboni). Block ids below POOL_BLOCKS are the
+// LDS ids of a document that continued in HBM, fresh ids start above them.
+MTE_HOSTDEV_ void hbm_caps(u64 n, u32& blk, u32& ord, u32& in, u32& heap) {
+    u64 b = n / 2 + 64 + POOL_BLOCKS;
+    if (b > 0x3FFFFFF0ull) b = 0x3FFFFFF0ull;
+    blk = (u32)b;
+    ord = (u32)b;
+    u64 i = b / 2 + 64;
+    in = (u32)(i > 0x3FFFFFF0ull ? 0x3FFFFFF0ull : i);
+    u64 h = 2 * n + 64;
+    heap = (u32)(h > 0x3FFFFFF0ull ? 0x3FFFFFF0ull : h);
+}
 
 // HBM-mode state layout of one document (byte offsets from DocCfg::hb_off).
 struct HbmLayout {

@@ -213,14 +213,14 @@ struct mte_engine {
     DevBuf<DocCfg> d_cfg;
     DevBuf<DocRes> d_res;
     DevBuf<uint4> d_out_vis, d_out_aux;
-    DevBuf<unsigned char> d_hbm;
+    DevBuf<unsigned char> d_hbm, d_spill;
     std::vector<uint64_t> n_ops_doc;
     // options (mte_set_option)
     bool force_hbm = false;
     uint32_t pool_limit = 0;
     // last run
     double last_lds_ms = 0, last_hbm_ms = 0;
-    uint32_t last_spilled = 0;
+    uint32_t last_spilled = 0, last_continued = 0;
     uint32_t n_groups = 256;
     // downloaded final state
     std::vector<uint32_t> h_maps;
@@ -334,7 +334,16 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     HIP_TRY(e, e->d_out_vis.alloc(out));
     HIP_TRY(e, e->d_out_aux.alloc(out));
     HIP_TRY(e, e->d_out_ovl.alloc(out));
-    HIP_TRY(e, e->d_counters.alloc(4));
+    HIP_TRY(e, e->d_counters.alloc(8));
+    // spill pool: HBM chunks for documents that leave the LDS plan mid-replay (device-allocated)
+    uint64_t spill = 0;
+    for (uint32_t d = 0; d < nd; d++) {
+        uint32_t cb, co, ci, ch;
+        hbm_caps(n_ops[d], cb, co, ci, ch);
+        spill += (HbmLayout::of(cb, co, ci, ch).bytes + 255) & ~255ull;
+    }
+    spill = std::min<uint64_t>(spill, 4ull << 30);
+    HIP_TRY(e, e->d_spill.alloc(spill));
     HIP_TRY(e, e->d_res.alloc(nd));
     HIP_TRY(e, e->d_prof.alloc((size_t)nd * PROF_SLOTS));
     HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, (size_t)nd * PROF_SLOTS * 8, e->stream));
@@ -361,6 +370,8 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     P.out_cap = out;
     P.counters = e->d_counters.p;
     P.prof = e->d_prof.p;
+    P.spill = e->d_spill.p;
+    P.spill_cap = spill;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || cus <= 0) cus = 256;
     e->n_groups = (uint32_t)cus;
@@ -480,12 +491,8 @@ int mte_load(mte_engine* e, const mte_batch* b) {
 
 // HBM-resident capacities for a document that outgrew the LDS plan (blocks hold >= 4 segments
 // except transiently; segments <= 2 per op + 1 without zamboni).
-static void hbm_caps(uint64_t n, DocCfg& c, uint64_t& bytes) {
-    uint64_t blk = std::min<uint64_t>(n / 2 + 64 + POOL_BLOCKS, 0x3FFFFFF0ull);
-    c.hb_blk = (uint32_t)blk;
-    c.hb_ord = (uint32_t)blk;
-    c.hb_in = (uint32_t)std::min<uint64_t>(blk / 2 + 64, 0x3FFFFFF0ull);
-    c.hb_heap = (uint32_t)std::min<uint64_t>(2 * n + 64, 0x3FFFFFF0ull);
+static void doc_hbm_caps(uint64_t n, DocCfg& c, uint64_t& bytes) {
+    hbm_caps(n, c.hb_blk, c.hb_ord, c.hb_in, c.hb_heap);
     bytes = HbmLayout::of(c.hb_blk, c.hb_ord, c.hb_in, c.hb_heap).bytes;
 }
 
@@ -495,7 +502,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     e->P.pool_limit = e->pool_limit;
     e->P.doc_list = e->d_order.p;
     e->P.n_list = nd;
-    HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 4 * sizeof(uint32_t), e->stream));
+    HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 8 * sizeof(uint32_t), e->stream));
     HIP_TRY(e, hipEventRecord(e->ev0, e->stream));
     std::vector<uint32_t> spill;
     float lds_ms = 0, hbm_ms = 0;
@@ -510,6 +517,9 @@ static int run_kernel(mte_engine* e, bool gen) {
         HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nd * sizeof(DocRes), hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < nd; i++)
             if (e->res[e->order[i]].status == DOC_SPILL) spill.push_back(e->order[i]);
+        uint32_t ctr[8];
+        HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
+        e->last_continued = ctr[4];
     } else {
         spill = e->order;
     }
@@ -519,7 +529,7 @@ static int run_kernel(mte_engine* e, bool gen) {
         uint64_t total = 0;
         for (uint32_t d : spill) {
             uint64_t bytes;
-            hbm_caps(e->n_ops_doc[d], e->cfg[d], bytes);
+            doc_hbm_caps(e->n_ops_doc[d], e->cfg[d], bytes);
             e->cfg[d].hb_off = total;
             total += (bytes + 255) & ~255ull;
         }
@@ -678,7 +688,7 @@ static int ensure_download(mte_engine* e) {
     int rc = ensure_host_ops(e);
     if (rc) return rc;
     HIP_TRY(e, hipSetDevice(e->device));
-    uint32_t ctr[4];
+    uint32_t ctr[8];
     HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
     const uint64_t rows = std::min<uint64_t>(ctr[1], e->P.out_cap);
     auto dl = [&](auto& h, auto& d, size_t n) -> int {
@@ -1111,9 +1121,11 @@ int mte_doc_result(mte_engine* e, uint32_t doc, void* out, size_t sz) {
 }
 // Diagnostics of the last replay/generate: documents that outgrew the LDS plan and ran the
 // HBM-resident pass, and the two passes' kernel times.
-int mte_run_info(mte_engine* e, uint32_t* spilled, double* lds_ms, double* hbm_ms, uint64_t* out_rows) {
+int mte_run_info(mte_engine* e, uint32_t* spilled, double* lds_ms, double* hbm_ms, uint64_t* out_rows,
+                 uint32_t* continued) {
     if (!e) return MTE_E_ARG;
-    uint32_t ctr[4] = {0, 0, 0, 0};
+    if (continued) *continued = e->last_continued;
+    uint32_t ctr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (e->d_counters.p) HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
     if (spilled) *spilled = e->last_spilled;
     if (lds_ms) *lds_ms = e->last_lds_ms;

@@ -14,9 +14,9 @@ namespace mte {
 
 template <bool GEN>
 __global__ __launch_bounds__(64 * LDS_WAVES) void k_lds(Params p) {
-    __shared__ __attribute__((aligned(16))) unsigned char raw[sizeof(LdsPlan)];
-    LdsPlan* lp = (LdsPlan*)raw;
-    const u32 t = threadIdx.x, w = t >> 6, L = t & 63;
+    LdsPlan* lp = &g_plan;
+    const u32 t = threadIdx.x, L = t & 63;
+    const u32 w = wave_first(t >> 6);  // wave-uniform (the compiler cannot infer it from threadIdx)
     u32 usable = POOL_BLOCKS;
     if (p.pool_limit && p.pool_limit < usable) usable = p.pool_limit;
     if (t < 16) {
@@ -27,6 +27,7 @@ __global__ __launch_bounds__(64 * LDS_WAVES) void k_lds(Params p) {
         lp->bitmap[t] = word;
     }
     for (u32 b = t; b < POOL_BLOCKS; b += 64 * LDS_WAVES) lp->owner[b] = 0xFF;
+    if (t == 0) lp->pool_avail = usable;
     __syncthreads();
     for (;;) {
         u32 i = 0;
@@ -35,10 +36,40 @@ __global__ __launch_bounds__(64 * LDS_WAVES) void k_lds(Params p) {
         if (i >= p.n_list) break;
         const u32 d = p.doc_list[i];
         Engine<true> e(p, d);
-        e.bind_lds(lp, w);
-        const bool fits = GEN ? e.generate() : e.replay();
-        if (fits) e.finish();
-        else e.mark_spilled();
+        e.bind_lds(w);
+        GenState g;
+        bool done;
+        u64 at = 0;
+        e.init();
+        if (GEN) {
+            e.gen_init(g);
+            done = e.generate_run(g);
+        } else {
+            at = e.replay_run(p.docs[d].op_begin);
+            done = at >= p.docs[d].op_end;
+        }
+        if (e.st.status == DOC_SPILL) {
+            e.mark_spilled();  // failed mid-op: the host re-runs it (rare)
+        } else if (!done && e.st.status == 0) {
+            // the LDS plan ran out of room between two ops: continue HBM-resident, same wave
+            Engine<false> h(p, d);
+            h.continued = true;
+            if (h.bind_spill()) {
+                h.adopt(e);
+                e.release();
+                if (L == 0) atomicAdd(&p.counters[4], 1u);
+                if (GEN) {
+                    h.generate_run(g);
+                } else {
+                    h.replay_run(at);
+                }
+                h.finish();
+            } else {
+                e.mark_spilled();
+            }
+        } else {
+            e.finish();
+        }
         e.release();
     }
 }
@@ -48,8 +79,14 @@ __global__ __launch_bounds__(64) void k_hbm(Params p) {
     const u32 d = p.doc_list[blockIdx.x];
     Engine<false> e(p, d);
     e.bind_hbm();
-    if (GEN) e.generate();
-    else e.replay();
+    e.init();
+    if (GEN) {
+        GenState g;
+        e.gen_init(g);
+        e.generate_run(g);
+    } else {
+        e.replay_run(p.docs[d].op_begin);
+    }
     e.finish();
 }
 

@@ -16,7 +16,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MTE_LIB=prof selects the phase-profiling build (csrc/Makefile `prof`, engine.hpp MTE_PROFILE)
 LIB_PATH = os.path.join(_HERE, "_build", "prof" if os.environ.get("MTE_LIB") == "prof" else "", "libmte.so")
 PROF_NAMES = ["apply", "resolve", "insert_slot", "range", "zamboni", "scour", "heap", "find_seg", "map", "pack",
-              "fetch", "lru", "text", "alloc", "ops", "total"]
+              "fetch", "lru", "text", "alloc", "ops", "total",
+              "n_resolve", "n_dirty", "n_scour", "n_scour_changed", "n_pack", "n_pop", "n_push", "n_split_blk"]
 
 MTE_OP_INSERT, MTE_OP_REMOVE, MTE_OP_ANNOTATE, MTE_OP_INSERT_MARKER, MTE_OP_NOOP = 0, 1, 2, 3, 4
 MTE_F_END_OF_MSG, MTE_F_REWRITE = 1, 2
@@ -106,7 +107,7 @@ def lib():
         L.mte_summaries.argtypes = [vp, ctypes.c_void_p, sz]
         L.mte_doc_result.argtypes = [vp, u32, ctypes.c_void_p, sz]
         L.mte_run_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_double),
-                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64)]
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.mte_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
         L.mte_profile.argtypes = [vp, ctypes.c_void_p, sz]
         L.mte_wave_selftest.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, u32]
@@ -251,10 +252,11 @@ class Engine:
 
     def run_info(self):
         """Last replay/generate: docs that outgrew the LDS plan (re-run HBM-resident) and pass times."""
-        sp, a, b, rows = ctypes.c_uint32(), ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+        sp, a, b, rows, co = ctypes.c_uint32(), ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint32()
         self._check(lib().mte_run_info(self._h, ctypes.byref(sp), ctypes.byref(a), ctypes.byref(b),
-                                       ctypes.byref(rows)), "mte_run_info")
-        return {"spilled": sp.value, "lds_ms": a.value, "hbm_ms": b.value, "out_rows": rows.value}
+                                       ctypes.byref(rows), ctypes.byref(co)), "mte_run_info")
+        return {"spilled": sp.value, "continued": co.value, "lds_ms": a.value, "hbm_ms": b.value,
+                "out_rows": rows.value}
 
     def profile(self):
         """Per-doc phase cycle counters (MTE_LIB=prof build), shape (n_docs, len(PROF_NAMES))."""

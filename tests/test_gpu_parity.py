@@ -197,8 +197,9 @@ def test_hbm_resident_pass_matches_lds_pass(engine):
 
 
 def test_lds_pool_exhaustion_spills_and_matches_oracle(engine):
-    """A tiny LDS block pool forces documents out of the LDS plan mid-replay; the host re-runs them
-    HBM-resident and every document still matches the oracle."""
+    """A tiny LDS block pool forces documents out of the LDS plan mid-replay: between ops they move
+    to HBM and continue in the same wave, mid-op failures are re-run by the host; every document
+    still matches the oracle."""
     engine.generate(2, 128, 3000, n_clients=8, seed=5)
     batch = engine.export_batch()
     engine.set_option("pool_limit", 48)
@@ -207,8 +208,37 @@ def test_lds_pool_exhaustion_spills_and_matches_oracle(engine):
         info = engine.run_info()
     finally:
         engine.set_option("pool_limit", 0)
-    assert info["spilled"] > 0, info
+    assert info["spilled"] + info["continued"] > 0, info
     bad, _, _ = compare_batch_checksums(engine, batch)
     if bad:
         compare_doc(engine, batch, bad[0])
     assert not bad
+
+
+def test_many_clients_overlap_masks_match_oracle(engine):
+    """48 writers: overlapping removes by clients >= 32 take the HBM half of the overlap mask."""
+    engine.generate(3, 48, 2500, n_clients=48, seed=21)
+    batch = engine.export_batch()
+    engine.replay()
+    bad, _, _ = compare_batch_checksums(engine, batch)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad
+    for d in range(0, 48, 12):
+        compare_doc(engine, batch, d)
+
+
+def test_generator_continues_hbm_resident(engine):
+    """Generation under a tiny LDS pool hands documents to HBM mid-log; the log recorded must be
+    the same as the one generated entirely in LDS (the generator is deterministic)."""
+    engine.generate(2, 64, 2000, n_clients=8, seed=4)
+    ref = mte.batch_ops(engine.export_batch()).copy()
+    engine.set_option("pool_limit", 40)
+    try:
+        engine.generate(2, 64, 2000, n_clients=8, seed=4)
+        info = engine.run_info()
+    finally:
+        engine.set_option("pool_limit", 0)
+    assert info["continued"] + info["spilled"] > 0, info
+    got = mte.batch_ops(engine.export_batch())
+    assert np.array_equal(ref, got)

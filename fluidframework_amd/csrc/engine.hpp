@@ -24,7 +24,8 @@
 namespace mte {
 
 // The LDS of the replay kernel: one plan per CU (k_lds declares nothing else).
-__shared__ LdsPlan g_plan;
+extern __shared__ uint4 g_lds_dyn[];  // LdsPlan, dynamic (so waves_per_eu bounds VGPRs)
+#define g_plan (*reinterpret_cast<LdsPlan*>(g_lds_dyn))
 
 // Phase profiling (compile with -DMTE_PROFILE): inclusive s_memtime cycles per phase.
 enum ProfSlot : u32 {
@@ -227,10 +228,8 @@ struct Engine {
         if (L < ST_WORDS) STATS()[L] = L == ST_FAILSEQ ? NONE : 0u;
         lds_order();
     }
-    MTE_DEV void bind_hbm() {
-        const DocCfg& c = p.docs[doc];
-        HbmLayout l = HbmLayout::of(c.hb_blk, c.hb_ord, c.hb_in, c.hb_heap);
-        unsigned char* b = p.hbm + c.hb_off;
+    MTE_DEV void bind_region(unsigned char* b, u32 cb, u32 co, u32 ci, u32 ch) {
+        const HbmLayout l = HbmLayout::of(cb, co, ci, ch);
         m_vis = (uint4*)(b + l.vis);
         m_aux = (uint4*)(b + l.aux);
         m_bmeta = (u32*)(b + l.bmeta);
@@ -241,12 +240,24 @@ struct Engine {
         m_heap = (uint2*)(b + l.heap);
         m_scratch = (u32*)(b + l.scratch);
         m_stats = m_scratch + 32;
-        m_blk_cap = c.hb_blk;
-        m_ord_cap = c.hb_ord;
-        m_in_cap = c.hb_in;
-        m_heap_cap = c.hb_heap;
+        m_blk_cap = cb;
+        m_ord_cap = co;
+        m_in_cap = ci;
+        m_heap_cap = ch;
+    }
+    MTE_DEV void reset_stats() {
         if (L < ST_WORDS) m_stats[L] = L == ST_FAILSEQ ? NONE : 0u;
         wave_sync();
+    }
+    // per-document HBM state laid out by the host (re-run of a document that failed mid-op)
+    MTE_DEV void bind_hbm() {
+        const DocCfg& c = p.docs[doc];
+        bind_region(p.hbm + c.hb_off, c.hb_blk, c.hb_ord, c.hb_in, c.hb_heap);
+        reset_stats();
+    }
+    // a wave's own HBM slot (Params::slot_*), reused by every document the wave takes over
+    MTE_DEV void bind_slot(u32 slot) {
+        bind_region(p.spill + (u64)slot * p.slot_bytes, p.slot_blk, p.slot_ord, p.slot_in, p.slot_heap);
     }
 
     // Wave-uniform reads: a load from a uniform address is broadcast through readfirstlane so the
@@ -1920,34 +1931,6 @@ struct Engine {
     }
 
     // ---------------------------------------------------------------- continue HBM-resident
-    // Engine<false>: take a chunk of the spill pool for this document.
-    MTE_DEV bool bind_spill() {
-        const DocCfg& c = p.docs[doc];
-        u32 cb, co, ci, ch;
-        hbm_caps(c.op_end - c.op_begin, cb, co, ci, ch);
-        const HbmLayout l = HbmLayout::of(cb, co, ci, ch);
-        const u32 units = (u32)((l.bytes + 255) >> 8);
-        u32 off = 0;
-        if (L == 0) off = atomicAdd(&p.counters[3], units);
-        off = wave_read(off, 0);
-        if (((u64)off + units) * 256 > p.spill_cap) return false;
-        unsigned char* base = p.spill + (u64)off * 256;
-        m_vis = (uint4*)(base + l.vis);
-        m_aux = (uint4*)(base + l.aux);
-        m_bmeta = (u32*)(base + l.bmeta);
-        m_ord = (uint4*)(base + l.ord);
-        m_in_child = (u32*)(base + l.in_child);
-        m_in_cnt = (u32*)(base + l.in_cnt);
-        m_in_par = (u32*)(base + l.in_par);
-        m_heap = (uint2*)(base + l.heap);
-        m_scratch = (u32*)(base + l.scratch);
-        m_stats = m_scratch + 32;
-        m_blk_cap = cb;
-        m_ord_cap = co;
-        m_in_cap = ci;
-        m_heap_cap = ch;
-        return true;
-    }
     // Engine<false>: copy an LDS-resident document's state (block ids, interior nodes, heap and
     // counters unchanged; fresh block ids start above the LDS pool's).
     template <class E>

@@ -138,9 +138,15 @@ struct Params {
     u64* out_ovl;
     u64 out_cap;
     u32* counters;            // [0] doc queue, [1] output rows, [2] docs re-run by the host,
-                              // [3] spill-pool bump (256-B units), [4] docs continued HBM-resident
-    unsigned char* spill;     // HBM chunks for documents that leave the LDS plan mid-replay
-    u64 spill_cap;
+                              // [3] unused, [4] docs continued HBM-resident
+    unsigned char* spill;     // per-wave HBM slots (slot_bytes each): LDS waves 0..8G-1 keep theirs for
+                              // documents that outgrow the LDS plan, HBM waves use slot_hbm0 + blockIdx
+    u64 slot_bytes;
+    u32 slot_blk, slot_ord, slot_in, slot_heap;  // capacities of a slot (hbm_caps of the longest doc)
+    u32 slot_hbm0;            // first slot of the k_hbmq waves (after the LDS waves' slots)
+    u32* slot_bits;           // k_hbmq slot bitmap (n_hslots bits, 1 = held)
+    u32 n_hslots;
+    u32 pad2;
     u32 pool_limit;           // test knob: LDS leaf blocks usable per CU (0 = all)
     u64* prof;                // MTE_PROFILE builds: per doc PROF_SLOTS cycle counters
     // synthetic workload generator

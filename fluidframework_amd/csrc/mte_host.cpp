@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/mte.h"
+#include "../../include/mte_diag.h"
 #include "engine_types.hpp"
 #include "jsonlite.hpp"
 #include "mte_kernels.h"
@@ -183,8 +184,8 @@ struct mte_builder {
 struct mte_engine {
     int device = 0;
     uint32_t chunk = 10000;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipStream_t stream = nullptr, stream2 = nullptr;  // stream2: the HBM-resident waves (k_hbmq)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     std::string err;
     HostBatch hb;
     bool generated = false;    // ops/payload live on the device; host copy filled on demand
@@ -214,13 +215,18 @@ struct mte_engine {
     DevBuf<DocRes> d_res;
     DevBuf<uint4> d_out_vis, d_out_aux;
     DevBuf<unsigned char> d_hbm, d_spill;
+    DevBuf<uint32_t> d_slot_bits;
     std::vector<uint64_t> n_ops_doc;
     // options (mte_set_option)
-    bool force_hbm = false;
+    bool force_hbm = false;           // no LDS-resident waves: every document HBM-resident
     uint32_t pool_limit = 0;
+    uint32_t hbm_waves_per_cu = 8;    // HBM-resident waves (slots) per CU beside the LDS workgroup (2 per SIMD)
+    uint64_t slot_budget = 48ull << 30;  // HBM for per-wave slots
+    // per-wave slot plan (layout_and_alloc)
+    uint32_t n_slots = 0;
     // last run
     double last_lds_ms = 0, last_hbm_ms = 0;
-    uint32_t last_spilled = 0, last_continued = 0;
+    uint32_t last_spilled = 0, last_continued = 0, last_hbm_docs = 0, last_hbm_waves = 0, last_lds_groups = 0;
     uint32_t n_groups = 256;
     // downloaded final state
     std::vector<uint32_t> h_maps;
@@ -293,6 +299,8 @@ static int upload(mte_engine* e, DevBuf<T>& d, const std::vector<T>& h) {
     return MTE_OK;
 }
 
+static int alloc_slots(mte_engine* e);
+
 // Per-document arena sizing (see DESIGN.md "HBM layout").
 static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, const std::vector<uint64_t>& pay_len,
                             const std::vector<uint64_t>& n_prop_ins, const std::vector<uint64_t>& n_ann,
@@ -335,15 +343,6 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     HIP_TRY(e, e->d_out_aux.alloc(out));
     HIP_TRY(e, e->d_out_ovl.alloc(out));
     HIP_TRY(e, e->d_counters.alloc(8));
-    // spill pool: HBM chunks for documents that leave the LDS plan mid-replay (device-allocated)
-    uint64_t spill = 0;
-    for (uint32_t d = 0; d < nd; d++) {
-        uint32_t cb, co, ci, ch;
-        hbm_caps(n_ops[d], cb, co, ci, ch);
-        spill += (HbmLayout::of(cb, co, ci, ch).bytes + 255) & ~255ull;
-    }
-    spill = std::min<uint64_t>(spill, 4ull << 30);
-    HIP_TRY(e, e->d_spill.alloc(spill));
     HIP_TRY(e, e->d_res.alloc(nd));
     HIP_TRY(e, e->d_prof.alloc((size_t)nd * PROF_SLOTS));
     HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, (size_t)nd * PROF_SLOTS * 8, e->stream));
@@ -370,11 +369,46 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     P.out_cap = out;
     P.counters = e->d_counters.p;
     P.prof = e->d_prof.p;
-    P.spill = e->d_spill.p;
-    P.spill_cap = spill;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || cus <= 0) cus = 256;
     e->n_groups = (uint32_t)cus;
+    // per-wave HBM slots, each sized for the longest document (hbm_caps)
+    uint64_t nmax = 0;
+    for (uint32_t d = 0; d < nd; d++) nmax = std::max<uint64_t>(nmax, n_ops[d]);
+    hbm_caps(nmax, P.slot_blk, P.slot_ord, P.slot_in, P.slot_heap);
+    P.slot_bytes = (HbmLayout::of(P.slot_blk, P.slot_ord, P.slot_in, P.slot_heap).bytes + 255) & ~255ull;
+    return alloc_slots(e);
+}
+
+// Wave plan of a replay: G LDS workgroups (LDS_WAVES waves each, one per CU) plus up to H
+// HBM-resident waves at a time (k_hbmq, one document per wave, H slots), or HBM-resident waves
+// alone when the LDS plan is off or the slots for its waves do not fit the budget. Every LDS wave
+// owns a slot for a document that outgrows the plan.
+static void wave_plan(const mte_engine* e, uint32_t nd, uint32_t& groups, uint32_t& hbm_waves) {
+    const uint64_t max_slots = std::max<uint64_t>(1, e->slot_budget / std::max<uint64_t>(e->P.slot_bytes, 1));
+    groups = std::min<uint32_t>(e->n_groups, (nd + LDS_WAVES - 1) / LDS_WAVES);
+    if (e->force_hbm || (uint64_t)groups * LDS_WAVES > max_slots) groups = 0;
+    // 16 = 4 SIMDs x 4 waves at <= 128 VGPRs (k_hbmq's bound): more can never be resident at once
+    const uint32_t per_cu = groups ? std::min<uint32_t>(e->hbm_waves_per_cu, 16) : 16;
+    uint64_t h = (uint64_t)per_cu * e->n_groups;
+    h = std::min<uint64_t>(h, max_slots - (uint64_t)groups * LDS_WAVES);
+    if (nd > (uint64_t)groups * LDS_WAVES) h = std::min<uint64_t>(h, nd - (uint64_t)groups * LDS_WAVES);
+    else h = 0;
+    if (groups == 0 && h == 0) h = 1;
+    hbm_waves = (uint32_t)h;
+}
+
+static int alloc_slots(mte_engine* e) {
+    uint32_t g, h;
+    wave_plan(e, e->P.n_docs, g, h);
+    const uint32_t n = g * LDS_WAVES + h;
+    const size_t bytes = (size_t)n * e->P.slot_bytes;
+    if (bytes > e->d_spill.n || !e->d_spill.p) HIP_TRY(e, e->d_spill.alloc(bytes));
+    const size_t words = (h + 31) / 32 + 1;
+    if (words > e->d_slot_bits.n || !e->d_slot_bits.p) HIP_TRY(e, e->d_slot_bits.alloc(words));
+    e->n_slots = n;
+    e->P.spill = e->d_spill.p;
+    e->P.slot_bits = e->d_slot_bits.p;
     return MTE_OK;
 }
 
@@ -426,6 +460,8 @@ int mte_create(const mte_config* cfg, mte_engine** out) {
     }
     HIP_TRY(e.get(), hipSetDevice(e->device));
     HIP_TRY(e.get(), hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    HIP_TRY(e.get(), hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+    HIP_TRY(e.get(), hipEventCreateWithFlags(&e->ev2, hipEventDisableTiming));
     HIP_TRY(e.get(), hipEventCreate(&e->ev0));
     HIP_TRY(e.get(), hipEventCreate(&e->ev1));
     *out = e.release();
@@ -438,6 +474,8 @@ void mte_destroy(mte_engine* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
+    if (e->ev2) (void)hipEventDestroy(e->ev2);
+    if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -502,28 +540,44 @@ static int run_kernel(mte_engine* e, bool gen) {
     e->P.pool_limit = e->pool_limit;
     e->P.doc_list = e->d_order.p;
     e->P.n_list = nd;
+    int rc;
+    if ((rc = alloc_slots(e))) return rc;  // options may have changed the wave plan
+    uint32_t groups, hbm_waves;
+    wave_plan(e, nd, groups, hbm_waves);
+    e->P.slot_hbm0 = groups * LDS_WAVES;
+    e->P.n_hslots = hbm_waves;
     HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 8 * sizeof(uint32_t), e->stream));
+    HIP_TRY(e, hipMemsetAsync(e->d_slot_bits.p, 0, e->d_slot_bits.n * sizeof(uint32_t), e->stream));
     HIP_TRY(e, hipEventRecord(e->ev0, e->stream));
     std::vector<uint32_t> spill;
     float lds_ms = 0, hbm_ms = 0;
-    if (!e->force_hbm) {
-        uint32_t groups = std::min<uint32_t>(e->n_groups, (nd + LDS_WAVES - 1) / LDS_WAVES);
-        if (groups == 0) groups = 1;
-        HIP_TRY(e, launch_lds(e->P, gen, groups, e->stream));
-        HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
-        HIP_TRY(e, hipStreamSynchronize(e->stream));
-        HIP_TRY(e, hipEventElapsedTime(&lds_ms, e->ev0, e->ev1));
-        e->res.resize(nd);
-        HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nd * sizeof(DocRes), hipMemcpyDeviceToHost));
-        for (uint32_t i = 0; i < nd; i++)
-            if (e->res[e->order[i]].status == DOC_SPILL) spill.push_back(e->order[i]);
-        uint32_t ctr[8];
-        HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
-        e->last_continued = ctr[4];
-    } else {
-        spill = e->order;
+    // pass 1: LDS workgroups first (one per CU, all of its LDS), then the HBM-resident waves on the
+    // second stream so they fill every CU's remaining wave slots; both drain one document queue
+    if (groups) HIP_TRY(e, launch_lds(e->P, gen, groups, e->stream));
+    // k_hbmq: one workgroup (wave) per document; those that find the queue drained exit at once
+    if (hbm_waves && !groups) {
+        HIP_TRY(e, launch_hbmq(e->P, gen, nd, e->stream));
+    } else if (hbm_waves) {
+        HIP_TRY(e, hipStreamWaitEvent(e->stream2, e->ev0, 0));
+        HIP_TRY(e, launch_hbmq(e->P, gen, nd, e->stream2));
+        HIP_TRY(e, hipEventRecord(e->ev2, e->stream2));
+        HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev2, 0));
     }
-    e->last_spilled = e->force_hbm ? 0 : (uint32_t)spill.size();
+    HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    HIP_TRY(e, hipEventElapsedTime(&lds_ms, e->ev0, e->ev1));
+    e->res.resize(nd);
+    HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nd * sizeof(DocRes), hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < nd; i++)
+        if (e->res[e->order[i]].status == DOC_SPILL) spill.push_back(e->order[i]);
+    uint32_t ctr[8];
+    HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
+    e->last_continued = ctr[4];
+    e->last_hbm_docs = 0;
+    for (uint32_t i = 0; i < nd; i++) e->last_hbm_docs += e->res[i].mode == 1;
+    e->last_hbm_waves = hbm_waves;
+    e->last_lds_groups = groups;
+    e->last_spilled = (uint32_t)spill.size();
     if (!spill.empty()) {
         // second pass: the spilled documents, HBM-resident, one wave each, longest first
         uint64_t total = 0;
@@ -534,7 +588,6 @@ static int run_kernel(mte_engine* e, bool gen) {
             total += (bytes + 255) & ~255ull;
         }
         HIP_TRY(e, e->d_hbm.alloc(total));
-        int rc;
         if ((rc = upload(e, e->d_cfg, e->cfg))) return rc;
         if ((rc = upload(e, e->d_list, spill))) return rc;
         e->P.docs = e->d_cfg.p;
@@ -1142,14 +1195,32 @@ int mte_profile(mte_engine* e, uint64_t* out, size_t cap) {
     HIP_TRY(e, hipMemcpy(out, e->d_prof.p, n * 8, hipMemcpyDeviceToHost));
     return MTE_OK;
 }
-// Engine options (tests / tuning): "force_hbm" (1 = skip the LDS pass), "pool_limit" (LDS leaf
-// blocks usable per CU; 0 = all).
+// Engine options (tests / tuning): "force_hbm" (1 = HBM-resident waves only), "pool_limit" (LDS
+// leaf blocks usable per CU; 0 = all), "hbm_waves_per_cu" (HBM-resident waves beside each LDS
+// workgroup; 0 = LDS waves only), "slot_budget_mb" (HBM for per-wave slots).
 int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     if (!e || !key) return MTE_E_ARG;
     std::string k(key);
     if (k == "force_hbm") e->force_hbm = value != 0;
     else if (k == "pool_limit") e->pool_limit = (uint32_t)std::max<int64_t>(0, value);
+    else if (k == "hbm_waves_per_cu") e->hbm_waves_per_cu = (uint32_t)std::min<int64_t>(std::max<int64_t>(0, value), 32);
+    else if (k == "slot_budget_mb") e->slot_budget = (uint64_t)std::max<int64_t>(1, value) << 20;
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
+    return MTE_OK;
+}
+// Wave plan and routing of the last run: "lds_groups", "hbm_waves", "hbm_docs" (documents taken by
+// HBM-resident waves), "continued", "spilled", "slot_bytes", "slots".
+int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
+    if (!e || !key || !value) return MTE_E_ARG;
+    std::string k(key);
+    if (k == "lds_groups") *value = e->last_lds_groups;
+    else if (k == "hbm_waves") *value = e->last_hbm_waves;
+    else if (k == "hbm_docs") *value = e->last_hbm_docs;
+    else if (k == "continued") *value = e->last_continued;
+    else if (k == "spilled") *value = e->last_spilled;
+    else if (k == "slot_bytes") *value = (int64_t)e->P.slot_bytes;
+    else if (k == "slots") *value = e->n_slots;
+    else return set_err(e, MTE_E_ARG, "unknown info key " + k);
     return MTE_OK;
 }
 int mte_wave_selftest(mte_engine* e, const uint32_t* in, uint32_t* out, uint32_t n_waves) {

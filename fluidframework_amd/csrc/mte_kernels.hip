@@ -3,9 +3,12 @@
 //   k_lds<GEN>: ONE workgroup per CU, LDS_WAVES waves, all 160 KiB of LDS (engine_types.hpp LdsPlan).
 //               Waves pull documents from a queue in LPT order (longest first) and replay
 //               (or generate) each with the whole per-document state resident in LDS. A document
-//               that outgrows the plan is marked DOC_SPILL and its blocks go back to the CU's pool.
+//               that outgrows the plan between two ops continues HBM-resident in the wave's own
+//               HBM slot; one that fails mid-op is marked DOC_SPILL for the host's re-run.
+//   k_hbmq<GEN>: one wave per document taken from the same queue, state HBM-resident in a slot
+//               from a bitmap, co-resident with k_lds on every CU (second stream).
 //   k_hbm<GEN>: one wave per listed document, state resident in HBM (DocCfg::hb_*): the host's
-//               second pass for spilled documents.
+//               re-run of DOC_SPILL documents.
 #include "wave_hip.hpp"
 #include "engine.hpp"
 #include "mte_kernels.h"
@@ -13,7 +16,7 @@
 namespace mte {
 
 template <bool GEN>
-__global__ __launch_bounds__(64 * LDS_WAVES) void k_lds(Params p) {
+__global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void k_lds(Params p) {
     LdsPlan* lp = &g_plan;
     const u32 t = threadIdx.x, L = t & 63;
     const u32 w = wave_first(t >> 6);  // wave-uniform (the compiler cannot infer it from threadIdx)
@@ -54,24 +57,92 @@ __global__ __launch_bounds__(64 * LDS_WAVES) void k_lds(Params p) {
             // the LDS plan ran out of room between two ops: continue HBM-resident, same wave
             Engine<false> h(p, d);
             h.continued = true;
-            if (h.bind_spill()) {
-                h.adopt(e);
-                e.release();
-                if (L == 0) atomicAdd(&p.counters[4], 1u);
-                if (GEN) {
-                    h.generate_run(g);
-                } else {
-                    h.replay_run(at);
-                }
-                h.finish();
+            h.bind_slot(blockIdx.x * LDS_WAVES + w);
+            h.adopt(e);
+            e.release();
+            if (L == 0) atomicAdd(&p.counters[4], 1u);
+            if (GEN) {
+                h.generate_run(g);
             } else {
-                e.mark_spilled();
+                h.replay_run(at);
             }
+            h.finish();
         } else {
             e.finish();
         }
         e.release();
     }
+}
+
+// HBM slot of a k_hbmq wave: a free bit of the slot bitmap (cleared by the host before each run).
+// At most n_hslots waves of k_hbmq are resident at once (the host sizes it from the occupancy
+// bound), so a search finds a free slot unless slots are budget-limited; then the wave waits for
+// a holder to finish its document.
+MTE_DEV u32 acquire_hslot(const Params& p) {
+    const u32 L = lane_id();
+    const u32 nw = (p.n_hslots + 31) >> 5;
+    const u32 start = blockIdx.x % nw;
+    for (;;) {
+        for (u32 base = 0; base < nw; base += 64) {
+            const u32 w = (start + base + L) % nw;
+            u32 word = 0xFFFFFFFFu;
+            if (base + L < nw) {
+                word = __hip_atomic_load(&p.slot_bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (w == nw - 1 && (p.n_hslots & 31)) word |= ~0u << (p.n_hslots & 31);
+            }
+            u64 m = wave_ballot(word != 0xFFFFFFFFu);
+            while (m) {
+                const u32 l = (u32)__builtin_ctzll(m);
+                const u32 ww = wave_read(w, l);
+                const u32 bit = (u32)__builtin_ctz(~wave_read(word, l));
+                u32 old = 0;
+                if (L == 0) old = atomicOr(&p.slot_bits[ww], 1u << bit);
+                old = wave_read(old, 0);
+                if (!(old & (1u << bit))) {
+                    // acquire: the previous holder (any CU, any XCD) released its writes
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    return ww * 32 + bit;
+                }
+                m &= m - 1;
+            }
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+// HBM-resident waves beside the LDS workgroups: each workgroup is one wave that takes ONE document
+// from the queue k_lds drains (LPT order), replays it in a free HBM slot and exits; the grid has a
+// workgroup per document, so waves keep arriving as CU resources free up. k_lds holds 2 waves per
+// SIMD and all the LDS, these waves hold no LDS: on the second stream they fill the issue slots
+// the LDS waves leave idle while they wait on LDS/ALU latency chains. (One document per workgroup
+// rather than a persistent loop: with the engine inlined into a loop, hipcc 7.2 built a divergent
+// loop latch that came back with EXEC narrowed to one lane.)
+template <bool GEN>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_hbmq(Params p) {
+    const u32 L = lane_id();
+    u32 i = 0;
+    if (L == 0) i = atomicAdd(&p.counters[0], 1u);
+    i = wave_read(i, 0);
+    if (i >= p.n_list) return;
+    const u32 d = p.doc_list[i];
+    const u32 slot = acquire_hslot(p);
+    Engine<false> e(p, d);
+    e.bind_slot(p.slot_hbm0 + slot);
+    e.reset_stats();
+    e.init();
+    if (GEN) {
+        GenState g;
+        e.gen_init(g);
+        e.generate_run(g);
+    } else {
+        e.replay_run(p.docs[d].op_begin);
+    }
+    e.finish();
+    // release: write this XCD's dirty lines of the slot back before another wave (possibly on
+    // another XCD, whose L2 is not coherent with this one) can take it over
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (L == 0) atomicAnd(&p.slot_bits[slot >> 5], ~(1u << (slot & 31)));
 }
 
 template <bool GEN>
@@ -104,8 +175,19 @@ __global__ __launch_bounds__(64) void k_wave_selftest(const u32* in, u32* out) {
 }
 
 hipError_t launch_lds(const Params& p, bool gen, u32 n_groups, hipStream_t s) {
-    if (gen) hipLaunchKernelGGL(k_lds<true>, dim3(n_groups), dim3(64 * LDS_WAVES), 0, s, p);
-    else hipLaunchKernelGGL(k_lds<false>, dim3(n_groups), dim3(64 * LDS_WAVES), 0, s, p);
+    // the LdsPlan is dynamic LDS: a static 160 KiB declaration makes the compiler size registers
+    // for the 2 waves/SIMD that LDS allows, while k_lds is kept to <= 128 VGPRs so k_hbmq waves fit
+    // beside it (2 + 2 per SIMD)
+    static const hipError_t attr = [] {
+        hipError_t a = hipFuncSetAttribute((const void*)k_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)sizeof(LdsPlan));
+        hipError_t b = hipFuncSetAttribute((const void*)k_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)sizeof(LdsPlan));
+        return a != hipSuccess ? a : b;
+    }();
+    if (attr != hipSuccess) return attr;
+    if (gen) hipLaunchKernelGGL(k_lds<true>, dim3(n_groups), dim3(64 * LDS_WAVES), sizeof(LdsPlan), s, p);
+    else hipLaunchKernelGGL(k_lds<false>, dim3(n_groups), dim3(64 * LDS_WAVES), sizeof(LdsPlan), s, p);
     return hipGetLastError();
 }
 hipError_t launch_hbm(const Params& p, bool gen, u32 n_docs, hipStream_t s) {
@@ -113,6 +195,12 @@ hipError_t launch_hbm(const Params& p, bool gen, u32 n_docs, hipStream_t s) {
     else hipLaunchKernelGGL(k_hbm<false>, dim3(n_docs), dim3(64), 0, s, p);
     return hipGetLastError();
 }
+hipError_t launch_hbmq(const Params& p, bool gen, u32 n_waves, hipStream_t s) {  // n_waves >= docs left
+    if (gen) hipLaunchKernelGGL(k_hbmq<true>, dim3(n_waves), dim3(64), 0, s, p);
+    else hipLaunchKernelGGL(k_hbmq<false>, dim3(n_waves), dim3(64), 0, s, p);
+    return hipGetLastError();
+}
+
 hipError_t launch_wave_selftest(const u32* in, u32* out, u32 n_waves, hipStream_t s) {
     hipLaunchKernelGGL(k_wave_selftest, dim3(n_waves), dim3(64), 0, s, in, out);
     return hipGetLastError();

@@ -109,6 +109,7 @@ def lib():
         L.mte_run_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.POINTER(u32)]
         L.mte_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_int64]
+        L.mte_get_info.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]
         L.mte_profile.argtypes = [vp, ctypes.c_void_p, sz]
         L.mte_wave_selftest.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, u32]
         L.mte_last_kernel_ms.argtypes = [vp]
@@ -255,8 +256,16 @@ class Engine:
         sp, a, b, rows, co = ctypes.c_uint32(), ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint32()
         self._check(lib().mte_run_info(self._h, ctypes.byref(sp), ctypes.byref(a), ctypes.byref(b),
                                        ctypes.byref(rows), ctypes.byref(co)), "mte_run_info")
-        return {"spilled": sp.value, "continued": co.value, "lds_ms": a.value, "hbm_ms": b.value,
-                "out_rows": rows.value}
+        out = {"spilled": sp.value, "continued": co.value, "lds_ms": a.value, "hbm_ms": b.value,
+               "out_rows": rows.value}
+        for k in ("lds_groups", "hbm_waves", "hbm_docs", "slot_bytes", "slots"):
+            out[k] = self.get_info(k)
+        return out
+
+    def get_info(self, key):
+        v = ctypes.c_int64()
+        self._check(lib().mte_get_info(self._h, key.encode(), ctypes.byref(v)), "mte_get_info")
+        return v.value
 
     def profile(self):
         """Per-doc phase cycle counters (MTE_LIB=prof build), shape (n_docs, len(PROF_NAMES))."""
@@ -265,7 +274,8 @@ class Engine:
         return out
 
     def set_option(self, key, value):
-        """"force_hbm" (skip the LDS-resident pass) or "pool_limit" (LDS leaf blocks per CU)."""
+        """"force_hbm" (HBM-resident waves only), "pool_limit" (LDS leaf blocks per CU),
+        "hbm_waves_per_cu" (HBM-resident waves beside each LDS workgroup), "slot_budget_mb"."""
         self._check(lib().mte_set_option(self._h, key.encode(), int(value)), "mte_set_option")
 
     def last_kernel_ms(self):

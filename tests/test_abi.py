@@ -1,4 +1,4 @@
-"""The C-ABI library loads and exports every symbol include/mte.h declares (no GPU needed)."""
+"""The C-ABI library loads and exports every symbol include/*.h declares (no GPU needed)."""
 import ctypes
 import os
 import re
@@ -8,8 +8,8 @@ from fluidframework_amd import mte
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
-    with open(os.path.join(ROOT, "include", "mte.h")) as f:
+def declared_symbols(header="mte.h"):
+    with open(os.path.join(ROOT, "include", header)) as f:
         text = f.read()
     return sorted(set(re.findall(r"\b(mte_[a-z0-9_]+)\s*\(", text)))
 
@@ -21,6 +21,14 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(L, s), f"libmte.so lacks {s}"
     assert set(syms) == set(mte.EXPORTS)
+
+
+def test_library_exports_diag_symbols():
+    L = ctypes.CDLL(mte.LIB_PATH)
+    syms = declared_symbols("mte_diag.h")
+    assert len(syms) == 7
+    for s in syms:
+        assert hasattr(L, s), f"libmte.so lacks {s}"
 
 
 def test_abi_version_and_info():

@@ -5,6 +5,8 @@ import json
 import os
 import sys
 
+KERNEL = "k_lds<false>"  # the LDS-resident replay kernel (mte_kernels.hip)
+
 
 def rows(pattern):
     out = []
@@ -21,12 +23,12 @@ def main(tag, docs=4096, ops=10000, kind=2):
     summary = {"tag": tag, "docs": docs, "ops": ops, "kind": kind, "kernels": {}}
     for r in stats:
         summary["kernels"][r["Name"]] = {k: r[k] for k in ("Calls", "TotalDurationNs", "AverageNs", "Percentage")}
-    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace if "k_replay" in r["Kernel_Name"]]
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace if KERNEL in r["Kernel_Name"]]
     if durs:
-        summary["k_replay_avg_ms_trace"] = sum(durs) / len(durs) / 1e6
+        summary["replay_kernel_avg_ms_trace"] = sum(durs) / len(durs) / 1e6
     for cname in ("FETCH_SIZE", "WRITE_SIZE"):
         pm = rows(f"{base}/pmc_{'fetch' if cname == 'FETCH_SIZE' else 'write'}/**/*counter_collection.csv")
-        vals = [float(r["Counter_Value"]) for r in pm if "k_replay" in r["Kernel_Name"] and r["Counter_Name"] == cname]
+        vals = [float(r["Counter_Value"]) for r in pm if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == cname]
         if vals:
             summary[cname + "_kib_per_launch"] = sum(vals) / len(vals)
     if "FETCH_SIZE_kib_per_launch" in summary and "WRITE_SIZE_kib_per_launch" in summary:

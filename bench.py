@@ -170,11 +170,13 @@ def main():
                        "parallelism": f"doc-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "mte::k_lds<false>", "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes},
+                         "kernel": "replay pass: mte::k_lds<false> + mte::k_hbmq<false> (concurrent streams)",
+                         "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "extra": {"ops_per_step_per_gpu": ops_applied, "lds_pass_ms": sum(lds_ms) / len(lds_ms),
                       "hbm_pass_ms": info["hbm_ms"], "docs_rerun_hbm": info["spilled"],
-                      "docs_continued_hbm": info["continued"], "gen_s": gen_s, "snapshot_host_s": snap_host_s,
+                      "docs_continued_hbm": info["continued"], "docs_hbm_waves": info["hbm_docs"],
+                      "lds_groups": info["lds_groups"], "hbm_wave_slots": info["hbm_waves"], "gen_s": gen_s, "snapshot_host_s": snap_host_s,
                       "snapshot_bytes": snap_bytes, "summaries_gathered": gathered, "oracle_verified_docs": verified},
         }
         print(json.dumps(line))

@@ -242,3 +242,36 @@ def test_generator_continues_hbm_resident(engine):
     assert info["continued"] + info["spilled"] > 0, info
     got = mte.batch_ops(engine.export_batch())
     assert np.array_equal(ref, got)
+
+
+def test_hybrid_pass_lds_and_hbm_waves_agree(engine):
+    """The hybrid pass (LDS workgroup + HBM-resident waves sharing one queue) routes documents to
+    both kinds of wave; results are identical to an LDS-only pass and to HBM waves waiting on a
+    handful of slots, and match the oracle."""
+    nd = 3072
+    engine.generate(3, nd, 300, n_clients=8, seed=17)
+    batch = engine.export_batch()
+    engine.replay()
+    info = engine.run_info()
+    modes = np.array([engine.doc_result(d)["mode"] for d in range(nd)])
+    assert info["hbm_waves"] > 0 and (modes == 1).sum() > 0 and (modes == 0).sum() > 0, info
+    hybrid = _summary_key(engine.summaries())
+    bad, _, _ = compare_batch_checksums(engine, batch)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad
+    try:
+        engine.set_option("hbm_waves_per_cu", 0)
+        engine.replay()
+        assert engine.run_info()["hbm_waves"] == 0
+        assert _summary_key(engine.summaries()) == hybrid
+        engine.set_option("hbm_waves_per_cu", 8)
+        slot = engine.get_info("slot_bytes")
+        engine.set_option("slot_budget_mb", ((2048 + 24) * slot >> 20) + 1)  # ~24 HBM slots
+        engine.replay()
+        info = engine.run_info()
+        assert 0 < info["hbm_waves"] < 64, info
+        assert _summary_key(engine.summaries()) == hybrid
+    finally:
+        engine.set_option("hbm_waves_per_cu", 8)
+        engine.set_option("slot_budget_mb", 48 << 10)

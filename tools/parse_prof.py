@@ -5,7 +5,8 @@ import json
 import os
 import sys
 
-KERNEL = "k_lds<false>"  # the LDS-resident replay kernel (mte_kernels.hip)
+# the replay pass: LDS workgroups and HBM-resident waves, launched together on two streams
+KERNELS = ("k_lds<false>", "k_hbmq<false>")
 
 
 def rows(pattern):
@@ -23,14 +24,28 @@ def main(tag, docs=4096, ops=10000, kind=2):
     summary = {"tag": tag, "docs": docs, "ops": ops, "kind": kind, "kernels": {}}
     for r in stats:
         summary["kernels"][r["Name"]] = {k: r[k] for k in ("Calls", "TotalDurationNs", "AverageNs", "Percentage")}
-    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace if KERNEL in r["Kernel_Name"]]
-    if durs:
-        summary["replay_kernel_avg_ms_trace"] = sum(durs) / len(durs) / 1e6
+    for k in KERNELS:
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace if k in r["Kernel_Name"]]
+        if durs:
+            summary[f"{k}_avg_ms_trace"] = sum(durs) / len(durs) / 1e6
+    # pass time: first start to last end of each (k_lds, k_hbmq) pair, in dispatch order
+    lds = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in trace if KERNELS[0] in r["Kernel_Name"])
+    hbq = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in trace if KERNELS[1] in r["Kernel_Name"])
+    if lds and len(lds) == len(hbq):
+        passes = [max(a[1], b[1]) - min(a[0], b[0]) for a, b in zip(lds, hbq)]
+        summary["replay_pass_avg_ms_trace"] = sum(passes) / len(passes) / 1e6
     for cname in ("FETCH_SIZE", "WRITE_SIZE"):
         pm = rows(f"{base}/pmc_{'fetch' if cname == 'FETCH_SIZE' else 'write'}/**/*counter_collection.csv")
-        vals = [float(r["Counter_Value"]) for r in pm if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == cname]
-        if vals:
-            summary[cname + "_kib_per_launch"] = sum(vals) / len(vals)
+        # per pass: the counters of one k_lds dispatch plus one k_hbmq dispatch (rocprofv3 serialises
+        # dispatches while it collects counters)
+        tot = 0.0
+        for k in KERNELS:
+            vals = [float(r["Counter_Value"]) for r in pm if k in r["Kernel_Name"] and r["Counter_Name"] == cname]
+            if vals:
+                summary[f"{cname}_kib_{k}"] = sum(vals) / len(vals)
+                tot += sum(vals) / len(vals)
+        if tot:
+            summary[cname + "_kib_per_launch"] = tot
     if "FETCH_SIZE_kib_per_launch" in summary and "WRITE_SIZE_kib_per_launch" in summary:
         summary["hbm_bytes_per_launch"] = (summary["FETCH_SIZE_kib_per_launch"] + summary["WRITE_SIZE_kib_per_launch"]) * 1024
     os.makedirs("profiles", exist_ok=True)

@@ -35,7 +35,12 @@ enum ProfSlot : u32 {
     PN_RESOLVE, PN_DIRTY, PN_SCOUR, PN_SCOUR_CHANGED, PN_PACK, PN_POP, PN_PUSH, PN_SPLIT_BLK
 };
 #ifdef MTE_PROFILE
-#define MTE_COUNT(slot, n) (prof[slot] += (n))
+// counters accumulate straight into the per-document HBM record (fire-and-forget atomics: no
+// registers held across the engine, which runs at its 128-VGPR bound)
+#define MTE_COUNT(slot, n)                                    \
+    do {                                                      \
+        if (lane_id() == 0) atomicAdd(prof + (slot), (u64)(n)); \
+    } while (0)
 #else
 #define MTE_COUNT(slot, n) \
     do {                   \
@@ -43,12 +48,15 @@ enum ProfSlot : u32 {
 #endif
 #ifdef MTE_PROFILE
 struct ProfScope {
-    u64& acc;
+    u64* acc;
     u64 t0;
-    MTE_DEV ProfScope(u64& a) : acc(a), t0(__builtin_amdgcn_s_memtime()) {}
-    MTE_DEV ~ProfScope() { acc += __builtin_amdgcn_s_memtime() - t0; }
+    MTE_DEV ProfScope(u64* a) : acc(a), t0(__builtin_amdgcn_s_memtime()) {}
+    MTE_DEV ~ProfScope() {
+        const u64 dt = __builtin_amdgcn_s_memtime() - t0;
+        if (lane_id() == 0) atomicAdd(acc, dt);
+    }
 };
-#define MTE_PROF(slot) ProfScope _prof_scope_##slot(prof[slot])
+#define MTE_PROF(slot) ProfScope _prof_scope_##slot(prof + (slot))
 #else
 #define MTE_PROF(slot) \
     do {               \
@@ -133,7 +141,7 @@ struct Engine {
     St st;
     bool collab, has_nl;
 #ifdef MTE_PROFILE
-    u64 prof[PROF_SLOTS];
+    u64* prof;  // p.prof + doc * PROF_SLOTS (zeroed by the host before each pass)
 #endif
     // HBM-resident state arrays (HBM mode); in LDS mode every array is an address in the CU's
     // LdsPlan (g_plan), a compile-time constant plus the wave's region offset.
@@ -147,6 +155,7 @@ struct Engine {
     uint2* m_heap;
     u32* m_scratch;
     u32* m_stats;
+    u32* m_hint;   // HBM mode: HBM_HINTS entries
     u32 m_blk_cap, m_ord_cap, m_in_cap, m_heap_cap;
     u32 wave;
     bool continued = false;  // HBM-resident after starting in LDS
@@ -172,6 +181,15 @@ struct Engine {
     MTE_ARR(unsigned char, OWNER, nullptr, g_plan.owner)       // pool block -> wave
     MTE_ARR(u32, POOLAV, nullptr, &g_plan.pool_avail)          // pool blocks free of credit
 #undef MTE_ARR
+    // LRU heap hints (verified on use, so a stale or uninitialised entry only costs a full search)
+    MTE_DEV u32 hint_get(u32 sid) const {
+        if constexpr (LDSM) return HINT()[sid & 255];
+        else return U(m_hint[sid & (HBM_HINTS - 1)]);
+    }
+    MTE_DEV void hint_set(u32 sid, u32 blk) const {  // per-lane store
+        if constexpr (LDSM) HINT()[sid & 255] = (u16)blk;
+        else m_hint[sid & (HBM_HINTS - 1)] = blk;
+    }
     MTE_DEV u32 blk_cap() const { if constexpr (LDSM) return POOL_BLOCKS; else return m_blk_cap; }
     MTE_DEV u32 ord_cap() const { if constexpr (LDSM) return ORD_CAP; else return m_ord_cap; }
     MTE_DEV u32 in_cap() const { if constexpr (LDSM) return IN_CAP; else return m_in_cap; }
@@ -185,7 +203,7 @@ struct Engine {
     MTE_DEV Engine(const Params& p_, u32 doc_) : p(p_), doc(doc_) {
         L = lane_id();
 #ifdef MTE_PROFILE
-        for (u32 i = 0; i < PROF_SLOTS; i++) prof[i] = 0;
+        prof = p.prof + (u64)doc_ * PROF_SLOTS;
 #endif
         const DocCfg& c = p.docs[doc];
         seg_cap = c.seg_cap;
@@ -240,6 +258,7 @@ struct Engine {
         m_heap = (uint2*)(b + l.heap);
         m_scratch = (u32*)(b + l.scratch);
         m_stats = m_scratch + 32;
+        m_hint = (u32*)(b + l.hint);
         m_blk_cap = cb;
         m_ord_cap = co;
         m_in_cap = ci;
@@ -696,8 +715,8 @@ struct Engine {
     // Current leaf block of segment `sid` (the LRU heap entry's segment.parent), NONE if unlinked.
     MTE_DEV bool find_seg(u32 sid, u32& k, u32& blk, u32& cnt) {
         MTE_PROF(PF_FIND_SEG);
-        if (LDSM) {  // the block recorded at push time (kept current by splits and packs)
-            const u32 hb = HINT()[sid & 255];
+        {  // the block recorded at push time (kept current by splits and packs)
+            const u32 hb = hint_get(sid);
             const u32 kk = ord_find(hb);
             if (kk != NONE) {
                 const uint4 o = ORD()[kk];
@@ -849,7 +868,7 @@ struct Engine {
         sync();
         if (L < 4) {
             store(nb, L, m);
-            if (LDSM) HINT()[m.sid & 255] = (u16)nb;
+            hint_set(m.sid, nb);
         }
         ord_shift_right(k + 1, 1);
         if (L == 0) {
@@ -880,7 +899,7 @@ struct Engine {
         MTE_COUNT(PN_PUSH, 1);
         if (L == 0) {
             HEAP()[n] = make_uint2(sid, (u32)maxSeq);
-            if (LDSM) HINT()[sid & 255] = (u16)blk;
+            hint_set(sid, blk);
         }
         sync();
     }
@@ -1337,7 +1356,7 @@ struct Engine {
         const u32 dstBlk = wave_shfl(nb, dj < kk ? dj : 0u);
         if (L < T) {
             store(dstBlk, dq, rec);
-            if (LDSM) HINT()[rec.sid & 255] = (u16)dstBlk;
+            hint_set(rec.sid, dstBlk);
         }
         if (L < kk) {
             BMETA()[nb] = (par & BM_PAR) | (SC_UNDEF << 30);
@@ -1710,9 +1729,7 @@ struct Engine {
     // when the MSN advanced. One zamboni call site.
     MTE_DEV void apply(const mte_op& op) {
         MTE_PROF(PF_APPLY);
-#ifdef MTE_PROFILE
-        prof[PF_OPS]++;
-#endif
+        MTE_COUNT(PF_OPS, 1);
         if (op.client >= MTE_MAX_CLIENTS) {
             fail(MTE_DOC_UNSUPPORTED, op.seq);
             return;
@@ -1799,10 +1816,6 @@ struct Engine {
 
     // Results + the final segments in doc order (walkAllSegments, mergeTree.ts:2969-2983).
     MTE_DEV void finish() {
-#ifdef MTE_PROFILE
-        if (L == 0 && p.prof)
-            for (u32 i = 0; i < PROF_SLOTS; i++) p.prof[(u64)doc * PROF_SLOTS + i] = prof[i];
-#endif
         u32 nseg = 0;
         for (u32 base = 0; base < st.n_lb; base += 64) {
             u32 k = base + L;
@@ -1894,7 +1907,7 @@ struct Engine {
     // continues HBM-resident from there) or on a failure (st.status).
     MTE_DEV u64 replay_run(u64 i) {
 #ifdef MTE_PROFILE
-        ProfScope _total(prof[PF_TOTAL]);
+        ProfScope _total(prof + PF_TOTAL);
 #endif
         const u64 b = i, e = p.docs[doc].op_end;
         if (LDSM) {

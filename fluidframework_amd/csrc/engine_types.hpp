@@ -175,10 +175,12 @@ MTE_HOSTDEV_ void hbm_caps(u64 n, u32& blk, u32& ord, u32& in, u32& heap) {
     heap = (u32)(h > 0x3FFFFFF0ull ? 0x3FFFFFF0ull : h);
 }
 
+constexpr u32 HBM_HINTS = 1024;  // HBM mode: segment id (mod 1024) -> leaf block at LRU push
+
 // HBM-mode state layout of one document (byte offsets from DocCfg::hb_off).
 struct HbmLayout {
     MTE_HOSTDEV_ static u64 a16(u64 n) { return (n + 15) & ~15ull; }
-    u64 vis, aux, bmeta, ord, in_child, in_cnt, in_par, heap, scratch, bytes;
+    u64 vis, aux, bmeta, ord, in_child, in_cnt, in_par, heap, scratch, hint, bytes;
     MTE_HOSTDEV_ static HbmLayout of(u32 blk, u32 ord, u32 in, u32 heap) {
         HbmLayout l;
         u64 o = 0;
@@ -200,6 +202,8 @@ struct HbmLayout {
         o += a16((u64)(heap + 1) * 8);
         l.scratch = o;
         o += 64 * 4;
+        l.hint = o;
+        o += HBM_HINTS * 4;
         l.bytes = o;
         return l;
     }

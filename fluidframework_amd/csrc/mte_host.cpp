@@ -548,6 +548,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     e->P.n_hslots = hbm_waves;
     HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 8 * sizeof(uint32_t), e->stream));
     HIP_TRY(e, hipMemsetAsync(e->d_slot_bits.p, 0, e->d_slot_bits.n * sizeof(uint32_t), e->stream));
+    HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, e->d_prof.n * sizeof(uint64_t), e->stream));  // profiling build
     HIP_TRY(e, hipEventRecord(e->ev0, e->stream));
     std::vector<uint32_t> spill;
     float lds_ms = 0, hbm_ms = 0;

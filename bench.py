@@ -1,12 +1,17 @@
 """bench.py — headline benchmark of the MI355X merge-tree replay engine.
 
-Workload (BASELINE.json configs[1], "C2"): 4096 synthetic SharedString documents x 10,000 sequenced
-ops each, insert/remove only, 8 simulated writers plus a read-only observer (SURVEY §8d generator,
-run on the GPU). A step = one replay of the whole batch (Client.applyMsg for every message of every
-document, client.ts:805-836) from empty state to every document's final state, inputs resident in
-HBM. Multi-GPU: documents are sharded by doc id (each rank replays its own 4096-doc shard; weak
-scaling); the only collective is the final all-gather of 32-B per-document summary records over
-RCCL/xGMI, outside the timed region.
+Default workload (BASELINE.json configs[1], "C2"): 4096 synthetic SharedString documents x 10,000
+sequenced ops each, insert/remove only, 8 simulated writers plus a read-only observer (SURVEY §8d
+generator, run on the GPU). A step = one replay of the whole batch (Client.applyMsg for every
+message of every document, client.ts:805-836) from empty state to every document's final state,
+inputs resident in HBM. Multi-GPU: documents are sharded by doc id (each rank replays its own
+4096-doc shard; weak scaling); the only collective is the final all-gather of 32-B per-document
+summary records over RCCL/xGMI, outside the timed region.
+
+Other configs (--config): C3 (65,536 docs x 10k ops with annotate, forced ties and overlapping
+removes, per GPU, weak), C4 (262,144 docs, Zipf op counts clamp(1e6/r, 1e3, 1e6), LPT-sharded over
+the ranks, strong), C5 (1,024 docs x 1M ops, MSN lag <= 64 so zamboni runs continuously, sharded
+over the ranks, strong).
 
 Prints ONE JSON line (rank 0).
 """
@@ -23,22 +28,41 @@ sys.path.insert(0, ROOT)
 METRIC = "sequenced ops applied/sec (whole node) + achieved HBM GB/s, 256k docs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 OP_RECORD_B, LEAF_BLOCK_B = 32, 512  # SURVEY §8(d) algorithmic bytes per op: 32 + P + 512
+# SURVEY §8(d) configs. docs: per GPU for weak-scaling configs, whole job for strong ones.
+CONFIGS = {
+    "C2": {"docs": 4096, "ops": 10000, "kind": 2, "scaling": "weak", "steps": 5, "warmup": 1,
+           "desc": "insert/remove around a 2048-char target"},
+    "C3": {"docs": 65536, "ops": 10000, "kind": 3, "scaling": "weak", "steps": 3, "warmup": 1,
+           "desc": "45/35/20 insert/remove/annotate, 15% forced ties and overlapping removes"},
+    "C4": {"docs": 262144, "ops": 0, "kind": 2, "scaling": "strong", "steps": 2, "warmup": 0,
+           "desc": "Zipf op counts clamp(1e6/r, 1e3, 1e6), C2 mix, LPT-sharded"},
+    "C5": {"docs": 1024, "ops": 1000000, "kind": 5, "scaling": "strong", "steps": 2, "warmup": 0,
+           "desc": "1M-op docs, C2 mix with MSN lag <= 64 (continuous zamboni)"},
+}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--docs", type=int, default=4096)
-    ap.add_argument("--ops", type=int, default=10000)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 5; 2 for C4/C5)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 1; 0 for C4/C5)")
+    ap.add_argument("--docs", type=int, default=None)
+    ap.add_argument("--ops", type=int, default=None)
     ap.add_argument("--clients", type=int, default=8)
-    ap.add_argument("--kind", type=int, default=2)
+    ap.add_argument("--kind", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-docs", type=int, default=32, help="docs checked against the oracle after timing")
-    return ap.parse_args()
+    a = ap.parse_args()
+    c = CONFIGS[a.config]
+    a.docs = c["docs"] if a.docs is None else a.docs
+    a.ops = c["ops"] if a.ops is None else a.ops
+    a.kind = c["kind"] if a.kind is None else a.kind
+    a.steps = c["steps"] if a.steps is None else a.steps
+    a.warmup = c["warmup"] if a.warmup is None else a.warmup
+    return a
 
 
 def log(msg):
@@ -59,12 +83,23 @@ def main():
         dist.init_process_group("nccl")  # RCCL over xGMI
     from fluidframework_amd import mte
 
+    cfg = CONFIGS[args.config]
     eng = mte.Engine(local)
     t0 = time.time()
-    # per-rank shard: distinct seeds => distinct documents (doc ids rank*docs + i)
-    eng.generate(args.kind, args.docs, args.ops, n_clients=args.clients, seed=1000 + rank)
+    # per-rank shard: distinct seeds => distinct documents
+    if cfg["scaling"] == "weak":
+        n_local, per_doc = args.docs, None
+    elif args.config == "C4":
+        from fluidframework_amd.shard import lpt_assign, zipf_op_counts
+
+        counts = zipf_op_counts(args.docs, seed=0)
+        mine = lpt_assign(counts, world)[rank]  # longest first
+        n_local, per_doc = len(mine), counts[mine]
+    else:  # C5: equal documents, contiguous shards
+        n_local, per_doc = len(range(rank, args.docs, world)), None
+    eng.generate(args.kind, n_local, args.ops, n_clients=args.clients, seed=1000 + rank, ops_per_doc=per_doc)
     gen_s = time.time() - t0
-    log(f"rank {rank}: generated {args.docs} docs x {args.ops} ops in {gen_s:.1f} s")
+    log(f"rank {rank}: generated {n_local} docs ({args.config}) in {gen_s:.1f} s")
     batch = eng.export_batch()
     ops_np = mte.batch_ops(batch)
     ins = ops_np["type"] == mte.MTE_OP_INSERT
@@ -97,7 +132,11 @@ def main():
         elapsed = float(t.item())
     assert st["failed_docs"] == 0, st
     ops_applied = st["ops"]
-    total_ops = ops_applied * world
+    total_ops = ops_applied
+    if world > 1:  # shards may differ (C4): sum what every rank applied
+        t = torch.tensor([ops_applied], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        total_ops = int(t.item())
     ms_per_step = elapsed / args.steps * 1000.0
     value = total_ops * args.steps / elapsed
 
@@ -108,10 +147,9 @@ def main():
     snap_host_s = time.time() - t1
     snap_bytes = int(summ["snapshot_bytes"].sum())
     if world > 1:
-        rec = torch.from_numpy(summ.view(np.uint8).copy()).cuda()
-        out = [torch.empty_like(rec) for _ in range(world)]
-        dist.all_gather(out, rec)
-        gathered = sum(o.numel() for o in out) // 32
+        from fluidframework_amd.shard import gather_summaries
+
+        gathered = len(gather_summaries(summ, device="cuda"))
     else:
         gathered = len(summ)
 
@@ -137,37 +175,39 @@ def main():
     if rank == 0:
         from oracle import replay_batch
 
-        nv = min(args.verify_docs, args.docs)
+        nv = min(args.verify_docs, n_local)
         if nv:
             o_ops, cks, sts = replay_batch(ctypes.addressof(batch), 0, nv, threads=args.cpu_threads)
+            assert all(sts[d] == 0 for d in range(nv)), "oracle reports failing documents"
             verified = all(int(summ["checksum"][d]) == cks[d] and int(summ["status"][d]) == sts[d] for d in range(nv))
         log(f"oracle verification of {nv} docs: {verified}")
         if not args.no_cpu_baseline:
             # bounded sample: grow the doc count until ~cpu_seconds of oracle replay on cpu_threads threads
             nd = max(args.cpu_threads, 16)
             while True:
-                nd = min(nd, args.docs)
+                nd = min(nd, n_local)
                 c0 = time.perf_counter()
                 c_ops, _, _ = replay_batch(ctypes.addressof(batch), 0, nd, threads=args.cpu_threads,
                                            with_snapshot=False)
                 dt = time.perf_counter() - c0
                 log(f"cpu baseline sample: {nd} docs, {c_ops} ops in {dt:.2f} s")
-                if dt >= args.cpu_seconds * 0.5 or nd >= args.docs:
+                if dt >= args.cpu_seconds * 0.5 or nd >= n_local:
                     break
                 nd = int(nd * min(8.0, max(2.0, args.cpu_seconds / max(dt, 1e-3))))
             cpu = {"value": c_ops / dt, "unit": "ops/s", "cores": args.cpu_threads, "kind": "port",
-                   "sample": f"oracle (tree-shaped C++ restatement) replaying docs 0..{nd - 1} of the same C2 batch "
+                   "sample": f"oracle (tree-shaped C++ restatement) replaying docs 0..{nd - 1} of the same {args.config} batch "
                              f"({c_ops} ops, replay only) on {args.cpu_threads} threads in {dt:.2f} s"}
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": cfg["scaling"],
             "vs_baseline": None, "dtype": "int32", "data": "synthetic (GPU generator, SURVEY §8d)",
-            "config": {"workload": f"C{args.kind}: {args.docs} docs x {args.ops} ops per GPU, "
-                                   f"{'insert/remove' if args.kind == 2 else 'mixed'}, {args.clients} writers",
-                       "docs_per_gpu": args.docs, "ops_per_doc": args.ops, "clients": args.clients,
-                       "parallelism": f"doc-sharded x{world}"},
+            "config": {"workload": f"{args.config}: {args.docs} docs"
+                                   + (" per GPU" if cfg["scaling"] == "weak" else " per job")
+                                   + (f" x {args.ops} ops" if args.ops else "") + f", {cfg['desc']}, {args.clients} writers",
+                       "config_id": args.config, "docs_per_gpu": n_local, "ops_per_doc": args.ops or "zipf",
+                       "clients": args.clients, "parallelism": f"doc-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "replay pass: mte::k_lds<false> + mte::k_hbmq<false> (concurrent streams)",

@@ -159,6 +159,7 @@ struct Engine {
     u32 m_blk_cap, m_ord_cap, m_in_cap, m_heap_cap;
     u32 wave;
     bool continued = false;  // HBM-resident after starting in LDS
+    bool capped = false;     // HBM slot smaller than this document's worst case
 
 #define MTE_ARR(T, NAME, MEM, LDSX)            \
     MTE_DEV T* NAME() const {                  \
@@ -277,6 +278,9 @@ struct Engine {
     // a wave's own HBM slot (Params::slot_*), reused by every document the wave takes over
     MTE_DEV void bind_slot(u32 slot) {
         bind_region(p.spill + (u64)slot * p.slot_bytes, p.slot_blk, p.slot_ord, p.slot_in, p.slot_heap);
+        u32 cb, co, ci, ch;
+        hbm_caps(p.docs[doc].op_end - p.docs[doc].op_begin, cb, co, ci, ch);
+        capped = cb > p.slot_blk || co > p.slot_ord || ci > p.slot_in || ch > p.slot_heap;
     }
 
     // Wave-uniform reads: a load from a uniform address is broadcast through readfirstlane so the
@@ -533,8 +537,10 @@ struct Engine {
     // ---------------------------------------------------------------- allocation
     // Out of room: in LDS mode the document leaves the LDS plan (DOC_SPILL: its LDS state is
     // dropped and the host re-runs it HBM-resident); in HBM mode it is a capacity failure.
+    // Out of room: LDS plan or an HBM slot smaller than the document's worst case -> DOC_SPILL
+    // (the host re-runs it with worst-case capacities); a worst-case region -> capacity error.
     MTE_DEV void fail_cap() {
-        if (LDSM) fail(DOC_SPILL, st.curSeq);
+        if (LDSM || capped) fail(DOC_SPILL, st.curSeq);
         else fail(MTE_DOC_CAPACITY, st.curSeq);
     }
 
@@ -1211,7 +1217,9 @@ struct Engine {
             jb.dst = jb.src = jb.len = 0;
             u32 top = st.arenaTop, need = 0;
             i32 prev = -1;  // kept index of the chain head
-            u32 pLen = 0, pOff = 0, pCap = 0, pProps = 0;
+            // pMat: leading chars of the head's text already in memory; [pMat, pLen) are pending
+            // in-place append jobs of this batch (a copy of the head must not read them)
+            u32 pLen = 0, pOff = 0, pCap = 0, pProps = 0, pMat = 0;
             bool pText = false, pNL = false, pFresh = false;
             for (u32 s = 0; s < cnt; s++) {
                 const u64 bit = 1ull << s;
@@ -1227,19 +1235,20 @@ struct Engine {
                     if (ok) {  // TextSegment.append (textSegment.ts:74-85)
                         if ((pOff & ARENA_BIT) && pLen + len <= pCap) {
                             job_add(jb, pOff + pLen, toff, len);
-                        } else if (pOff + pLen == toff) {
+                        } else if (pOff + pLen == toff && pMat == pLen) {  // text already contiguous
                             if (pOff & ARENA_BIT) pCap = toff + tcap - pOff;
+                            pMat += len;
                         } else {
                             u32 ncap = 2 * (pLen + len);
                             if (ncap < 32) ncap = 32;
                             const u32 dst = top | ARENA_BIT;
                             top += ncap;
                             need += ncap;
-                            if (pFresh) {  // the head's chunk is built by this batch: retarget its jobs
-                                if (L < jb.n && jb.dst >= pOff && jb.dst < pOff + pLen) jb.dst = jb.dst - pOff + dst;
-                            } else {
-                                job_add(jb, dst, pOff, pLen);
-                            }
+                            // pending jobs into the head's chunk follow it to the new one; the
+                            // materialised prefix (none for a chunk built by this batch) is copied
+                            const u32 m0 = pFresh ? 0u : pMat;
+                            if (L < jb.n && jb.dst >= pOff + m0 && jb.dst < pOff + pLen) jb.dst = jb.dst - pOff + dst;
+                            if (m0) job_add(jb, dst, pOff, m0);
                             job_add(jb, dst + pLen, toff, len);
                             pOff = dst;
                             pCap = ncap;
@@ -1256,6 +1265,7 @@ struct Engine {
                     } else {
                         prev = (i32)nkeep;
                         pLen = len;
+                        pMat = len;
                         pOff = toff;
                         pCap = tcap;
                         pProps = props;

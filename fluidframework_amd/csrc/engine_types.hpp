@@ -83,6 +83,8 @@ struct DocCfg {
     u32 hb_blk, hb_ord, hb_in, hb_heap;  // HBM-mode capacities
     u32 collab;        // 1 = observer replay, 0 = local non-collaborative edits
     u32 has_nl;        // payload contains '\n' (TextSegment.canAppend reads last chars only then)
+    u32 prio;          // critical-path document (far longer than the batch mean): high wave priority
+    u32 pad;
 };
 
 // Per-document results written by the kernel.

@@ -222,6 +222,8 @@ struct mte_engine {
     uint32_t pool_limit = 0;
     uint32_t hbm_waves_per_cu = 8;    // HBM-resident waves (slots) per CU beside the LDS workgroup (2 per SIMD)
     uint64_t slot_budget = 48ull << 30;  // HBM for per-wave slots
+    uint64_t slot_ops_cap = 65536;       // slots are sized for documents of at most this many ops
+    uint32_t slot_blk_limit = 0;         // test knob: leaf blocks per slot (0 = from slot_ops_cap)
     // per-wave slot plan (layout_and_alloc)
     uint32_t n_slots = 0;
     // last run
@@ -305,7 +307,8 @@ static int alloc_slots(mte_engine* e);
 static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, const std::vector<uint64_t>& pay_len,
                             const std::vector<uint64_t>& n_prop_ins, const std::vector<uint64_t>& n_ann,
                             const std::vector<uint8_t>& collab, const std::vector<uint8_t>& has_nl,
-                            uint64_t arena_limit = 0) {
+                            uint64_t arena_limit = 0, const uint64_t* op_offsets = nullptr,
+                            const uint64_t* payload_offsets = nullptr) {
     const uint32_t nd = (uint32_t)n_ops.size();
     e->cfg.assign(nd, DocCfg{});
     e->n_ops_doc = n_ops;
@@ -313,10 +316,11 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     for (uint32_t d = 0; d < nd; d++) {
         DocCfg& c = e->cfg[d];
         uint64_t n = n_ops[d];
-        c.op_begin = op;
-        c.op_end = op + n;
+        // a loaded batch's documents need not start at op / payload 0 (mte_batch offsets are absolute)
+        c.op_begin = op_offsets ? op_offsets[d] : op;
+        c.op_end = c.op_begin + n;
         op += n;
-        c.payload_off = pay;
+        c.payload_off = payload_offsets ? payload_offsets[d] : pay;
         c.payload_len = (uint32_t)pay_len[d];
         pay += pay_len[d];
         // merge arena semispace: live arena text <= 2x live text, a scour needs <= 4x a block's text
@@ -333,9 +337,16 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
         mp += c.map_cap;
         c.collab = collab[d];
         c.has_nl = has_nl[d];
+        c.prio = 0;
         out += std::min<uint64_t>(3 * n + 8, 4096);
     }
     out += 1u << 20;
+    // critical-path documents (Zipf heads): at least 8x the mean op count
+    if (nd > 1) {
+        const double mean = (double)op / nd;
+        for (uint32_t d = 0; d < nd; d++)
+            if ((double)n_ops[d] >= 8.0 * mean) e->cfg[d].prio = 1;
+    }
     HIP_TRY(e, e->d_arena.alloc(ar));
     HIP_TRY(e, e->d_ovl.alloc(seg));
     HIP_TRY(e, e->d_maps.alloc(mp * MAP_WORDS));
@@ -372,10 +383,15 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || cus <= 0) cus = 256;
     e->n_groups = (uint32_t)cus;
-    // per-wave HBM slots, each sized for the longest document (hbm_caps)
+    // per-wave HBM slots, each sized for the longest document up to slot_ops_cap ops (hbm_caps);
+    // a longer document that outgrows its slot is re-run by the host with worst-case capacities
     uint64_t nmax = 0;
     for (uint32_t d = 0; d < nd; d++) nmax = std::max<uint64_t>(nmax, n_ops[d]);
-    hbm_caps(nmax, P.slot_blk, P.slot_ord, P.slot_in, P.slot_heap);
+    hbm_caps(std::min<uint64_t>(nmax, e->slot_ops_cap), P.slot_blk, P.slot_ord, P.slot_in, P.slot_heap);
+    if (e->slot_blk_limit) {  // test knob: slots that overflow (documents re-run by the host)
+        P.slot_blk = std::min(P.slot_blk, e->slot_blk_limit);
+        P.slot_ord = std::min(P.slot_ord, e->slot_blk_limit);
+    }
     P.slot_bytes = (HbmLayout::of(P.slot_blk, P.slot_ord, P.slot_in, P.slot_heap).bytes + 255) & ~255ull;
     return alloc_slots(e);
 }
@@ -516,7 +532,8 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     }
     auto t0 = std::chrono::steady_clock::now();
     int rc;
-    if ((rc = layout_and_alloc(e, n_ops, pay, pi, an, collab, has_nl))) return rc;
+    if ((rc = layout_and_alloc(e, n_ops, pay, pi, an, collab, has_nl, 0, b->doc_op_offsets, b->doc_payload_offsets)))
+        return rc;
     if ((rc = upload(e, e->d_ops, e->hb.ops))) return rc;
     if ((rc = upload(e, e->d_payload, e->hb.payload))) return rc;
     if ((rc = upload_props(e))) return rc;
@@ -1206,6 +1223,8 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "pool_limit") e->pool_limit = (uint32_t)std::max<int64_t>(0, value);
     else if (k == "hbm_waves_per_cu") e->hbm_waves_per_cu = (uint32_t)std::min<int64_t>(std::max<int64_t>(0, value), 32);
     else if (k == "slot_budget_mb") e->slot_budget = (uint64_t)std::max<int64_t>(1, value) << 20;
+    else if (k == "slot_ops_cap") e->slot_ops_cap = (uint64_t)std::max<int64_t>(64, value);  // next load
+    else if (k == "slot_blk_limit") e->slot_blk_limit = (uint32_t)std::max<int64_t>(0, value);  // next load
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
 }

@@ -38,6 +38,8 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
         i = wave_read(i, 0);
         if (i >= p.n_list) break;
         const u32 d = p.doc_list[i];
+        const bool prio = p.docs[d].prio != 0;
+        if (prio) __builtin_amdgcn_s_setprio(3);  // the critical path issues first on its SIMD
         Engine<true> e(p, d);
         e.bind_lds(w);
         GenState g;
@@ -53,6 +55,8 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
         }
         if (e.st.status == DOC_SPILL) {
             e.mark_spilled();  // failed mid-op: the host re-runs it (rare)
+        } else if (!done && e.st.status == 0 && p.slot_blk < POOL_BLOCKS + 64) {
+            e.mark_spilled();  // slots too small to hold the LDS block ids (test knob): host re-run
         } else if (!done && e.st.status == 0) {
             // the LDS plan ran out of room between two ops: continue HBM-resident, same wave
             Engine<false> h(p, d);
@@ -71,6 +75,7 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
             e.finish();
         }
         e.release();
+        if (prio) __builtin_amdgcn_s_setprio(0);
     }
 }
 
@@ -125,6 +130,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     i = wave_read(i, 0);
     if (i >= p.n_list) return;
     const u32 d = p.doc_list[i];
+    if (p.docs[d].prio) __builtin_amdgcn_s_setprio(3);
     const u32 slot = acquire_hslot(p);
     Engine<false> e(p, d);
     e.bind_slot(p.slot_hbm0 + slot);

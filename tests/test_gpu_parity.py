@@ -275,3 +275,69 @@ def test_hybrid_pass_lds_and_hbm_waves_agree(engine):
     finally:
         engine.set_option("hbm_waves_per_cu", 8)
         engine.set_option("slot_budget_mb", 48 << 10)
+
+
+def test_slot_overflow_reruns_with_worst_case_capacity(engine):
+    """HBM slots are sized for typical documents; one that outgrows its slot is marked for the
+    host's re-run with worst-case capacities and still matches the oracle."""
+    engine.set_option("slot_blk_limit", 24)
+    try:
+        engine.generate(2, 48, 3000, n_clients=8, seed=23)
+        batch = engine.export_batch()
+        engine.set_option("force_hbm", 1)
+        engine.replay()
+        info = engine.run_info()
+    finally:
+        engine.set_option("force_hbm", 0)
+        engine.set_option("slot_blk_limit", 0)
+    assert info["spilled"] > 0 and info["hbm_ms"] > 0, info
+    bad, _, _ = compare_batch_checksums(engine, batch)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad
+
+
+def test_long_documents_match_oracle(engine):
+    """50k-op documents: merge chains that append in place and then outgrow their chunk within one
+    scour (the copy of the head must not read bytes the same batch has yet to write), arena GC,
+    LDS-to-HBM continuation."""
+    engine.generate(2, 16, 50000, n_clients=8, seed=1000)
+    batch = engine.export_batch()
+    engine.replay()
+    assert engine.run_info()["continued"] > 0
+    bad, _, _ = compare_batch_checksums(engine, batch)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad
+
+
+def test_one_document_view_of_a_batch(engine):
+    """mte_batch offsets are absolute: a batch whose only document starts mid-array (a prefix of
+    document 5's log here) replays exactly that document."""
+    import ctypes
+
+    from oracle import replay_batch
+
+    engine.generate(2, 8, 3000, n_clients=8, seed=31)
+    full = engine.export_batch()
+    d, n = 5, 2000
+    ob = full.doc_op_offsets[d]
+    b = mte.mte_batch()
+    ctypes.pointer(b)[0] = full
+    b.n_docs = 1
+    opo = (ctypes.c_uint64 * 2)(ob, ob + n)
+    pyo = (ctypes.c_uint64 * 2)(full.doc_payload_offsets[d], full.doc_payload_offsets[d + 1])
+    cli = (ctypes.c_uint32 * 2)(full.doc_client_offsets[d], full.doc_client_offsets[d + 1])
+    b.doc_op_offsets = ctypes.cast(opo, ctypes.POINTER(ctypes.c_uint64))
+    b.doc_payload_offsets = ctypes.cast(pyo, ctypes.POINTER(ctypes.c_uint64))
+    b.doc_client_offsets = ctypes.cast(cli, ctypes.POINTER(ctypes.c_uint32))
+    e2 = mte.Engine(0)
+    try:
+        e2.load(b)
+        st = e2.replay()
+        assert st["ops"] == n
+        _, cks, sts = replay_batch(ctypes.addressof(b), 0, 1, threads=1)
+        s = e2.summaries()
+        assert int(s["status"][0]) == sts[0] == 0 and int(s["checksum"][0]) == cks[0]
+    finally:
+        e2.close()

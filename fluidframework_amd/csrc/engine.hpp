@@ -57,6 +57,14 @@ struct ProfScope {
     }
 };
 #define MTE_PROF(slot) ProfScope _prof_scope_##slot(prof + (slot))
+#elif defined(MTE_MARKERS)
+// static code-size analysis (tools/asm_regions.py): phase scopes as assembly comments
+template <u32 S>
+struct MarkScope {
+    MTE_DEV MarkScope() { asm volatile("; MTE_BEGIN %0" ::"i"(S)); }
+    MTE_DEV ~MarkScope() { asm volatile("; MTE_END %0" ::"i"(S)); }
+};
+#define MTE_PROF(slot) MarkScope<slot> _mark_scope_##slot
 #else
 #define MTE_PROF(slot) \
     do {               \
@@ -423,7 +431,16 @@ struct Engine {
     }
     // Visible lengths of the leaf blocks held one per lane (ord entries) for (R, C). A block whose
     // children are all settled at R (max seq <= R) has the same length for every client; the others
-    // read their slots (independent LDS reads) and evaluate the predicate in integer arithmetic.
+    // read their slots (independent LDS reads) and evaluate the predicate. C != 0 there (the
+    // observer sees every block settled), so the writer form below applies; the overlap masks
+    // (aux.z) are read only when some slot of the batch carries one.
+    MTE_DEV static u32 vis_w(uint4 q, u32 z, i32 R, u32 C) {  // nodeLength for a writer C in 1..31
+        const u32 meta = q.w;
+        const bool ins = ((meta & 0xffu) == C) | ((i32)q.y <= R);
+        const bool ovh = (((z >> C) & 1u) != 0) & ((meta & F_OVL) != 0);
+        const bool rem = ((meta & F_REMOVED) != 0) & ((((meta >> 8) & 0xffu) == C) | ((i32)q.z <= R) | ovh);
+        return (ins & !rem) ? q.x : 0u;
+    }
     MTE_DEV u32 blen_all(uint4 o, bool valid, i32 R, u32 C) const {
         const u32 cz = C == 0 ? 1u : 0u;
         const bool fast = !valid | (cz != 0) | ((i32)o.z <= R);
@@ -431,15 +448,28 @@ struct Engine {
         if (wave_ballot(!fast)) {
             const u32 b = o.x < blk_cap() ? o.x : 0u;
             uint4 q[8];
-            u32 z[8];
 #pragma unroll
-            for (u32 s = 0; s < 8; s++) {
-                q[s] = VIS()[b * 8 + s];
-                z[s] = AUX()[b * 8 + s].z;
-            }
+            for (u32 s = 0; s < 8; s++) q[s] = VIS()[b * 8 + s];
             u32 sv = 0;
+            if (C >= 32) {  // clients 32..63: the general predicate (HBM half of the overlap mask)
 #pragma unroll
-            for (u32 s = 0; s < 8; s++) sv += s < o.w ? vis_len(q[s], z[s], b * 8 + s, R, C, cz) : 0u;
+                for (u32 s = 0; s < 8; s++)
+                    sv += s < o.w ? vis_len(q[s], AUX()[b * 8 + s].z, b * 8 + s, R, C, cz) : 0u;
+            } else {
+                u32 anyo = 0;
+#pragma unroll
+                for (u32 s = 0; s < 8; s++) anyo |= q[s].w;
+                if (wave_ballot(!fast && (anyo & F_OVL) != 0)) {
+                    u32 z[8];
+#pragma unroll
+                    for (u32 s = 0; s < 8; s++) z[s] = AUX()[b * 8 + s].z;
+#pragma unroll
+                    for (u32 s = 0; s < 8; s++) sv += s < o.w ? vis_w(q[s], z[s], R, C) : 0u;
+                } else {
+#pragma unroll
+                    for (u32 s = 0; s < 8; s++) sv += s < o.w ? vis_w(q[s], 0u, R, C) : 0u;
+                }
+            }
             v = fast ? v : sv;
         }
         return v;

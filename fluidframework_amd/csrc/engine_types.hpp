@@ -148,6 +148,8 @@ struct Params {
     u32 slot_hbm0;            // first slot of the k_hbmq waves (after the LDS waves' slots)
     u32* slot_bits;           // k_hbmq slot bitmap (n_hslots bits, 1 = held)
     u32 n_hslots;
+    u32 lds_active;           // waves per k_lds workgroup that take documents (spread small batches)
+    u32 n_prio;               // doc_list[0 .. n_prio): critical-path documents, taken by LDS waves only
     u32 pad2;
     u32 pool_limit;           // test knob: LDS leaf blocks usable per CU (0 = all)
     u64* prof;                // MTE_PROFILE builds: per doc PROF_SLOTS cycle counters

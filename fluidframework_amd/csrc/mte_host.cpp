@@ -400,10 +400,14 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
 // HBM-resident waves at a time (k_hbmq, one document per wave, H slots), or HBM-resident waves
 // alone when the LDS plan is off or the slots for its waves do not fit the budget. Every LDS wave
 // owns a slot for a document that outgrows the plan.
-static void wave_plan(const mte_engine* e, uint32_t nd, uint32_t& groups, uint32_t& hbm_waves) {
+static void wave_plan(const mte_engine* e, uint32_t nd, uint32_t& groups, uint32_t& hbm_waves,
+                      uint32_t* lds_active = nullptr) {
     const uint64_t max_slots = std::max<uint64_t>(1, e->slot_budget / std::max<uint64_t>(e->P.slot_bytes, 1));
-    groups = std::min<uint32_t>(e->n_groups, (nd + LDS_WAVES - 1) / LDS_WAVES);
+    // fewer documents than LDS waves: every CU still gets a workgroup, with fewer active waves
+    // (each with its own SIMD and a larger share of the CU's block pool)
+    groups = std::min<uint32_t>(e->n_groups, nd);
     if (e->force_hbm || (uint64_t)groups * LDS_WAVES > max_slots) groups = 0;
+    if (lds_active) *lds_active = groups ? std::min<uint32_t>(LDS_WAVES, (nd + groups - 1) / groups) : 0;
     // 16 = 4 SIMDs x 4 waves at <= 128 VGPRs (k_hbmq's bound): more can never be resident at once
     const uint32_t per_cu = groups ? std::min<uint32_t>(e->hbm_waves_per_cu, 16) : 16;
     uint64_t h = (uint64_t)per_cu * e->n_groups;
@@ -559,9 +563,13 @@ static int run_kernel(mte_engine* e, bool gen) {
     e->P.n_list = nd;
     int rc;
     if ((rc = alloc_slots(e))) return rc;  // options may have changed the wave plan
-    uint32_t groups, hbm_waves;
-    wave_plan(e, nd, groups, hbm_waves);
+    uint32_t groups, hbm_waves, lds_active;
+    wave_plan(e, nd, groups, hbm_waves, &lds_active);
     e->P.slot_hbm0 = groups * LDS_WAVES;
+    e->P.lds_active = lds_active;
+    e->P.n_prio = 0;
+    if (groups)  // critical-path documents lead the LPT order
+        while (e->P.n_prio < nd && e->cfg[e->order[e->P.n_prio]].prio) e->P.n_prio++;
     e->P.n_hslots = hbm_waves;
     HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 8 * sizeof(uint32_t), e->stream));
     HIP_TRY(e, hipMemsetAsync(e->d_slot_bits.p, 0, e->d_slot_bits.n * sizeof(uint32_t), e->stream));

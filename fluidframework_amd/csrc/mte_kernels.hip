@@ -32,9 +32,14 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
     for (u32 b = t; b < POOL_BLOCKS; b += 64 * LDS_WAVES) lp->owner[b] = 0xFF;
     if (t == 0) lp->pool_avail = usable;
     __syncthreads();
-    for (;;) {
+    // a small batch is spread over every CU (lds_active waves per workgroup); critical-path
+    // documents (doc_list[0, n_prio), counters[5]) are taken by LDS waves only
+    for (; w < p.lds_active;) {
         u32 i = 0;
-        if (L == 0) i = atomicAdd(&p.counters[0], 1u);
+        if (L == 0) {
+            i = p.n_prio ? atomicAdd(&p.counters[5], 1u) : p.n_prio;
+            if (i >= p.n_prio) i = p.n_prio + atomicAdd(&p.counters[0], 1u);
+        }
         i = wave_read(i, 0);
         if (i >= p.n_list) break;
         const u32 d = p.doc_list[i];
@@ -126,11 +131,10 @@ template <bool GEN>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_hbmq(Params p) {
     const u32 L = lane_id();
     u32 i = 0;
-    if (L == 0) i = atomicAdd(&p.counters[0], 1u);
+    if (L == 0) i = p.n_prio + atomicAdd(&p.counters[0], 1u);
     i = wave_read(i, 0);
     if (i >= p.n_list) return;
     const u32 d = p.doc_list[i];
-    if (p.docs[d].prio) __builtin_amdgcn_s_setprio(3);
     const u32 slot = acquire_hslot(p);
     Engine<false> e(p, d);
     e.bind_slot(p.slot_hbm0 + slot);

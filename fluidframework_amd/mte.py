@@ -13,8 +13,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# MTE_LIB=prof selects the phase-profiling build (csrc/Makefile `prof`, engine.hpp MTE_PROFILE)
-LIB_PATH = os.path.join(_HERE, "_build", "prof" if os.environ.get("MTE_LIB") == "prof" else "", "libmte.so")
+# MTE_LIB=<name> selects an alternative build in _build/<name>/ (csrc/Makefile `prof`: the
+# phase-profiling build, engine.hpp MTE_PROFILE; `variant`: experiments with extra flags)
+LIB_PATH = os.path.join(_HERE, "_build", os.environ.get("MTE_LIB", ""), "libmte.so")
 PROF_NAMES = ["apply", "resolve", "insert_slot", "range", "zamboni", "scour", "heap", "find_seg", "map", "pack",
               "fetch", "lru", "text", "alloc", "ops", "total",
               "n_resolve", "n_dirty", "n_scour", "n_scour_changed", "n_pack", "n_pop", "n_push", "n_split_blk"]

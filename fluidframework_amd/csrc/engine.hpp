@@ -1855,17 +1855,36 @@ struct Engine {
     }
 
     // Results + the final segments in doc order (walkAllSegments, mergeTree.ts:2969-2983).
+    // The text of every row is gathered into the document's run of the output text pool (the
+    // row's aux.y becomes its offset in that run) and its property map is copied beside it, so the
+    // host reads final state only: rows, maps and text, never the op log, payload, arena or map
+    // region.
+    MTE_DEV u32 block_text(uint4 o) const {  // text units of the block held by this lane
+        u32 t = 0;
+        const u32 c = o.w > 8 ? 8u : o.w;
+        for (u32 s = 0; s < c; s++) {
+            const uint4 v = VIS()[o.x * 8 + s];
+            t += (v.w & F_MARKER) ? 0u : v.x;
+        }
+        return t;
+    }
     MTE_DEV void finish() {
-        u32 nseg = 0;
+        u32 nseg = 0, ntext = 0;
         for (u32 base = 0; base < st.n_lb; base += 64) {
             u32 k = base + L;
-            nseg += wave_sum(k < st.n_lb ? ORD()[k].w : 0u);
+            const uint4 o = k < st.n_lb ? ORD()[k] : make_uint4(0, 0, 0, 0);
+            nseg += wave_sum(o.w);
+            ntext += wave_sum(k < st.n_lb ? block_text(o) : 0u);
         }
-        u32 off = 0;
+        u32 off = 0, toff = 0;
         if (st.status == 0) {
-            if (L == 0) off = atomicAdd(&p.counters[1], nseg);
+            if (L == 0) {
+                off = atomicAdd(&p.counters[1], nseg);
+                toff = (u32)atomicAdd((unsigned long long*)&p.counters[6], (unsigned long long)ntext);
+            }
             off = wave_read(off, 0);
-            if ((u64)off + nseg > p.out_cap) {
+            toff = wave_read(toff, 0);
+            if ((u64)off + nseg > p.out_cap || (u64)toff + ntext > p.out_text_cap) {
                 fail(MTE_DOC_CAPACITY, st.curSeq);
                 nseg = 0;
             }
@@ -1873,16 +1892,44 @@ struct Engine {
             nseg = 0;
         }
         if (nseg) {
-            fence_ovl();
-            u32 run = off;
+            wave_sync();  // overlap masks, merge-arena text and property maps written by other lanes
+            st.gdirty = st.adirty = 0;
+            u32 run = off, trun = 0;
+            u16* __restrict__ tdst = p.out_text + toff;
             for (u32 base = 0; base < st.n_lb; base += 64) {
                 const u32 k = base + L;
                 uint4 o = k < st.n_lb ? ORD()[k] : make_uint4(0, 0, 0, 0);
                 const u32 c = o.w > 8 ? 8u : o.w;
                 const u32 incl = wave_scan_incl(c);
+                const u32 bt = k < st.n_lb ? block_text(o) : 0u;
+                const u32 tincl = wave_scan_incl(bt);
                 u32 at = run + incl - c;
+                u32 tat = trun + tincl - bt;
                 for (u32 s = 0; s < c; s++) {
                     uint4 v = VIS()[o.x * 8 + s], a = AUX()[o.x * 8 + s];
+                    if (!(v.w & F_MARKER)) {  // wave-divergent copy, 8 units in flight per lane
+                        const u16* __restrict__ src = text_ptr(a.y);
+                        u16* __restrict__ dst = tdst + tat;
+                        for (u32 i = 0; i < v.x; i += 8) {
+                            u16 t[8];
+#pragma unroll
+                            for (u32 j = 0; j < 8; j++) t[j] = i + j < v.x ? src[i + j] : (u16)0;
+#pragma unroll
+                            for (u32 j = 0; j < 8; j++)
+                                if (i + j < v.x) dst[i + j] = t[j];
+                        }
+                        a.y = tat;  // offset in the document's text run
+                        tat += v.x;
+                    }
+                    if (a.x && p.out_maps) {  // the row's property map, indexed by row
+                        const uint4* ms = (const uint4*)(maps + (u64)a.x * MAP_WORDS);
+                        uint4* md = (uint4*)(p.out_maps + (u64)(at + s) * MAP_WORDS);
+                        const uint4 m0 = ms[0], m1 = ms[1], m2 = ms[2], m3 = ms[3];
+                        md[0] = m0;
+                        md[1] = m1;
+                        md[2] = m2;
+                        md[3] = m3;
+                    }
                     p.out_vis[at + s] = v;
                     p.out_aux[at + s] = a;
                     u64 m = (v.w & F_OVL) ? (u64)a.z : 0ull;
@@ -1890,6 +1937,7 @@ struct Engine {
                     p.out_ovl[at + s] = m;
                 }
                 run += wave_read(incl, 63);
+                trun += wave_read(tincl, 63);
             }
         }
         const u32 fseq = stat_get(ST_FAILSEQ), ops = stat_get(ST_OPS), msgs = stat_get(ST_MSGS);
@@ -1912,6 +1960,7 @@ struct Engine {
             o.n_gc = ngc;
             o.out_off = off;
             o.n_segs = nseg;
+            o.text_off = toff;
             o.max_lb = maxlb;
             o.mode = LDSM ? 0u : (continued ? 2u : 1u);
         }

@@ -108,7 +108,7 @@ struct DocRes {
     u32 max_lb;      // peak leaf-block count
     u32 mode;        // 0 LDS-resident, 1 HBM-resident
     u32 spill_why;   // why the LDS pass gave the doc up (engine.hpp St::spillWhy)
-    u32 pad;
+    u32 text_off;    // first unit of this doc's gathered final text in the output text pool
 };
 
 // internal status: the LDS-resident replay ran out of room (leaf-block pool, interior nodes, heap
@@ -139,6 +139,9 @@ struct Params {
     uint4* out_aux;
     u64* out_ovl;
     u64 out_cap;
+    u16* out_text;            // final segment texts, one run per document (Engine::finish)
+    u32* out_maps;            // property map of each final row with props (MAP_WORDS per row), or null
+    u64 out_text_cap;
     u32* counters;            // [0] doc queue, [1] output rows, [2] docs re-run by the host,
                               // [3] unused, [4] docs continued HBM-resident
     unsigned char* spill;     // per-wave HBM slots (slot_bytes each): LDS waves 0..8G-1 keep theirs for

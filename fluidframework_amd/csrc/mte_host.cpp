@@ -206,9 +206,9 @@ struct mte_engine {
     double last_kernel_ms = 0, last_h2d_ms = 0;
     // device buffers
     DevBuf<mte_op> d_ops;
-    DevBuf<uint16_t> d_payload, d_arena;
+    DevBuf<uint16_t> d_payload, d_arena, d_out_text;
     DevBuf<mte_propset> d_propsets;
-    DevBuf<uint32_t> d_prop_keys, d_prop_vals, d_val_flags, d_val_objidx, d_order, d_list, d_maps, d_counters,
+    DevBuf<uint32_t> d_out_maps, d_prop_keys, d_prop_vals, d_val_flags, d_val_objidx, d_order, d_list, d_maps, d_counters,
         d_first_seen;
     DevBuf<uint64_t> d_val_objmatch, d_ovl, d_out_ovl, d_prof;
     DevBuf<DocCfg> d_cfg;
@@ -234,7 +234,7 @@ struct mte_engine {
     std::vector<uint32_t> h_maps;
     std::vector<uint4> h_out_vis, h_out_aux;
     std::vector<uint64_t> h_out_ovl;
-    std::vector<uint16_t> h_arena;
+    std::vector<uint16_t> h_out_text;
 };
 
 static int set_err(mte_engine* e, int code, const std::string& m) {
@@ -313,6 +313,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     e->cfg.assign(nd, DocCfg{});
     e->n_ops_doc = n_ops;
     uint64_t op = 0, pay = 0, ar = 0, seg = 0, mp = 0, out = 0;
+    bool any_props = false;
     for (uint32_t d = 0; d < nd; d++) {
         DocCfg& c = e->cfg[d];
         uint64_t n = n_ops[d];
@@ -335,6 +336,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
         c.map_cap = (uint32_t)(n_prop_ins[d] + 4 * n_ann[d] + 16);
         c.map_off = mp;
         mp += c.map_cap;
+        any_props |= n_prop_ins[d] + n_ann[d] > 0;
         c.collab = collab[d];
         c.has_nl = has_nl[d];
         c.prio = 0;
@@ -353,6 +355,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     HIP_TRY(e, e->d_out_vis.alloc(out));
     HIP_TRY(e, e->d_out_aux.alloc(out));
     HIP_TRY(e, e->d_out_ovl.alloc(out));
+    if (any_props) HIP_TRY(e, e->d_out_maps.alloc(out * MAP_WORDS));  // some document can carry props
     HIP_TRY(e, e->d_counters.alloc(8));
     HIP_TRY(e, e->d_res.alloc(nd));
     HIP_TRY(e, e->d_prof.alloc((size_t)nd * PROF_SLOTS));
@@ -378,6 +381,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     P.out_aux = e->d_out_aux.p;
     P.out_ovl = e->d_out_ovl.p;
     P.out_cap = out;
+    P.out_maps = any_props ? e->d_out_maps.p : nullptr;
     P.counters = e->d_counters.p;
     P.prof = e->d_prof.p;
     int cus = 0;
@@ -416,6 +420,16 @@ static void wave_plan(const mte_engine* e, uint32_t nd, uint32_t& groups, uint32
     else h = 0;
     if (groups == 0 && h == 0) h = 1;
     hbm_waves = (uint32_t)h;
+}
+
+// Output text pool: a document's final text never exceeds the text its log inserted, so the
+// payload's size bounds the whole batch (Engine::finish gathers into it).
+static int alloc_out_text(mte_engine* e) {
+    const uint64_t n = std::max<uint64_t>(1, std::min<uint64_t>(e->d_payload.n, 0xFFFFFFFFull));
+    if (n > e->d_out_text.n || !e->d_out_text.p) HIP_TRY(e, e->d_out_text.alloc(n));
+    e->P.out_text = e->d_out_text.p;
+    e->P.out_text_cap = n;
+    return MTE_OK;
 }
 
 static int alloc_slots(mte_engine* e) {
@@ -545,6 +559,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     e->last_h2d_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     e->P.ops = e->d_ops.p;
     e->P.payload = e->d_payload.p;
+    if ((rc = alloc_out_text(e))) return rc;
     return MTE_OK;
 }
 
@@ -711,6 +726,7 @@ int mte_generate(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, 
     if ((rc = upload_props(e))) return rc;
     e->P.ops = e->d_ops.p;
     e->P.payload = e->d_payload.p;
+    if ((rc = alloc_out_text(e))) return rc;
     e->P.gen_first_seen = e->d_first_seen.p;
     e->P.gen_kind = kind;
     e->P.gen_nclients = n_clients;
@@ -764,8 +780,7 @@ int mte_export_batch(mte_engine* e, mte_batch* out) {
 static int ensure_download(mte_engine* e) {
     if (!e->replayed) return set_err(e, MTE_E_STATE, "no replay results yet");
     if (e->downloaded) return MTE_OK;
-    int rc = ensure_host_ops(e);
-    if (rc) return rc;
+    int rc;
     HIP_TRY(e, hipSetDevice(e->device));
     uint32_t ctr[8];
     HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
@@ -775,11 +790,13 @@ static int ensure_download(mte_engine* e) {
         if (n) HIP_TRY(e, hipMemcpy(h.data(), d.p, n * sizeof(h[0]), hipMemcpyDeviceToHost));
         return MTE_OK;
     };
-    if ((rc = dl(e->h_maps, e->d_maps, e->d_maps.n))) return rc;
+    if (e->P.out_maps && (rc = dl(e->h_maps, e->d_out_maps, rows * MAP_WORDS))) return rc;
     if ((rc = dl(e->h_out_vis, e->d_out_vis, rows))) return rc;
     if ((rc = dl(e->h_out_aux, e->d_out_aux, rows))) return rc;
     if ((rc = dl(e->h_out_ovl, e->d_out_ovl, rows))) return rc;
-    if ((rc = dl(e->h_arena, e->d_arena, e->d_arena.n))) return rc;
+    uint64_t units;
+    memcpy(&units, ctr + 6, sizeof units);
+    if ((rc = dl(e->h_out_text, e->d_out_text, std::min<uint64_t>(units, e->P.out_text_cap)))) return rc;
     e->downloaded = true;
     return MTE_OK;
 }
@@ -803,8 +820,7 @@ struct DocView {
     void build() {
         const DocCfg& c = e->cfg[d];
         const DocRes& r = e->res[d];
-        const uint16_t* pay = e->hb.payload.data() + c.payload_off;
-        const uint16_t* ar = e->h_arena.data() + c.arena_off + (uint64_t)r.arena_sel * c.arena_cap;
+        const uint16_t* txt = e->h_out_text.data() + r.text_off;  // gathered by Engine::finish
         if (r.status || (uint64_t)r.out_off + r.n_segs > e->h_out_vis.size()) return;
         for (uint32_t q = 0; q < r.n_segs; q++) {
             {
@@ -821,9 +837,9 @@ struct DocView {
                 sv.client = c.collab ? (int32_t)(v.w & 0xff) : -1;
                 sv.rclient = c.collab ? (int32_t)((v.w >> 8) & 0xff) : -1;
                 sv.ovl = e->h_out_ovl[i];
-                sv.props = a.x;
+                sv.props = a.x ? (uint32_t)(i + 1) : 0u;
                 sv.reftype = sv.kind ? t.x : 0;
-                sv.text = sv.kind ? nullptr : ((t.x & ARENA_BIT) ? ar + (t.x & ~ARENA_BIT) : pay + t.x);
+                sv.text = sv.kind ? nullptr : txt + t.x;
                 segs.push_back(sv);
             }
         }
@@ -832,7 +848,8 @@ struct DocView {
         if (shortId < 0) return "original";
         return e->hb.client(d, (uint32_t)shortId);
     }
-    const uint32_t* map(uint32_t id) const { return e->h_maps.data() + (e->cfg[d].map_off + id) * MAP_WORDS; }
+    // SegView::props: 1 + the row's index in the output pool (its map was copied there), 0 = none
+    const uint32_t* map(uint32_t id) const { return e->h_maps.data() + (uint64_t)(id - 1) * MAP_WORDS; }
     // JSON of a property map in JS key order (integer-like keys ascending first, then insertion order)
     void props_json(std::string& o, uint32_t id) const {
         const uint32_t* m = map(id);

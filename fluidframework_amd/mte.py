@@ -245,7 +245,7 @@ class Engine:
 
     DOC_RESULT_FIELDS = ["status", "failing_seq", "ops", "msgs", "min_seq", "cur_seq", "height", "n_lb",
                          "arena_sel", "arena_top", "map_next", "seg_next", "heap_size", "n_gc", "out_off", "n_segs",
-                         "max_lb", "mode", "spill_why"]
+                         "max_lb", "mode", "spill_why", "text_off"]
 
     def doc_result(self, doc):
         buf = (ctypes.c_int32 * 20)()

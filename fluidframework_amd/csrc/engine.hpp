@@ -1764,6 +1764,100 @@ struct Engine {
         st.gdirty = U(st.gdirty);
     }
 
+    // ---------------------------------------------------------------- resume from a summary
+    // SnapshotLoader (snapshotLoader.ts:113-216) as records (include/mte.h MTE_OP_LOAD_*).
+    // LOAD_SEG: reloadFromSegments fills leaf blocks 7 at a time in document order
+    // (mergeTree.ts:1195-1251); LOAD_END links them into 7-wide interior levels and starts the
+    // collaboration window; LOAD_APPEND is loadBody's insertSegments at the end (refSeq 0, seq 0:
+    // never enqueued for zamboni, blockInsert/saveIfLocal :2164-2179).
+    MTE_DEV void load_record(const mte_op& op) {
+        if (op.type == MTE_OP_LOAD_END) {
+            load_link(op.seq, op.msn);
+            return;
+        }
+        const bool mk = (op.flags & MTE_F_LOAD_MARKER) != 0;
+        Seg rec;
+        rec.len = mk ? 1u : op.b;
+        rec.props = op.props ? build_map(0, op.props, false) : 0u;
+        if (st.status) return;
+        rec.toff = (u32)op.a;  // text offset, or the marker's refType
+        rec.tcap = 0;          // (the overlap mask of a removed segment: empty)
+        rec.sid = 0;
+        if (op.type != MTE_OP_LOAD_SEG || st.root == NONE) {
+            fail(MTE_DOC_UNSUPPORTED, op.seq);
+            return;
+        }
+        const bool rm = (op.flags & MTE_F_LOAD_REMOVED) != 0;
+        rec.seq = op.seq;
+        rec.rseq = rm ? op.ref_seq : 0;
+        rec.meta = (op.client & 0xffu) | (mk ? F_MARKER : 0u) | (rm ? ((((u32)op.pos1 & 0xffu) << 8) | F_REMOVED) : 0u);
+        rec.sid = new_sid();
+        if (rec.sid == NONE) return;
+        u32 k = st.n_lb - 1;
+        uint4 o = ord_u(k);
+        if (o.w >= 7) {  // MaxNodesInBlock - 1 children per reloaded block
+            if (st.n_lb + 1 > ord_cap()) {
+                fail_cap();
+                return;
+            }
+            const u32 nb = alloc_lb();
+            if (nb == NONE) return;
+            k = st.n_lb++;
+            stat_max(ST_MAXLB, st.n_lb);
+            o = make_uint4(nb, 0, 0, 0);
+        }
+        if (L == 0) {
+            store(o.x, o.w, rec);
+            o.y += obs_len(rec.len, rec.meta);
+            const i32 hi = seq_hi(rec.seq, rec.rseq, rec.meta);
+            if (hi > (i32)o.z) o.z = (u32)hi;
+            o.w += 1;
+            ORD()[k] = o;
+        }
+        sync();
+    }
+    // buildMergeBlock (mergeTree.ts:1202-1230) over the reloaded leaves, then
+    // startOrUpdateCollaboration(minSeq, currentSeq) (snapshotLoader.ts:126-140).
+    MTE_DEV void load_link(i32 cur, i32 msn) {
+        if (msn > cur || st.heapSize != 0 || st.inUsed != 0 || st.inFree != NONE) {
+            fail(MTE_DOC_SEQ_ORDER, cur);
+            return;
+        }
+        u32 m = st.n_lb;    // nodes on the level below
+        u32 below = NONE;   // first interior id of the level below (NONE: the leaves, in doc order)
+        u32 height = 1;
+        while (m > 1) {
+            const u32 groups = (m + 6) / 7;
+            u32 base = NONE;
+            for (u32 g = 0; g < groups; g++) {
+                const u32 id = alloc_in();
+                if (id == NONE) return;
+                if (g == 0) base = id;
+                if (id != base + g) {  // a fresh document's interior ids are consecutive
+                    fail(MTE_DOC_CAPACITY, cur);
+                    return;
+                }
+                const u32 c0 = g * 7, cn = m - c0 < 7 ? m - c0 : 7u;
+                if (L < cn) {
+                    const u32 child = below == NONE ? ORD()[c0 + L].x : below + c0 + L;
+                    INCH()[id * 8 + L] = child;
+                    if (below == NONE) set_bpar_lane(child, id);
+                    else if (child < in_cap()) INPAR()[child] = id;
+                }
+                if (L == 0) INCNT()[id] = cn;
+                sync();
+            }
+            below = base;
+            m = groups;
+            height++;
+        }
+        st.root = below == NONE ? U(ORD()[0].x) : below;
+        st.height = height;
+        st.curSeq = cur;
+        st.minSeq = msn;
+        sync();
+    }
+
     // Client.applyMsg for one op record (client.ts:805-836): the edit, zamboni, then
     // updateSeqNumbers / setMinSeq (client.ts:829-836, mergeTree.ts:1718-1736) and zamboni again
     // when the MSN advanced. One zamboni call site.
@@ -1774,29 +1868,37 @@ struct Engine {
             fail(MTE_DOC_UNSUPPORTED, op.seq);
             return;
         }
+        // LOAD_APPEND (loadBody's insertSegments: refSeq 0, seq 0) shares the insert path below
+        const bool app = op.type == MTE_OP_LOAD_APPEND;
+        if (op.type >= MTE_OP_LOAD_SEG && !app) {
+            if (collab) load_record(op);
+            else fail(MTE_DOC_UNSUPPORTED, op.seq);
+            return;
+        }
         const u32 C = collab ? (u32)op.client : 0u;
-        const i32 seq = collab ? op.seq : 0;
-        const i32 R = collab ? op.ref_seq : 0;
-        if (collab && op.type != MTE_OP_NOOP && !(st.curSeq < op.seq)) {
+        const i32 seq = collab && !app ? op.seq : 0;
+        const i32 R = collab && !app ? op.ref_seq : 0;
+        if (collab && !app && op.type != MTE_OP_NOOP && !(st.curSeq < op.seq)) {
             fail(MTE_DOC_SEQ_ORDER, op.seq);
             return;
         }
         bool edited = false;
-        if (op.type <= MTE_OP_INSERT_MARKER) {
+        if (op.type <= MTE_OP_INSERT_MARKER || app) {
             Seg rec;
-            const bool mk = op.type == MTE_OP_INSERT_MARKER;
-            const bool ins = op.type == MTE_OP_INSERT || mk;
+            const bool mk = op.type == MTE_OP_INSERT_MARKER || (app && (op.flags & MTE_F_LOAD_MARKER));
+            const bool ins = op.type == MTE_OP_INSERT || op.type == MTE_OP_INSERT_MARKER || app;
             rec.len = mk ? 1u : op.b;
             rec.seq = seq;
             rec.rseq = 0;
             rec.meta = (C & 0xff) | (mk ? F_MARKER : 0u);
             rec.props = (ins && op.props) ? build_map(0, op.props, false) : 0u;
             if (st.status) return;
-            rec.toff = mk ? op.b : (u32)op.a;
+            rec.toff = mk && !app ? op.b : (u32)op.a;
             rec.tcap = 0;
             rec.sid = 0;
-            edited = edit(op.type, op.pos1, op.a, R, C, seq, rec, op.props, (op.flags & MTE_F_REWRITE) != 0);
-            stat_add(ST_OPS, 1);
+            edited = edit(app ? (u32)MTE_OP_INSERT : (u32)op.type, op.pos1, op.a, R, C, seq, rec, op.props,
+                          (op.flags & MTE_F_REWRITE) != 0);
+            if (!app) stat_add(ST_OPS, 1);
             if (st.status) return;
         }
         for (u32 z = 0; z < 2; z++) {

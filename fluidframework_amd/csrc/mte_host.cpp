@@ -520,7 +520,9 @@ static void count_doc_ops(const HostBatch& hb, uint32_t d, uint64_t& pi, uint64_
     pi = an = 0;
     for (uint64_t i = hb.doc_op_offsets[d]; i < hb.doc_op_offsets[d + 1]; i++) {
         const mte_op& o = hb.ops[i];
-        if ((o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER) && o.props) pi++;
+        if ((o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER || o.type == MTE_OP_LOAD_SEG ||
+             o.type == MTE_OP_LOAD_APPEND) && o.props)
+            pi++;
         if (o.type == MTE_OP_ANNOTATE) an++;
     }
 }
@@ -1300,32 +1302,57 @@ static int num_field(const json::Value& o, const char16_t* k, int32_t* out) {
     return 1;
 }
 
-int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* text, size_t len) {
-    if (!b || !text) return MTE_E_ARG;
-    HostBatch& hb = b->hb;
-    json::Value doc;
-    try {
-        doc = json::parse(text, len);
-    } catch (std::exception& ex) {
-        b->err = ex.what();
-        return MTE_E_PARSE;
-    }
-    if (doc.kind != json::Value::Array) {
-        b->err = "op log must be a JSON array of messages";
-        return MTE_E_PARSE;
-    }
+// One document under construction: its records, payload and short-id table (observer = 0).
+struct DocBuild {
     std::vector<mte_op> ops;
     std::vector<uint16_t> payload;
     std::vector<std::string> names;
     std::unordered_map<std::string, uint32_t> ids;
-    const std::string observer = observer_name ? observer_name : "";
-    names.push_back(observer);
-    ids[observer] = 0;
-    const bool collab = !observer.empty();
-    auto fail = [&](int code, const std::string& m) {
-        b->err = m;
+    bool collab = false;
+    std::string err;
+    explicit DocBuild(const char* observer_name) {
+        const std::string observer = observer_name ? observer_name : "";
+        names.push_back(observer);
+        ids[observer] = 0;
+        collab = !observer.empty();
+    }
+    int fail(int code, const std::string& m) {
+        err = m;
         return code;
-    };
+    }
+    // getOrAddShortClientId (client.ts:644-668)
+    int short_id(const std::string& name, uint32_t* out) {
+        auto it = ids.find(name);
+        if (it != ids.end()) {
+            *out = it->second;
+            return MTE_OK;
+        }
+        if (names.size() >= MTE_MAX_CLIENTS) return fail(MTE_E_UNSUPPORTED, "more than 64 clients in a document");
+        *out = (uint32_t)names.size();
+        names.push_back(name);
+        ids[name] = *out;
+        return MTE_OK;
+    }
+    void commit(HostBatch& hb) {
+        hb.ops.insert(hb.ops.end(), ops.begin(), ops.end());
+        hb.doc_op_offsets.push_back(hb.ops.size());
+        hb.payload.insert(hb.payload.end(), payload.begin(), payload.end());
+        hb.doc_payload_offsets.push_back(hb.payload.size());
+        for (auto& nm : names) {
+            hb.client_names += nm;
+            hb.client_name_offsets.push_back(hb.client_names.size());
+        }
+        hb.doc_client_offsets.push_back(hb.doc_client_offsets.back() + (uint32_t)names.size());
+    }
+};
+
+// A JSON array of ISequencedDocumentMessage -> op records appended to `db`.
+static int add_messages(mte_builder* b, const json::Value& doc, DocBuild& db) {
+    std::vector<mte_op>& ops = db.ops;
+    std::vector<uint16_t>& payload = db.payload;
+    const bool collab = db.collab;
+    auto fail = [&](int code, const std::string& m) { return db.fail(code, m); };
+    if (doc.kind != json::Value::Array) return fail(MTE_E_PARSE, "op log must be a JSON array of messages");
     for (const json::Value& m : doc.items) {
         if (m.kind != json::Value::Object) return fail(MTE_E_PARSE, "message is not an object");
         mte_op base{};
@@ -1335,16 +1362,8 @@ int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* t
         const json::Value* cid = m.get(u"clientId");
         std::string name = (cid && cid->kind == json::Value::String) ? json::to_utf8(cid->str.data(), cid->str.size()) : "";
         if (!collab) name = "";
-        auto it = ids.find(name);
         uint32_t sid;
-        if (it == ids.end()) {
-            sid = (uint32_t)names.size();
-            if (sid >= MTE_MAX_CLIENTS) return fail(MTE_E_UNSUPPORTED, "more than 64 clients in a document");
-            names.push_back(name);
-            ids[name] = sid;
-        } else {
-            sid = it->second;
-        }
+        if (int rc = db.short_id(name, &sid)) return rc;
         base.client = (uint8_t)sid;
         const json::Value* type = m.get(u"type");
         const json::Value* contents = m.get(u"contents");
@@ -1431,15 +1450,191 @@ int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* t
         }
         ops.back().flags |= MTE_F_END_OF_MSG;
     }
-    hb.ops.insert(hb.ops.end(), ops.begin(), ops.end());
-    hb.doc_op_offsets.push_back(hb.ops.size());
-    hb.payload.insert(hb.payload.end(), payload.begin(), payload.end());
-    hb.doc_payload_offsets.push_back(hb.payload.size());
-    for (auto& nm : names) {
-        hb.client_names += nm;
-        hb.client_name_offsets.push_back(hb.client_names.size());
+    return MTE_OK;
+}
+
+int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* text, size_t len) {
+    if (!b || !text) return MTE_E_ARG;
+    json::Value doc;
+    try {
+        doc = json::parse(text, len);
+    } catch (std::exception& ex) {
+        b->err = ex.what();
+        return MTE_E_PARSE;
     }
-    hb.doc_client_offsets.push_back(hb.doc_client_offsets.back() + (uint32_t)names.size());
+    DocBuild db(observer_name);
+    if (int rc = add_messages(b, doc, db)) {
+        b->err = db.err;
+        return rc;
+    }
+    db.commit(b->hb);
+    return MTE_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Resume from a summary: SnapshotLoader (snapshotLoader.ts:38-216) as LOAD records (include/mte.h).
+
+// A segment spec (sequenceFactory.ts:31-37: string | {text, props} | {marker, props}) -> o.a/o.b/props.
+static int load_spec(mte_builder* b, DocBuild& db, const json::Value& seg, mte_op& o) {
+    const json::Value* props = nullptr;
+    if (seg.kind == json::Value::String) {
+        o.a = (int32_t)db.payload.size();
+        o.b = (uint32_t)seg.str.size();
+        db.payload.insert(db.payload.end(), seg.str.begin(), seg.str.end());
+    } else if (seg.kind == json::Value::Object && seg.get(u"marker")) {
+        const json::Value* mk = seg.get(u"marker");
+        int32_t rt = 0;
+        if (mk->kind == json::Value::Object) num_field(*mk, u"refType", &rt);
+        o.a = rt;
+        o.b = 1;
+        o.flags |= MTE_F_LOAD_MARKER;
+        props = seg.get(u"props");
+    } else if (seg.kind == json::Value::Object && seg.get(u"text") && seg.get(u"text")->kind == json::Value::String) {
+        const json::Value* tx = seg.get(u"text");
+        o.a = (int32_t)db.payload.size();
+        o.b = (uint32_t)tx->str.size();
+        db.payload.insert(db.payload.end(), tx->str.begin(), tx->str.end());
+        props = seg.get(u"props");
+    } else {
+        return db.fail(MTE_E_UNSUPPORTED, "unknown segment spec");
+    }
+    if (props && json::truthy(props)) {
+        if (props->kind != json::Value::Object) return db.fail(MTE_E_UNSUPPORTED, "non-object props");
+        o.props = b->in->propset(*props);
+    }
+    return MTE_OK;
+}
+
+static const json::Value* tree_entry(const json::Value& tree, const char16_t* path) {
+    const json::Value* es = tree.kind == json::Value::Object ? tree.get(u"entries") : nullptr;
+    if (!es || es->kind != json::Value::Array) return nullptr;
+    for (const json::Value& e : es->items) {
+        const json::Value* p = e.kind == json::Value::Object ? e.get(u"path") : nullptr;
+        if (p && p->kind == json::Value::String && p->str == path) return &e;
+    }
+    return nullptr;
+}
+
+// storage.read(path) + SnapshotV1.processChunk (snapshotV1.ts:249-270) for a utf-8 blob
+static int load_chunk(DocBuild& db, const json::Value& tree, const std::u16string& path, json::Value* out) {
+    const json::Value* e = tree_entry(tree, path.c_str());
+    const json::Value* v = e ? e->get(u"value") : nullptr;
+    const json::Value* c = v && v->kind == json::Value::Object ? v->get(u"contents") : nullptr;
+    const json::Value* enc = v && v->kind == json::Value::Object ? v->get(u"encoding") : nullptr;
+    if (!c || c->kind != json::Value::String) return db.fail(MTE_E_PARSE, "summary blob missing");
+    if (enc && !(enc->kind == json::Value::String && enc->str == u"utf-8"))
+        return db.fail(MTE_E_UNSUPPORTED, "only utf-8 blob contents are supported");
+    const std::string text = json::to_utf8(c->str.data(), c->str.size());
+    try {
+        *out = json::parse(text.data(), text.size());
+    } catch (std::exception& ex) {
+        return db.fail(MTE_E_PARSE, ex.what());
+    }
+    const json::Value* ver = out->kind == json::Value::Object ? out->get(u"version") : nullptr;
+    if (!ver || ver->kind != json::Value::String || ver->str != u"1")
+        return db.fail(MTE_E_UNSUPPORTED, "legacy (pre-v1) snapshot chunks are out of scope");
+    return MTE_OK;
+}
+
+// NonCollabClient (constants.ts) as a short id: the name getLongClientId gives it (client.ts:653-659).
+// SnapshotV1 never emits it: universal segments carry no merge info (snapshotV1.ts:219-223).
+static const char* const kNonCollabName = "original";
+
+static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db) {
+    if (!db.collab) return db.fail(MTE_E_ARG, "a summary is loaded by a collaborating client (observer name)");
+    const json::Value* t = &summary;
+    const json::Value* content = tree_entry(summary, u"content");
+    if (content && content->get(u"value")) t = content->get(u"value");  // SharedString summary (sequence.ts:413-438)
+    json::Value header;
+    if (int rc = load_chunk(db, *t, u"header", &header)) return rc;
+    const json::Value* md = header.get(u"headerMetadata");
+    if (!md || md->kind != json::Value::Object) return db.fail(MTE_E_PARSE, "header metadata not available");
+    bool mergeInfo = false;
+    const json::Value* hs = header.get(u"segments");
+    if (hs && hs->kind == json::Value::Array) {
+        for (const json::Value& sp : hs->items) {
+            mte_op o{};
+            o.type = MTE_OP_LOAD_SEG;
+            const json::Value* js = sp.kind == json::Value::Object ? sp.get(u"json") : nullptr;  // hasMergeInfo
+            if (int rc = load_spec(b, db, js ? *js : sp, o)) return rc;
+            std::string client = kNonCollabName;
+            if (js) {
+                mergeInfo = true;
+                const json::Value* c = sp.get(u"client");
+                if (c && c->kind == json::Value::String) client = json::to_utf8(c->str.data(), c->str.size());
+                num_field(sp, u"seq", &o.seq);
+            }
+            uint32_t cid;
+            if (int rc = db.short_id(client, &cid)) return rc;
+            o.client = (uint8_t)cid;
+            if (js && num_field(sp, u"removedSeq", &o.ref_seq)) {
+                o.flags |= MTE_F_LOAD_REMOVED;
+                const json::Value* rc = sp.get(u"removedClient");
+                std::string rn = rc && rc->kind == json::Value::String ? json::to_utf8(rc->str.data(), rc->str.size())
+                                                                       : kNonCollabName;
+                uint32_t rid;
+                if (int e = db.short_id(rn, &rid)) return e;
+                o.pos1 = (int32_t)rid;
+            }
+            db.ops.push_back(o);
+        }
+    }
+    mte_op end{};
+    end.type = MTE_OP_LOAD_END;
+    num_field(*md, u"sequenceNumber", &end.seq);
+    end.msn = end.seq;
+    num_field(*md, u"minSequenceNumber", &end.msn);
+    db.ops.push_back(end);
+    // loadBody (:150-216): later chunks appended at root.cachedLength, refSeq 0, NonCollab, seq 0
+    const json::Value* ocm = md->get(u"orderedChunkMetadata");
+    if (!ocm || ocm->kind != json::Value::Array || ocm->items.size() <= 1) return MTE_OK;
+    if (mergeInfo) return db.fail(MTE_E_UNSUPPORTED, "body chunks after a header with merge info");
+    int32_t pos = 0;
+    for (const mte_op& o : db.ops)
+        if (o.type == MTE_OP_LOAD_SEG && !(o.flags & MTE_F_LOAD_REMOVED)) pos += (int32_t)o.b;
+    uint32_t nc;
+    if (int rc = db.short_id(kNonCollabName, &nc)) return rc;
+    for (size_t i = 1; i < ocm->items.size(); i++) {
+        const json::Value* id = ocm->items[i].kind == json::Value::Object ? ocm->items[i].get(u"id") : nullptr;
+        if (!id || id->kind != json::Value::String) return db.fail(MTE_E_PARSE, "chunk id");
+        json::Value ch;
+        if (int rc = load_chunk(db, *t, id->str, &ch)) return rc;
+        const json::Value* cs = ch.get(u"segments");
+        if (!cs || cs->kind != json::Value::Array) continue;
+        for (const json::Value& sp : cs->items) {
+            if (sp.kind == json::Value::Object && sp.get(u"json"))  // flushBatch never clears (:196-199)
+                return db.fail(MTE_E_UNSUPPORTED, "merge-info segment in a body chunk");
+            mte_op o{};
+            o.type = MTE_OP_LOAD_APPEND;
+            if (int rc = load_spec(b, db, sp, o)) return rc;
+            o.client = (uint8_t)nc;
+            o.pos1 = pos;
+            pos += (int32_t)o.b;
+            db.ops.push_back(o);
+        }
+    }
+    return MTE_OK;
+}
+
+int mte_builder_add_doc_from_summary(mte_builder* b, const char* observer_name, const char* summary,
+                                     size_t summary_len, const char* ops, size_t ops_len) {
+    if (!b || !summary) return MTE_E_ARG;
+    DocBuild db(observer_name);
+    json::Value s, log;
+    try {
+        s = json::parse(summary, summary_len);
+        if (ops) log = json::parse(ops, ops_len);
+    } catch (std::exception& ex) {
+        b->err = ex.what();
+        return MTE_E_PARSE;
+    }
+    int rc = add_summary(b, s, db);
+    if (!rc && ops) rc = add_messages(b, log, db);
+    if (rc) {
+        b->err = db.err;
+        return rc;
+    }
+    db.commit(b->hb);
     return MTE_OK;
 }
 

@@ -77,7 +77,7 @@ SUMMARY_DTYPE = np.dtype([("checksum", "<u8"), ("ops", "<u4"), ("length", "<u4")
 # Every symbol declared in include/mte.h (checked by tests/test_abi.py).
 EXPORTS = ["mte_abi_version", "mte_build_info", "mte_create", "mte_destroy", "mte_last_error", "mte_load",
            "mte_replay", "mte_generate", "mte_export_batch", "mte_doc_status", "mte_text", "mte_segments",
-           "mte_snapshot_v1", "mte_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_batch",
+           "mte_snapshot_v1", "mte_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_batch",
            "mte_builder_error", "mte_builder_destroy"]
 
 _lib = None
@@ -117,6 +117,7 @@ def lib():
         L.mte_last_kernel_ms.restype = ctypes.c_double
         L.mte_builder_create.argtypes = [ctypes.POINTER(vp)]
         L.mte_builder_add_doc.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
+        L.mte_builder_add_doc_from_summary.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, sz]
         L.mte_builder_batch.argtypes = [vp, ctypes.POINTER(mte_batch)]
         L.mte_builder_error.argtypes = [vp]
         L.mte_builder_error.restype = ctypes.c_char_p
@@ -148,6 +149,19 @@ class Builder:
         rc = lib().mte_builder_add_doc(self._h, observer.encode(), b, len(b))
         if rc:
             raise MteError(f"mte_builder_add_doc: {rc}: {lib().mte_builder_error(self._h).decode()}")
+
+    def add_doc_from_summary(self, summary, messages=None, observer="__observer__"):
+        """Catch-up: a SnapshotV1 summary (ITree JSON text or dict) then an op-log suffix
+        (SnapshotLoader.initialize + applyMsg, snapshotLoader.ts:38-216)."""
+        def enc(x):
+            if x is None:
+                return None
+            t = x if isinstance(x, (str, bytes)) else json.dumps(x, separators=(",", ":"), ensure_ascii=False)
+            return t.encode() if isinstance(t, str) else t
+        s, m = enc(summary), enc(messages)
+        rc = lib().mte_builder_add_doc_from_summary(self._h, observer.encode(), s, len(s), m, len(m) if m else 0)
+        if rc:
+            raise MteError(f"mte_builder_add_doc_from_summary: {rc}: {lib().mte_builder_error(self._h).decode()}")
 
     def batch(self):
         b = mte_batch()

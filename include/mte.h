@@ -62,11 +62,24 @@ enum {
     MTE_OP_ANNOTATE = 2,      /* annotate [pos1, a) with prop set `props` */
     MTE_OP_INSERT_MARKER = 3, /* insert Marker: b = refType, props = marker props */
     MTE_OP_NOOP = 4,          /* sequenced message with no merge-tree op (only seq/msn advance) */
+    /* Resume from a summary (SnapshotLoader, snapshotLoader.ts:98-216); records precede the op log.
+     * LOAD_SEG: one header segment in document order (specToSegment :79-111): a = payload offset
+     *   (text) or refType (marker, MTE_F_LOAD_MARKER), b = length, seq = seg.seq (0 = universal),
+     *   client = seg.clientId, props; MTE_F_LOAD_REMOVED: ref_seq = removedSeq, pos1 = removedClient.
+     * LOAD_END: reloadFromSegments of the LOAD_SEGs (mergeTree.ts:1195-1251), then
+     *   startOrUpdateCollaboration(minSeq = msn, currentSeq = seq) (snapshotLoader.ts:126-140).
+     * LOAD_APPEND: one body segment appended (loadBody, :166-213: insertSegments at the end with
+     *   refSeq 0, client NonCollab, seq 0); fields as INSERT / INSERT_MARKER (marker flag). */
+    MTE_OP_LOAD_SEG = 5,
+    MTE_OP_LOAD_END = 6,
+    MTE_OP_LOAD_APPEND = 7,
 };
 
 /* flags */
 #define MTE_F_END_OF_MSG 0x1u   /* last op of its ISequencedDocumentMessage: currentSeq=seq, setMinSeq(msn) */
 #define MTE_F_REWRITE 0x2u      /* annotate combiningOp {name:"rewrite"} (segmentPropertiesManager.ts:65-78) */
+#define MTE_F_LOAD_MARKER 0x4u  /* LOAD_SEG / LOAD_APPEND: a Marker (a = refType, length 1) */
+#define MTE_F_LOAD_REMOVED 0x8u /* LOAD_SEG: removed (ref_seq = removedSeq, pos1 = removedClient) */
 
 typedef struct mte_op {
     int32_t seq;        /* sequenceNumber */
@@ -197,6 +210,13 @@ int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap);
 typedef struct mte_builder mte_builder;
 int mte_builder_create(mte_builder** out);
 int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* json, size_t len);
+/* Catch-up from a summary: SharedSegmentSequence.load + SnapshotLoader.initialize
+ * (sequence.ts:593-633, snapshotLoader.ts:38-216) then applyMsg for the op-log suffix.
+ * summary: the ITree JSON of mte_snapshot_v1 ({"entries":[header, body_0, ...]}) or a SharedString
+ * tree holding it under "content"; blob contents utf-8. ops may be NULL (no suffix).
+ * MTE_E_UNSUPPORTED for legacy (non-"1") chunks and for body chunks next to merge-info segments. */
+int mte_builder_add_doc_from_summary(mte_builder* b, const char* observer_name, const char* summary,
+                                     size_t summary_len, const char* ops, size_t ops_len);
 int mte_builder_batch(mte_builder* b, mte_batch* out);   /* view valid until destroy */
 const char* mte_builder_error(const mte_builder* b);
 void mte_builder_destroy(mte_builder* b);

@@ -30,6 +30,7 @@ def lib():
         L.orc_str_free.argtypes = [vp]
         L.orc_apply_json.argtypes = [vp, cp, ctypes.c_size_t]
         L.orc_apply_batch.argtypes = [vp, vp, u32]
+        L.orc_load_summary.argtypes = [vp, cp, ctypes.c_size_t]
         L.orc_local_insert_text.argtypes = [vp, i32, cp, cp]
         L.orc_local_insert_marker.argtypes = [vp, i32, i32, cp]
         L.orc_local_remove.argtypes = [vp, i32, i32]
@@ -74,6 +75,11 @@ class OracleDoc:
     def apply_json(self, text):
         b = text.encode() if isinstance(text, str) else text
         return lib().orc_apply_json(self._h, b, len(b))
+
+    def load_summary(self, text):
+        """SnapshotLoader: resume from a summary ITree (JSON text); the doc must be fresh."""
+        b = text.encode() if isinstance(text, str) else text
+        return lib().orc_load_summary(self._h, b, len(b))
 
     def apply_batch(self, batch_ptr, doc):
         return lib().orc_apply_batch(self._h, batch_ptr, doc)

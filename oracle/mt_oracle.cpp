@@ -239,6 +239,31 @@ class MergeTree {
         heap = Heap();
     }
 
+    // reloadFromSegments (mergeTree.ts:1195-1251): the B-tree is built bottom-up, level by level,
+    // MaxNodesInBlock - 1 = 7 children per block, until one block remains (the root).
+    void reloadFromSegments(std::vector<Node*> nodes) {
+        const int maxChildren = MaxNodesInBlock - 1;
+        if (nodes.empty()) {
+            root = makeBlock(0);
+            return;
+        }
+        for (;;) {
+            std::vector<Node*> blocks;
+            for (size_t ni = 0; ni < nodes.size();) {
+                Block* b = makeBlock(0);
+                for (int c = 0; c < maxChildren && ni < nodes.size(); c++, ni++) assignChild(b, nodes[ni], b->childCount++);
+                blocks.push_back(b);
+            }
+            if (blocks.size() == 1) {
+                root = (Block*)blocks[0];
+                break;
+            }
+            nodes.swap(blocks);
+        }
+        root->parent = nullptr;
+        root->index = 0;
+    }
+
     // mergeTree.ts:1161-1172
     int localNetLength(const Segment* s) const { return s->removed ? 0 : s->len; }
 
@@ -863,6 +888,105 @@ class Doc {
         }
     }
 
+    // ---- resume from a summary (SnapshotLoader, snapshotLoader.ts) ----------------------------
+    // specToSegment (snapshotLoader.ts:79-111): merge info (hasMergeInfo, snapshotChunks.ts:71-73)
+    // carries client / seq / removedSeq / removedClient; a bare spec is universal and NonCollab.
+    Segment* loadSpec(const JV& spec) {
+        JVP json = spec.t == JV::Obj ? spec.o.get(u"json") : nullptr;
+        if (!json) {
+            Segment* s = makeSegment(spec);
+            s->seq = UniversalSequenceNumber;
+            s->clientId = NonCollabClient;
+            return s;
+        }
+        Segment* s = makeSegment(*json);
+        JVP c = spec.o.get(u"client"), sq = spec.o.get(u"seq"), rs = spec.o.get(u"removedSeq"),
+            rc = spec.o.get(u"removedClient");
+        s->clientId = c && c->t == JV::Str ? getOrAddShortClientId(u16_to_utf8(c->s)) : NonCollabClient;
+        s->seq = sq && sq->t == JV::Num ? (int)sq->n : UniversalSequenceNumber;
+        if (rs && rs->t == JV::Num) {
+            s->removed = true;
+            s->removedSeq = (int)rs->n;
+        }
+        if (rc && rc->t == JV::Str) s->removedClientId = getOrAddShortClientId(u16_to_utf8(rc->s));
+        return s;
+    }
+    static JVP treeEntry(const JV& tree, const u16s& path) {
+        JVP es = tree.t == JV::Obj ? tree.o.get(u"entries") : nullptr;
+        if (!es || es->t != JV::Arr) return nullptr;
+        for (auto& e : es->a) {
+            JVP p = e->t == JV::Obj ? e->o.get(u"path") : nullptr;
+            if (p && p->t == JV::Str && p->s == path) return e;
+        }
+        return nullptr;
+    }
+    // storage.read(path) + SnapshotV1.processChunk (snapshotV1.ts:249-270) for a utf-8 blob
+    static JVP chunkAt(const JV& tree, const u16s& path) {
+        JVP e = treeEntry(tree, path);
+        JVP v = e ? e->o.get(u"value") : nullptr;
+        JVP c = v && v->t == JV::Obj ? v->o.get(u"contents") : nullptr;
+        JVP enc = v && v->t == JV::Obj ? v->o.get(u"encoding") : nullptr;
+        if (!c || c->t != JV::Str) throw EngineError(MTE_DOC_UNSUPPORTED, "summary blob missing");
+        if (enc && !(enc->t == JV::Str && enc->s == u"utf-8")) throw EngineError(MTE_DOC_UNSUPPORTED, "blob encoding");
+        std::string s = u16_to_utf8(c->s);
+        JVP ch = parse(s.data(), s.size());
+        JVP ver = ch->t == JV::Obj ? ch->o.get(u"version") : nullptr;
+        if (!ver || ver->t != JV::Str || ver->s != u"1") throw EngineError(MTE_DOC_UNSUPPORTED, "legacy chunk");
+        return ch;
+    }
+    // SnapshotLoader.initialize: loadHeader (:113-148) then loadBody (:150-216).
+    void loadSnapshot(const JV& summary) {
+        const JV* t = &summary;
+        JVP content = treeEntry(summary, u"content"), inner;
+        if (content) {  // SharedString summary: the merge-tree lives under "content" (sequence.ts:413-438)
+            inner = content->o.get(u"value");
+            if (inner) t = inner.get();
+        }
+        JVP header = chunkAt(*t, u"header");
+        JVP md = header->o.get(u"headerMetadata");
+        if (!md || md->t != JV::Obj) throw EngineError(MTE_DOC_UNSUPPORTED, "header metadata not available");
+        std::vector<Node*> segs;
+        JVP hs = header->o.get(u"segments");
+        if (hs && hs->t == JV::Arr)
+            for (auto& sp : hs->a) segs.push_back(loadSpec(*sp));
+        mt.reloadFromSegments(segs);
+        bool hasMin = false;
+        const int cur = num(md->o, u"sequenceNumber");
+        const int minSeq = num(md->o, u"minSequenceNumber", &hasMin);
+        mt.startCollaboration(0, hasMin ? minSeq : cur, cur);
+        // loadBody: every later chunk's segments, appended at root.cachedLength with refSeq 0
+        std::vector<Segment*> batch;
+        JVP ocm = md->o.get(u"orderedChunkMetadata");
+        for (size_t i = 1; ocm && ocm->t == JV::Arr && i < ocm->a.size(); i++) {
+            JVP id = ocm->a[i]->t == JV::Obj ? ocm->a[i]->o.get(u"id") : nullptr;
+            if (!id || id->t != JV::Str) throw EngineError(MTE_DOC_UNSUPPORTED, "chunk id");
+            JVP ch = chunkAt(*t, id->s);
+            JVP cs = ch->o.get(u"segments");
+            if (!cs || cs->t != JV::Arr) continue;
+            for (auto& sp : cs->a) {
+                Segment* s = loadSpec(*sp);
+                // a merge-info body segment would hit flushBatch's never-cleared batch (:196-199)
+                if (!(s->clientId == NonCollabClient && s->seq == UniversalSequenceNumber))
+                    throw EngineError(MTE_DOC_UNSUPPORTED, "merge-info segment in a body chunk");
+                batch.push_back(s);
+            }
+        }
+        if (!batch.empty()) mt.insertSegments(mt.localLength(mt.root), batch, 0, NonCollabClient, 0);
+    }
+    int loadSnapshotJson(const char* json, size_t len) {
+        try {
+            JVP v = parse(json, len);
+            loadSnapshot(*v);
+        } catch (EngineError& e) {
+            status = e.code;
+            error = e.what();
+        } catch (std::exception& e) {
+            status = MTE_DOC_UNSUPPORTED;
+            error = e.what();
+        }
+        return status;
+    }
+
     void updateSeqNumbers(int msn, int seq) {
         if (seq < mt.cw.currentSeq) throw EngineError(MTE_DOC_SEQ_ORDER, "seq < currentSeq");
         mt.cw.currentSeq = seq;
@@ -893,12 +1017,48 @@ class Doc {
             names.emplace_back(b->client_names + b->client_name_offsets[c],
                                b->client_names + b->client_name_offsets[c + 1]);
         const uint16_t* payload = b->payload + b->doc_payload_offsets[d];
+        std::vector<Node*> loadSegs;
         for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1] && !status; i++) {
             const mte_op& op = b->ops[i];
             try {
                 if (op.client >= names.size()) throw EngineError(MTE_DOC_UNSUPPORTED, "client id out of range");
                 int shortId = getOrAddShortClientId(names[op.client]);
                 if (shortId != op.client) throw EngineError(MTE_DOC_UNSUPPORTED, "client ids not in first-appearance order");
+                if (op.type >= MTE_OP_LOAD_SEG) {  // summary records (include/mte.h; loadSnapshot above)
+                    if (op.type == MTE_OP_LOAD_END) {
+                        mt.reloadFromSegments(loadSegs);
+                        loadSegs.clear();
+                        mt.startCollaboration(0, op.msn, op.seq);
+                        continue;
+                    }
+                    Segment* s = mt.newSegment();
+                    if (op.flags & MTE_F_LOAD_MARKER) {
+                        s->marker = true;
+                        s->refType = op.a;
+                        s->len = 1;
+                    } else {
+                        s->text.assign((const char16_t*)payload + op.a, op.b);
+                        s->len = (int)op.b;
+                    }
+                    if (op.props) MergeTree::addProperties(s, propset(b, op.props), false);
+                    if (op.type == MTE_OP_LOAD_APPEND) {
+                        std::vector<Segment*> segs{s};
+                        mt.insertSegments(op.pos1, segs, 0, op.client, 0);
+                        continue;
+                    }
+                    s->seq = op.seq;
+                    s->clientId = op.client;
+                    if (op.flags & MTE_F_LOAD_REMOVED) {
+                        if (op.pos1 < 0 || (size_t)op.pos1 >= names.size() ||
+                            getOrAddShortClientId(names[op.pos1]) != op.pos1)
+                            throw EngineError(MTE_DOC_UNSUPPORTED, "removed client id");
+                        s->removed = true;
+                        s->removedSeq = op.ref_seq;
+                        s->removedClientId = op.pos1;
+                    }
+                    loadSegs.push_back(s);
+                    continue;
+                }
                 if (op.type != MTE_OP_NOOP && !(mt.cw.currentSeq < op.seq))
                     throw EngineError(MTE_DOC_SEQ_ORDER, "seq <= currentSeq");
                 switch (op.type) {
@@ -1151,6 +1311,9 @@ int orc_apply_json(Doc* d, const char* json, size_t len) {
     }
     return d->status;
 }
+
+// Resume from a summary ITree JSON (SnapshotLoader); the doc must be fresh (observer set).
+int orc_load_summary(Doc* d, const char* json, size_t len) { return d->loadSnapshotJson(json, len); }
 
 int orc_apply_batch(Doc* d, const mte_batch* b, uint32_t doc) {
     d->applyBatch(b, doc);

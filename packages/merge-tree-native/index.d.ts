@@ -8,7 +8,8 @@ export interface DocSummary {
     checksum: bigint | string; ops: number; length: number; segments: number;
     snapshotBytes: number; status: number; docId: number;
 }
-export interface DocLog { observer?: string; messages: ISequencedDocumentMessage[]; }
+/** summary: a SnapshotV1 ITree to resume from (SnapshotLoader); messages then are the catch-up suffix. */
+export interface DocLog { observer?: string; messages: ISequencedDocumentMessage[]; summary?: ITree | string; }
 
 export declare class BatchedMergeEngine {
     constructor(options?: { device?: number; chunkSize?: number });
@@ -24,6 +25,7 @@ export declare class BatchedMergeEngine {
 /** Client-shaped facade (merge-tree client.ts:42) for one document. */
 export declare class MergeTreeClient {
     constructor(observer?: string, options?: { device?: number; chunkSize?: number });
+    load(summary: ITree | string): void;
     applyMsg(msg: ISequencedDocumentMessage): void;
     getText(): string;
     getLength(): number;

@@ -19,11 +19,18 @@ class BatchedMergeEngine {
         this._engine = addon.createEngine(this.device, this.chunkSize);
         this._docs = 0;
     }
-    /** Stage per-document logs: docs = [{ observer, messages: ISequencedDocumentMessage[] }] */
+    /** Stage per-document logs: docs = [{ observer, messages: ISequencedDocumentMessage[], summary? }]
+     *  summary (optional): a SnapshotV1 ITree to resume from (SnapshotLoader); messages are the suffix. */
     load(docs) {
         const b = addon.createBuilder();
         for (const d of docs) {
-            addon.builderAddDoc(b, d.observer === undefined ? "__observer__" : d.observer, JSON.stringify(d.messages));
+            const obs = d.observer === undefined ? "__observer__" : d.observer;
+            if (d.summary !== undefined) {
+                const s = typeof d.summary === "string" ? d.summary : JSON.stringify(d.summary);
+                addon.builderAddDocFromSummary(b, obs, s, d.messages ? JSON.stringify(d.messages) : null);
+            } else {
+                addon.builderAddDoc(b, obs, JSON.stringify(d.messages));
+            }
         }
         addon.load(this._engine, b);
         this._docs = docs.length;
@@ -59,14 +66,17 @@ class MergeTreeClient {
         this.observer = observer;
         this.options = options;
         this.messages = [];
+        this.summary = undefined;
         this._engine = undefined;
         this._dirty = true;
     }
+    /** Client.load / SnapshotLoader (client.ts:944-952): resume from a summary ITree before applyMsg. */
+    load(summary) { this.summary = summary; this.messages = []; this._dirty = true; }
     applyMsg(msg) { this.messages.push(msg); this._dirty = true; }
     _run() {
         if (this._dirty) {
             if (!this._engine) this._engine = new BatchedMergeEngine(this.options);
-            this._engine.load([{ observer: this.observer, messages: this.messages }]);
+            this._engine.load([{ observer: this.observer, messages: this.messages, summary: this.summary }]);
             this._engine.replay();
             const [code, seq] = this._engine.docStatus(0);
             if (code === DocStatus.InsertFailed) throw new Error(`MergeTree insert failed at seq ${seq}`);
@@ -84,4 +94,5 @@ module.exports = {
     BatchedMergeEngine, MergeTreeClient, DocStatus,
     abiVersion: addon.abiVersion, buildInfo: addon.buildInfo,
     createBuilder: addon.createBuilder, builderAddDoc: addon.builderAddDoc, builderDocCount: addon.builderDocCount,
+    builderAddDocFromSummary: addon.builderAddDocFromSummary,
 };

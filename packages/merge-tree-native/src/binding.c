@@ -130,6 +130,29 @@ static napi_value js_builder_add_doc(napi_env env, napi_callback_info info) {
     return NULL;
 }
 
+/* builderAddDocFromSummary(builder, observerName, summaryJson, messagesJson | null): void
+ * (SnapshotLoader.initialize + applyMsg of the catch-up suffix, snapshotLoader.ts:38-216) */
+static napi_value js_builder_add_doc_from_summary(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) {
+        napi_throw_type_error(env, NULL, "builderAddDocFromSummary(builder, observer, summary, json|null)");
+        return NULL;
+    }
+    mte_builder* b = (mte_builder*)get_external(env, argv[0]);
+    size_t slen = 0, mlen = 0;
+    napi_valuetype t = napi_undefined;
+    napi_typeof(env, argv[3], &t);
+    char* obs = get_string(env, argv[1], NULL);
+    char* summ = get_string(env, argv[2], &slen);
+    char* msgs = t == napi_string ? get_string(env, argv[3], &mlen) : NULL;
+    int rc = (b && obs && summ) ? mte_builder_add_doc_from_summary(b, obs, summ, slen, msgs, mlen) : MTE_E_ARG;
+    free(obs);
+    free(summ);
+    free(msgs);
+    if (rc) return throw_mte(env, "mte_builder_add_doc_from_summary", rc, b ? mte_builder_error(b) : NULL);
+    return NULL;
+}
+
 /* builderDocCount(builder): number */
 static napi_value js_builder_doc_count(napi_env env, napi_callback_info info) {
     napi_value argv[1];
@@ -267,6 +290,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"createEngine", 0, js_create_engine, 0, 0, 0, napi_default, 0},
         {"createBuilder", 0, js_create_builder, 0, 0, 0, napi_default, 0},
         {"builderAddDoc", 0, js_builder_add_doc, 0, 0, 0, napi_default, 0},
+        {"builderAddDocFromSummary", 0, js_builder_add_doc_from_summary, 0, 0, 0, napi_default, 0},
         {"builderDocCount", 0, js_builder_doc_count, 0, 0, 0, napi_default, 0},
         {"load", 0, js_load, 0, 0, 0, napi_default, 0},
         {"generate", 0, js_generate, 0, 0, 0, napi_default, 0},

@@ -14,4 +14,11 @@ m.builderAddDoc(b, "__observer__", JSON.stringify([msg("a", 1, 0, { pos1: 0, seg
 m.builderAddDoc(b, "__observer__", JSON.stringify([msg("a", 1, 0, { pos1: 0, pos2: 1, type: 1 })]));
 assert.strictEqual(m.builderDocCount(b), 2);
 assert.throws(() => m.builderAddDoc(b, "__observer__", "[{]"), /mte_builder_add_doc/);
+// resume from a reference SnapshotV1 fixture, then a catch-up suffix
+const fs = require("fs");
+const summary = fs.readFileSync(__dirname + "/../../../tests/golden/v1/headerOnly.json", "utf8");
+m.builderAddDocFromSummary(b, "catchup", summary, JSON.stringify([msg("w", 1, 0, { pos1: 0, seg: "x", type: 0 })]));
+m.builderAddDocFromSummary(b, "catchup", summary, null);
+assert.strictEqual(m.builderDocCount(b), 4);
+assert.throws(() => m.builderAddDocFromSummary(b, "catchup", "{\"entries\":[]}", null), /mte_builder_add_doc_from_summary/);
 console.log("exports ok");

@@ -14,6 +14,15 @@ c1.applyMsg(msg("remote", 13, 11, { pos1: 0, seg: "text", type: 0 }));
 assert.strictEqual(c1.getText(), "text");
 const tree = c1.snapshot();
 assert.strictEqual(tree.entries[0].path, "header");
+// Client.load (SnapshotLoader) from a reference v1 fixture: re-emits the same tree, then catches up
+const fixture = JSON.parse(require("fs").readFileSync(__dirname + "/../../../tests/golden/v1/withAnnotations.json", "utf8"));
+const c2 = new MergeTreeClient("catchup");
+c2.load(fixture);
+assert.deepStrictEqual(c2.snapshot(), fixture.entries[1].value);
+const len0 = c2.getLength();
+c2.applyMsg(msg("w", 1, 0, { pos1: 3, seg: "XYZ", type: 0 }));
+assert.strictEqual(c2.getLength(), len0 + 3);
+assert.strictEqual(c2.getText().slice(3, 6), "XYZ");
 const e = new BatchedMergeEngine();
 e.generate(2, 8, 500, 8, 3);
 const st = e.replay();

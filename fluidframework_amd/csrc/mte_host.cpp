@@ -15,6 +15,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <string>
@@ -178,6 +179,7 @@ struct mte_builder {
     HostBatch hb;
     std::unique_ptr<Interner> in;
     std::string err;
+    std::vector<std::string> paths;  // per document: channel full path (container logs), else ""
     mte_builder() { in.reset(new Interner(&hb)); }
 };
 
@@ -1468,6 +1470,7 @@ int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* t
         return rc;
     }
     db.commit(b->hb);
+    b->paths.emplace_back();
     return MTE_OK;
 }
 
@@ -1635,7 +1638,198 @@ int mte_builder_add_doc_from_summary(mte_builder* b, const char* observer_name, 
         return rc;
     }
     db.commit(b->hb);
+    b->paths.emplace_back();
     return MTE_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Container-level op logs (clientReplayTool.ts:113-192, 258-347; fileDeltaStorageService.ts:23-31).
+
+static const char16_t* const kSharedStringType = u"https://graph.microsoft.com/types/mergeTree";  // SharedStringFactory.Type
+
+static std::string u8(const std::u16string& s) { return json::to_utf8(s.data(), s.size()); }
+
+// getDssTreesFromAttach + processAttachMessage: every SharedString tree of an attach snapshot, by
+// full path (the attach id, then "/"-joined tree entry paths). Later attaches of a path replace it.
+static void attach_trees(const json::Value& attach, const std::string& id, std::deque<json::Value>& store,
+                         std::vector<std::pair<std::string, const json::Value*>>& out) {
+    const json::Value* snap = attach.get(u"snapshot");
+    if (!snap || snap->kind != json::Value::Object) return;
+    store.push_back(*snap);
+    auto put = [&](const std::string& path, const json::Value* tree) {
+        for (auto& o : out)
+            if (o.first == path) {
+                o.second = tree;
+                return;
+            }
+        out.emplace_back(path, tree);
+    };
+    const json::Value* ty = attach.get(u"type");
+    if (ty && ty->kind == json::Value::String && ty->str == kSharedStringType) put(id, &store.back());
+    std::deque<std::pair<std::string, const json::Value*>> q{{id, &store.back()}};
+    while (!q.empty()) {
+        auto [full, tree] = q.front();
+        q.pop_front();
+        const json::Value* es = tree->get(u"entries");
+        if (!es || es->kind != json::Value::Array) continue;
+        for (const json::Value& e : es->items) {
+            const json::Value* t = e.get(u"type");
+            const json::Value* p = e.get(u"path");
+            const json::Value* v = e.get(u"value");
+            if (!t || t->kind != json::Value::String || !p || p->kind != json::Value::String || !v) continue;
+            if (t->str == u"Tree") {
+                q.emplace_back(full + "/" + u8(p->str), v);
+            } else if (t->str == u"Blob" && p->str == u".attributes") {
+                const json::Value* c = v->get(u"contents");
+                if (!c || c->kind != json::Value::String) continue;
+                try {
+                    json::Value a = json::parse(u8(c->str).c_str(), u8(c->str).size());
+                    const json::Value* at = a.get(u"type");
+                    if (at && at->kind == json::Value::String && at->str == kSharedStringType) put(full, tree);
+                } catch (std::exception&) {
+                }
+            }
+        }
+    }
+}
+
+int mte_builder_add_container_log(mte_builder* b, const char* observer_name, const char* text, size_t len,
+                                  uint32_t* n_docs) {
+    if (!b || !text) return MTE_E_ARG;
+    if (n_docs) *n_docs = 0;
+    json::Value log;
+    try {
+        log = json::parse(text, len);
+    } catch (std::exception& ex) {
+        b->err = ex.what();
+        return MTE_E_PARSE;
+    }
+    if (log.kind != json::Value::Array) {
+        b->err = "container log must be a JSON array of messages";
+        return MTE_E_PARSE;
+    }
+    std::deque<json::Value> store;                                   // attach snapshots / parsed strings
+    std::vector<std::pair<std::string, const json::Value*>> trees;   // mergeTreeAttachTrees (insertion order)
+    std::unordered_map<std::string, std::vector<json::Value>> msgs;  // merge-tree messages by full path
+    std::unordered_map<std::string, std::vector<std::u16string>> chunks;
+    std::vector<uint8_t> have;
+    auto parse_str = [&](const std::u16string& s) -> const json::Value* {
+        const std::string t = u8(s);
+        store.push_back(json::parse(t.data(), t.size()));
+        return &store.back();
+    };
+    try {
+        for (const json::Value& m0 : log.items) {
+            if (m0.kind != json::Value::Object) continue;
+            json::Value m = m0;
+            const json::Value* ty = m.get(u"type");
+            const json::Value* cid = m.get(u"clientId");
+            const std::string client = cid && cid->kind == json::Value::String ? u8(cid->str) : "";
+            if (ty && ty->kind == json::Value::String && ty->str == u"chunkedOp") {  // ChunkedOp reassembly
+                const json::Value* c = m.get(u"contents");
+                const json::Value* ch = c && c->kind == json::Value::String ? parse_str(c->str) : c;
+                if (!ch || ch->kind != json::Value::Object) continue;
+                int32_t id = 0, total = 0;
+                num_field(*ch, u"chunkId", &id);
+                num_field(*ch, u"totalChunks", &total);
+                const json::Value* part = ch->get(u"contents");
+                if (total <= 0 || id < 1 || id > total) throw std::runtime_error("chunk id out of range");
+                auto& vec = chunks[client];
+                if (vec.empty()) vec.assign((size_t)total, std::u16string(1, (char16_t)0xFFFF));
+                auto& slot = vec[(size_t)(id - 1)];
+                if (!(slot.size() == 1 && slot[0] == 0xFFFF)) throw std::runtime_error("Chunk already assigned");
+                slot = part && part->kind == json::Value::String ? part->str : std::u16string();
+                if (id != total) continue;
+                std::u16string joined;
+                for (auto& x : vec) {
+                    if (x.size() == 1 && x[0] == 0xFFFF) throw std::runtime_error("Chunk not assigned");
+                    joined += x;
+                }
+                chunks.erase(client);
+                const json::Value* orig = ch->get(u"originalType");
+                for (auto& mem : m.members) {
+                    if (mem.first == u"contents") {
+                        mem.second = json::Value();
+                        mem.second.kind = json::Value::String;
+                        mem.second.str = joined;
+                    } else if (mem.first == u"type" && orig) {
+                        mem.second = *orig;
+                    }
+                }
+                ty = m.get(u"type");
+            }
+            if (!ty || ty->kind != json::Value::String) continue;
+            const json::Value* contents = m.get(u"contents");
+            if (ty->str == u"attach") {  // ContainerMessageType.Attach
+                const json::Value* a = contents && contents->kind == json::Value::String ? parse_str(contents->str) : contents;
+                const json::Value* id = a ? a->get(u"id") : nullptr;
+                if (a && id && id->kind == json::Value::String) attach_trees(*a, u8(id->str), store, trees);
+                continue;
+            }
+            if (ty->str != u"op" || !contents || contents->kind == json::Value::Null) continue;
+            // address envelopes: {address, contents: {address, contents: ...}}
+            std::vector<std::string> parts;
+            const json::Value* cur = contents;
+            do {
+                if (cur->kind == json::Value::String) cur = parse_str(cur->str);
+                const json::Value* ad = cur->get(u"address");
+                parts.push_back(ad && ad->kind == json::Value::String ? u8(ad->str) : "undefined");
+                cur = cur->get(u"contents");
+                if (!cur) break;
+            } while (cur->get(u"contents"));
+            if (!cur) continue;
+            auto join = [&](const std::string& last) {
+                std::string o;
+                for (auto& x : parts) o += x + "/";
+                return o + last;
+            };
+            const json::Value* ity = cur->get(u"type");
+            if (ity && ity->kind == json::Value::String && ity->str == u"attach") {  // legacy attach envelope
+                const json::Value* a = cur->get(u"content");
+                const json::Value* id = a ? a->get(u"id") : nullptr;
+                if (a && id && id->kind == json::Value::String) attach_trees(*a, join(u8(id->str)), store, trees);
+                continue;
+            }
+            const json::Value* content = cur->get(u"content");
+            if (!content || content->kind != json::Value::Object) continue;
+            const json::Value* ad = content->get(u"address");
+            const std::string path = join(ad && ad->kind == json::Value::String ? u8(ad->str) : "undefined");
+            bool known = false;
+            for (auto& t : trees) known |= t.first == path;
+            const json::Value* op = content->get(u"contents");
+            if (!known || !op || op->kind != json::Value::Object || op->get(u"key")) continue;  // interval ops: "key"
+            json::Value nm = m;
+            for (auto& mem : nm.members)
+                if (mem.first == u"contents") mem.second = *op;
+            msgs[path].push_back(std::move(nm));
+        }
+    } catch (std::exception& ex) {
+        b->err = ex.what();
+        return MTE_E_PARSE;
+    }
+    uint32_t added = 0;
+    for (auto& [path, tree] : trees) {
+        DocBuild db(observer_name);
+        json::Value arr;
+        arr.kind = json::Value::Array;
+        auto it = msgs.find(path);
+        if (it != msgs.end()) arr.items = std::move(it->second);
+        int rc = add_summary(b, *tree, db);
+        if (!rc) rc = add_messages(b, arr, db);
+        if (rc) {
+            b->err = path + ": " + db.err;
+            return rc;
+        }
+        db.commit(b->hb);
+        b->paths.push_back(path);
+        added++;
+    }
+    if (n_docs) *n_docs = added;
+    return MTE_OK;
+}
+
+const char* mte_builder_doc_path(const mte_builder* b, uint32_t doc) {
+    return b && doc < b->paths.size() ? b->paths[doc].c_str() : nullptr;
 }
 
 int mte_builder_batch(mte_builder* b, mte_batch* out) {

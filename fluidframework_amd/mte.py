@@ -77,7 +77,8 @@ SUMMARY_DTYPE = np.dtype([("checksum", "<u8"), ("ops", "<u4"), ("length", "<u4")
 # Every symbol declared in include/mte.h (checked by tests/test_abi.py).
 EXPORTS = ["mte_abi_version", "mte_build_info", "mte_create", "mte_destroy", "mte_last_error", "mte_load",
            "mte_replay", "mte_generate", "mte_export_batch", "mte_doc_status", "mte_text", "mte_segments",
-           "mte_snapshot_v1", "mte_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_batch",
+           "mte_snapshot_v1", "mte_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
+           "mte_builder_batch",
            "mte_builder_error", "mte_builder_destroy"]
 
 _lib = None
@@ -118,6 +119,9 @@ def lib():
         L.mte_builder_create.argtypes = [ctypes.POINTER(vp)]
         L.mte_builder_add_doc.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
         L.mte_builder_add_doc_from_summary.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, sz]
+        L.mte_builder_add_container_log.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_uint32)]
+        L.mte_builder_doc_path.argtypes = [vp, ctypes.c_uint32]
+        L.mte_builder_doc_path.restype = ctypes.c_char_p
         L.mte_builder_batch.argtypes = [vp, ctypes.POINTER(mte_batch)]
         L.mte_builder_error.argtypes = [vp]
         L.mte_builder_error.restype = ctypes.c_char_p
@@ -162,6 +166,24 @@ class Builder:
         rc = lib().mte_builder_add_doc_from_summary(self._h, observer.encode(), s, len(s), m, len(m) if m else 0)
         if rc:
             raise MteError(f"mte_builder_add_doc_from_summary: {rc}: {lib().mte_builder_error(self._h).decode()}")
+
+    def add_container_log(self, messages, observer="readonly"):
+        """Container messages (messages*.json concatenated) -> one document per attached SharedString
+        channel (clientReplayTool.ts:113-192). Returns the channel paths of the documents added."""
+        t = messages if isinstance(messages, (str, bytes)) else json.dumps(messages, separators=(",", ":"),
+                                                                            ensure_ascii=False)
+        t = t.encode() if isinstance(t, str) else t
+        n = ctypes.c_uint32()
+        rc = lib().mte_builder_add_container_log(self._h, observer.encode(), t, len(t), ctypes.byref(n))
+        if rc:
+            raise MteError(f"mte_builder_add_container_log: {rc}: {lib().mte_builder_error(self._h).decode()}")
+        first = self.n_docs() - n.value
+        return [lib().mte_builder_doc_path(self._h, first + i).decode() for i in range(n.value)]
+
+    def n_docs(self):
+        b = mte_batch()
+        lib().mte_builder_batch(self._h, ctypes.byref(b))
+        return b.n_docs
 
     def batch(self):
         b = mte_batch()

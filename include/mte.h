@@ -217,6 +217,15 @@ int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* j
  * MTE_E_UNSUPPORTED for legacy (non-"1") chunks and for body chunks next to merge-info segments. */
 int mte_builder_add_doc_from_summary(mte_builder* b, const char* observer_name, const char* summary,
                                      size_t summary_len, const char* ops, size_t ops_len);
+/* Container-level op log (clientReplayTool.ts:113-192,258-347 over FileDeltaStorageService's
+ * messages*.json, fileDeltaStorageService.ts:23-31): a JSON array of container messages is split into
+ * one document per attached SharedString channel — ChunkedOp reassembly (containerRuntime.ts:1445-1460),
+ * address-envelope unwrapping, the attach snapshot as the summary, the channel's merge-tree ops (not
+ * interval-collection "key" ops) as the suffix. *n_docs (may be NULL) = documents added, in attach
+ * order; mte_builder_doc_path names each one's channel ("" for documents added otherwise). */
+int mte_builder_add_container_log(mte_builder* b, const char* observer_name, const char* json, size_t len,
+                                  uint32_t* n_docs);
+const char* mte_builder_doc_path(const mte_builder* b, uint32_t doc);
 int mte_builder_batch(mte_builder* b, mte_batch* out);   /* view valid until destroy */
 const char* mte_builder_error(const mte_builder* b);
 void mte_builder_destroy(mte_builder* b);

@@ -34,3 +34,7 @@ export declare class MergeTreeClient {
 
 export declare function abiVersion(): number;
 export declare function buildInfo(): string;
+
+/** Low-level builder (the addon's own surface): container logs split per SharedString channel. */
+export declare function createBuilder(): unknown;
+export declare function builderAddContainerLog(builder: unknown, observer: string, containerMessagesJson: string): string[];

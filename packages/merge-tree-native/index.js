@@ -94,5 +94,5 @@ module.exports = {
     BatchedMergeEngine, MergeTreeClient, DocStatus,
     abiVersion: addon.abiVersion, buildInfo: addon.buildInfo,
     createBuilder: addon.createBuilder, builderAddDoc: addon.builderAddDoc, builderDocCount: addon.builderDocCount,
-    builderAddDocFromSummary: addon.builderAddDocFromSummary,
+    builderAddDocFromSummary: addon.builderAddDocFromSummary, builderAddContainerLog: addon.builderAddContainerLog,
 };

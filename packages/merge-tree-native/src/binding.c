@@ -153,6 +153,36 @@ static napi_value js_builder_add_doc_from_summary(napi_env env, napi_callback_in
     return NULL;
 }
 
+/* builderAddContainerLog(builder, observerName, containerMessagesJson): string[] (channel paths)
+ * (clientReplayTool.ts:113-192: chunk reassembly, envelope unwrapping, attach snapshots) */
+static napi_value js_builder_add_container_log(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) {
+        napi_throw_type_error(env, NULL, "builderAddContainerLog(builder, observer, json)");
+        return NULL;
+    }
+    mte_builder* b = (mte_builder*)get_external(env, argv[0]);
+    size_t len = 0;
+    uint32_t n = 0;
+    char* obs = get_string(env, argv[1], NULL);
+    char* json = get_string(env, argv[2], &len);
+    int rc = (b && obs && json) ? mte_builder_add_container_log(b, obs, json, len, &n) : MTE_E_ARG;
+    free(obs);
+    free(json);
+    if (rc) return throw_mte(env, "mte_builder_add_container_log", rc, b ? mte_builder_error(b) : NULL);
+    mte_batch batch;
+    mte_builder_batch(b, &batch);
+    napi_value arr;
+    CHECK(env, napi_create_array_with_length(env, n, &arr));
+    for (uint32_t i = 0; i < n; i++) {
+        const char* p = mte_builder_doc_path(b, batch.n_docs - n + i);
+        napi_value sv;
+        CHECK(env, napi_create_string_utf8(env, p ? p : "", NAPI_AUTO_LENGTH, &sv));
+        CHECK(env, napi_set_element(env, arr, i, sv));
+    }
+    return arr;
+}
+
 /* builderDocCount(builder): number */
 static napi_value js_builder_doc_count(napi_env env, napi_callback_info info) {
     napi_value argv[1];
@@ -291,6 +321,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"createBuilder", 0, js_create_builder, 0, 0, 0, napi_default, 0},
         {"builderAddDoc", 0, js_builder_add_doc, 0, 0, 0, napi_default, 0},
         {"builderAddDocFromSummary", 0, js_builder_add_doc_from_summary, 0, 0, 0, napi_default, 0},
+        {"builderAddContainerLog", 0, js_builder_add_container_log, 0, 0, 0, napi_default, 0},
         {"builderDocCount", 0, js_builder_doc_count, 0, 0, 0, napi_default, 0},
         {"load", 0, js_load, 0, 0, 0, napi_default, 0},
         {"generate", 0, js_generate, 0, 0, 0, napi_default, 0},

@@ -21,4 +21,5 @@ m.builderAddDocFromSummary(b, "catchup", summary, JSON.stringify([msg("w", 1, 0,
 m.builderAddDocFromSummary(b, "catchup", summary, null);
 assert.strictEqual(m.builderDocCount(b), 4);
 assert.throws(() => m.builderAddDocFromSummary(b, "catchup", "{\"entries\":[]}", null), /mte_builder_add_doc_from_summary/);
+assert.deepStrictEqual(m.builderAddContainerLog(b, "readonly", "[]"), []);
 console.log("exports ok");

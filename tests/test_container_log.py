@@ -1,0 +1,161 @@
+"""Container-level op-log ingestion: clientReplayTool.ts:113-192,258-347 over
+FileDeltaStorageService's messages*.json. A synthetic container log (no reference messages*.json fixture
+exists: parity unpinned beyond the reference's own code paths) with a SharedString attached by a
+container Attach message and a second one by a legacy attach envelope, address envelopes (object and
+JSON-string forms), a ChunkedOp split in three, and noise (another DDS, interval-collection ops, joins)
+must give the same documents as the summaries + unwrapped merge-tree messages added directly."""
+import ctypes
+import json
+import os
+
+import pytest
+
+from fluidframework_amd import mte
+from oracle import OracleDoc
+from tests.oplog import dumps, ins, msg, rem
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "v1")
+SS = "https://graph.microsoft.com/types/mergeTree"
+OBS = "readonly"
+
+
+def blob(path, contents):
+    return {"mode": "100644", "path": path, "type": "Blob", "value": {"contents": contents, "encoding": "utf-8"}}
+
+
+def tree(path, entries):
+    return {"mode": "040000", "path": path, "type": "Tree", "value": {"entries": entries}}
+
+
+def attributes(t):
+    return blob(".attributes", json.dumps({"type": t, "snapshotFormatVersion": "0.1", "packageVersion": "0.31.0"}))
+
+
+EMPTY_CHUNK = json.dumps({"version": "1", "segmentCount": 0, "length": 0, "segments": [], "startIndex": 0,
+                          "headerMetadata": {"minSequenceNumber": 0, "sequenceNumber": 0,
+                                             "orderedChunkMetadata": [{"id": "header"}], "totalLength": 0,
+                                             "totalSegmentCount": 0}})
+
+
+def container_log():
+    fixture = json.load(open(os.path.join(GOLDEN, "withAnnotations.json")))
+    mt_tree = fixture["entries"][1]["value"]  # the merge-tree ITree under "content"
+    length = json.loads(mt_tree["entries"][0]["value"]["contents"])["headerMetadata"]["totalLength"]
+    root_ss = [attributes(SS), blob("header", "{}"), {"mode": "040000", "path": "content", "type": "Tree",
+                                                       "value": mt_tree}]
+    attach = {"id": "ds1", "type": "@fluid-example/app",
+              "snapshot": {"entries": [blob(".component", "{}"), tree("root", root_ss),
+                                       tree("map1", [attributes("https://graph.microsoft.com/types/map")])]}}
+    text2_snap = {"entries": [attributes(SS), blob("header", "{}"),
+                              tree("content", [blob("header", EMPTY_CHUNK)])]}
+    out, expect = [], {"ds1/root": [], "ds1/text2": []}
+    seq = [0]
+
+    def nxt():
+        seq[0] += 1
+        return seq[0]
+
+    def envelope(channel, op, stringify=False):
+        inner = {"address": "ds1", "contents": {"content": {"address": channel, "contents": op}, "type": "op"}}
+        return json.dumps(inner) if stringify else inner
+
+    out.append({"clientId": None, "sequenceNumber": nxt(), "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+                "type": "join", "contents": json.dumps({"clientId": "A"})})
+    out.append({"clientId": "A", "sequenceNumber": nxt(), "referenceSequenceNumber": 0, "minimumSequenceNumber": 0,
+                "type": "attach", "contents": attach})
+    # legacy attach: an op whose innermost envelope is {type: "attach", content: IAttachMessage}
+    out.append(msg("A", nxt(), seq[0] - 1, {"address": "ds1", "contents": {"type": "attach", "content": {
+        "id": "text2", "type": SS, "snapshot": text2_snap}}}, seq[0] - 1))
+    lengths = {"ds1/root": length, "ds1/text2": 0}
+    for i in range(60):
+        ch = "root" if i % 3 else "text2"
+        path = "ds1/" + ch
+        L = lengths[path]
+        if L > 20 and i % 4 == 0:
+            op = rem(i % 17, i % 17 + 5)
+            lengths[path] -= 5
+        else:
+            op = ins((i * 31) % (L + 1), f"<{i}>")
+            lengths[path] += len(f"<{i}>")
+        s = nxt()
+        writer = "A" if i % 2 else "B"
+        m = msg(writer, s, s - 1, envelope(ch, op, stringify=(i % 5 == 0)), s - 1)
+        if i == 30:  # ChunkedOp: the serialized op split into three sequenced chunks
+            body = json.dumps(envelope(ch, op))  # the runtime serializes the contents object once
+            parts = [body[: len(body) // 3], body[len(body) // 3: 2 * len(body) // 3], body[2 * len(body) // 3:]]
+            for k, p in enumerate(parts):
+                if k:
+                    s = nxt()
+                out.append(msg(writer, s, s - 1, json.dumps({"chunkId": k + 1, "totalChunks": 3, "contents": p,
+                                                             "originalType": "op"}), s - 1, mtype="chunkedOp"))
+            final = dict(out[-1])
+            final["type"] = "op"
+            final["contents"] = op
+            expect[path].append(final)
+        else:
+            out.append(m)
+            expect[path].append(dict(m, contents=op))
+        if i % 7 == 0:  # noise: a map op and an interval-collection op on the string
+            s = nxt()
+            out.append(msg("A", s, s - 1, envelope("map1", {"key": "k", "type": "set", "value": {"value": i}}), s - 1))
+            s = nxt()
+            out.append(msg("B", s, s - 1, envelope("root", {"key": "intervals", "type": "add", "value": {}}), s - 1))
+    return out, expect, mt_tree, text2_snap
+
+
+def test_container_log_matches_direct_documents():
+    log, expect, mt_tree, text2_snap = container_log()
+    b = mte.Builder()
+    paths = b.add_container_log(log, observer=OBS)
+    assert paths == ["ds1/root", "ds1/text2"]
+    d = mte.Builder()
+    d.add_doc_from_summary({"entries": [blob("header", "{}"), {"mode": "040000", "path": "content",
+                                                                "type": "Tree", "value": mt_tree}]},
+                           expect["ds1/root"], observer=OBS)
+    d.add_doc_from_summary(text2_snap, expect["ds1/text2"], observer=OBS)
+    bc, bd = b.batch(), d.batch()
+    for i in range(2):
+        x, y = OracleDoc(OBS), OracleDoc(OBS)
+        x.apply_batch(ctypes.addressof(bc), i)
+        y.apply_batch(ctypes.addressof(bd), i)
+        assert x.status()[0] == 0 and y.status()[0] == 0, (x.status(), y.status())
+        assert x.segments_json() == y.segments_json()
+        assert x.snapshot_json() == y.snapshot_json()
+        # and the oracle's own JSON path: SnapshotLoader + applyMsg of the unwrapped messages
+        z = OracleDoc(OBS)
+        z.load_summary(json.dumps(mt_tree if i == 0 else text2_snap))
+        z.apply_json(dumps(expect[paths[i]]))
+        assert z.text() == x.text()
+        assert z.snapshot_json() == x.snapshot_json()
+
+
+def test_container_log_errors():
+    b = mte.Builder()
+    with pytest.raises(mte.MteError):
+        b.add_container_log("{}")
+    dup = [msg("A", 1, 0, json.dumps({"chunkId": 1, "totalChunks": 2, "contents": "x", "originalType": "op"}),
+               mtype="chunkedOp"),
+           msg("A", 2, 1, json.dumps({"chunkId": 1, "totalChunks": 2, "contents": "x", "originalType": "op"}),
+               mtype="chunkedOp")]
+    with pytest.raises(mte.MteError):
+        b.add_container_log(dup)
+    assert b.add_container_log([]) == []
+
+
+@pytest.mark.gpu
+def test_gpu_container_log_matches_oracle():
+    from tests.gpu_helpers import compare_doc
+
+    log, expect, _, _ = container_log()
+    b = mte.Builder()
+    paths = b.add_container_log(log, observer=OBS)
+    batch = b.batch()
+    e = mte.Engine(0)
+    try:
+        e.load(batch)
+        st = e.replay()
+        assert st["failed_docs"] == 0, st
+        for i in range(len(paths)):
+            compare_doc(e, batch, i, observer=OBS)
+    finally:
+        e.close()

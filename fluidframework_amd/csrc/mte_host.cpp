@@ -1149,6 +1149,25 @@ int mte_segments_json(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t
     return MTE_OK;
 }
 
+// SharedSegmentSequence.snapshotCore (sequence.ts:413-438): the interval-collection blob "header"
+// (MapKernel.serialize of no collections: "{}"; interval ops are outside the path) and the merge-tree
+// ITree as "content".
+int mte_snapshot_shared_string(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len) {
+    size_t n = 0;
+    int rc = mte_snapshot_v1(e, doc, nullptr, 0, &n, nullptr);
+    if (rc) return rc;
+    std::string inner(n, '\0');
+    if ((rc = mte_snapshot_v1(e, doc, &inner[0], n, &n, nullptr))) return rc;
+    std::string o = "{\"entries\":[{\"mode\":\"100644\",\"path\":\"header\",\"type\":\"Blob\",\"value\":"
+                    "{\"contents\":\"{}\",\"encoding\":\"utf-8\"}},{\"mode\":\"040000\",\"path\":\"content\","
+                    "\"type\":\"Tree\",\"value\":" + inner + "}],\"id\":null}";
+    if (len) *len = o.size();
+    if (!buf) return MTE_OK;
+    if (cap < o.size()) return MTE_E_RANGE;
+    memcpy(buf, o.data(), o.size());
+    return MTE_OK;
+}
+
 int mte_snapshot_v1(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len, uint32_t* n_blobs) {
     DocView v;
     int rc = doc_view(e, doc, v);

@@ -77,7 +77,7 @@ SUMMARY_DTYPE = np.dtype([("checksum", "<u8"), ("ops", "<u4"), ("length", "<u4")
 # Every symbol declared in include/mte.h (checked by tests/test_abi.py).
 EXPORTS = ["mte_abi_version", "mte_build_info", "mte_create", "mte_destroy", "mte_last_error", "mte_load",
            "mte_replay", "mte_generate", "mte_export_batch", "mte_doc_status", "mte_text", "mte_segments",
-           "mte_snapshot_v1", "mte_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
+           "mte_snapshot_v1", "mte_snapshot_shared_string", "mte_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
            "mte_builder_batch",
            "mte_builder_error", "mte_builder_destroy"]
 
@@ -106,6 +106,7 @@ def lib():
         L.mte_text.argtypes = [vp, u32, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
         L.mte_segments_json.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.mte_snapshot_v1.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz), ctypes.POINTER(u32)]
+        L.mte_snapshot_shared_string.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.mte_summaries.argtypes = [vp, ctypes.c_void_p, sz]
         L.mte_doc_result.argtypes = [vp, u32, ctypes.c_void_p, sz]
         L.mte_run_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_double),
@@ -273,6 +274,10 @@ class Engine:
     def snapshot_json(self, doc):
         nb = ctypes.c_uint32()
         return self._str_call(lib().mte_snapshot_v1, doc, ctypes.byref(nb))
+
+    def snapshot_shared_string(self, doc):
+        """SharedString summary tree: {"header": intervals "{}", "content": SnapshotV1 tree}."""
+        return self._str_call(lib().mte_snapshot_shared_string, doc)
 
     def summaries(self):
         out = np.zeros(self.n_docs, dtype=SUMMARY_DTYPE)

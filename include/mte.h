@@ -202,6 +202,9 @@ int mte_segments(mte_engine* e, uint32_t doc, mte_seg_row* rows, size_t cap, siz
  * {"entries":[{"mode":"100644","path":"header","type":"Blob","value":{"contents":...,"encoding":"utf-8"}},...],"id":null}
  * buf may be NULL to query *len. */
 int mte_snapshot_v1(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len, uint32_t* n_blobs);
+/* SharedSegmentSequence.snapshotCore (sequence.ts:413-438): the SharedString summary tree, "header"
+ * (interval collections: "{}") + "content" (the tree of mte_snapshot_v1). buf may be NULL. */
+int mte_snapshot_shared_string(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len);
 /* Per-doc summaries for all docs of the batch (checksum over text + snapshot blobs). */
 int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap);
 

@@ -186,6 +186,9 @@ def test_gpu_catchup_matches_oracle(engine):
         assert engine.snapshot_json(d) == ref.snapshot_json()
     for d, n in enumerate(FIXTURES):  # pinned: load + re-emit reproduces the reference's bytes
         assert json.loads(engine.snapshot_json(d)) == merge_tree_tree(fixture(n))
+        # the whole SharedString summary (sequence.ts:413-438) equals the fixture file
+        # (snapshotVersion.spec.ts:87-98 compares the parsed objects)
+        assert json.loads(engine.snapshot_shared_string(d)) == json.loads(fixture(n))
 
 
 @pytest.mark.gpu

@@ -1765,29 +1765,33 @@ struct Engine {
     }
 
     // ---------------------------------------------------------------- resume from a summary
-    // SnapshotLoader (snapshotLoader.ts:113-216) as records (include/mte.h MTE_OP_LOAD_*).
-    // LOAD_SEG: reloadFromSegments fills leaf blocks 7 at a time in document order
-    // (mergeTree.ts:1195-1251); LOAD_END links them into 7-wide interior levels and starts the
-    // collaboration window; LOAD_APPEND is loadBody's insertSegments at the end (refSeq 0, seq 0:
-    // never enqueued for zamboni, blockInsert/saveIfLocal :2164-2179).
-    MTE_DEV void load_record(const mte_op& op) {
+    // SnapshotLoader (snapshotLoader.ts:113-216) as records (include/mte.h MTE_OP_LOAD_*), applied
+    // outside the op path (replay_run dispatches them). LOAD_SEG fills the leaf blocks in document
+    // order (a new block at MTE_F_LOAD_LEAF); LOAD_END links the interior levels described by the
+    // LOAD_NODE records before it (the shape of reloadFromSegments + loadBody's appends, computed by
+    // the builder and checked against the oracle's insertingWalk) and opens the collaboration window.
+    MTE_DEV void load_record(const mte_op& op, u64 i) {
+        if (!collab || op.type > MTE_OP_LOAD_NODE) {
+            fail(MTE_DOC_UNSUPPORTED, op.seq);
+            return;
+        }
+        if (op.type == MTE_OP_LOAD_NODE) return;  // consumed by LOAD_END
         if (op.type == MTE_OP_LOAD_END) {
-            load_link(op.seq, op.msn);
+            load_link(op, i);
+            return;
+        }
+        if (st.root == NONE) {
+            fail(MTE_DOC_UNSUPPORTED, op.seq);
             return;
         }
         const bool mk = (op.flags & MTE_F_LOAD_MARKER) != 0;
+        const bool rm = (op.flags & MTE_F_LOAD_REMOVED) != 0;
         Seg rec;
         rec.len = mk ? 1u : op.b;
         rec.props = op.props ? build_map(0, op.props, false) : 0u;
         if (st.status) return;
         rec.toff = (u32)op.a;  // text offset, or the marker's refType
         rec.tcap = 0;          // (the overlap mask of a removed segment: empty)
-        rec.sid = 0;
-        if (op.type != MTE_OP_LOAD_SEG || st.root == NONE) {
-            fail(MTE_DOC_UNSUPPORTED, op.seq);
-            return;
-        }
-        const bool rm = (op.flags & MTE_F_LOAD_REMOVED) != 0;
         rec.seq = op.seq;
         rec.rseq = rm ? op.ref_seq : 0;
         rec.meta = (op.client & 0xffu) | (mk ? F_MARKER : 0u) | (rm ? ((((u32)op.pos1 & 0xffu) << 8) | F_REMOVED) : 0u);
@@ -1795,7 +1799,7 @@ struct Engine {
         if (rec.sid == NONE) return;
         u32 k = st.n_lb - 1;
         uint4 o = ord_u(k);
-        if (o.w >= 7) {  // MaxNodesInBlock - 1 children per reloaded block
+        if (op.flags & MTE_F_LOAD_LEAF) {
             if (st.n_lb + 1 > ord_cap()) {
                 fail_cap();
                 return;
@@ -1805,6 +1809,9 @@ struct Engine {
             k = st.n_lb++;
             stat_max(ST_MAXLB, st.n_lb);
             o = make_uint4(nb, 0, 0, 0);
+        } else if (o.w >= 7) {  // a block holds <= 7 children between ops
+            fail(MTE_DOC_CAPACITY, op.seq);
+            return;
         }
         if (L == 0) {
             store(o.x, o.w, rec);
@@ -1816,45 +1823,62 @@ struct Engine {
         }
         sync();
     }
-    // buildMergeBlock (mergeTree.ts:1202-1230) over the reloaded leaves, then
+    // buildMergeBlock (mergeTree.ts:1202-1230) generalised to the recorded child counts, then
     // startOrUpdateCollaboration(minSeq, currentSeq) (snapshotLoader.ts:126-140).
-    MTE_DEV void load_link(i32 cur, i32 msn) {
-        if (msn > cur || st.heapSize != 0 || st.inUsed != 0 || st.inFree != NONE) {
-            fail(MTE_DOC_SEQ_ORDER, cur);
+    MTE_DEV void load_link(const mte_op& end, u64 i) {
+        const u64 nn = (u64)(u32)end.a;
+        const u64 b0 = p.docs[doc].op_begin;
+        if (end.msn > end.seq || st.heapSize != 0 || st.inUsed != 0 || st.inFree != NONE || i < b0 + nn) {
+            fail(MTE_DOC_SEQ_ORDER, end.seq);
             return;
         }
-        u32 m = st.n_lb;    // nodes on the level below
-        u32 below = NONE;   // first interior id of the level below (NONE: the leaves, in doc order)
-        u32 height = 1;
-        while (m > 1) {
-            const u32 groups = (m + 6) / 7;
-            u32 base = NONE;
-            for (u32 g = 0; g < groups; g++) {
-                const u32 id = alloc_in();
-                if (id == NONE) return;
-                if (g == 0) base = id;
-                if (id != base + g) {  // a fresh document's interior ids are consecutive
-                    fail(MTE_DOC_CAPACITY, cur);
+        u32 lvl = 1, below = NONE, nBelow = st.n_lb, cur = 0, first = NONE, made = 0, last = NONE;
+        for (u64 j = i - nn; j < i; j++) {
+            const mte_op nd = read_op(p.ops + j);
+            const u32 cnt = nd.b;
+            if (nd.type != MTE_OP_LOAD_NODE || cnt == 0 || cnt > 7) {
+                fail(MTE_DOC_CAPACITY, end.seq);
+                return;
+            }
+            if ((u32)nd.a != lvl) {  // next level up: its children are the nodes just made
+                if ((u32)nd.a != lvl + 1 || cur != nBelow) {
+                    fail(MTE_DOC_CAPACITY, end.seq);
                     return;
                 }
-                const u32 c0 = g * 7, cn = m - c0 < 7 ? m - c0 : 7u;
-                if (L < cn) {
-                    const u32 child = below == NONE ? ORD()[c0 + L].x : below + c0 + L;
-                    INCH()[id * 8 + L] = child;
-                    if (below == NONE) set_bpar_lane(child, id);
-                    else if (child < in_cap()) INPAR()[child] = id;
-                }
-                if (L == 0) INCNT()[id] = cn;
-                sync();
+                lvl++;
+                below = first;
+                nBelow = made;
+                cur = 0;
+                first = NONE;
+                made = 0;
             }
-            below = base;
-            m = groups;
-            height++;
+            const u32 id = alloc_in();
+            if (id == NONE) return;
+            if (first == NONE) first = id;
+            if (id != first + made || cur + cnt > nBelow) {  // a fresh document's ids are consecutive
+                fail(MTE_DOC_CAPACITY, end.seq);
+                return;
+            }
+            if (L < cnt) {
+                const u32 child = below == NONE ? ORD()[cur + L].x : below + cur + L;
+                INCH()[id * 8 + L] = child;
+                if (below == NONE) set_bpar_lane(child, id);
+                else if (child < in_cap()) INPAR()[child] = id;
+            }
+            if (L == 0) INCNT()[id] = cnt;
+            sync();
+            cur += cnt;
+            made++;
+            last = id;
         }
-        st.root = below == NONE ? U(ORD()[0].x) : below;
-        st.height = height;
-        st.curSeq = cur;
-        st.minSeq = msn;
+        if (nn && (cur != nBelow || made != 1)) {  // every node linked, one root
+            fail(MTE_DOC_CAPACITY, end.seq);
+            return;
+        }
+        st.root = nn ? last : U(ORD()[0].x);
+        st.height = nn ? lvl + 1 : 1u;
+        st.curSeq = end.seq;
+        st.minSeq = end.msn;
         sync();
     }
 
@@ -1868,37 +1892,29 @@ struct Engine {
             fail(MTE_DOC_UNSUPPORTED, op.seq);
             return;
         }
-        // LOAD_APPEND (loadBody's insertSegments: refSeq 0, seq 0) shares the insert path below
-        const bool app = op.type == MTE_OP_LOAD_APPEND;
-        if (op.type >= MTE_OP_LOAD_SEG && !app) {
-            if (collab) load_record(op);
-            else fail(MTE_DOC_UNSUPPORTED, op.seq);
-            return;
-        }
         const u32 C = collab ? (u32)op.client : 0u;
-        const i32 seq = collab && !app ? op.seq : 0;
-        const i32 R = collab && !app ? op.ref_seq : 0;
-        if (collab && !app && op.type != MTE_OP_NOOP && !(st.curSeq < op.seq)) {
+        const i32 seq = collab ? op.seq : 0;
+        const i32 R = collab ? op.ref_seq : 0;
+        if (collab && op.type != MTE_OP_NOOP && !(st.curSeq < op.seq)) {
             fail(MTE_DOC_SEQ_ORDER, op.seq);
             return;
         }
         bool edited = false;
-        if (op.type <= MTE_OP_INSERT_MARKER || app) {
+        if (op.type <= MTE_OP_INSERT_MARKER) {
             Seg rec;
-            const bool mk = op.type == MTE_OP_INSERT_MARKER || (app && (op.flags & MTE_F_LOAD_MARKER));
-            const bool ins = op.type == MTE_OP_INSERT || op.type == MTE_OP_INSERT_MARKER || app;
+            const bool mk = op.type == MTE_OP_INSERT_MARKER;
+            const bool ins = op.type == MTE_OP_INSERT || mk;
             rec.len = mk ? 1u : op.b;
             rec.seq = seq;
             rec.rseq = 0;
             rec.meta = (C & 0xff) | (mk ? F_MARKER : 0u);
             rec.props = (ins && op.props) ? build_map(0, op.props, false) : 0u;
             if (st.status) return;
-            rec.toff = mk && !app ? op.b : (u32)op.a;
+            rec.toff = mk ? op.b : (u32)op.a;
             rec.tcap = 0;
             rec.sid = 0;
-            edited = edit(app ? (u32)MTE_OP_INSERT : (u32)op.type, op.pos1, op.a, R, C, seq, rec, op.props,
-                          (op.flags & MTE_F_REWRITE) != 0);
-            if (!app) stat_add(ST_OPS, 1);
+            edited = edit(op.type, op.pos1, op.a, R, C, seq, rec, op.props, (op.flags & MTE_F_REWRITE) != 0);
+            stat_add(ST_OPS, 1);
             if (st.status) return;
         }
         for (u32 z = 0; z < 2; z++) {
@@ -2123,12 +2139,14 @@ struct Engine {
                     op = read_op(RING() + r);
                 }
                 if (!room()) break;
-                apply(op);
+                if (op.type >= MTE_OP_LOAD_SEG) load_record(op, i);  // summary records (cold)
+                else apply(op);
             }
         } else {
             for (; i < e && !st.status; i++) {
                 mte_op op = p.ops[i];
-                apply(op);
+                if (op.type >= MTE_OP_LOAD_SEG) load_record(op, i);
+                else apply(op);
             }
         }
         return i;

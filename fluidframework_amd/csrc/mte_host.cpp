@@ -522,8 +522,7 @@ static void count_doc_ops(const HostBatch& hb, uint32_t d, uint64_t& pi, uint64_
     pi = an = 0;
     for (uint64_t i = hb.doc_op_offsets[d]; i < hb.doc_op_offsets[d + 1]; i++) {
         const mte_op& o = hb.ops[i];
-        if ((o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER || o.type == MTE_OP_LOAD_SEG ||
-             o.type == MTE_OP_LOAD_APPEND) && o.props)
+        if ((o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER || o.type == MTE_OP_LOAD_SEG) && o.props)
             pi++;
         if (o.type == MTE_OP_ANNOTATE) an++;
     }
@@ -1572,6 +1571,7 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
     const json::Value* md = header.get(u"headerMetadata");
     if (!md || md->kind != json::Value::Object) return db.fail(MTE_E_PARSE, "header metadata not available");
     bool mergeInfo = false;
+    const size_t first = db.ops.size();
     const json::Value* hs = header.get(u"segments");
     if (hs && hs->kind == json::Value::Array) {
         for (const json::Value& sp : hs->items) {
@@ -1601,40 +1601,79 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
             db.ops.push_back(o);
         }
     }
+    const size_t nHeader = db.ops.size() - first;
+    // loadBody (:150-216): later chunks appended at root.cachedLength, refSeq 0, NonCollab, seq 0
+    const json::Value* ocm = md->get(u"orderedChunkMetadata");
+    if (ocm && ocm->kind == json::Value::Array && ocm->items.size() > 1) {
+        if (mergeInfo) return db.fail(MTE_E_UNSUPPORTED, "body chunks after a header with merge info");
+        uint32_t nc;
+        if (int rc = db.short_id(kNonCollabName, &nc)) return rc;
+        for (size_t i = 1; i < ocm->items.size(); i++) {
+            const json::Value* id = ocm->items[i].kind == json::Value::Object ? ocm->items[i].get(u"id") : nullptr;
+            if (!id || id->kind != json::Value::String) return db.fail(MTE_E_PARSE, "chunk id");
+            json::Value ch;
+            if (int rc = load_chunk(db, *t, id->str, &ch)) return rc;
+            const json::Value* cs = ch.get(u"segments");
+            if (!cs || cs->kind != json::Value::Array) continue;
+            for (const json::Value& sp : cs->items) {
+                if (sp.kind == json::Value::Object && sp.get(u"json"))  // flushBatch never clears (:196-199)
+                    return db.fail(MTE_E_UNSUPPORTED, "merge-info segment in a body chunk");
+                mte_op o{};
+                o.type = MTE_OP_LOAD_SEG;
+                o.flags = MTE_F_LOAD_BODY;
+                if (int rc = load_spec(b, db, sp, o)) return rc;
+                if (o.b == 0) continue;  // blockInsert skips empty segments (mergeTree.ts:2196)
+                o.client = (uint8_t)nc;
+                db.ops.push_back(o);
+            }
+        }
+    }
+    // The loaded tree's shape (child counts per level, document order): reloadFromSegments packs the
+    // header 7 to a block, level by level; each body append then lands at the end of the last leaf
+    // (insertingWalk at the document end) and a block reaching 8 children splits 4+4 up to the root
+    // (mergeTree.ts:2446-2489, 1876-1887). Segment ids and text are not part of the shape.
+    std::vector<std::vector<uint32_t>> lv(1);
+    for (size_t i = 0; i < nHeader; i += 7) lv[0].push_back((uint32_t)std::min<size_t>(7, nHeader - i));
+    if (lv[0].empty()) lv[0].push_back(0);
+    while (lv.back().size() > 1) {
+        const size_t m = lv.back().size();
+        std::vector<uint32_t> up;
+        for (size_t i = 0; i < m; i += 7) up.push_back((uint32_t)std::min<size_t>(7, m - i));
+        lv.push_back(up);
+    }
+    for (size_t k = first + nHeader; k < db.ops.size(); k++) {
+        size_t l = 0;
+        for (lv[0].back()++; l < lv.size() && lv[l].back() == 8; l++) {
+            lv[l].back() = 4;
+            lv[l].push_back(4);
+            if (l + 1 == lv.size()) lv.push_back({2});  // the root split: updateRoot
+            else lv[l + 1].back()++;
+        }
+    }
+    // leaf boundaries onto the LOAD_SEG records
+    size_t k = first;
+    for (size_t leaf = 0; leaf < lv[0].size(); leaf++) {
+        if (leaf > 0 && k < db.ops.size()) db.ops[k].flags |= MTE_F_LOAD_LEAF;
+        k += lv[0][leaf];
+    }
+    if (k != db.ops.size()) return db.fail(MTE_E_PARSE, "loaded tree shape does not cover the segments");
+    uint32_t nodes = 0;
+    for (size_t l = 1; l < lv.size(); l++)
+        for (uint32_t c : lv[l]) {
+            mte_op o{};
+            o.type = MTE_OP_LOAD_NODE;
+            o.a = (int32_t)l;
+            o.b = c;
+            db.ops.push_back(o);
+            nodes++;
+        }
     mte_op end{};
     end.type = MTE_OP_LOAD_END;
+    end.a = (int32_t)nodes;
     num_field(*md, u"sequenceNumber", &end.seq);
     end.msn = end.seq;
     num_field(*md, u"minSequenceNumber", &end.msn);
     db.ops.push_back(end);
-    // loadBody (:150-216): later chunks appended at root.cachedLength, refSeq 0, NonCollab, seq 0
-    const json::Value* ocm = md->get(u"orderedChunkMetadata");
-    if (!ocm || ocm->kind != json::Value::Array || ocm->items.size() <= 1) return MTE_OK;
-    if (mergeInfo) return db.fail(MTE_E_UNSUPPORTED, "body chunks after a header with merge info");
-    int32_t pos = 0;
-    for (const mte_op& o : db.ops)
-        if (o.type == MTE_OP_LOAD_SEG && !(o.flags & MTE_F_LOAD_REMOVED)) pos += (int32_t)o.b;
-    uint32_t nc;
-    if (int rc = db.short_id(kNonCollabName, &nc)) return rc;
-    for (size_t i = 1; i < ocm->items.size(); i++) {
-        const json::Value* id = ocm->items[i].kind == json::Value::Object ? ocm->items[i].get(u"id") : nullptr;
-        if (!id || id->kind != json::Value::String) return db.fail(MTE_E_PARSE, "chunk id");
-        json::Value ch;
-        if (int rc = load_chunk(db, *t, id->str, &ch)) return rc;
-        const json::Value* cs = ch.get(u"segments");
-        if (!cs || cs->kind != json::Value::Array) continue;
-        for (const json::Value& sp : cs->items) {
-            if (sp.kind == json::Value::Object && sp.get(u"json"))  // flushBatch never clears (:196-199)
-                return db.fail(MTE_E_UNSUPPORTED, "merge-info segment in a body chunk");
-            mte_op o{};
-            o.type = MTE_OP_LOAD_APPEND;
-            if (int rc = load_spec(b, db, sp, o)) return rc;
-            o.client = (uint8_t)nc;
-            o.pos1 = pos;
-            pos += (int32_t)o.b;
-            db.ops.push_back(o);
-        }
-    }
     return MTE_OK;
 }
 

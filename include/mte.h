@@ -63,23 +63,28 @@ enum {
     MTE_OP_INSERT_MARKER = 3, /* insert Marker: b = refType, props = marker props */
     MTE_OP_NOOP = 4,          /* sequenced message with no merge-tree op (only seq/msn advance) */
     /* Resume from a summary (SnapshotLoader, snapshotLoader.ts:98-216); records precede the op log.
-     * LOAD_SEG: one header segment in document order (specToSegment :79-111): a = payload offset
-     *   (text) or refType (marker, MTE_F_LOAD_MARKER), b = length, seq = seg.seq (0 = universal),
-     *   client = seg.clientId, props; MTE_F_LOAD_REMOVED: ref_seq = removedSeq, pos1 = removedClient.
-     * LOAD_END: reloadFromSegments of the LOAD_SEGs (mergeTree.ts:1195-1251), then
-     *   startOrUpdateCollaboration(minSeq = msn, currentSeq = seq) (snapshotLoader.ts:126-140).
-     * LOAD_APPEND: one body segment appended (loadBody, :166-213: insertSegments at the end with
-     *   refSeq 0, client NonCollab, seq 0); fields as INSERT / INSERT_MARKER (marker flag). */
+     * LOAD_SEG: one segment in document order (specToSegment :79-111): a = payload offset (text) or
+     *   refType (marker, MTE_F_LOAD_MARKER), b = length, seq = seg.seq (0 = universal), client =
+     *   seg.clientId, props; MTE_F_LOAD_REMOVED: ref_seq = removedSeq, pos1 = removedClient;
+     *   MTE_F_LOAD_LEAF: starts a new leaf block; MTE_F_LOAD_BODY: a body-chunk segment (loadBody,
+     *   :166-213: insertSegments at the end, refSeq 0, client NonCollab, seq 0).
+     * LOAD_NODE: one interior node of the loaded tree: a = level (1 = parent of leaves), b = child
+     *   count; in level order, then document order. The shape is that of reloadFromSegments
+     *   (mergeTree.ts:1195-1251) over the header followed by the body appends (8 -> 4+4 splits).
+     * LOAD_END: a = number of LOAD_NODE records just before it; links the tree, then
+     *   startOrUpdateCollaboration(minSeq = msn, currentSeq = seq) (snapshotLoader.ts:126-140). */
     MTE_OP_LOAD_SEG = 5,
     MTE_OP_LOAD_END = 6,
-    MTE_OP_LOAD_APPEND = 7,
+    MTE_OP_LOAD_NODE = 7,
 };
 
 /* flags */
 #define MTE_F_END_OF_MSG 0x1u   /* last op of its ISequencedDocumentMessage: currentSeq=seq, setMinSeq(msn) */
 #define MTE_F_REWRITE 0x2u      /* annotate combiningOp {name:"rewrite"} (segmentPropertiesManager.ts:65-78) */
-#define MTE_F_LOAD_MARKER 0x4u  /* LOAD_SEG / LOAD_APPEND: a Marker (a = refType, length 1) */
+#define MTE_F_LOAD_MARKER 0x4u  /* LOAD_SEG: a Marker (a = refType, length 1) */
 #define MTE_F_LOAD_REMOVED 0x8u /* LOAD_SEG: removed (ref_seq = removedSeq, pos1 = removedClient) */
+#define MTE_F_LOAD_LEAF 0x10u   /* LOAD_SEG: first segment of a new leaf block */
+#define MTE_F_LOAD_BODY 0x20u   /* LOAD_SEG: appended from a body chunk */
 
 typedef struct mte_op {
     int32_t seq;        /* sequenceNumber */

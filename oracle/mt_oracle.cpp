@@ -1018,6 +1018,8 @@ class Doc {
                                b->client_names + b->client_name_offsets[c + 1]);
         const uint16_t* payload = b->payload + b->doc_payload_offsets[d];
         std::vector<Node*> loadSegs;
+        std::vector<Segment*> bodySegs;
+        int bodyClient = NonCollabClient;
         for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1] && !status; i++) {
             const mte_op& op = b->ops[i];
             try {
@@ -1025,12 +1027,17 @@ class Doc {
                 int shortId = getOrAddShortClientId(names[op.client]);
                 if (shortId != op.client) throw EngineError(MTE_DOC_UNSUPPORTED, "client ids not in first-appearance order");
                 if (op.type >= MTE_OP_LOAD_SEG) {  // summary records (include/mte.h; loadSnapshot above)
+                    if (op.type == MTE_OP_LOAD_NODE) continue;  // the engine's shape hint; rebuilt here
                     if (op.type == MTE_OP_LOAD_END) {
                         mt.reloadFromSegments(loadSegs);
                         loadSegs.clear();
                         mt.startCollaboration(0, op.msn, op.seq);
+                        if (!bodySegs.empty())  // loadBody's single flush (snapshotLoader.ts:203-213)
+                            mt.insertSegments(mt.localLength(mt.root), bodySegs, 0, bodyClient, 0);
+                        bodySegs.clear();
                         continue;
                     }
+                    if (op.type != MTE_OP_LOAD_SEG) throw EngineError(MTE_DOC_UNSUPPORTED, "unknown record");
                     Segment* s = mt.newSegment();
                     if (op.flags & MTE_F_LOAD_MARKER) {
                         s->marker = true;
@@ -1041,9 +1048,9 @@ class Doc {
                         s->len = (int)op.b;
                     }
                     if (op.props) MergeTree::addProperties(s, propset(b, op.props), false);
-                    if (op.type == MTE_OP_LOAD_APPEND) {
-                        std::vector<Segment*> segs{s};
-                        mt.insertSegments(op.pos1, segs, 0, op.client, 0);
+                    if (op.flags & MTE_F_LOAD_BODY) {
+                        bodySegs.push_back(s);
+                        bodyClient = op.client;
                         continue;
                     }
                     s->seq = op.seq;

@@ -2116,7 +2116,16 @@ struct Engine {
 #ifdef MTE_PROFILE
         ProfScope _total(prof + PF_TOTAL);
 #endif
-        const u64 b = i, e = p.docs[doc].op_end;
+        const u64 e = p.docs[doc].op_end;
+        // summary records (resume from a summary) precede the op log: a cold prefix loop, so the op
+        // loops below carry no branch for them
+        for (; i < e && !st.status; i++) {
+            const mte_op op = read_op(p.ops + i);
+            if (op.type < MTE_OP_LOAD_SEG) break;
+            if (!room()) return i;
+            load_record(op, i);
+        }
+        const u64 b = i;
         if (LDSM) {
             // op records are staged RING_OPS at a time through LDS; the next batch is prefetched
             // into registers one batch ahead (lane l holds 16 B of record l/2 of the batch).
@@ -2139,14 +2148,12 @@ struct Engine {
                     op = read_op(RING() + r);
                 }
                 if (!room()) break;
-                if (op.type >= MTE_OP_LOAD_SEG) load_record(op, i);  // summary records (cold)
-                else apply(op);
+                apply(op);
             }
         } else {
             for (; i < e && !st.status; i++) {
                 mte_op op = p.ops[i];
-                if (op.type >= MTE_OP_LOAD_SEG) load_record(op, i);
-                else apply(op);
+                apply(op);
             }
         }
         return i;

@@ -205,3 +205,29 @@ def test_gpu_rebuild_edits_after_load(engine):
     for d in range(len(FIXTURES)):
         compare_doc(engine, batch, d, observer=OBS)
         assert engine.text(d) == ""
+
+
+@pytest.mark.gpu
+def test_gpu_mixed_batch_of_logs_and_summaries(engine):
+    """Catch-up documents interleaved with plain op logs in one batch (one pass, shared queues)."""
+    from tests.gpu_helpers import compare_doc
+
+    farm = c1_farm_log(seed=5, total_ops=600)
+    collab = collab_summaries()
+    b = mte.Builder()
+    kinds = []
+    for k in range(12):
+        if k % 3 == 0:
+            b.add_doc(farm[: 200 + 30 * k], observer=OBS)
+        elif k % 3 == 1:
+            summ, suffix = collab[k % len(collab)]
+            b.add_doc_from_summary(summ, suffix, observer=OBS)
+        else:
+            b.add_doc_from_summary(fixture(FIXTURES[k % len(FIXTURES)]), None, observer=OBS)
+        kinds.append(k % 3)
+    batch = b.batch()
+    engine.load(batch)
+    st = engine.replay()
+    assert st["failed_docs"] == 0, st
+    for d in range(len(kinds)):
+        compare_doc(engine, batch, d, observer=OBS)

@@ -1539,6 +1539,55 @@ static const json::Value* tree_entry(const json::Value& tree, const char16_t* pa
     return nullptr;
 }
 
+static json::Value jstr(const std::u16string& v) {
+    json::Value x;
+    x.kind = json::Value::String;
+    x.str = v;
+    return x;
+}
+static json::Value jnum(double v) {
+    json::Value x;
+    x.kind = json::Value::Number;
+    x.num = v;
+    return x;
+}
+// toLatestVersion for a legacy chunk (snapshotChunks.ts:135-176): segmentTexts -> segments, and for
+// the header the metadata it carries or buildHeaderMetadataForLegecyChunk's (a "body" chunk when the
+// header holds fewer chars than the document).
+static int legacy_to_v1(const std::u16string& path, json::Value& c) {
+    json::Value v1;
+    v1.kind = json::Value::Object;
+    v1.members.emplace_back(u"version", jstr(u"1"));
+    for (auto& m : c.members) {
+        if (m.first == u"segmentTexts") v1.members.emplace_back(u"segments", m.second);
+        else if (m.first == u"headerMetadata") v1.members.emplace_back(u"headerMetadata", m.second);
+    }
+    if (path == u"header" && !c.get(u"headerMetadata")) {
+        json::Value md, ids;
+        md.kind = json::Value::Object;
+        ids.kind = json::Value::Array;
+        auto id = [&](const char16_t* n) {
+            json::Value o;
+            o.kind = json::Value::Object;
+            o.members.emplace_back(u"id", jstr(n));
+            ids.items.push_back(o);
+        };
+        id(u"header");
+        const json::Value* cl = c.get(u"chunkLengthChars");
+        const json::Value* tl = c.get(u"totalLengthChars");
+        if (cl && tl && cl->num < tl->num) id(u"body");
+        md.members.emplace_back(u"orderedChunkMetadata", ids);
+        if (const json::Value* m = c.get(u"chunkMinSequenceNumber")) md.members.emplace_back(u"minSequenceNumber", *m);
+        if (const json::Value* q = c.get(u"chunkSequenceNumber")) md.members.emplace_back(u"sequenceNumber", *q);
+        if (tl) md.members.emplace_back(u"totalLength", *tl);
+        if (const json::Value* ts = c.get(u"totalSegmentCount")) md.members.emplace_back(u"totalSegmentCount", *ts);
+        v1.members.emplace_back(u"headerMetadata", md);
+    }
+    (void)jnum;
+    c = v1;
+    return MTE_OK;
+}
+
 // storage.read(path) + SnapshotV1.processChunk (snapshotV1.ts:249-270) for a utf-8 blob
 static int load_chunk(DocBuild& db, const json::Value& tree, const std::u16string& path, json::Value* out) {
     const json::Value* e = tree_entry(tree, path.c_str());
@@ -1555,8 +1604,9 @@ static int load_chunk(DocBuild& db, const json::Value& tree, const std::u16strin
         return db.fail(MTE_E_PARSE, ex.what());
     }
     const json::Value* ver = out->kind == json::Value::Object ? out->get(u"version") : nullptr;
+    if (!ver && out->kind == json::Value::Object && out->get(u"segmentTexts")) return legacy_to_v1(path, *out);
     if (!ver || ver->kind != json::Value::String || ver->str != u"1")
-        return db.fail(MTE_E_UNSUPPORTED, "legacy (pre-v1) snapshot chunks are out of scope");
+        return db.fail(MTE_E_UNSUPPORTED, "unsupported snapshot chunk version");
     return MTE_OK;
 }
 
@@ -1677,6 +1727,37 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
     end.msn = end.seq;
     num_field(*md, u"minSequenceNumber", &end.msn);
     db.ops.push_back(end);
+    // loadBodyAndCatchupOps (snapshotLoader.ts:55-77): one blob beyond the chunks holds catch-up
+    // messages (legacy summaries), applied after the load like any sequenced message
+    const json::Value* es = t->get(u"entries");
+    size_t nChunks = ocm && ocm->kind == json::Value::Array ? ocm->items.size() : 1, nBlobs = 0;
+    const json::Value* extra = nullptr;
+    static const std::vector<json::Value> none;
+    for (const json::Value& e : es ? es->items : none) {  // (a reference: `extra` points into it)
+        const json::Value* ty = e.get(u"type");
+        const json::Value* pth = e.get(u"path");
+        if (!ty || ty->kind != json::Value::String || ty->str != u"Blob" || !pth) continue;
+        nBlobs++;
+        bool isChunk = false;
+        for (size_t i = 0; ocm && ocm->kind == json::Value::Array && i < ocm->items.size(); i++) {
+            const json::Value* id = ocm->items[i].get(u"id");
+            isChunk |= id && id->kind == json::Value::String && id->str == pth->str;
+        }
+        if (!isChunk) extra = &e;
+    }
+    if (nBlobs == nChunks + 1 && extra) {
+        const json::Value* v = extra->get(u"value");
+        const json::Value* c = v ? v->get(u"contents") : nullptr;
+        if (!c || c->kind != json::Value::String) return db.fail(MTE_E_PARSE, "catch-up ops blob");
+        const std::string text = json::to_utf8(c->str.data(), c->str.size());
+        json::Value msgs;
+        try {
+            msgs = json::parse(text.data(), text.size());
+        } catch (std::exception& ex) {
+            return db.fail(MTE_E_PARSE, ex.what());
+        }
+        if (int rc = add_messages(b, msgs, db)) return rc;
+    }
     return MTE_OK;
 }
 

@@ -921,7 +921,7 @@ class Doc {
         return nullptr;
     }
     // storage.read(path) + SnapshotV1.processChunk (snapshotV1.ts:249-270) for a utf-8 blob
-    static JVP chunkAt(const JV& tree, const u16s& path) {
+    static JVP chunkAt(const JV& tree, const u16s& path) {  // (legacy chunks converted to v1)
         JVP e = treeEntry(tree, path);
         JVP v = e ? e->o.get(u"value") : nullptr;
         JVP c = v && v->t == JV::Obj ? v->o.get(u"contents") : nullptr;
@@ -931,7 +931,34 @@ class Doc {
         std::string s = u16_to_utf8(c->s);
         JVP ch = parse(s.data(), s.size());
         JVP ver = ch->t == JV::Obj ? ch->o.get(u"version") : nullptr;
-        if (!ver || ver->t != JV::Str || ver->s != u"1") throw EngineError(MTE_DOC_UNSUPPORTED, "legacy chunk");
+        if (!ver && ch->t == JV::Obj && ch->o.get(u"segmentTexts")) {  // toLatestVersion (snapshotChunks.ts:135-176)
+            auto v1 = std::make_shared<JV>();
+            v1->t = JV::Obj;
+            v1->o.set(u"version", JV::str(u"1"));
+            v1->o.set(u"segments", ch->o.get(u"segmentTexts"));
+            JVP md = ch->o.get(u"headerMetadata");
+            if (!md && path == u"header") {  // buildHeaderMetadataForLegecyChunk (:158-176)
+                md = std::make_shared<JV>();
+                md->t = JV::Obj;
+                auto ids = std::make_shared<JV>();
+                ids->t = JV::Arr;
+                auto id = [&](const char16_t* n) {
+                    auto o = std::make_shared<JV>();
+                    o->t = JV::Obj;
+                    o->o.set(u"id", JV::str(n));
+                    ids->a.push_back(o);
+                };
+                id(u"header");
+                JVP cl = ch->o.get(u"chunkLengthChars"), tl = ch->o.get(u"totalLengthChars");
+                if (cl && tl && cl->n < tl->n) id(u"body");
+                md->o.set(u"orderedChunkMetadata", ids);
+                if (JVP m = ch->o.get(u"chunkMinSequenceNumber")) md->o.set(u"minSequenceNumber", m);
+                if (JVP q = ch->o.get(u"chunkSequenceNumber")) md->o.set(u"sequenceNumber", q);
+            }
+            if (md) v1->o.set(u"headerMetadata", md);
+            return v1;
+        }
+        if (!ver || ver->t != JV::Str || ver->s != u"1") throw EngineError(MTE_DOC_UNSUPPORTED, "chunk version");
         return ch;
     }
     // SnapshotLoader.initialize: loadHeader (:113-148) then loadBody (:150-216).
@@ -972,6 +999,31 @@ class Doc {
             }
         }
         if (!batch.empty()) mt.insertSegments(mt.localLength(mt.root), batch, 0, NonCollabClient, 0);
+        // loadBodyAndCatchupOps (snapshotLoader.ts:55-77): a blob beyond the chunks holds catch-up
+        // messages, applied after the load (sequence.ts:499-527, processMergeTreeMsg -> applyMsg)
+        JVP es = t->t == JV::Obj ? t->o.get(u"entries") : nullptr;
+        size_t nBlobs = 0, nChunks = ocm && ocm->t == JV::Arr ? ocm->a.size() : 1;
+        JVP extra;
+        for (auto& e : es && es->t == JV::Arr ? es->a : std::vector<JVP>{}) {
+            JVP ty = e->o.get(u"type"), p = e->o.get(u"path");
+            if (!ty || ty->t != JV::Str || ty->s != u"Blob" || !p) continue;
+            nBlobs++;
+            bool isChunk = false;
+            for (size_t i = 0; ocm && ocm->t == JV::Arr && i < ocm->a.size(); i++) {
+                JVP id = ocm->a[i]->o.get(u"id");
+                isChunk |= id && id->t == JV::Str && id->s == p->s;
+            }
+            if (!isChunk) extra = e;
+        }
+        if (nBlobs == nChunks + 1 && extra) {
+            JVP v = extra->o.get(u"value");
+            JVP c = v ? v->o.get(u"contents") : nullptr;
+            if (!c || c->t != JV::Str) throw EngineError(MTE_DOC_UNSUPPORTED, "catch-up ops blob");
+            std::string txt = u16_to_utf8(c->s);
+            JVP msgs = parse(txt.data(), txt.size());
+            if (msgs->t == JV::Arr)
+                for (auto& m : msgs->a) applyMsg(*m);
+        }
     }
     int loadSnapshotJson(const char* json, size_t len) {
         try {

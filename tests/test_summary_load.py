@@ -157,10 +157,10 @@ def test_summary_errors():
     b = mte.Builder()
     with pytest.raises(mte.MteError):
         b.add_doc_from_summary('{"entries":[]}')
-    legacy = {"entries": [{"mode": "100644", "path": "header", "type": "Blob",
-                           "value": {"contents": json.dumps({"segmentTexts": []}), "encoding": "utf-8"}}]}
-    with pytest.raises(mte.MteError):
-        b.add_doc_from_summary(legacy)
+    future = {"entries": [{"mode": "100644", "path": "header", "type": "Blob",
+                           "value": {"contents": json.dumps({"version": "2", "segments": []}), "encoding": "utf-8"}}]}
+    with pytest.raises(mte.MteError):  # toLatestVersion throws on unknown versions (snapshotChunks.ts:153-155)
+        b.add_doc_from_summary(future)
     with pytest.raises(mte.MteError):
         b.add_doc_from_summary(fixture("headerOnly"), observer="")  # loading needs a collaborating client
 
@@ -231,3 +231,43 @@ def test_gpu_mixed_batch_of_logs_and_summaries(engine):
     assert st["failed_docs"] == 0, st
     for d in range(len(kinds)):
         compare_doc(engine, batch, d, observer=OBS)
+
+
+# Legacy (pre-v1) summaries: packages/dds/sequence/src/test/snapshots/legacy{,WithCatchUp}/*.json, copied as
+# data into tests/golden. toLatestVersion (snapshotChunks.ts:135-176) converts their chunks; the extra
+# blob of catch-up messages is applied after the load (snapshotLoader.ts:55-77). Pinned: the loaded
+# document re-emits exactly the v1 fixture generated from the same strings.
+LEGACY = [(k, n) for k in ("legacy", "legacyWithCatchUp") for n in FIXTURES]
+
+
+def legacy_fixture(kind, name):
+    with open(os.path.join(os.path.dirname(GOLDEN), kind, name + ".json")) as f:
+        return f.read()
+
+
+@pytest.mark.parametrize("kind,name", LEGACY)
+def test_legacy_summary_loads_as_v1(kind, name):
+    o = oracle_catchup(legacy_fixture(kind, name), None)
+    assert json.loads(o.snapshot_json()) == merge_tree_tree(fixture(name))
+    b = mte.Builder()
+    b.add_doc_from_summary(legacy_fixture(kind, name), observer=OBS)
+    batch = b.batch()
+    r = OracleDoc(OBS)
+    r.apply_batch(ctypes.addressof(batch), 0)
+    assert r.status()[0] == 0 and r.segments_json() == o.segments_json()
+
+
+@pytest.mark.gpu
+def test_gpu_legacy_summaries_reemit_v1(engine):
+    from tests.gpu_helpers import compare_doc
+
+    b = mte.Builder()
+    for kind, name in LEGACY:
+        b.add_doc_from_summary(legacy_fixture(kind, name), None, observer=OBS)
+    batch = b.batch()
+    engine.load(batch)
+    st = engine.replay()
+    assert st["failed_docs"] == 0, st
+    for d, (kind, name) in enumerate(LEGACY):
+        compare_doc(engine, batch, d, observer=OBS)
+        assert json.loads(engine.snapshot_shared_string(d)) == json.loads(fixture(name))

@@ -1,24 +1,30 @@
 """bench.py — headline benchmark of the MI355X merge-tree replay engine.
 
-Default workload (BASELINE.json configs[1], "C2"): 4096 synthetic SharedString documents x 10,000
-sequenced ops each, insert/remove only, 8 simulated writers plus a read-only observer (SURVEY §8d
-generator, run on the GPU). A step = one replay of the whole batch (Client.applyMsg for every
-message of every document, client.ts:805-836) from empty state to every document's final state,
-inputs resident in HBM. Multi-GPU: documents are sharded by doc id (each rank replays its own
-4096-doc shard; weak scaling); the only collective is the final all-gather of 32-B per-document
-summary records over RCCL/xGMI, outside the timed region.
+Default workload = the configuration BASELINE.json's metric is quoted on ("... 256k docs"), C4:
+262,144 synthetic SharedString documents with Zipf-skewed op counts clamp(1e6/r, 1e3, 1e6)
+(268.6 M sequenced ops, one document of 1 M ops), 8 simulated writers plus a read-only observer
+(SURVEY §8d generator, run on the GPU). A step = one replay of the whole batch (Client.applyMsg for
+every message of every document, client.ts:805-836) from empty state to every document's final
+state, inputs resident in HBM.
 
-Other configs (--config): C3 (65,536 docs x 10k ops with annotate, forced ties and overlapping
-removes, per GPU, weak), C4 (262,144 docs, Zipf op counts clamp(1e6/r, 1e3, 1e6), LPT-sharded over
-the ranks, strong), C5 (1,024 docs x 1M ops, MSN lag <= 64 so zamboni runs continuously, sharded
-over the ranks, strong).
+Multi-GPU: documents are sharded by GLOBAL doc id, one process per GPU. C4 is strong
+scaling: the same 262,144 documents at every N, LPT-assigned by op count, each document seeded by
+its global id, so an N-GPU run replays exactly the documents of the 1-GPU run. The only collective
+is the final RCCL all-gather of the 32-B per-document summary records (outside the timed region).
+`python bench.py --gpus N` with no WORLD_SIZE in the environment spawns the N ranks itself
+(fresh processes, before anything touches a GPU); under torch.distributed.run it is one rank.
 
-Prints ONE JSON line (rank 0).
+Other configs (--config): C2 (4,096 docs x 10k ops per GPU, weak), C3 (65,536 docs x 10k ops with
+annotate, forced ties and overlapping removes, per GPU, weak), C5 (1,024 docs x 1M ops, MSN lag <= 64
+so zamboni runs continuously, strided over the ranks, strong).
+
+Prints ONE JSON line (rank 0). Exits non-zero if a document fails or the oracle check disagrees.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
 import sys
 import time
 
@@ -34,28 +40,29 @@ CONFIGS = {
            "desc": "insert/remove around a 2048-char target"},
     "C3": {"docs": 65536, "ops": 10000, "kind": 3, "scaling": "weak", "steps": 3, "warmup": 1,
            "desc": "45/35/20 insert/remove/annotate, 15% forced ties and overlapping removes"},
-    "C4": {"docs": 262144, "ops": 0, "kind": 2, "scaling": "strong", "steps": 2, "warmup": 0,
-           "desc": "Zipf op counts clamp(1e6/r, 1e3, 1e6), C2 mix, LPT-sharded"},
+    "C4": {"docs": 262144, "ops": 0, "kind": 2, "scaling": "strong", "steps": 3, "warmup": 1,
+           "desc": "Zipf op counts clamp(1e6/r, 1e3, 1e6), C2 mix, LPT-sharded by global doc id"},
     "C5": {"docs": 1024, "ops": 1000000, "kind": 5, "scaling": "strong", "steps": 2, "warmup": 0,
            "desc": "1M-op docs, C2 mix with MSN lag <= 64 (continuous zamboni)"},
 }
+GEN_SEED = 1000  # one seed for every rank: documents differ by global id only
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
-    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 5; 2 for C4/C5)")
-    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 1; 0 for C4/C5)")
+    ap.add_argument("--config", default="C4", choices=sorted(CONFIGS))
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (config default)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (config default)")
     ap.add_argument("--docs", type=int, default=None)
     ap.add_argument("--ops", type=int, default=None)
     ap.add_argument("--clients", type=int, default=8)
     ap.add_argument("--kind", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None, help="default: one per host core available")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-docs", type=int, default=32, help="docs checked against the oracle after timing")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     c = CONFIGS[a.config]
     a.docs = c["docs"] if a.docs is None else a.docs
     a.ops = c["ops"] if a.ops is None else a.ops
@@ -65,12 +72,59 @@ def parse():
     return a
 
 
+def host_cores():
+    """(cores this process can use, how that was determined): its CPU affinity, capped by the cgroup
+    CPU quota (cpu.max), which is what bounds a container's parallel CPU throughput."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    why = f"sched_getaffinity {avail}, os.cpu_count {os.cpu_count()}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) / int(period)))
+            why += f", cgroup cpu.max quota {q} CPUs"
+            avail = min(avail, q)
+    except (OSError, ValueError):
+        pass
+    return avail, why
+
+
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def main():
-    args = parse()
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_entry(rank, world, port, argv):
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    run(parse(argv))
+
+
+def launch(args, argv):
+    """`--gpus N` without a launcher: N fresh rank processes (spawned before any GPU call here)."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_entry, args=(r, args.gpus, port, argv)) for r in range(args.gpus)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join()
+    return max(abs(p.exitcode or 0) for p in procs)
+
+
+def run(args):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -80,48 +134,37 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")  # RCCL over xGMI
+        dist.init_process_group("nccl")  # RCCL; carries only barriers, the max-time reduce and the RCCL id
     from fluidframework_amd import mte
+    from fluidframework_amd.shard import gather_summaries_rccl, plan_shard
 
     cfg = CONFIGS[args.config]
     eng = mte.Engine(local)
     t0 = time.time()
-    # per-rank shard: distinct seeds => distinct documents
-    if cfg["scaling"] == "weak":
-        n_local, per_doc = args.docs, None
-    elif args.config == "C4":
-        from fluidframework_amd.shard import lpt_assign, zipf_op_counts
-
-        counts = zipf_op_counts(args.docs, seed=0)
-        mine = lpt_assign(counts, world)[rank]  # longest first
-        n_local, per_doc = len(mine), counts[mine]
-    else:  # C5: equal documents, contiguous shards
-        n_local, per_doc = len(range(rank, args.docs, world)), None
-    eng.generate(args.kind, n_local, args.ops, n_clients=args.clients, seed=1000 + rank, ops_per_doc=per_doc)
+    ids, counts = plan_shard(args.config, world, rank, args.docs, args.ops)
+    n_local = len(ids)
+    eng.generate(args.kind, n_local, args.ops, n_clients=args.clients, seed=GEN_SEED, ops_per_doc=counts,
+                 doc_ids=ids)
     gen_s = time.time() - t0
-    log(f"rank {rank}: generated {n_local} docs ({args.config}) in {gen_s:.1f} s")
+    log(f"rank {rank}/{world}: generated {n_local} docs ({args.config}, {int(counts.sum())} ops) in {gen_s:.1f} s")
     batch = eng.export_batch()
     ops_np = mte.batch_ops(batch)
     ins = ops_np["type"] == mte.MTE_OP_INSERT
     payload_chars = int(ops_np["b"][ins].sum())
     n_ops_rank = int(len(ops_np))
 
-    def step():
-        return eng.replay()
-
     for _ in range(args.warmup):
-        w = step()
+        w = eng.replay()
         log(f"warmup step: {w['kernel_ms']:.1f} ms kernel, {w['ops']} ops")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    kms, lds_ms = [], []
+    kms = []
     st = None
     for _ in range(args.steps):
-        st = step()
+        st = eng.replay()
         kms.append(st["kernel_ms"])
-        lds_ms.append(eng.run_info()["lds_ms"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -130,73 +173,87 @@ def main():
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    assert st["failed_docs"] == 0, st
+    if st["failed_docs"]:
+        log(f"FAILED documents: {st}")
+        sys.exit(3)
     ops_applied = st["ops"]
     total_ops = ops_applied
-    if world > 1:  # shards may differ (C4): sum what every rank applied
+    if world > 1:  # shards differ in size (C4): sum what every rank applied
         t = torch.tensor([ops_applied], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         total_ops = int(t.item())
     ms_per_step = elapsed / args.steps * 1000.0
     value = total_ops * args.steps / elapsed
-
     log(f"timed {args.steps} steps: {ms_per_step:.1f} ms/step, {value / 1e6:.1f} Mops/s")
+    info = eng.run_info()
+    solo = [eng.doc_result(d) for d in range(min(info["solo"], n_local))]
+
     # final summary gather (RCCL all-gather of 32-B records), outside the timed region
     t1 = time.time()
-    summ = eng.summaries()
+    summ = eng.summaries()  # this rank's records: checksum of text + SnapshotV1 bytes per document
     snap_host_s = time.time() - t1
+    gathered = len(gather_summaries_rccl(eng)) if world > 1 else len(summ)
     snap_bytes = int(summ["snapshot_bytes"].sum())
-    if world > 1:
-        from fluidframework_amd.shard import gather_summaries
 
-        gathered = len(gather_summaries(summ, device="cuda"))
-    else:
-        gathered = len(summ)
-
-    # roofline on the replay kernel: algorithmic bytes per launch / HIP-event kernel time
+    # roofline of the replay pass: algorithmic bytes per launch / HIP-event pass time
     alg_bytes = n_ops_rank * (OP_RECORD_B + LEAF_BLOCK_B) + payload_chars  # 1 B/char ASCII payload
     kernel_ms = sum(kms) / len(kms)
-    info = eng.run_info()
     achieved = alg_bytes / (kernel_ms / 1000.0) / 1e9
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_replay.json")
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_replay_{args.config}.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("docs") == args.docs and pmc.get("ops") == args.ops and pmc.get("kind") == args.kind:
+            if pmc.get("docs") == n_local and pmc.get("ops") == int(counts.sum()) and pmc.get("kind") == args.kind:
                 traffic = pmc.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
 
-    # verify a sample of documents against the CPU oracle (checker only)
-    verified = None
-    cpu = None
-    if rank == 0:
-        from oracle import replay_batch
+    # verify a sample of this rank's documents against the CPU oracle (checker only)
+    from oracle import replay_batch
 
-        nv = min(args.verify_docs, n_local)
-        if nv:
-            o_ops, cks, sts = replay_batch(ctypes.addressof(batch), 0, nv, threads=args.cpu_threads)
-            assert all(sts[d] == 0 for d in range(nv)), "oracle reports failing documents"
-            verified = all(int(summ["checksum"][d]) == cks[d] and int(summ["status"][d]) == sts[d] for d in range(nv))
-        log(f"oracle verification of {nv} docs: {verified}")
-        if not args.no_cpu_baseline:
-            # bounded sample: grow the doc count until ~cpu_seconds of oracle replay on cpu_threads threads
-            nd = max(args.cpu_threads, 16)
-            while True:
-                nd = min(nd, n_local)
-                c0 = time.perf_counter()
-                c_ops, _, _ = replay_batch(ctypes.addressof(batch), 0, nd, threads=args.cpu_threads,
-                                           with_snapshot=False)
-                dt = time.perf_counter() - c0
-                log(f"cpu baseline sample: {nd} docs, {c_ops} ops in {dt:.2f} s")
-                if dt >= args.cpu_seconds * 0.5 or nd >= n_local:
-                    break
-                nd = int(nd * min(8.0, max(2.0, args.cpu_seconds / max(dt, 1e-3))))
-            cpu = {"value": c_ops / dt, "unit": "ops/s", "cores": args.cpu_threads, "kind": "port",
-                   "sample": f"oracle (tree-shaped C++ restatement) replaying docs 0..{nd - 1} of the same {args.config} batch "
-                             f"({c_ops} ops, replay only) on {args.cpu_threads} threads in {dt:.2f} s"}
+    nv = min(args.verify_docs, n_local)
+    verified = True
+    if nv:
+        o_ops, cks, sts = replay_batch(ctypes.addressof(batch), 0, nv, threads=min(16, nv))
+        verified = all(sts[d] == 0 for d in range(nv)) and all(
+            int(summ["checksum"][d]) == cks[d] and int(summ["status"][d]) == sts[d] and int(summ["doc_id"][d]) == ids[d]
+            for d in range(nv))
+    if world > 1:
+        t = torch.tensor([1 if verified else 0], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        verified = bool(t.item())
+    log(f"oracle verification of {nv} docs per rank (incl. the longest): {verified}")
+    if not verified:
+        sys.exit(4)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import replay_list
+
+        cores, why = host_cores()
+        threads = args.cpu_threads or cores
+        # bounded, size-stratified sample of the same batch: every k-th document of the LPT order
+        # (longest first, so the critical-path document is in it and the op-count distribution is
+        # kept); k from a short calibration so the sample takes ~cpu_seconds on `threads` threads
+        mid = n_local // 2
+        m = min(n_local - mid, 64 * threads)
+        c0 = time.perf_counter()
+        cal = replay_list(ctypes.addressof(batch), np.arange(mid, mid + m), threads=threads)
+        per_s = cal / max(time.perf_counter() - c0, 1e-3)
+        k = 1
+        while k < n_local and counts[::k].sum() / per_s > args.cpu_seconds:
+            k *= 2
+        sample = np.arange(0, n_local, k)
+        c0 = time.perf_counter()
+        c_ops = replay_list(ctypes.addressof(batch), sample, threads=threads)
+        dt = time.perf_counter() - c0
+        log(f"cpu baseline sample: every {k}th doc ({len(sample)} docs), {c_ops} ops in {dt:.2f} s on {threads} threads")
+        cpu = {"value": c_ops / dt, "unit": "ops/s", "cores": threads, "kind": "port",
+               "sample": f"oracle (tree-shaped C++ restatement of the reference path) replaying every {k}th "
+                         f"document ({len(sample)} docs, {c_ops} ops, replay only, longest first) of the same "
+                         f"{args.config} batch on {threads} threads, one per usable host core ({why}), in {dt:.2f} s"}
 
     if rank == 0:
         line = {
@@ -205,23 +262,33 @@ def main():
             "vs_baseline": None, "dtype": "int32", "data": "synthetic (GPU generator, SURVEY §8d)",
             "config": {"workload": f"{args.config}: {args.docs} docs"
                                    + (" per GPU" if cfg["scaling"] == "weak" else " per job")
-                                   + (f" x {args.ops} ops" if args.ops else "") + f", {cfg['desc']}, {args.clients} writers",
+                                   + (f" x {args.ops} ops" if args.ops else f", {total_ops} ops")
+                                   + f", {cfg['desc']}, {args.clients} writers",
                        "config_id": args.config, "docs_per_gpu": n_local, "ops_per_doc": args.ops or "zipf",
-                       "clients": args.clients, "parallelism": f"doc-sharded x{world}"},
+                       "ops_per_step": total_ops, "clients": args.clients, "parallelism": f"doc-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "replay pass: mte::k_lds<false> + mte::k_hbmq<false> (concurrent streams)",
+                         "kernel": "replay pass: mte::k_solo + mte::k_lds + mte::k_hbmq (concurrent streams)",
                          "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
-            "extra": {"ops_per_step_per_gpu": ops_applied, "lds_pass_ms": sum(lds_ms) / len(lds_ms),
-                      "hbm_pass_ms": info["hbm_ms"], "docs_rerun_hbm": info["spilled"],
-                      "docs_continued_hbm": info["continued"], "docs_hbm_waves": info["hbm_docs"],
-                      "lds_groups": info["lds_groups"], "hbm_wave_slots": info["hbm_waves"], "gen_s": gen_s, "snapshot_host_s": snap_host_s,
-                      "snapshot_bytes": snap_bytes, "summaries_gathered": gathered, "oracle_verified_docs": verified},
+            "extra": {"ops_per_step_rank0": ops_applied, "longest_doc_ops": int(counts.max()),
+                      "solo_docs": info["solo"], "solo_modes": [r["mode"] for r in solo],
+                      "docs_rerun_hbm": info["spilled"], "docs_continued_hbm": info["continued"],
+                      "docs_hbm_waves": info["hbm_docs"], "lds_groups": info["lds_groups"],
+                      "hbm_wave_slots": info["hbm_waves"], "gen_s": gen_s, "summary_s": snap_host_s,
+                      "snapshot_bytes": snap_bytes, "summaries_gathered": gathered, "oracle_verified_docs": nv},
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args, argv))
+    run(args)
 
 
 if __name__ == "__main__":

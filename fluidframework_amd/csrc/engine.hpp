@@ -26,6 +26,7 @@ namespace mte {
 // The LDS of the replay kernel: one plan per CU (k_lds declares nothing else).
 extern __shared__ uint4 g_lds_dyn[];  // LdsPlan, dynamic (so waves_per_eu bounds VGPRs)
 #define g_plan (*reinterpret_cast<LdsPlan*>(g_lds_dyn))
+#define g_solo (*reinterpret_cast<SoloPlan*>(g_lds_dyn))  // k_solo's plan (the same dynamic LDS)
 
 // Phase profiling (compile with -DMTE_PROFILE): inclusive s_memtime cycles per phase.
 enum ProfSlot : u32 {
@@ -139,8 +140,9 @@ struct St {
     u32 adirty, gdirty;
 };
 
-template <bool LDSM>
+template <bool LDSM, bool SOLO = false>
 struct Engine {
+    static_assert(LDSM || !SOLO, "the solo plan is LDS-resident");
     const Params& p;
     u32 doc;
     // hot per-document limits (DocCfg, engine_types.hpp)
@@ -169,40 +171,45 @@ struct Engine {
     bool continued = false;  // HBM-resident after starting in LDS
     bool capped = false;     // HBM slot smaller than this document's worst case
 
-#define MTE_ARR(T, NAME, MEM, LDSX)            \
+#define MTE_ARR(T, NAME, MEM, LDSX, SOLOX)     \
     MTE_DEV T* NAME() const {                  \
-        if constexpr (LDSM) return (T*)(LDSX); \
+        if constexpr (SOLO) return (T*)(SOLOX); \
+        else if constexpr (LDSM) return (T*)(LDSX); \
         else return MEM;                       \
     }
-    MTE_ARR(uint4, VIS, m_vis, g_plan.vis)
-    MTE_ARR(uint4, AUX, m_aux, g_plan.aux)
-    MTE_ARR(u32, BMETA, m_bmeta, g_plan.bmeta)
-    MTE_ARR(uint4, ORD, m_ord, g_plan.wave[wave].ord)
-    MTE_ARR(u32, INCH, m_in_child, g_plan.wave[wave].in_child)
-    MTE_ARR(u32, INCNT, m_in_cnt, g_plan.wave[wave].in_cnt)
-    MTE_ARR(u32, INPAR, m_in_par, g_plan.wave[wave].in_par)
-    MTE_ARR(uint2, HEAP, m_heap, g_plan.wave[wave].heap)
-    MTE_ARR(u32, SCRATCH, m_scratch, g_plan.wave[wave].scratch)
-    MTE_ARR(u32, STATS, m_stats, g_plan.wave[wave].stats)
-    MTE_ARR(mte_op, RING, nullptr, g_plan.wave[wave].ring)
-    MTE_ARR(u16, HINT, nullptr, g_plan.wave[wave].hint)        // segment id (mod 256) -> block at push
-    MTE_ARR(u32, BITMAP, nullptr, g_plan.bitmap)               // pool allocation bitmap
-    MTE_ARR(unsigned char, OWNER, nullptr, g_plan.owner)       // pool block -> wave
-    MTE_ARR(u32, POOLAV, nullptr, &g_plan.pool_avail)          // pool blocks free of credit
+    MTE_ARR(uint4, VIS, m_vis, g_plan.vis, g_solo.vis)
+    MTE_ARR(uint4, AUX, m_aux, g_plan.aux, g_solo.aux)
+    MTE_ARR(u32, BMETA, m_bmeta, g_plan.bmeta, g_solo.bmeta)
+    MTE_ARR(uint4, ORD, m_ord, g_plan.wave[wave].ord, g_solo.w.ord)
+    MTE_ARR(u32, INCH, m_in_child, g_plan.wave[wave].in_child, g_solo.w.in_child)
+    MTE_ARR(u32, INCNT, m_in_cnt, g_plan.wave[wave].in_cnt, g_solo.w.in_cnt)
+    MTE_ARR(u32, INPAR, m_in_par, g_plan.wave[wave].in_par, g_solo.w.in_par)
+    MTE_ARR(uint2, HEAP, m_heap, g_plan.wave[wave].heap, g_solo.w.heap)
+    MTE_ARR(u32, SCRATCH, m_scratch, g_plan.wave[wave].scratch, g_solo.w.scratch)
+    MTE_ARR(u32, STATS, m_stats, g_plan.wave[wave].stats, g_solo.w.stats)
+    MTE_ARR(mte_op, RING, nullptr, g_plan.wave[wave].ring, g_solo.w.ring)
+    MTE_ARR(u16, HINT, nullptr, g_plan.wave[wave].hint, g_solo.w.hint)  // segment id -> block at push
+    MTE_ARR(u32, BITMAP, nullptr, g_plan.bitmap, nullptr)               // pool allocation bitmap
+    MTE_ARR(unsigned char, OWNER, nullptr, g_plan.owner, nullptr)       // pool block -> wave
+    MTE_ARR(u32, POOLAV, nullptr, &g_plan.pool_avail, nullptr)          // pool blocks free of credit
 #undef MTE_ARR
+    // the CU's leaf blocks are shared by its waves (k_lds) rather than owned by one (k_solo, HBM)
+    static constexpr bool SHARED = LDSM && !SOLO;
     // LRU heap hints (verified on use, so a stale or uninitialised entry only costs a full search)
     MTE_DEV u32 hint_get(u32 sid) const {
-        if constexpr (LDSM) return HINT()[sid & 255];
+        if constexpr (SOLO) return HINT()[sid & (SOLO_HINTS - 1)];
+        else if constexpr (LDSM) return HINT()[sid & 255];
         else return U(m_hint[sid & (HBM_HINTS - 1)]);
     }
     MTE_DEV void hint_set(u32 sid, u32 blk) const {  // per-lane store
-        if constexpr (LDSM) HINT()[sid & 255] = (u16)blk;
+        if constexpr (SOLO) HINT()[sid & (SOLO_HINTS - 1)] = (u16)blk;
+        else if constexpr (LDSM) HINT()[sid & 255] = (u16)blk;
         else m_hint[sid & (HBM_HINTS - 1)] = blk;
     }
-    MTE_DEV u32 blk_cap() const { if constexpr (LDSM) return POOL_BLOCKS; else return m_blk_cap; }
-    MTE_DEV u32 ord_cap() const { if constexpr (LDSM) return ORD_CAP; else return m_ord_cap; }
-    MTE_DEV u32 in_cap() const { if constexpr (LDSM) return IN_CAP; else return m_in_cap; }
-    MTE_DEV u32 heap_cap() const { if constexpr (LDSM) return HEAP_CAP; else return m_heap_cap; }
+    MTE_DEV u32 blk_cap() const { if constexpr (SOLO) return SOLO_POOL; else if constexpr (LDSM) return POOL_BLOCKS; else return m_blk_cap; }
+    MTE_DEV u32 ord_cap() const { if constexpr (SOLO) return SOLO_ORD; else if constexpr (LDSM) return ORD_CAP; else return m_ord_cap; }
+    MTE_DEV u32 in_cap() const { if constexpr (SOLO) return SOLO_IN; else if constexpr (LDSM) return IN_CAP; else return m_in_cap; }
+    MTE_DEV u32 heap_cap() const { if constexpr (SOLO) return SOLO_HEAP; else if constexpr (LDSM) return HEAP_CAP; else return m_heap_cap; }
     // doc-relative HBM bases
     u16* payload;
     u16* arena0;
@@ -289,6 +296,13 @@ struct Engine {
         u32 cb, co, ci, ch;
         hbm_caps(p.docs[doc].op_end - p.docs[doc].op_begin, cb, co, ci, ch);
         capped = cb > p.slot_blk || co > p.slot_ord || ci > p.slot_in || ch > p.slot_heap;
+    }
+    // the HBM slot of solo document i (sized for the longest solo document)
+    MTE_DEV void bind_solo_slot(u32 i) {
+        bind_region(p.solo_spill + (u64)i * p.solo_slot_bytes, p.solo_blk, p.solo_ord, p.solo_in, p.solo_heap);
+        u32 cb, co, ci, ch;
+        hbm_caps(p.docs[doc].op_end - p.docs[doc].op_begin, cb, co, ci, ch);
+        capped = cb > p.solo_blk || co > p.solo_ord || ci > p.solo_in || ch > p.solo_heap;
     }
 
     // Wave-uniform reads: a load from a uniform address is broadcast through readfirstlane so the
@@ -604,6 +618,7 @@ struct Engine {
         if (!LDSM) return true;
         if (st.n_lb + 16 > ord_cap() || st.inUsed + 12 > in_cap() || st.heapSize + st.n_lb + 8 > heap_cap())
             return false;
+        if (SOLO) return st.lbFree != NONE || st.lbBump + OP_CREDIT <= blk_cap();
         if (st.credit >= OP_CREDIT) return true;
         return take_credit(OP_CREDIT - st.credit, 2 * OP_CREDIT - st.credit);
     }
@@ -611,7 +626,7 @@ struct Engine {
     MTE_DEV u32 alloc_lb() {
         MTE_PROF(PF_ALLOC);
         u32 id = NONE;
-        if (LDSM) {
+        if (SHARED) {
             if (st.credit == 0) {
                 // mid-op and the CU's pool is dry: the other waves return blocks as their scours,
                 // packs and documents complete, so wait (bounded) rather than abandon the replay
@@ -667,7 +682,7 @@ struct Engine {
     }
     MTE_DEV void free_lb(u32 id) {
         if (id >= blk_cap()) return;
-        if (LDSM) {
+        if (SHARED) {
             if (L == 0) {
                 OWNER()[id] = 0xFF;
                 atomicAnd(&BITMAP()[id >> 5], ~(1u << (id & 31)));
@@ -954,7 +969,7 @@ struct Engine {
         uint2* H = HEAP();
         const u32 n = st.heapSize;
         uint2 x;
-        if constexpr (LDSM) {
+        if constexpr (SHARED) {
             static_assert(HEAP_CAP < 192, "heap register image holds 192 positions");
             uint2 h0 = make_uint2(0, 0), h1 = h0, h2 = h0;
             if (L <= n) h0 = H[L];
@@ -1954,7 +1969,10 @@ struct Engine {
     // LDS mode: give every leaf block this wave holds back to the CU's pool (also after an
     // abandoned replay, whose blocks need not all be linked).
     MTE_DEV void release() {
-        if (!LDSM) return;
+        if (!SHARED) {
+            st.n_lb = 0;
+            return;
+        }
         u32 n = 0;
         for (u32 base = 0; base < blk_cap(); base += 64) {
             const u32 b = base + L;
@@ -2080,7 +2098,7 @@ struct Engine {
             o.n_segs = nseg;
             o.text_off = toff;
             o.max_lb = maxlb;
-            o.mode = LDSM ? 0u : (continued ? 2u : 1u);
+            o.mode = SOLO ? 3u : (LDSM ? 0u : (continued ? 2u : 1u));
         }
     }
 
@@ -2165,7 +2183,7 @@ struct Engine {
     template <class E>
     MTE_DEV void adopt(const E& e) {
         st = e.st;
-        st.lbBump = POOL_BLOCKS;
+        st.lbBump = e.blk_cap();
         st.lbFree = NONE;
         st.credit = 0;
         const u32 g = L >> 3, s = L & 7;
@@ -2194,7 +2212,8 @@ struct Engine {
     // applied immediately, so the recorded log is exactly what a replay will see. The writers'
     // state lives in GenState so a document that leaves the LDS plan continues HBM-resident.
     MTE_DEV void gen_init(GenState& g) const {
-        const u64 sx = 0xF1D0C0DEull ^ (u64)doc ^ (p.gen_seed * 0x9E3779B97F4A7C15ull);
+        // seeded by the GLOBAL document id, so a document is the same whichever rank generates it
+        const u64 sx = 0xF1D0C0DEull ^ (u64)p.docs[doc].gid ^ (p.gen_seed * 0x9E3779B97F4A7C15ull);
         g.rng.seed(sx);
         for (u32 c = 0; c < MTE_MAX_CLIENTS; c++) {
             g.ref[c] = 0;

@@ -68,6 +68,35 @@ struct LdsPlan {
 static_assert(sizeof(LdsPlan) <= LDS_BYTES, "LDS plan exceeds 160 KiB");
 static_assert(POOL_BLOCKS <= 16 * 32, "bitmap too small");
 
+// LDS plan of the solo kernel (k_solo): ONE wave owns a whole CU's LDS and replays one
+// critical-path document (the Zipf heads of C4) with room for the block list, interior
+// nodes and LRU heap such a long document reaches, so it never has to continue HBM-resident.
+constexpr u32 SOLO_ORD = 512;
+constexpr u32 SOLO_IN = 192;
+constexpr u32 SOLO_HEAP = 1023;
+constexpr u32 SOLO_HINTS = 1024;
+struct SoloRegion {
+    uint4 ord[SOLO_ORD];
+    u32 in_child[SOLO_IN * 8];
+    u32 in_cnt[SOLO_IN];
+    u32 in_par[SOLO_IN];
+    uint2 heap[SOLO_HEAP + 1];
+    mte_op ring[RING_OPS];
+    u32 scratch[64];
+    u16 hint[SOLO_HINTS];
+    u32 stats[8];
+};
+constexpr u32 SOLO_POOL = ((LDS_BYTES - (u32)sizeof(SoloRegion) - 64) / (8 * 32 + 4)) & ~3u;
+struct SoloPlan {
+    SoloRegion w;
+    uint4 vis[SOLO_POOL * 8];
+    uint4 aux[SOLO_POOL * 8];
+    u32 bmeta[SOLO_POOL];
+};
+static_assert(sizeof(SoloPlan) <= LDS_BYTES, "solo LDS plan exceeds 160 KiB");
+// block ids below MAX_POOL are LDS ids of a document that continued HBM-resident
+constexpr u32 MAX_POOL = SOLO_POOL > POOL_BLOCKS ? SOLO_POOL : POOL_BLOCKS;
+
 // Host-computed per-document layout.
 struct DocCfg {
     u64 op_begin, op_end;
@@ -84,7 +113,7 @@ struct DocCfg {
     u32 collab;        // 1 = observer replay, 0 = local non-collaborative edits
     u32 has_nl;        // payload contains '\n' (TextSegment.canAppend reads last chars only then)
     u32 prio;          // critical-path document (far longer than the batch mean): high wave priority
-    u32 pad;
+    u32 gid;           // global document id (summary records; the generator's per-document seed)
 };
 
 // Per-document results written by the kernel.
@@ -106,7 +135,7 @@ struct DocRes {
     u32 out_off;     // first row of this doc's final segments in the output pool
     u32 n_segs;
     u32 max_lb;      // peak leaf-block count
-    u32 mode;        // 0 LDS-resident, 1 HBM-resident
+    u32 mode;        // 0 LDS-resident, 1 HBM-resident, 2 continued HBM-resident, 3 solo LDS-resident
     u32 spill_why;   // why the LDS pass gave the doc up (engine.hpp St::spillWhy)
     u32 text_off;    // first unit of this doc's gathered final text in the output text pool
 };
@@ -153,7 +182,10 @@ struct Params {
     u32 n_hslots;
     u32 lds_active;           // waves per k_lds workgroup that take documents (spread small batches)
     u32 n_prio;               // doc_list[0 .. n_prio): critical-path documents, taken by LDS waves only
-    u32 pad2;
+    u32 n_solo;               // doc_list[0 .. n_solo) <= n_prio: one k_solo workgroup each
+    unsigned char* solo_spill;  // per solo document: an HBM slot for continuing (solo_slot_bytes each)
+    u64 solo_slot_bytes;
+    u32 solo_blk, solo_ord, solo_in, solo_heap;  // capacities of a solo slot (hbm_caps of its longest doc)
     u32 pool_limit;           // test knob: LDS leaf blocks usable per CU (0 = all)
     u64* prof;                // MTE_PROFILE builds: per doc PROF_SLOTS cycle counters
     // synthetic workload generator
@@ -172,7 +204,7 @@ constexpr u32 PROF_SLOTS = 24;
 // transiently; segments <= 2 per op + 1 without zamboni). Block ids below POOL_BLOCKS are the
 // LDS ids of a document that continued in HBM, fresh ids start above them.
 MTE_HOSTDEV_ void hbm_caps(u64 n, u32& blk, u32& ord, u32& in, u32& heap) {
-    u64 b = n / 2 + 64 + POOL_BLOCKS;
+    u64 b = n / 2 + 64 + MAX_POOL;
     if (b > 0x3FFFFFF0ull) b = 0x3FFFFFF0ull;
     blk = (u32)b;
     ord = (u32)b;

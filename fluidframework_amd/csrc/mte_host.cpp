@@ -9,7 +9,9 @@
 //   * outputs: text (textSegment.ts:154-172), segment table (walkAllSegments, mergeTree.ts:2969),
 //     SnapshotV1 ITree (snapshotV1.ts:85-247), per-doc FNV-1a-64 summary.
 // There is no CPU execution path for replay: without a HIP device mte_create fails.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -18,6 +20,7 @@
 #include <deque>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -187,7 +190,8 @@ struct mte_engine {
     int device = 0;
     uint32_t chunk = 10000;
     hipStream_t stream = nullptr, stream2 = nullptr;  // stream2: the HBM-resident waves (k_hbmq)
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    hipStream_t stream3 = nullptr;                    // stream3: the solo workgroups (k_solo)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
     std::string err;
     HostBatch hb;
     bool generated = false;    // ops/payload live on the device; host copy filled on demand
@@ -216,7 +220,7 @@ struct mte_engine {
     DevBuf<DocCfg> d_cfg;
     DevBuf<DocRes> d_res;
     DevBuf<uint4> d_out_vis, d_out_aux;
-    DevBuf<unsigned char> d_hbm, d_spill;
+    DevBuf<unsigned char> d_hbm, d_spill, d_solo_spill;
     DevBuf<uint32_t> d_slot_bits;
     std::vector<uint64_t> n_ops_doc;
     // options (mte_set_option)
@@ -226,11 +230,18 @@ struct mte_engine {
     uint64_t slot_budget = 48ull << 30;  // HBM for per-wave slots
     uint64_t slot_ops_cap = 65536;       // slots are sized for documents of at most this many ops
     uint32_t slot_blk_limit = 0;         // test knob: leaf blocks per slot (0 = from slot_ops_cap)
+    // critical-path documents replayed by k_solo (a whole CU's LDS for one wave each)
+    uint32_t solo_max = 16;              // at most this many (0 = off)
+    uint64_t solo_min_ops = 20000;       // ... each at least this long
+    uint32_t solo_div = 6;               // ... and at least 1/solo_div of the longest document
+    uint64_t doc_id_base = 0;            // global id of a loaded batch's document 0 (summary records)
     // per-wave slot plan (layout_and_alloc)
     uint32_t n_slots = 0;
     // last run
     double last_lds_ms = 0, last_hbm_ms = 0;
     uint32_t last_spilled = 0, last_continued = 0, last_hbm_docs = 0, last_hbm_waves = 0, last_lds_groups = 0;
+    uint32_t last_solo = 0;
+    double last_solo_ms = 0;
     uint32_t n_groups = 256;
     // downloaded final state
     std::vector<uint32_t> h_maps;
@@ -310,7 +321,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
                             const std::vector<uint64_t>& n_prop_ins, const std::vector<uint64_t>& n_ann,
                             const std::vector<uint8_t>& collab, const std::vector<uint8_t>& has_nl,
                             uint64_t arena_limit = 0, const uint64_t* op_offsets = nullptr,
-                            const uint64_t* payload_offsets = nullptr) {
+                            const uint64_t* payload_offsets = nullptr, const uint32_t* doc_ids = nullptr) {
     const uint32_t nd = (uint32_t)n_ops.size();
     e->cfg.assign(nd, DocCfg{});
     e->n_ops_doc = n_ops;
@@ -342,6 +353,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
         c.collab = collab[d];
         c.has_nl = has_nl[d];
         c.prio = 0;
+        c.gid = doc_ids ? doc_ids[d] : (uint32_t)(e->doc_id_base + d);
         out += std::min<uint64_t>(3 * n + 8, 4096);
     }
     out += 1u << 20;
@@ -407,20 +419,22 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
 // alone when the LDS plan is off or the slots for its waves do not fit the budget. Every LDS wave
 // owns a slot for a document that outgrows the plan.
 static void wave_plan(const mte_engine* e, uint32_t nd, uint32_t& groups, uint32_t& hbm_waves,
-                      uint32_t* lds_active = nullptr) {
+                      uint32_t* lds_active = nullptr, uint32_t n_solo = 0) {
+    const uint32_t cus = e->n_groups > n_solo ? e->n_groups - n_solo : 1u;  // k_solo holds n_solo CUs
+    nd -= std::min(nd, n_solo);
     const uint64_t max_slots = std::max<uint64_t>(1, e->slot_budget / std::max<uint64_t>(e->P.slot_bytes, 1));
     // fewer documents than LDS waves: every CU still gets a workgroup, with fewer active waves
     // (each with its own SIMD and a larger share of the CU's block pool)
-    groups = std::min<uint32_t>(e->n_groups, nd);
+    groups = std::min<uint32_t>(cus, nd);
     if (e->force_hbm || (uint64_t)groups * LDS_WAVES > max_slots) groups = 0;
     if (lds_active) *lds_active = groups ? std::min<uint32_t>(LDS_WAVES, (nd + groups - 1) / groups) : 0;
     // 16 = 4 SIMDs x 4 waves at <= 128 VGPRs (k_hbmq's bound): more can never be resident at once
     const uint32_t per_cu = groups ? std::min<uint32_t>(e->hbm_waves_per_cu, 16) : 16;
-    uint64_t h = (uint64_t)per_cu * e->n_groups;
+    uint64_t h = (uint64_t)per_cu * cus;
     h = std::min<uint64_t>(h, max_slots - (uint64_t)groups * LDS_WAVES);
     if (nd > (uint64_t)groups * LDS_WAVES) h = std::min<uint64_t>(h, nd - (uint64_t)groups * LDS_WAVES);
     else h = 0;
-    if (groups == 0 && h == 0) h = 1;
+    if (groups == 0 && h == 0 && nd) h = 1;
     hbm_waves = (uint32_t)h;
 }
 
@@ -434,9 +448,31 @@ static int alloc_out_text(mte_engine* e) {
     return MTE_OK;
 }
 
+// Critical-path documents for k_solo: the leading documents of the LPT order that are far longer
+// than the batch mean (or the only document) and within 1/solo_div of the longest one.
+static uint32_t solo_count(const mte_engine* e) {
+    const uint32_t nd = (uint32_t)e->order.size();
+    if (!nd || !e->solo_max || e->force_hbm) return 0;
+    uint64_t total = 0, nmax = 0;
+    for (uint64_t n : e->n_ops_doc) {
+        total += n;
+        nmax = std::max(nmax, n);
+    }
+    const double mean = (double)total / nd;
+    const uint32_t cap = std::min<uint32_t>(e->solo_max, std::max<uint32_t>(1, e->n_groups / 8));
+    uint32_t k = 0;
+    while (k < nd && k < cap) {
+        const uint64_t n = e->n_ops_doc[e->order[k]];
+        if (n < e->solo_min_ops || n * e->solo_div < nmax || (nd > 1 && (double)n < 8.0 * mean)) break;
+        k++;
+    }
+    return k;
+}
+
 static int alloc_slots(mte_engine* e) {
     uint32_t g, h;
-    wave_plan(e, e->P.n_docs, g, h);
+    const uint32_t ns = solo_count(e);
+    wave_plan(e, e->P.n_docs, g, h, nullptr, ns);
     const uint32_t n = g * LDS_WAVES + h;
     const size_t bytes = (size_t)n * e->P.slot_bytes;
     if (bytes > e->d_spill.n || !e->d_spill.p) HIP_TRY(e, e->d_spill.alloc(bytes));
@@ -445,6 +481,18 @@ static int alloc_slots(mte_engine* e) {
     e->n_slots = n;
     e->P.spill = e->d_spill.p;
     e->P.slot_bits = e->d_slot_bits.p;
+    // solo documents continue in slots of their own, sized for the longest of them
+    e->P.n_solo = ns;
+    if (ns) {
+        uint64_t nmax = 0;
+        for (uint32_t k = 0; k < ns; k++) nmax = std::max(nmax, e->n_ops_doc[e->order[k]]);
+        hbm_caps(nmax, e->P.solo_blk, e->P.solo_ord, e->P.solo_in, e->P.solo_heap);
+        e->P.solo_slot_bytes =
+            (HbmLayout::of(e->P.solo_blk, e->P.solo_ord, e->P.solo_in, e->P.solo_heap).bytes + 255) & ~255ull;
+        const size_t sb = (size_t)ns * e->P.solo_slot_bytes;
+        if (sb > e->d_solo_spill.n || !e->d_solo_spill.p) HIP_TRY(e, e->d_solo_spill.alloc(sb));
+        e->P.solo_spill = e->d_solo_spill.p;
+    }
     return MTE_OK;
 }
 
@@ -497,6 +545,8 @@ int mte_create(const mte_config* cfg, mte_engine** out) {
     HIP_TRY(e.get(), hipSetDevice(e->device));
     HIP_TRY(e.get(), hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     HIP_TRY(e.get(), hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+    HIP_TRY(e.get(), hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking));
+    HIP_TRY(e.get(), hipEventCreateWithFlags(&e->ev3, hipEventDisableTiming));
     HIP_TRY(e.get(), hipEventCreateWithFlags(&e->ev2, hipEventDisableTiming));
     HIP_TRY(e.get(), hipEventCreate(&e->ev0));
     HIP_TRY(e.get(), hipEventCreate(&e->ev1));
@@ -511,6 +561,8 @@ void mte_destroy(mte_engine* e) {
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->ev2) (void)hipEventDestroy(e->ev2);
+    if (e->ev3) (void)hipEventDestroy(e->ev3);
+    if (e->stream3) (void)hipStreamDestroy(e->stream3);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -582,12 +634,14 @@ static int run_kernel(mte_engine* e, bool gen) {
     int rc;
     if ((rc = alloc_slots(e))) return rc;  // options may have changed the wave plan
     uint32_t groups, hbm_waves, lds_active;
-    wave_plan(e, nd, groups, hbm_waves, &lds_active);
+    const uint32_t n_solo = e->P.n_solo;
+    wave_plan(e, nd, groups, hbm_waves, &lds_active, n_solo);
     e->P.slot_hbm0 = groups * LDS_WAVES;
     e->P.lds_active = lds_active;
     e->P.n_prio = 0;
     if (groups)  // critical-path documents lead the LPT order
         while (e->P.n_prio < nd && e->cfg[e->order[e->P.n_prio]].prio) e->P.n_prio++;
+    e->P.n_prio = std::max(e->P.n_prio, n_solo);  // k_lds / k_hbmq start after the solo documents
     e->P.n_hslots = hbm_waves;
     HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 8 * sizeof(uint32_t), e->stream));
     HIP_TRY(e, hipMemsetAsync(e->d_slot_bits.p, 0, e->d_slot_bits.n * sizeof(uint32_t), e->stream));
@@ -595,8 +649,14 @@ static int run_kernel(mte_engine* e, bool gen) {
     HIP_TRY(e, hipEventRecord(e->ev0, e->stream));
     std::vector<uint32_t> spill;
     float lds_ms = 0, hbm_ms = 0;
-    // pass 1: LDS workgroups first (one per CU, all of its LDS), then the HBM-resident waves on the
-    // second stream so they fill every CU's remaining wave slots; both drain one document queue
+    // pass 1: the solo workgroups first (third stream: each takes a CU), then the LDS workgroups
+    // (one per remaining CU, all of its LDS), then the HBM-resident waves on the second stream so
+    // they fill every CU's remaining wave slots; k_lds and k_hbmq drain one document queue
+    if (n_solo) {
+        HIP_TRY(e, hipStreamWaitEvent(e->stream3, e->ev0, 0));
+        HIP_TRY(e, launch_solo(e->P, gen, n_solo, e->stream3));
+        HIP_TRY(e, hipEventRecord(e->ev3, e->stream3));
+    }
     if (groups) HIP_TRY(e, launch_lds(e->P, gen, groups, e->stream));
     // k_hbmq: one workgroup (wave) per document; those that find the queue drained exit at once
     if (hbm_waves && !groups) {
@@ -607,6 +667,7 @@ static int run_kernel(mte_engine* e, bool gen) {
         HIP_TRY(e, hipEventRecord(e->ev2, e->stream2));
         HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev2, 0));
     }
+    if (n_solo) HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev3, 0));
     HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     HIP_TRY(e, hipEventElapsedTime(&lds_ms, e->ev0, e->ev1));
@@ -621,6 +682,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     for (uint32_t i = 0; i < nd; i++) e->last_hbm_docs += e->res[i].mode == 1;
     e->last_hbm_waves = hbm_waves;
     e->last_lds_groups = groups;
+    e->last_solo = n_solo;
     e->last_spilled = (uint32_t)spill.size();
     if (!spill.empty()) {
         // second pass: the spilled documents, HBM-resident, one wave each, longest first
@@ -702,6 +764,11 @@ static uint32_t build_generator_props(mte_engine* e) {
 
 int mte_generate(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, const uint32_t* ops_per_doc,
                  uint32_t n_clients, uint64_t seed_base) {
+    return mte_generate_ids(e, kind, n_docs, n_ops, ops_per_doc, nullptr, n_clients, seed_base);
+}
+
+int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, const uint32_t* ops_per_doc,
+                     const uint32_t* doc_ids, uint32_t n_clients, uint64_t seed_base) {
     if (!e || n_docs == 0 || n_clients == 0 || n_clients >= MTE_MAX_CLIENTS) return MTE_E_ARG;
     if (kind != 2 && kind != 3 && kind != 5) return set_err(e, MTE_E_ARG, "generator kind must be 2, 3 or 5");
     HIP_TRY(e, hipSetDevice(e->device));
@@ -723,7 +790,7 @@ int mte_generate(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, 
     }
     int rc;
     // generated docs hover around a 2048-char target length: 64K-unit semispaces are ample
-    if ((rc = layout_and_alloc(e, nops, pay, pi, an, collab, has_nl, 65536))) return rc;
+    if ((rc = layout_and_alloc(e, nops, pay, pi, an, collab, has_nl, 65536, nullptr, nullptr, doc_ids))) return rc;
     HIP_TRY(e, e->d_ops.alloc(e->hb.doc_op_offsets.back()));
     HIP_TRY(e, e->d_payload.alloc(e->hb.doc_payload_offsets.back()));
     HIP_TRY(e, hipMemsetAsync(e->d_payload.p, 0, e->d_payload.n * sizeof(uint16_t), e->stream));
@@ -1224,13 +1291,141 @@ int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap) {
             s.segments = (uint32_t)v.segs.size();
             s.snapshot_bytes = sb;
             s.status = e->res[d].status;
-            s.doc_id = d;
+            s.doc_id = e->cfg[d].gid;
         }
     };
     unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> ts;
     for (unsigned i = 0; i < nt; i++) ts.emplace_back(work);
     for (auto& t : ts) t.join();
+    return MTE_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// The one collective of the path: an all-gather of the per-document summary records over
+// RCCL (xGMI on one node). librccl is opened on first use, so hosts that never gather (one GPU, the
+// CPU tests) do not need it.
+}  // extern "C"
+namespace {
+struct Rccl {
+    void* h = nullptr;
+    decltype(&ncclGetUniqueId) getUniqueId = nullptr;
+    decltype(&ncclCommInitRank) commInitRank = nullptr;
+    decltype(&ncclCommDestroy) commDestroy = nullptr;
+    decltype(&ncclAllGather) allGather = nullptr;
+    decltype(&ncclGetErrorString) errStr = nullptr;
+    bool ok() {
+        if (h) return true;
+        for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            h = dlopen(n, RTLD_NOW | RTLD_LOCAL);
+            if (h) break;
+        }
+        if (!h) return false;
+        getUniqueId = (decltype(getUniqueId))dlsym(h, "ncclGetUniqueId");
+        commInitRank = (decltype(commInitRank))dlsym(h, "ncclCommInitRank");
+        commDestroy = (decltype(commDestroy))dlsym(h, "ncclCommDestroy");
+        allGather = (decltype(allGather))dlsym(h, "ncclAllGather");
+        errStr = (decltype(errStr))dlsym(h, "ncclGetErrorString");
+        if (!getUniqueId || !commInitRank || !commDestroy || !allGather || !errStr) {
+            dlclose(h);
+            h = nullptr;
+        }
+        return h != nullptr;
+    }
+};
+Rccl& rccl() {
+    static Rccl r;
+    return r;
+}
+std::mutex& rccl_mu() {
+    static std::mutex m;
+    return m;
+}
+}  // namespace
+static_assert(sizeof(ncclUniqueId) == MTE_RCCL_ID_BYTES, "ncclUniqueId size");
+extern "C" {
+
+int mte_rccl_unique_id(uint8_t* id) {
+    if (!id) return MTE_E_ARG;
+    std::lock_guard<std::mutex> g(rccl_mu());
+    if (!rccl().ok()) return MTE_E_UNSUPPORTED;
+    ncclUniqueId u;
+    if (rccl().getUniqueId(&u) != ncclSuccess) return MTE_E_HIP;
+    memcpy(id, &u, sizeof u);
+    return MTE_OK;
+}
+
+int mte_rccl_comm_create(mte_engine* e, const uint8_t* id, int rank, int world, void** comm) {
+    if (!e || !id || !comm || world < 1 || rank < 0 || rank >= world) return MTE_E_ARG;
+    *comm = nullptr;
+    {
+        std::lock_guard<std::mutex> g(rccl_mu());
+        if (!rccl().ok()) return set_err(e, MTE_E_UNSUPPORTED, "librccl not available");
+    }
+    HIP_TRY(e, hipSetDevice(e->device));
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    ncclComm_t c = nullptr;
+    ncclResult_t r = rccl().commInitRank(&c, world, u, rank);
+    if (r != ncclSuccess) return set_err(e, MTE_E_HIP, std::string("ncclCommInitRank: ") + rccl().errStr(r));
+    *comm = (void*)c;
+    return MTE_OK;
+}
+
+void mte_rccl_comm_destroy(void* comm) {
+    if (comm && rccl().ok()) rccl().commDestroy((ncclComm_t)comm);
+}
+
+int mte_gather_summaries(mte_engine* e, int rank, int world, void* comm, mte_doc_summary* out, size_t cap,
+                         size_t* n) {
+    if (!e || world < 1 || rank < 0 || rank >= world || (world > 1 && !comm)) return MTE_E_ARG;
+    const size_t nd = e->P.n_docs;
+    std::vector<mte_doc_summary> mine(nd);
+    int rc = nd ? mte_summaries(e, mine.data(), nd) : MTE_OK;
+    if (rc) return rc;
+    if (world == 1) {
+        if (n) *n = nd;
+        if (!out) return MTE_OK;
+        if (cap < nd) return MTE_E_RANGE;
+        std::copy(mine.begin(), mine.end(), out);
+        return MTE_OK;
+    }
+    HIP_TRY(e, hipSetDevice(e->device));
+    ncclComm_t c = (ncclComm_t)comm;
+    // 1) every rank's record count, 2) the records padded to the largest count
+    DevBuf<uint64_t> cnt, all_cnt;
+    HIP_TRY(e, cnt.alloc(1));
+    HIP_TRY(e, all_cnt.alloc((size_t)world));
+    const uint64_t mine_n = nd;
+    HIP_TRY(e, hipMemcpyAsync(cnt.p, &mine_n, 8, hipMemcpyHostToDevice, e->stream));
+    ncclResult_t r = rccl().allGather(cnt.p, all_cnt.p, 1, ncclUint64, c, e->stream);
+    if (r != ncclSuccess) return set_err(e, MTE_E_HIP, std::string("ncclAllGather: ") + rccl().errStr(r));
+    std::vector<uint64_t> counts((size_t)world);
+    HIP_TRY(e, hipMemcpyAsync(counts.data(), all_cnt.p, 8 * (size_t)world, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    uint64_t mx = 0, total = 0;
+    for (uint64_t x : counts) {
+        mx = std::max(mx, x);
+        total += x;
+    }
+    if (n) *n = total;
+    if (!out) return MTE_OK;
+    if (cap < total) return MTE_E_RANGE;
+    const size_t words = sizeof(mte_doc_summary) / 8;  // 32-B records as 4 u64 words
+    DevBuf<uint64_t> send, recv;
+    HIP_TRY(e, send.alloc(std::max<uint64_t>(mx, 1) * words));
+    HIP_TRY(e, recv.alloc(std::max<uint64_t>(mx, 1) * words * (size_t)world));
+    HIP_TRY(e, hipMemsetAsync(send.p, 0, std::max<uint64_t>(mx, 1) * words * 8, e->stream));
+    if (nd) HIP_TRY(e, hipMemcpyAsync(send.p, mine.data(), nd * sizeof(mte_doc_summary), hipMemcpyHostToDevice, e->stream));
+    r = rccl().allGather(send.p, recv.p, std::max<uint64_t>(mx, 1) * words, ncclUint64, c, e->stream);
+    if (r != ncclSuccess) return set_err(e, MTE_E_HIP, std::string("ncclAllGather: ") + rccl().errStr(r));
+    std::vector<mte_doc_summary> flat(std::max<uint64_t>(mx, 1) * (size_t)world);
+    HIP_TRY(e, hipMemcpyAsync(flat.data(), recv.p, flat.size() * sizeof(mte_doc_summary), hipMemcpyDeviceToHost,
+                              e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    size_t k = 0;
+    for (int q = 0; q < world; q++)
+        for (uint64_t i = 0; i < counts[(size_t)q]; i++) out[k++] = flat[(size_t)q * std::max<uint64_t>(mx, 1) + i];
     return MTE_OK;
 }
 
@@ -1275,6 +1470,9 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "slot_budget_mb") e->slot_budget = (uint64_t)std::max<int64_t>(1, value) << 20;
     else if (k == "slot_ops_cap") e->slot_ops_cap = (uint64_t)std::max<int64_t>(64, value);  // next load
     else if (k == "slot_blk_limit") e->slot_blk_limit = (uint32_t)std::max<int64_t>(0, value);  // next load
+    else if (k == "doc_id_base") e->doc_id_base = (uint64_t)std::max<int64_t>(0, value);  // next load
+    else if (k == "solo_max") e->solo_max = (uint32_t)std::max<int64_t>(0, value);
+    else if (k == "solo_min_ops") e->solo_min_ops = (uint64_t)std::max<int64_t>(1, value);
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
 }
@@ -1290,6 +1488,7 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "spilled") *value = e->last_spilled;
     else if (k == "slot_bytes") *value = (int64_t)e->P.slot_bytes;
     else if (k == "slots") *value = e->n_slots;
+    else if (k == "solo") *value = e->last_solo;
     else return set_err(e, MTE_E_ARG, "unknown info key " + k);
     return MTE_OK;
 }
@@ -1853,7 +2052,8 @@ int mte_builder_add_container_log(mte_builder* b, const char* observer_name, con
     std::deque<json::Value> store;                                   // attach snapshots / parsed strings
     std::vector<std::pair<std::string, const json::Value*>> trees;   // mergeTreeAttachTrees (insertion order)
     std::unordered_map<std::string, std::vector<json::Value>> msgs;  // merge-tree messages by full path
-    std::unordered_map<std::string, std::vector<std::u16string>> chunks;
+    // ChunkedOp parts per client (clientReplayTool.ts:118-141: any order, each index once)
+    std::unordered_map<std::string, std::pair<std::vector<std::u16string>, std::vector<bool>>> chunks;
     std::vector<uint8_t> have;
     auto parse_str = [&](const std::u16string& s) -> const json::Value* {
         const std::string t = u8(s);
@@ -1876,26 +2076,35 @@ int mte_builder_add_container_log(mte_builder* b, const char* observer_name, con
                 num_field(*ch, u"totalChunks", &total);
                 const json::Value* part = ch->get(u"contents");
                 if (total <= 0 || id < 1 || id > total) throw std::runtime_error("chunk id out of range");
-                auto& vec = chunks[client];
-                if (vec.empty()) vec.assign((size_t)total, std::u16string(1, (char16_t)0xFFFF));
-                auto& slot = vec[(size_t)(id - 1)];
-                if (!(slot.size() == 1 && slot[0] == 0xFFFF)) throw std::runtime_error("Chunk already assigned");
-                slot = part && part->kind == json::Value::String ? part->str : std::u16string();
+                auto& pending = chunks[client];  // (texts, assigned) by chunk index
+                if (pending.first.empty()) {
+                    pending.first.assign((size_t)total, std::u16string());
+                    pending.second.assign((size_t)total, false);
+                }
+                if ((size_t)id > pending.first.size()) throw std::runtime_error("chunk id out of range");
+                if (pending.second[(size_t)(id - 1)]) throw std::runtime_error("Chunk already assigned");
+                pending.second[(size_t)(id - 1)] = true;
+                pending.first[(size_t)(id - 1)] = part && part->kind == json::Value::String ? part->str : std::u16string();
                 if (id != total) continue;
                 std::u16string joined;
-                for (auto& x : vec) {
-                    if (x.size() == 1 && x[0] == 0xFFFF) throw std::runtime_error("Chunk not assigned");
-                    joined += x;
+                for (size_t q = 0; q < pending.first.size(); q++) {
+                    if (!pending.second[q]) throw std::runtime_error("Chunk not assigned");
+                    joined += pending.first[q];
                 }
                 chunks.erase(client);
-                const json::Value* orig = ch->get(u"originalType");
+                // `ch` may point into m's own "contents" member (object-form chunks): copy what is
+                // needed from it before m's members are rewritten
+                const json::Value* origp = ch->get(u"originalType");
+                const bool hasOrig = origp != nullptr;
+                const json::Value orig = hasOrig ? *origp : json::Value();
                 for (auto& mem : m.members) {
                     if (mem.first == u"contents") {
-                        mem.second = json::Value();
-                        mem.second.kind = json::Value::String;
-                        mem.second.str = joined;
-                    } else if (mem.first == u"type" && orig) {
-                        mem.second = *orig;
+                        json::Value joinedv;
+                        joinedv.kind = json::Value::String;
+                        joinedv.str = joined;
+                        mem.second = std::move(joinedv);
+                    } else if (mem.first == u"type" && hasOrig) {
+                        mem.second = orig;
                     }
                 }
                 ty = m.get(u"type");
@@ -1950,8 +2159,12 @@ int mte_builder_add_container_log(mte_builder* b, const char* observer_name, con
         return MTE_E_PARSE;
     }
     uint32_t added = 0;
+    // every channel's document is built before any is committed: a failing channel leaves the
+    // builder as it was (interned property sets aside, which no document references)
+    std::vector<std::unique_ptr<DocBuild>> built;
     for (auto& [path, tree] : trees) {
-        DocBuild db(observer_name);
+        built.emplace_back(new DocBuild(observer_name));
+        DocBuild& db = *built.back();
         json::Value arr;
         arr.kind = json::Value::Array;
         auto it = msgs.find(path);
@@ -1962,8 +2175,10 @@ int mte_builder_add_container_log(mte_builder* b, const char* observer_name, con
             b->err = path + ": " + db.err;
             return rc;
         }
-        db.commit(b->hb);
-        b->paths.push_back(path);
+    }
+    for (size_t i = 0; i < built.size(); i++) {
+        built[i]->commit(b->hb);
+        b->paths.push_back(trees[i].first);
         added++;
     }
     if (n_docs) *n_docs = added;

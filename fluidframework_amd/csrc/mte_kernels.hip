@@ -36,8 +36,8 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
     // documents (doc_list[0, n_prio), counters[5]) are taken by LDS waves only
     for (; w < p.lds_active;) {
         u32 i = 0;
-        if (L == 0) {
-            i = p.n_prio ? atomicAdd(&p.counters[5], 1u) : p.n_prio;
+        if (L == 0) {  // doc_list[0, n_solo) belongs to k_solo
+            i = p.n_prio > p.n_solo ? p.n_solo + atomicAdd(&p.counters[5], 1u) : p.n_prio;
             if (i >= p.n_prio) i = p.n_prio + atomicAdd(&p.counters[0], 1u);
         }
         i = wave_read(i, 0);
@@ -82,6 +82,49 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
         e.release();
         if (prio) __builtin_amdgcn_s_setprio(0);
     }
+}
+
+// Critical-path documents (doc_list[0, n_solo), the longest of the batch): one single-wave
+// workgroup each, owning all of a CU's LDS (SoloPlan), at the highest wave priority. The replay
+// latency of the longest document bounds a Zipf batch, so it gets the plan with the
+// most room and no LDS-pool sharing; it continues HBM-resident only if it outgrows even that.
+template <bool GEN>
+__global__ __launch_bounds__(64) void k_solo(Params p) {
+    const u32 i = blockIdx.x;
+    if (i >= p.n_solo) return;
+    const u32 d = p.doc_list[i];
+    __builtin_amdgcn_s_setprio(3);
+    Engine<true, true> e(p, d);
+    e.bind_lds(0);
+    GenState g;
+    bool done;
+    u64 at = 0;
+    e.init();
+    if (GEN) {
+        e.gen_init(g);
+        done = e.generate_run(g);
+    } else {
+        at = e.replay_run(p.docs[d].op_begin);
+        done = at >= p.docs[d].op_end;
+    }
+    if (e.st.status == DOC_SPILL) {
+        e.mark_spilled();
+    } else if (!done && e.st.status == 0) {
+        Engine<false> h(p, d);
+        h.continued = true;
+        h.bind_solo_slot(i);
+        h.adopt(e);
+        if (lane_id() == 0) atomicAdd(&p.counters[4], 1u);
+        if (GEN) {
+            h.generate_run(g);
+        } else {
+            h.replay_run(at);
+        }
+        h.finish();
+    } else {
+        e.finish();
+    }
+    __builtin_amdgcn_s_setprio(0);
 }
 
 // HBM slot of a k_hbmq wave: a free bit of the slot bitmap (cleared by the host before each run).
@@ -198,6 +241,19 @@ hipError_t launch_lds(const Params& p, bool gen, u32 n_groups, hipStream_t s) {
     if (attr != hipSuccess) return attr;
     if (gen) hipLaunchKernelGGL(k_lds<true>, dim3(n_groups), dim3(64 * LDS_WAVES), sizeof(LdsPlan), s, p);
     else hipLaunchKernelGGL(k_lds<false>, dim3(n_groups), dim3(64 * LDS_WAVES), sizeof(LdsPlan), s, p);
+    return hipGetLastError();
+}
+hipError_t launch_solo(const Params& p, bool gen, u32 n_solo, hipStream_t s) {
+    static const hipError_t attr = [] {
+        hipError_t a = hipFuncSetAttribute((const void*)k_solo<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)sizeof(SoloPlan));
+        hipError_t b = hipFuncSetAttribute((const void*)k_solo<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)sizeof(SoloPlan));
+        return a != hipSuccess ? a : b;
+    }();
+    if (attr != hipSuccess) return attr;
+    if (gen) hipLaunchKernelGGL(k_solo<true>, dim3(n_solo), dim3(64), sizeof(SoloPlan), s, p);
+    else hipLaunchKernelGGL(k_solo<false>, dim3(n_solo), dim3(64), sizeof(SoloPlan), s, p);
     return hipGetLastError();
 }
 hipError_t launch_hbm(const Params& p, bool gen, u32 n_docs, hipStream_t s) {

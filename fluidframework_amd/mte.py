@@ -33,6 +33,22 @@ class MteError(RuntimeError):
     pass
 
 
+RCCL_ID_BYTES = 128  # MTE_RCCL_ID_BYTES
+
+
+def rccl_unique_id():
+    buf = (ctypes.c_uint8 * RCCL_ID_BYTES)()
+    rc = lib().mte_rccl_unique_id(buf)
+    if rc:
+        raise MteError(f"mte_rccl_unique_id failed ({rc})")
+    return bytes(buf)
+
+
+def rccl_comm_destroy(comm):
+    if comm:
+        lib().mte_rccl_comm_destroy(comm)
+
+
 class mte_batch(ctypes.Structure):
     _fields_ = [
         ("n_docs", ctypes.c_uint32),
@@ -76,8 +92,9 @@ SUMMARY_DTYPE = np.dtype([("checksum", "<u8"), ("ops", "<u4"), ("length", "<u4")
 
 # Every symbol declared in include/mte.h (checked by tests/test_abi.py).
 EXPORTS = ["mte_abi_version", "mte_build_info", "mte_create", "mte_destroy", "mte_last_error", "mte_load",
-           "mte_replay", "mte_generate", "mte_export_batch", "mte_doc_status", "mte_text", "mte_segments",
-           "mte_snapshot_v1", "mte_snapshot_shared_string", "mte_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
+           "mte_replay", "mte_generate", "mte_generate_ids", "mte_export_batch", "mte_doc_status", "mte_text", "mte_segments",
+           "mte_snapshot_v1", "mte_snapshot_shared_string", "mte_summaries", "mte_rccl_unique_id",
+           "mte_rccl_comm_create", "mte_rccl_comm_destroy", "mte_gather_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
            "mte_builder_batch",
            "mte_builder_error", "mte_builder_destroy"]
 
@@ -101,6 +118,7 @@ def lib():
         L.mte_load.argtypes = [vp, ctypes.POINTER(mte_batch)]
         L.mte_replay.argtypes = [vp, ctypes.POINTER(mte_stats)]
         L.mte_generate.argtypes = [vp, u32, u32, u32, ctypes.POINTER(u32), u32, u64]
+        L.mte_generate_ids.argtypes = [vp, u32, u32, u32, ctypes.POINTER(u32), ctypes.POINTER(u32), u32, u64]
         L.mte_export_batch.argtypes = [vp, ctypes.POINTER(mte_batch)]
         L.mte_doc_status.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]
         L.mte_text.argtypes = [vp, u32, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
@@ -108,6 +126,11 @@ def lib():
         L.mte_snapshot_v1.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz), ctypes.POINTER(u32)]
         L.mte_snapshot_shared_string.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.mte_summaries.argtypes = [vp, ctypes.c_void_p, sz]
+        L.mte_rccl_unique_id.argtypes = [ctypes.c_void_p]
+        L.mte_rccl_comm_create.argtypes = [vp, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        L.mte_rccl_comm_destroy.argtypes = [vp]
+        L.mte_rccl_comm_destroy.restype = None
+        L.mte_gather_summaries.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
         L.mte_doc_result.argtypes = [vp, u32, ctypes.c_void_p, sz]
         L.mte_run_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.POINTER(u32)]
@@ -230,11 +253,15 @@ class Engine:
         self._check(lib().mte_load(self._h, ctypes.byref(batch)), "mte_load")
         self.n_docs = batch.n_docs
 
-    def generate(self, kind, n_docs, n_ops, n_clients=8, seed=0, ops_per_doc=None):
-        arr = None
+    def generate(self, kind, n_docs, n_ops, n_clients=8, seed=0, ops_per_doc=None, doc_ids=None):
+        """Synthetic logs on the device. doc_ids: GLOBAL ids (default 0..n_docs-1); a
+        document's log depends only on its id, op count, kind, n_clients and seed."""
+        arr = ids = None
         if ops_per_doc is not None:
             arr = (ctypes.c_uint32 * n_docs)(*[int(x) for x in ops_per_doc])
-        self._check(lib().mte_generate(self._h, kind, n_docs, n_ops, arr, n_clients, seed), "mte_generate")
+        if doc_ids is not None:
+            ids = (ctypes.c_uint32 * n_docs)(*[int(x) for x in doc_ids])
+        self._check(lib().mte_generate_ids(self._h, kind, n_docs, n_ops, arr, ids, n_clients, seed), "mte_generate")
         self.n_docs = n_docs
 
     def replay(self):
@@ -284,6 +311,23 @@ class Engine:
         self._check(lib().mte_summaries(self._h, out.ctypes.data, self.n_docs), "mte_summaries")
         return out
 
+    def gather_summaries(self, rank=0, world=1, comm=None):
+        """Every rank's summary records over RCCL (mte_gather_summaries), rank order. Collective."""
+        n = ctypes.c_size_t()
+        self._check(lib().mte_gather_summaries(self._h, rank, world, comm, None, 0, ctypes.byref(n)),
+                    "mte_gather_summaries")
+        out = np.zeros(n.value, dtype=SUMMARY_DTYPE)
+        self._check(lib().mte_gather_summaries(self._h, rank, world, comm, out.ctypes.data, n.value, ctypes.byref(n)),
+                    "mte_gather_summaries")
+        return out
+
+    def rccl_comm(self, unique_id, rank, world):
+        """RCCL communicator on this engine's device from a MTE_RCCL_ID_BYTES id (rank 0's)."""
+        c = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * RCCL_ID_BYTES).from_buffer_copy(bytes(unique_id))
+        self._check(lib().mte_rccl_comm_create(self._h, buf, rank, world, ctypes.byref(c)), "mte_rccl_comm_create")
+        return c
+
     DOC_RESULT_FIELDS = ["status", "failing_seq", "ops", "msgs", "min_seq", "cur_seq", "height", "n_lb",
                          "arena_sel", "arena_top", "map_next", "seg_next", "heap_size", "n_gc", "out_off", "n_segs",
                          "max_lb", "mode", "spill_why", "text_off"]
@@ -300,7 +344,7 @@ class Engine:
                                        ctypes.byref(rows), ctypes.byref(co)), "mte_run_info")
         out = {"spilled": sp.value, "continued": co.value, "lds_ms": a.value, "hbm_ms": b.value,
                "out_rows": rows.value}
-        for k in ("lds_groups", "hbm_waves", "hbm_docs", "slot_bytes", "slots"):
+        for k in ("lds_groups", "hbm_waves", "hbm_docs", "slot_bytes", "slots", "solo"):
             out[k] = self.get_info(k)
         return out
 

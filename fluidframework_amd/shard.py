@@ -30,6 +30,39 @@ def zipf_op_counts(n_docs, seed=0, lo=1000, hi=1_000_000):
     return np.clip(hi // ranks, lo, hi).astype(np.int64)
 
 
+def plan_shard(config, world, rank, docs, ops, zipf_lo=1000, zipf_hi=1_000_000):
+    """The documents rank `rank` of `world` replays, as GLOBAL ids with their op counts (bench.py).
+    C4: Zipf op counts over `docs` documents, LPT-assigned, longest first (strong scaling: the same
+    262,144 documents at every world size). C5: `docs` equal documents, strided over the ranks.
+    C2/C3 (weak scaling): `docs` documents per rank, ids rank*docs .. rank*docs+docs-1."""
+    if config == "C4":
+        counts = zipf_op_counts(docs, seed=0, lo=zipf_lo, hi=zipf_hi)
+        mine = lpt_assign(counts, world)[rank]
+        return mine.astype(np.int64), counts[mine].astype(np.int64)
+    if config == "C5":
+        ids = np.arange(rank, docs, world, dtype=np.int64)
+        return ids, np.full(len(ids), ops, dtype=np.int64)
+    ids = np.arange(rank * docs, (rank + 1) * docs, dtype=np.int64)
+    return ids, np.full(docs, ops, dtype=np.int64)
+
+
+def gather_summaries_rccl(engine, group=None):
+    """The product path of the final gather: RCCL all-gather of the engine's summary records
+    (include/mte.h mte_gather_summaries). torch.distributed only carries rank 0's 128-byte RCCL id."""
+    import torch.distributed as dist
+
+    from . import mte
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    obj = [mte.rccl_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    comm = engine.rccl_comm(obj[0], rank, world)
+    try:
+        return engine.gather_summaries(rank, world, comm)
+    finally:
+        mte.rccl_comm_destroy(comm)
+
+
 def gather_summaries(summaries, group=None, device=None):
     """All-gather every rank's mte_doc_summary records (numpy SUMMARY_DTYPE) with torch.distributed.
     Ranks may hold different numbers of docs; counts are exchanged first."""

@@ -193,6 +193,13 @@ int mte_replay(mte_engine* e, mte_stats* out);
 int mte_generate(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops,
                  const uint32_t* ops_per_doc, uint32_t n_clients, uint64_t seed_base);
 
+/* As mte_generate, with the GLOBAL id of each document (NULL = 0..n_docs-1): a document's log
+ * depends only on (kind, its op count, its global id, n_clients, seed_base), so a multi-GPU run that
+ * shards documents by id generates exactly the documents a single GPU would. The ids are also the
+ * doc_id of the summary records (mte_summaries). */
+int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, const uint32_t* ops_per_doc,
+                     const uint32_t* doc_ids, uint32_t n_clients, uint64_t seed_base);
+
 /* Copy the (generated or loaded) op logs back to the host in mte_batch form. Buffers are owned by
  * the engine and stay valid until the next load/generate/destroy. */
 int mte_export_batch(mte_engine* e, mte_batch* out);
@@ -212,6 +219,21 @@ int mte_snapshot_v1(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* 
 int mte_snapshot_shared_string(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len);
 /* Per-doc summaries for all docs of the batch (checksum over text + snapshot blobs). */
 int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap);
+
+/* Multi-GPU: documents are sharded by id across ranks (one process per GPU) and the
+ * only collective of the path is this all-gather of the per-document summary records, over RCCL
+ * (xGMI inside a node). The communicator is RCCL's own: rank 0 makes an id (mte_rccl_unique_id),
+ * the host passes the same MTE_RCCL_ID_BYTES to every rank over its own channel, and each rank calls
+ * mte_rccl_comm_create on its engine's device. librccl is opened on first use.
+ * mte_gather_summaries: every rank's mte_summaries records, concatenated in rank order (ranks may
+ * hold different document counts; each record carries its global doc_id). out may be NULL to query
+ * *n; world == 1 needs no communicator. Collective: every rank must call it. */
+#define MTE_RCCL_ID_BYTES 128
+int mte_rccl_unique_id(uint8_t* id);
+int mte_rccl_comm_create(mte_engine* e, const uint8_t* id, int rank, int world, void** comm);
+void mte_rccl_comm_destroy(void* comm);
+int mte_gather_summaries(mte_engine* e, int rank, int world, void* rccl_comm, mte_doc_summary* out, size_t cap,
+                         size_t* n);
 
 /* Op-log ingestion: build a batch from per-doc JSON arrays of ISequencedDocumentMessage
  * (protocol.ts:126-166). The builder owns the memory. */

@@ -48,6 +48,11 @@ def lib():
         L.orc_ops_applied.argtypes = [vp]
         L.orc_status.argtypes = [vp, cp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_longlong)]
         L.orc_stats.argtypes = [vp, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)]
+        L.orc_generate.argtypes = [vp, u32, u32, u64, u32, u64, vp, vp, ctypes.POINTER(u64)]
+        L.orc_generate_batch.restype = u64
+        L.orc_generate_batch.argtypes = [u32, vp, vp, u32, u32, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int32)]
+        L.orc_replay_list.restype = u64
+        L.orc_replay_list.argtypes = [vp, vp, u32, i32, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int32), i32]
         L.orc_replay_batch.restype = u64
         L.orc_replay_batch.argtypes = [vp, u32, u32, i32, cp, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int32), i32]
         _lib = L
@@ -80,6 +85,18 @@ class OracleDoc:
         """SnapshotLoader: resume from a summary ITree (JSON text); the doc must be fresh."""
         b = text.encode() if isinstance(text, str) else text
         return lib().orc_load_summary(self._h, b, len(b))
+
+    def generate(self, kind, gid, n_ops, n_clients=8, seed=0, export=False):
+        """Synthetic log (the GPU generator restated), replayed into this (fresh) document. With
+        export=True returns (ops numpy records, payload uint16 array)."""
+        import numpy as np
+
+        ops = np.zeros(n_ops, dtype=_op_dtype()) if export else None
+        pay = np.zeros(8 * n_ops + 1, dtype=np.uint16) if export else None
+        pl = ctypes.c_uint64()
+        lib().orc_generate(self._h, kind, gid, n_ops, n_clients, seed,
+                           ops.ctypes.data if export else None, pay.ctypes.data if export else None, ctypes.byref(pl))
+        return (ops, pay[: pl.value]) if export else None
 
     def apply_batch(self, batch_ptr, doc):
         return lib().orc_apply_batch(self._h, batch_ptr, doc)
@@ -128,6 +145,35 @@ class OracleDoc:
         a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         lib().orc_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
         return {"leafCount": a.value, "removedLeafCount": b.value, "maxHeight": c.value}
+
+
+def _op_dtype():
+    import numpy as np
+
+    return np.dtype([("seq", "<i4"), ("ref_seq", "<i4"), ("msn", "<i4"), ("pos1", "<i4"), ("a", "<i4"),
+                     ("b", "<u4"), ("props", "<u4"), ("type", "u1"), ("client", "u1"), ("flags", "<u2")])
+
+
+def generate_batch(kind, gids, n_ops, n_clients=8, seed=0, threads=1):
+    """Generate + replay documents with global ids `gids` (op counts n_ops) on the CPU; returns
+    (ops, checksums[list], statuses[list])."""
+    import numpy as np
+
+    g = np.ascontiguousarray(gids, dtype=np.uint32)
+    n = np.ascontiguousarray(n_ops, dtype=np.uint64)
+    k = len(g)
+    cs = (ctypes.c_uint64 * max(k, 1))()
+    st = (ctypes.c_int32 * max(k, 1))()
+    ops = lib().orc_generate_batch(kind, g.ctypes.data, n.ctypes.data, k, n_clients, seed, threads, cs, st)
+    return ops, list(cs)[:k], list(st)[:k]
+
+
+def replay_list(batch_ptr, docs, threads=1, with_snapshot=False):
+    """Replay the listed documents of an mte_batch (list order, dynamic queue); returns ops applied."""
+    import numpy as np
+
+    d = np.ascontiguousarray(docs, dtype=np.uint32)
+    return lib().orc_replay_list(batch_ptr, d.ctypes.data, len(d), threads, None, None, 1 if with_snapshot else 0)
 
 
 def replay_batch(batch_ptr, d0, d1, threads=1, with_snapshot=True):

@@ -1158,6 +1158,142 @@ class Doc {
         }
     }
 
+    // ---- synthetic workload ------------------------------------------------------
+    // A CPU restatement of the GPU generator (fluidframework_amd/csrc/engine.hpp generate_run; the
+    // generator is this build's own code, not the reference's): 8 writers draw each op from their own
+    // view getLength(refSeq, client) of the tree as it stands, and the op is applied at once. Used to
+    // check that a document's log depends only on its global id (multi-GPU sharding) and that the
+    // device generator emits exactly these records.
+    struct GenRng {  // xoshiro256** seeded through splitmix64
+        uint64_t s[4];
+        static uint64_t splitmix(uint64_t& x) {
+            uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            return z ^ (z >> 31);
+        }
+        explicit GenRng(uint64_t x) {
+            for (int i = 0; i < 4; i++) s[i] = splitmix(x);
+        }
+        static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+        uint64_t next() {
+            uint64_t r = rotl(s[1] * 5, 7) * 9, t = s[1] << 17;
+            s[2] ^= s[0];
+            s[3] ^= s[1];
+            s[1] ^= s[2];
+            s[0] ^= s[3];
+            s[2] ^= t;
+            s[3] = rotl(s[3], 45);
+            return r;
+        }
+        uint32_t below(uint32_t n) { return (uint32_t)(((next() >> 32) * (uint64_t)n) >> 32); }
+    };
+    // The generator's property sets in the host's interning order (mte_host.cpp
+    // build_generator_props): ids 1..28 one key, then every two-key set.
+    static constexpr uint32_t kGenPropsets = 28 + 6 * 49;
+    static JObj genPropset(uint32_t id) {
+        static const char* keys[4] = {"bold", "italic", "color", "size"};
+        static const char* vals[7] = {"true", "false", "\"red\"", "\"blue\"", "10", "12", "null"};
+        std::string j;
+        if (id >= 1 && id <= 28) {
+            j = std::string("{\"") + keys[(id - 1) / 7] + "\":" + vals[(id - 1) % 7] + "}";
+        } else {
+            uint32_t q = id - 29, pair = q / 49, k1 = 0, k2 = 1;
+            for (uint32_t a = 0, n = 0; a < 4; a++)
+                for (uint32_t b2 = a + 1; b2 < 4; b2++, n++)
+                    if (n == pair) k1 = a, k2 = b2;
+            j = std::string("{\"") + keys[k1] + "\":" + vals[(q % 49) / 7] + ",\"" + keys[k2] + "\":" + vals[q % 7] + "}";
+        }
+        return parse(j)->o;
+    }
+    // kind 2: C2 insert/remove around a 2048-char target; 3: C3 annotate + forced ties/overlaps;
+    // 5: the C2 mix with every writer's refSeq within 64 of the current seq.
+    void generate(uint32_t kind, uint32_t gid, uint64_t nops, uint32_t nc, uint64_t seed, mte_op* opsOut,
+                  std::vector<uint16_t>* payOut) {
+        GenRng rng(0xF1D0C0DEull ^ (uint64_t)gid ^ (seed * 0x9E3779B97F4A7C15ull));
+        std::vector<int> ref(nc, 0), sidOf(nc, 0);
+        int nextShort = 1, lastC = -1, lastR = 0, lastPos = 0;
+        uint32_t pay = 0;
+        for (uint64_t step = 0; step < nops && !status; step++) {
+            const int seq = (int)step + 1, cur = seq - 1;
+            const uint32_t c = rng.below(nc);
+            if (rng.below(4) == 0) {
+                ref[c] = cur;
+            } else {
+                int nr = ref[c] + (int)rng.below(5);
+                ref[c] = nr < cur ? nr : cur;
+            }
+            if (kind == 5 && ref[c] < cur - 64) ref[c] = cur - 64;
+            bool forced = false;  // (short-circuit order: the draw happens only past the first tests)
+            if (kind == 3 && lastC >= 0 && (uint32_t)lastC != c && rng.below(100) < 15 && lastR >= ref[c]) {
+                ref[c] = lastR;
+                forced = true;
+            }
+            if (sidOf[c] == 0) {
+                sidOf[c] = nextShort++;
+                getOrAddShortClientId("client-" + std::to_string(c));
+            }
+            const int C = sidOf[c], R = ref[c];
+            const int len = mt.getLength(R, C);
+            const uint32_t roll = rng.below(100);
+            uint32_t type;
+            if (len == 0) type = MTE_OP_INSERT;
+            else if (kind == 3) type = roll < 45 ? MTE_OP_INSERT : (roll < 80 ? MTE_OP_REMOVE : MTE_OP_ANNOTATE);
+            else type = roll < (len < 2048 ? 60u : 40u) ? MTE_OP_INSERT : MTE_OP_REMOVE;
+            mte_op op{};
+            op.seq = seq;
+            op.ref_seq = R;
+            op.client = (uint8_t)C;
+            op.flags = MTE_F_END_OF_MSG;
+            op.type = (uint8_t)type;
+            try {
+                if (type == MTE_OP_INSERT) {
+                    const int pos = forced ? (lastPos < len ? lastPos : len) : (int)rng.below((uint32_t)len + 1);
+                    const uint32_t n = 1 + rng.below(8);
+                    op.pos1 = pos;
+                    op.a = (int32_t)pay;
+                    op.b = n;
+                    Segment* s = mt.newSegment();
+                    for (uint32_t i = 0; i < n; i++) {
+                        const char16_t ch = (char16_t)(u'a' + rng.below(26));
+                        s->text.push_back(ch);
+                        if (payOut) payOut->push_back((uint16_t)ch);
+                    }
+                    s->len = (int)n;
+                    pay += n;
+                    if (kind == 3 && rng.below(4) == 0) op.props = 1 + rng.below(kGenPropsets);
+                    if (op.props) MergeTree::addProperties(s, genPropset(op.props), false);
+                    std::vector<Segment*> segs{s};
+                    mt.insertSegments(pos, segs, R, C, seq);
+                } else {
+                    const int a = forced ? (lastPos < len ? lastPos : len - 1) : (int)rng.below((uint32_t)len);
+                    const int n = 1 + (int)rng.below(16);
+                    op.pos1 = a;
+                    op.a = a + n < len ? a + n : len;
+                    if (type == MTE_OP_ANNOTATE) {
+                        op.props = 1 + rng.below(kGenPropsets);
+                        mt.annotateRange(op.pos1, op.a, genPropset(op.props), false, R, C, seq);
+                    } else {
+                        mt.markRangeRemoved(op.pos1, op.a, R, C, seq);
+                    }
+                }
+                opsApplied++;
+                int msn = ref[0];
+                for (uint32_t q = 1; q < nc; q++) msn = ref[q] < msn ? ref[q] : msn;
+                op.msn = msn;
+                lastC = (int)c;
+                lastR = R;
+                lastPos = op.pos1;
+                if (opsOut) opsOut[step] = op;
+                updateSeqNumbers(msn, seq);
+            } catch (EngineError& e) {
+                status = e.code;
+                failingSeq = seq;
+                error = e.what();
+            }
+        }
+    }
+
     // ---- local, non-collaborative ops (SharedString before attach; generateSharedStrings.ts) --
     void localInsert(int pos, Segment* s) {
         std::vector<Segment*> segs{s};
@@ -1453,6 +1589,32 @@ int orc_stats(Doc* d, int* leaves, int* removed, int* height) {
     return 0;
 }
 
+// CPU baseline over a sample: replay the listed documents of a batch (in list order, dynamic queue)
+// on `threads` threads; returns ops applied. checksums/statuses may be NULL.
+uint64_t orc_replay_list(const mte_batch* b, const uint32_t* docs, uint32_t n, int threads, uint64_t* checksums,
+                         int32_t* statuses, int with_snapshot) {
+    std::atomic<uint32_t> next{0};
+    std::atomic<uint64_t> ops{0};
+    auto work = [&]() {
+        uint64_t local = 0;
+        for (uint32_t i; (i = next.fetch_add(1)) < n;) {
+            const uint32_t d = docs[i];
+            uint32_t c0 = b->doc_client_offsets[d];
+            std::string obs(b->client_names + b->client_name_offsets[c0], b->client_names + b->client_name_offsets[c0 + 1]);
+            Doc doc(obs.c_str());
+            doc.applyBatch(b, d);
+            local += doc.opsApplied;
+            if (checksums) checksums[i] = with_snapshot ? doc.checksum(10000) : 0;
+            if (statuses) statuses[i] = doc.status;
+        }
+        ops += local;
+    };
+    std::vector<std::thread> ts;
+    for (int i = 0; i < std::max(1, threads); i++) ts.emplace_back(work);
+    for (auto& t : ts) t.join();
+    return ops.load();
+}
+
 // CPU baseline / bulk parity: replay docs [d0, d1) of a batch on `threads` threads. Writes one
 // checksum (text + SnapshotV1 blobs) and status per doc; returns ops applied.
 uint64_t orc_replay_batch(const mte_batch* b, uint32_t d0, uint32_t d1, int threads, const char* observer,
@@ -1482,6 +1644,40 @@ uint64_t orc_replay_batch(const mte_batch* b, uint32_t d0, uint32_t d1, int thre
         for (int i = 0; i < threads; i++) ts.emplace_back(work);
         for (auto& t : ts) t.join();
     }
+    return ops.load();
+}
+
+// Synthetic log of one document (the GPU generator restated, Doc::generate), replayed into `d`
+// (a fresh document with an observer). ops_out: n_ops records or NULL; pay_out: the inserted text
+// (at most 8 units per op) or NULL, *pay_len its length.
+int orc_generate(Doc* d, uint32_t kind, uint32_t gid, uint64_t n_ops, uint32_t n_clients, uint64_t seed,
+                 mte_op* ops_out, uint16_t* pay_out, uint64_t* pay_len) {
+    std::vector<uint16_t> pay;
+    d->generate(kind, gid, n_ops, n_clients, seed, ops_out, pay_out || pay_len ? &pay : nullptr);
+    if (pay_out) memcpy(pay_out, pay.data(), pay.size() * 2);
+    if (pay_len) *pay_len = pay.size();
+    return d->status;
+}
+
+// Generate + replay documents gids[0..n) on `threads` threads: checksum and status per document.
+uint64_t orc_generate_batch(uint32_t kind, const uint32_t* gids, const uint64_t* n_ops, uint32_t n, uint32_t n_clients,
+                            uint64_t seed, int threads, uint64_t* checksums, int32_t* statuses) {
+    std::atomic<uint32_t> next{0};
+    std::atomic<uint64_t> ops{0};
+    auto work = [&]() {
+        uint64_t local = 0;
+        for (uint32_t i; (i = next.fetch_add(1)) < n;) {
+            Doc doc("__observer__");
+            doc.generate(kind, gids[i], n_ops[i], n_clients, seed, nullptr, nullptr);
+            local += doc.opsApplied;
+            if (checksums) checksums[i] = doc.checksum(10000);
+            if (statuses) statuses[i] = doc.status;
+        }
+        ops += local;
+    };
+    std::vector<std::thread> ts;
+    for (int i = 0; i < std::max(1, threads); i++) ts.emplace_back(work);
+    for (auto& t : ts) t.join();
     return ops.load();
 }
 

@@ -159,3 +159,47 @@ def test_gpu_container_log_matches_oracle():
             compare_doc(e, batch, i, observer=OBS)
     finally:
         e.close()
+
+
+def _reorder_chunks_object_form(log):
+    """ChunkedOp messages with object-form contents and "type" AFTER "contents" (the key order of a
+    serialized ISequencedDocumentMessage)."""
+    out = []
+    for m in log:
+        if m.get("type") == "chunkedOp":
+            m2 = {k: v for k, v in m.items() if k not in ("contents", "type")}
+            m2["contents"] = json.loads(m["contents"])
+            m2["type"] = "chunkedOp"
+            out.append(m2)
+        else:
+            out.append(m)
+    return out
+
+
+def test_container_log_object_form_chunks():
+    log, expect, mt_tree, text2_snap = container_log()
+    b1, b2 = mte.Builder(), mte.Builder()
+    assert b1.add_container_log(log, observer=OBS) == b2.add_container_log(_reorder_chunks_object_form(log),
+                                                                           observer=OBS)
+    x, y = b1.batch(), b2.batch()
+    for i in range(2):
+        p, q = OracleDoc(OBS), OracleDoc(OBS)
+        p.apply_batch(ctypes.addressof(x), i)
+        q.apply_batch(ctypes.addressof(y), i)
+        assert p.status()[0] == 0 and p.snapshot_json() == q.snapshot_json()
+
+
+def test_container_log_failure_leaves_builder_unchanged():
+    """A channel whose attach summary is malformed fails the whole call and adds no document, even
+    when an earlier channel of the same log was fine."""
+    log, _, _, _ = container_log()
+    bad_snap = {"entries": [attributes(SS), blob("header", "{}"), tree("content", [blob("header", "not json")])]}
+    log = list(log) + [msg("A", 10_000, 9_999, {"address": "ds1", "contents": {"type": "attach", "content": {
+        "id": "text3", "type": SS, "snapshot": bad_snap}}}, 9_999)]
+    b = mte.Builder()
+    b.add_doc([msg("A", 1, 0, ins(0, "x"))], observer=OBS)
+    with pytest.raises(mte.MteError):
+        b.add_container_log(log, observer=OBS)
+    assert b.n_docs() == 1
+    assert b.add_container_log(container_log()[0], observer=OBS) == ["ds1/root", "ds1/text2"]
+    assert b.n_docs() == 3

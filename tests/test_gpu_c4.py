@@ -1,0 +1,113 @@
+"""GPU: the metric's own configuration (C4) at test scale, the solo route of its
+critical-path documents, the device generator against its CPU restatement (global doc ids), and the
+RCCL summary gather. Every comparison is bit-exact against the oracle."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from fluidframework_amd import mte
+from fluidframework_amd.shard import plan_shard, zipf_op_counts
+from oracle import OracleDoc, replay_batch
+from tests.gpu_helpers import compare_batch_checksums, compare_doc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = mte.Engine(0)
+    yield e
+    e.close()
+
+
+def test_scaled_c4_zipf_batch_matches_oracle(engine):
+    """C4's shape at 1/64 of its documents: Zipf op counts clamp(250k/r, 250, 250k) over 4,096
+    documents (one 250k-op document, the critical path, on the solo route; the next heads on the
+    k_lds priority route), LPT order, every document's checksum against the oracle."""
+    ids, counts = plan_shard("C4", 1, 0, 4096, 0, zipf_lo=250, zipf_hi=250_000)
+    engine.generate(2, len(ids), 0, n_clients=8, seed=1000, ops_per_doc=counts, doc_ids=ids)
+    batch = engine.export_batch()
+    st = engine.replay()
+    assert st["failed_docs"] == 0 and st["ops"] == int(counts.sum())
+    info = engine.run_info()
+    assert info["solo"] >= 1, info
+    head = engine.doc_result(0)
+    assert head["ops"] == 250_000 and head["mode"] == 3, head  # solo, stayed LDS-resident
+    bad, _, _ = compare_batch_checksums(engine, batch)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad
+    s = engine.summaries()
+    assert s["doc_id"].tolist() == ids.tolist()  # summary records carry the global ids
+
+
+def test_lone_long_document_solo_matches_oracle(engine):
+    """A lone 200k-op document (the C4 critical path at 1/5 scale) replays on the solo plan."""
+    engine.generate(2, 1, 200_000, n_clients=8, seed=1000)
+    batch = engine.export_batch()
+    engine.replay()
+    r = engine.doc_result(0)
+    assert r["mode"] == 3 and r["status"] == 0, r
+    bad, _, _ = compare_batch_checksums(engine, batch, threads=1)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad
+
+
+def test_solo_off_matches_solo_on(engine):
+    """The same Zipf batch with the solo route disabled (k_lds priority route only) gives the same
+    checksums."""
+    counts = zipf_op_counts(256, seed=3, lo=100, hi=60_000)
+    engine.generate(2, 256, 0, n_clients=8, seed=7, ops_per_doc=counts)
+    engine.replay()
+    a = engine.summaries()["checksum"].copy()
+    assert engine.run_info()["solo"] >= 1
+    engine.set_option("solo_max", 0)
+    try:
+        engine.replay()
+        assert engine.run_info()["solo"] == 0
+        b = engine.summaries()["checksum"].copy()
+    finally:
+        engine.set_option("solo_max", 16)
+    assert a.tolist() == b.tolist()
+
+
+@pytest.mark.parametrize("kind", [2, 3, 5])
+def test_device_generator_matches_cpu_generator(engine, kind):
+    """The device generator's records and payload equal the CPU restatement's for the same global
+    ids (so a sharded run generates exactly the documents a single GPU would)."""
+    gids = [0, 5, 70001, 262143]
+    n = 1500
+    engine.generate(kind, len(gids), n, n_clients=8, seed=1000, doc_ids=gids)
+    batch = engine.export_batch()
+    ops = mte.batch_ops(batch)
+    pay = np.ctypeslib.as_array(batch.payload, shape=(batch.doc_payload_offsets[len(gids)],))
+    for i, g in enumerate(gids):
+        o = OracleDoc()
+        oops, opay = o.generate(kind, g, n, n_clients=8, seed=1000, export=True)
+        mine = ops[batch.doc_op_offsets[i]: batch.doc_op_offsets[i + 1]]
+        assert mine.tobytes() == oops.tobytes(), f"kind {kind} gid {g}: op records differ"
+        p0 = batch.doc_payload_offsets[i]
+        assert pay[p0: p0 + len(opay)].tolist() == opay.tolist()
+    engine.replay()
+    s = engine.summaries()
+    for i, g in enumerate(gids):
+        o = OracleDoc()
+        o.generate(kind, g, n, n_clients=8, seed=1000)
+        assert int(s["checksum"][i]) == o.checksum(), f"kind {kind} gid {g}"
+
+
+def test_gather_summaries_world1_and_rccl_comm(engine):
+    """mte_gather_summaries at world 1 returns the local records; an RCCL communicator of one rank
+    can be created and destroyed on this device."""
+    engine.generate(2, 8, 500, n_clients=8, seed=3, doc_ids=list(range(100, 108)))
+    engine.replay()
+    g = engine.gather_summaries(0, 1, None)
+    assert g.tobytes() == engine.summaries().tobytes()
+    assert g["doc_id"].tolist() == list(range(100, 108))
+    uid = mte.rccl_unique_id()
+    assert len(uid) == mte.RCCL_ID_BYTES
+    comm = engine.rccl_comm(uid, 0, 1)
+    assert comm
+    mte.rccl_comm_destroy(comm)

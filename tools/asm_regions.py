@@ -9,7 +9,7 @@ NAMES = ["apply", "resolve", "insert_slot", "range", "zamboni", "scour", "heap",
          "fetch", "lru", "text", "alloc", "ops", "total"]
 path = sys.argv[1]
 kernel = sys.argv[2] if len(sys.argv) > 2 else "k_lds<false>"
-mangled = {"k_lds<false>": "_ZN3mte5k_ldsILb0EEEvNS_6ParamsE", "k_hbmq<false>": "_ZN3mte6k_hbmqILb0EEEvNS_6ParamsE"}[kernel]
+mangled = {"k_lds<false>": "_ZN3mte5k_ldsILb0EEEvNS_6ParamsE", "k_solo<false>": "_ZN3mte6k_soloILb0EEEvNS_6ParamsE", "k_hbmq<false>": "_ZN3mte6k_hbmqILb0EEEvNS_6ParamsE"}[kernel]
 lines = open(path).read().split("\n")
 start = next(i for i, l in enumerate(lines) if l.startswith(mangled + ":"))
 end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i] and i > start)

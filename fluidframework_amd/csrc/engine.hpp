@@ -33,7 +33,10 @@ enum ProfSlot : u32 {
     PF_APPLY = 0, PF_RESOLVE, PF_INSERT_SLOT, PF_RANGE, PF_ZAMBONI, PF_SCOUR, PF_HEAP, PF_FIND_SEG,
     PF_MAP, PF_PACK, PF_FETCH, PF_LRU, PF_TEXT, PF_ALLOC, PF_OPS, PF_TOTAL,
     // event counts
-    PN_RESOLVE, PN_DIRTY, PN_SCOUR, PN_SCOUR_CHANGED, PN_PACK, PN_POP, PN_PUSH, PN_SPLIT_BLK
+    PN_RESOLVE, PN_DIRTY, PN_SCOUR, PN_SCOUR_CHANGED, PN_PACK, PN_POP, PN_PUSH, PN_SPLIT_BLK,
+    // finer scopes
+    PF_OP_INS, PF_OP_REM, PF_EDIT, PF_SPLIT, PF_ZAM_EDIT, PF_ZAM_MSN, PF_RES_BLOCKS, PF_RES_SLOT, PF_BLEN_DIRTY,
+    PF_SCOUR_CHAIN, PF_SCOUR_WRITE, PF_LOOP, PN_INS, PN_REM
 };
 #ifdef MTE_PROFILE
 // counters accumulate straight into the per-document HBM record (fire-and-forget atomics: no
@@ -135,6 +138,7 @@ struct St {
     u32 root, height, n_lb;
     i32 minSeq, curSeq;
     u32 heapSize, segNext, arenaTop, arenaSel, mapNext;
+    i32 heapTop;  // key (maxSeq) of the heap's root; meaningful while heapSize > 0
     u32 lbFree, lbBump, inFree, inBump, inUsed, credit;
     i32 status;
     u32 adirty, gdirty;
@@ -232,11 +236,17 @@ struct Engine {
         maps = p.maps + c.map_off * MAP_WORDS;
         collab = c.collab != 0;
         has_nl = c.has_nl != 0;
+#ifdef MTE_VCONST
+        // per-document constants held in VGPRs: the replay state needs every SGPR it can get
+        asm volatile("" : "+v"(seg_cap), "+v"(arena_cap), "+v"(payload_len), "+v"(map_cap));
+        asm volatile("" : "+v"(payload), "+v"(arena0), "+v"(ovl), "+v"(maps));
+#endif
         st.root = NONE;
         st.height = 1;
         st.n_lb = 0;
         st.minSeq = st.curSeq = 0;
         st.heapSize = st.segNext = st.arenaTop = st.arenaSel = 0;
+        st.heapTop = 0;
         st.mapNext = 1;  // map id 0 == undefined
         st.lbFree = st.inFree = NONE;
         st.lbBump = st.inBump = st.inUsed = st.credit = 0;
@@ -455,15 +465,67 @@ struct Engine {
         const bool rem = ((meta & F_REMOVED) != 0) & ((((meta >> 8) & 0xffu) == C) | ((i32)q.z <= R) | ovh);
         return (ins & !rem) ? q.x : 0u;
     }
+    // The dirty blocks (max seq > R) are evaluated slot by slot, lane = slot: up to 8 blocks per
+    // pass, lanes 8g..8g+7 holding the slots of the g-th dirty block of the batch; each block's sum
+    // goes back to the lane that holds it (mbcnt rank -> bpermute from its group's last lane).
+#ifdef MTE_NEW_BLEN
+    MTE_DEV u32 blen_all(uint4 o, bool valid, i32 R, u32 C) const {
+        u32 v = valid ? o.y : 0u;
+        if (C == 0) return v;  // the observer sees every block settled
+        u64 dirty = wave_ballot(valid && (i32)o.z > R);
+        if (!dirty) return v;
+        const u32 g = L >> 3, s = L & 7;
+        const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(dirty >> 32), __builtin_amdgcn_mbcnt_lo((u32)dirty, 0u));
+        for (u32 pass = 0; dirty; pass++) {
+            // group g takes the g-th remaining dirty block
+            u32 b = NONE, cnt = 0;
+            u64 m = dirty;
+            for (u32 i = 0; i < 8 && m; i++) {
+                const u32 j = (u32)__builtin_ctzll(m);
+                m &= m - 1;
+                const u32 bj = wave_read(o.x, j), cj = wave_read(o.w, j);
+                b = g == i ? bj : b;
+                cnt = g == i ? cj : cnt;
+            }
+            const bool act = s < cnt && b < blk_cap();
+            const u32 idx = (act ? b : 0u) * 8 + s;
+            const uint4 q = VIS()[idx];
+            const u32 z = AUX()[idx].z;
+            const u32 sv = act ? vis_len(q, z, idx, R, C, 0u) : 0u;
+            const u32 tot = group8_scan(sv);
+            // the lanes whose block was taken in this pass read their group's total
+            const u32 r = below - pass * 8;
+            const bool mine = ((dirty >> L) & 1ull) && r < 8;
+            const u32 t = wave_shfl(tot, (mine ? r : 0u) * 8 + 7);
+            v = mine ? t : v;
+            dirty = m;
+        }
+        return v;
+    }
+
+#else
     MTE_DEV u32 blen_all(uint4 o, bool valid, i32 R, u32 C) const {
         const u32 cz = C == 0 ? 1u : 0u;
         const bool fast = !valid | (cz != 0) | ((i32)o.z <= R);
         u32 v = valid ? o.y : 0u;
         if (wave_ballot(!fast)) {
+            MTE_PROF(PF_BLEN_DIRTY);
             const u32 b = o.x < blk_cap() ? o.x : 0u;
             uint4 q[8];
+#ifdef MTE_MASK_BLEN
+            // only the dirty lanes read: the same slot of 64 different blocks (128-B stride) would
+            // hit two bank groups with every lane of the wave
+            if (!fast) {
+#pragma unroll
+                for (u32 s = 0; s < 8; s++) q[s] = VIS()[b * 8 + s];
+            } else {
+#pragma unroll
+                for (u32 s = 0; s < 8; s++) q[s] = make_uint4(0, 0, 0, 0);
+            }
+#else
 #pragma unroll
             for (u32 s = 0; s < 8; s++) q[s] = VIS()[b * 8 + s];
+#endif
             u32 sv = 0;
             if (C >= 32) {  // clients 32..63: the general predicate (HBM half of the overlap mask)
 #pragma unroll
@@ -489,6 +551,7 @@ struct Engine {
         return v;
     }
 
+#endif
     // Recompute (visible length, max seq) of ORD()[k0 .. k0+n), n <= 8, from the slots.
     MTE_DEV void refresh(u32 k0, u32 n) {
         const u32 g = L >> 3, s = L & 7;
@@ -524,6 +587,9 @@ struct Engine {
         f.cum = 0;
         fence_ovl();
         i32 cum = 0;
+#ifdef MTE_PROFILE
+        ProfScope _rb(prof + PF_RES_BLOCKS);
+#endif
         for (u32 base = 0; base < st.n_lb; base += 64) {
             const u32 k = base + L;
             const bool valid = k < st.n_lb;
@@ -545,6 +611,7 @@ struct Engine {
             cum += (i32)wave_read(incl, 63);
         }
         if (!f.ok) return f;
+        MTE_PROF(PF_RES_SLOT);
         // inside the block: first slot with r < vislen, or a zero-visible slot at r == 0 that wins breakTie
         const u32 s = L;
         const u32 idx = sidx(f.blk, s);
@@ -947,6 +1014,7 @@ struct Engine {
             return;
         }
         const u32 n = U(++st.heapSize);
+        if (n == 1) st.heapTop = maxSeq;  // keys only grow: a push moves the root only into an empty heap
         MTE_COUNT(PN_PUSH, 1);
         if (L == 0) {
             HEAP()[n] = make_uint2(sid, (u32)maxSeq);
@@ -954,22 +1022,36 @@ struct Engine {
         }
         sync();
     }
+    // Pop: sift-down of collections.ts:252-264 (the smaller child, left on ties, moves up while
+    // strictly below the moved last entry). LDS modes: one round of reads gives every lane l the
+    // smaller child of node l and of node 64 + l; the root-to-leaf path is then followed with
+    // readlanes (deeper nodes, heaps over 255 entries, read their child pair directly). Only the
+    // moved entries are written. HBM mode: lane 0 walks the pairs in memory.
+#ifdef MTE_NEW_HEAP
+    static constexpr bool NEW_HEAP = true;
+#else
+    static constexpr bool NEW_HEAP = false;
+#endif
     // heap entry at a uniform position held in registers (position i: lane i % 64 of set i / 64)
     MTE_DEV static uint2 hent(uint2 h0, uint2 h1, uint2 h2, u32 i) {
         if (i < 64) return make_uint2(wave_read(h0.x, i), wave_read(h0.y, i));
         if (i < 128) return make_uint2(wave_read(h1.x, i - 64), wave_read(h1.y, i - 64));
         return make_uint2(wave_read(h2.x, i - 128), wave_read(h2.y, i - 128));
     }
-    // Pop: sift-down of collections.ts:252-264 (the smaller child, left on ties, moves up while
-    // strictly below the moved last entry). LDS mode: the whole heap (<= HEAP_CAP) is read once
-    // into registers and walked with scalar reads; only the moved entries are written back.
+    MTE_DEV static void min_child(uint4 pr, u32 i, u32 m, u32& j, uint2& e) {
+        const bool right = (2 * i + 1 <= m) && ((i32)pr.y - (i32)pr.w > 0);
+        j = 2 * i + (right ? 1u : 0u);
+        e = right ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
+    }
     MTE_DEV uint2 heap_pop() {
         MTE_PROF(PF_HEAP);
         MTE_COUNT(PN_POP, 1);
         uint2* H = HEAP();
         const u32 n = st.heapSize;
+        const u32 m = n - 1;
         uint2 x;
-        if constexpr (SHARED) {
+#ifndef MTE_NEW_HEAP
+        if constexpr (SHARED) {  // the whole heap (<= HEAP_CAP) as a register image, scalar walk
             static_assert(HEAP_CAP < 192, "heap register image holds 192 positions");
             uint2 h0 = make_uint2(0, 0), h1 = h0, h2 = h0;
             if (L <= n) h0 = H[L];
@@ -977,7 +1059,7 @@ struct Engine {
             if (n >= 128 && 128 + L <= n) h2 = H[128 + L];
             x = hent(h0, h1, h2, 1);
             const uint2 last = hent(h0, h1, h2, n);
-            const u32 m = n - 1;
+            i32 newTop = (i32)last.y;
             u32 k = 1;
             while ((k << 1) <= m) {
                 u32 j = k << 1;
@@ -990,17 +1072,55 @@ struct Engine {
                     }
                 }
                 if ((i32)last.y - (i32)hj.y <= 0) break;
+                if (k == 1) newTop = (i32)hj.y;
                 if (L == 0) H[k] = hj;
                 k = j;
             }
             if (m >= 1 && L == 0) H[k] = last;
+            st.heapTop = newTop;
+        } else
+#endif
+        if constexpr (LDSM && NEW_HEAP) {
+            const u32 i1 = 64 + L;
+            uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0;
+            if (L >= 1 && 2 * L <= m) p0 = *(const uint4*)(H + 2 * L);
+            if (2 * i1 <= m) p1 = *(const uint4*)(H + 2 * i1);
+            const uint2 top = H[1], lst = H[n];
+            x = make_uint2(U(top.x), U(top.y));
+            const uint2 last = make_uint2(U(lst.x), U(lst.y));
+            u32 j0, j1;
+            uint2 e0, e1;
+            min_child(p0, L, m, j0, e0);
+            min_child(p1, i1, m, j1, e1);
+            u32 k = 1;
+            i32 newTop = (i32)last.y;
+            while (2 * k <= m) {
+                u32 j;
+                uint2 hj;
+                if (k < 64) {
+                    j = wave_read(j0, k);
+                    hj = make_uint2(wave_read(e0.x, k), wave_read(e0.y, k));
+                } else if (k < 128) {
+                    j = wave_read(j1, k - 64);
+                    hj = make_uint2(wave_read(e1.x, k - 64), wave_read(e1.y, k - 64));
+                } else {
+                    const uint4 pr = U(*(const uint4*)(H + 2 * k));
+                    min_child(pr, k, m, j, hj);
+                }
+                if ((i32)last.y - (i32)hj.y <= 0) break;
+                if (k == 1) newTop = (i32)hj.y;
+                if (L == 0) H[k] = hj;
+                k = j;
+            }
+            if (m >= 1 && L == 0) H[k] = last;
+            st.heapTop = newTop;
         } else {
             x = make_uint2(0, 0);
+            i32 newTop = 0;
             if (L == 0) {
                 x = H[1];
-                u32 m = n;
-                const uint2 last = H[m];
-                m--;
+                const uint2 last = H[n];
+                newTop = (i32)last.y;
                 u32 k = 1;
                 while ((k << 1) <= m) {
                     u32 j = k << 1;
@@ -1016,6 +1136,7 @@ struct Engine {
                         hj = H[j];
                     }
                     if ((i32)last.y - (i32)hj.y <= 0) break;
+                    if (k == 1) newTop = (i32)hj.y;
                     H[k] = hj;
                     k = j;
                 }
@@ -1023,8 +1144,9 @@ struct Engine {
             }
             x.x = wave_read(x.x, 0);
             x.y = wave_read(x.y, 0);
+            st.heapTop = wave_read(newTop, 0);
         }
-        st.heapSize = n - 1;
+        st.heapSize = m;
         sync();
         return x;
     }
@@ -1256,6 +1378,9 @@ struct Engine {
         u32 nkeep = 0;
         u32 kSrc = 0, kLen = 0, kOff = 0, kCap = 0;  // lane i < nkeep: kept slot i
         Jobs jb;
+#ifdef MTE_PROFILE
+        u64 _tc0 = __builtin_amdgcn_s_memtime();
+#endif
         for (u32 attempt = 0; attempt < 2; attempt++) {
             nkeep = 0;
             jb.n = 0;
@@ -1344,6 +1469,10 @@ struct Engine {
             if (st.status) return cnt;
             if (act) me = load(blk, L);
         }
+#ifdef MTE_PROFILE
+        if (L == 0) atomicAdd(prof + PF_SCOUR_CHAIN, __builtin_amdgcn_s_memtime() - _tc0);
+        ProfScope _sw(prof + PF_SCOUR_WRITE);
+#endif
         if (jb.n) run_jobs(jb);
         Seg out = load(blk, L < nkeep ? kSrc : 0u);  // the kept slots, re-read (not yet overwritten)
         if (L < nkeep) {
@@ -1517,9 +1646,7 @@ struct Engine {
         if (!collab) return;
         MTE_PROF(PF_ZAMBONI);
         for (int i = 0; i < 2 && !st.status; i++) {
-            if (st.heapSize == 0) break;
-            const i32 top = wave_first((i32)HEAP()[1].y);
-            if (top > st.minSeq) break;
+            if (st.heapSize == 0 || st.heapTop > st.minSeq) break;
             uint2 e = heap_pop();
             u32 k, blk, cnt;
             if (!find_seg(e.x, k, blk, cnt)) continue;  // segment no longer linked
@@ -1570,6 +1697,7 @@ struct Engine {
     // (mergeTree.ts:2565-2719): split at p1 and p2, then mark the range. The phases share ONE
     // resolve and ONE insert_slot call site. Returns false when nothing was edited (empty insert).
     MTE_DEV bool edit(u32 type, i32 p1, i32 p2, i32 R, u32 C, i32 seq, Seg rec, u32 propset, bool rewrite) {
+        MTE_PROF(PF_EDIT);
         const bool ins = type == MTE_OP_INSERT || type == MTE_OP_INSERT_MARKER;
         const u32 nphase = ins ? 2u : 3u;
         Found known;  // insert after a split: the insertion point follows from the split (below)
@@ -1598,6 +1726,7 @@ struct Engine {
                 j = f.slot >= 0 ? (u32)f.slot : f.cnt;
             } else {
                 if (!(f.slot >= 0 && f.r > 0)) continue;
+                MTE_PROF(PF_SPLIT);
                 // ensureIntervalBoundary: split slot f.slot at f.r (BaseSegment.splitAt, :524-568)
                 Seg left = load_u(f.blk, (u32)f.slot);
                 const u32 sid = new_sid();
@@ -1765,6 +1894,7 @@ struct Engine {
         st.minSeq = (i32)U((u32)st.minSeq);
         st.curSeq = (i32)U((u32)st.curSeq);
         st.heapSize = U(st.heapSize);
+        st.heapTop = (i32)U((u32)st.heapTop);
         st.segNext = U(st.segNext);
         st.arenaTop = U(st.arenaTop);
         st.arenaSel = U(st.arenaSel);
@@ -1786,11 +1916,15 @@ struct Engine {
     // LOAD_NODE records before it (the shape of reloadFromSegments + loadBody's appends, computed by
     // the builder and checked against the oracle's insertingWalk) and opens the collaboration window.
     MTE_DEV void load_record(const mte_op& op, u64 i) {
-        if (!collab || op.type > MTE_OP_LOAD_NODE) {
+        if (!collab || op.type > MTE_OP_LOAD_APPEND) {
             fail(MTE_DOC_UNSUPPORTED, op.seq);
             return;
         }
         if (op.type == MTE_OP_LOAD_NODE) return;  // consumed by LOAD_END
+        if (op.type == MTE_OP_LOAD_APPEND) {  // applied by apply() (one edit call site)
+            fail(MTE_DOC_UNSUPPORTED, op.seq);
+            return;
+        }
         if (op.type == MTE_OP_LOAD_END) {
             load_link(op, i);
             return;
@@ -1801,6 +1935,10 @@ struct Engine {
         }
         const bool mk = (op.flags & MTE_F_LOAD_MARKER) != 0;
         const bool rm = (op.flags & MTE_F_LOAD_REMOVED) != 0;
+        if (op.client >= MTE_MAX_CLIENTS || (rm && (u32)op.pos1 >= MTE_MAX_CLIENTS)) {
+            fail(MTE_DOC_UNSUPPORTED, op.seq);
+            return;
+        }
         Seg rec;
         rec.len = mk ? 1u : op.b;
         rec.props = op.props ? build_map(0, op.props, false) : 0u;
@@ -1900,36 +2038,83 @@ struct Engine {
     // Client.applyMsg for one op record (client.ts:805-836): the edit, zamboni, then
     // updateSeqNumbers / setMinSeq (client.ts:829-836, mergeTree.ts:1718-1736) and zamboni again
     // when the MSN advanced. One zamboni call site.
+    // LOAD_APPEND position (snapshotLoader.ts:184-213, blockInsert mergeTree.ts:2193-2223): pos =
+    // root.cachedLength (every segment not removed) at the first segment of an append call, then
+    // advanced by each segment's length whether it is linked or skipped; the running position is a
+    // per-document counter, so it survives a hand-off to an HBM slot between two records. A repeated
+    // object (flushBatch never clears its batch, :196-199) is re-linked by the reference when its walk
+    // finds pos -- one object in two places, which this engine does not model (MTE_DOC_UNSUPPORTED)
+    // -- and skipped otherwise. Returns true when the segment is to be inserted at p1.
+    MTE_DEV bool load_append_pos(const mte_op& op, Seg& rec, i32& p1) {
+        const bool rm = (op.flags & MTE_F_LOAD_REMOVED) != 0;
+        if (st.root == NONE || (rm && (u32)op.pos1 >= MTE_MAX_CLIENTS)) {
+            fail(MTE_DOC_UNSUPPORTED, op.seq);
+            return false;
+        }
+        i32 pos;
+        if (op.flags & MTE_F_APPEND_FIRST) pos = get_length(st.curSeq, 0u);
+        else pos = (i32)stat_get(ST_APPEND);
+        sync();
+        if (L == 0) STATS()[ST_APPEND] = (u32)(pos + (i32)rec.len);
+        sync();
+        if (rec.len == 0) return false;
+        if (op.flags & MTE_F_APPEND_REPEAT) {
+            if (resolve(pos, 0, op.client).ok) fail(MTE_DOC_UNSUPPORTED, op.seq);
+            return false;
+        }
+        if (rm) {
+            rec.rseq = op.ref_seq;
+            rec.meta |= ((((u32)op.pos1 & 0xffu) << 8) | F_REMOVED);
+        }
+        p1 = pos;
+        return true;
+    }
+
     MTE_DEV void apply(const mte_op& op) {
         MTE_PROF(PF_APPLY);
         MTE_COUNT(PF_OPS, 1);
+#ifdef MTE_PROFILE
+        const u64 t_op0 = __builtin_amdgcn_s_memtime();
+        struct OpScope {
+            u64* acc; u64 t0; u32 L;
+            MTE_DEV ~OpScope() { if (L == 0) atomicAdd(acc, __builtin_amdgcn_s_memtime() - t0); }
+        } _op_scope{prof + (op.type == MTE_OP_REMOVE ? PF_OP_REM : PF_OP_INS), t_op0, L};
+        MTE_COUNT(op.type == MTE_OP_REMOVE ? PN_REM : PN_INS, 1);
+#endif
+        // a loadBody append of a summary load (include/mte.h MTE_OP_LOAD_APPEND) shares the insert
+        // path: insertSegments(pos, [seg], refSeq 0, client, seq) with the segment's own merge info
+        const bool ld = op.type == MTE_OP_LOAD_APPEND;
         if (op.client >= MTE_MAX_CLIENTS) {
             fail(MTE_DOC_UNSUPPORTED, op.seq);
             return;
         }
         const u32 C = collab ? (u32)op.client : 0u;
         const i32 seq = collab ? op.seq : 0;
-        const i32 R = collab ? op.ref_seq : 0;
-        if (collab && op.type != MTE_OP_NOOP && !(st.curSeq < op.seq)) {
+        const i32 R = collab && !ld ? op.ref_seq : 0;
+        if (collab && op.type != MTE_OP_NOOP && !ld && !(st.curSeq < op.seq)) {
             fail(MTE_DOC_SEQ_ORDER, op.seq);
             return;
         }
         bool edited = false;
-        if (op.type <= MTE_OP_INSERT_MARKER) {
+        if (op.type <= MTE_OP_INSERT_MARKER || ld) {
             Seg rec;
-            const bool mk = op.type == MTE_OP_INSERT_MARKER;
-            const bool ins = op.type == MTE_OP_INSERT || mk;
+            const bool mk = ld ? (op.flags & MTE_F_LOAD_MARKER) != 0 : op.type == MTE_OP_INSERT_MARKER;
+            const bool ins = op.type == MTE_OP_INSERT || mk || ld;
             rec.len = mk ? 1u : op.b;
             rec.seq = seq;
             rec.rseq = 0;
             rec.meta = (C & 0xff) | (mk ? F_MARKER : 0u);
+            u32 type = op.type;
+            i32 p1 = op.pos1;
+            if (ld && !load_append_pos(op, rec, p1)) return;  // skipped (a repeated object) or failed
+            type = ld ? (mk ? (u32)MTE_OP_INSERT_MARKER : (u32)MTE_OP_INSERT) : type;
             rec.props = (ins && op.props) ? build_map(0, op.props, false) : 0u;
             if (st.status) return;
-            rec.toff = mk ? op.b : (u32)op.a;
+            rec.toff = (mk && !ld) ? op.b : (u32)op.a;
             rec.tcap = 0;
             rec.sid = 0;
-            edited = edit(op.type, op.pos1, op.a, R, C, seq, rec, op.props, (op.flags & MTE_F_REWRITE) != 0);
-            stat_add(ST_OPS, 1);
+            edited = edit(type, p1, op.a, R, C, seq, rec, op.props, (op.flags & MTE_F_REWRITE) != 0);
+            if (!ld) stat_add(ST_OPS, 1);
             if (st.status) return;
         }
         for (u32 z = 0; z < 2; z++) {
@@ -1949,7 +2134,12 @@ struct Engine {
                     }
                 }
             }
-            if (run) zamboni();
+            if (run) {
+#ifdef MTE_PROFILE
+                ProfScope _zs(prof + (z == 0 ? PF_ZAM_EDIT : PF_ZAM_MSN));
+#endif
+                zamboni();
+            }
             if (st.status) return;
         }
     }
@@ -2139,7 +2329,7 @@ struct Engine {
         // loops below carry no branch for them
         for (; i < e && !st.status; i++) {
             const mte_op op = read_op(p.ops + i);
-            if (op.type < MTE_OP_LOAD_SEG) break;
+            if (op.type < MTE_OP_LOAD_SEG || op.type == MTE_OP_LOAD_APPEND) break;
             if (!room()) return i;
             load_record(op, i);
         }
@@ -2165,7 +2355,10 @@ struct Engine {
                     MTE_PROF(PF_FETCH);
                     op = read_op(RING() + r);
                 }
-                if (!room()) break;
+                {
+                    MTE_PROF(PF_LOOP);
+                    if (!room()) break;
+                }
                 apply(op);
             }
         } else {

@@ -51,7 +51,7 @@ struct WaveRegion {
     u16 hint[256];              // LRU heap: segment id (mod 256) -> leaf block
     u32 stats[8];               // per-document counters (engine.hpp ST_*)
 };
-constexpr u32 ST_OPS = 0, ST_MSGS = 1, ST_GC = 2, ST_MAXLB = 3, ST_FAILSEQ = 4, ST_WORDS = 8;
+constexpr u32 ST_OPS = 0, ST_MSGS = 1, ST_GC = 2, ST_MAXLB = 3, ST_FAILSEQ = 4, ST_APPEND = 5, ST_WORDS = 8;
 constexpr u32 POOL_HDR = 80;  // 16-word allocation bitmap + pool_avail
 constexpr u32 POOL_BLOCKS = ((LDS_BYTES - LDS_WAVES * (u32)sizeof(WaveRegion) - POOL_HDR - 16) / (8 * 32 + 4 + 1)) & ~3u;
 
@@ -198,7 +198,7 @@ struct Params {
 };
 
 // MTE_PROFILE builds: s_memtime cycles per engine phase, per document (engine.hpp PROF_*).
-constexpr u32 PROF_SLOTS = 24;
+constexpr u32 PROF_SLOTS = 40;
 
 // HBM-resident capacities of a document with n ops (leaf blocks hold >= 4 segments except
 // transiently; segments <= 2 per op + 1 without zamboni). Block ids below POOL_BLOCKS are the

@@ -574,7 +574,8 @@ static void count_doc_ops(const HostBatch& hb, uint32_t d, uint64_t& pi, uint64_
     pi = an = 0;
     for (uint64_t i = hb.doc_op_offsets[d]; i < hb.doc_op_offsets[d + 1]; i++) {
         const mte_op& o = hb.ops[i];
-        if ((o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER || o.type == MTE_OP_LOAD_SEG) && o.props)
+        if ((o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER || o.type == MTE_OP_LOAD_SEG ||
+             o.type == MTE_OP_LOAD_APPEND) && o.props)
             pi++;
         if (o.type == MTE_OP_ANNOTATE) an++;
     }
@@ -600,8 +601,8 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         pay[d] = b->doc_payload_offsets[d + 1] - b->doc_payload_offsets[d];
         count_doc_ops(e->hb, d, pi[d], an[d]);
         collab[d] = e->hb.client(d, 0).empty() ? 0 : 1;  // empty observer name => local, non-collab
-        if (b->doc_client_offsets[d + 1] - b->doc_client_offsets[d] > MTE_MAX_CLIENTS)
-            return set_err(e, MTE_E_UNSUPPORTED, "more than 64 clients in a document");
+        // a document with more than MTE_MAX_CLIENTS clients fails alone (MTE_DOC_UNSUPPORTED at its
+        // first op from a client beyond the cap), never the batch
     }
     auto t0 = std::chrono::steady_clock::now();
     int rc;
@@ -1134,6 +1135,17 @@ int mte_text(mte_engine* e, uint32_t doc, uint16_t* buf, size_t cap, size_t* len
     return MTE_OK;
 }
 
+int mte_length(mte_engine* e, uint32_t doc, uint64_t* len) {
+    DocView v;
+    int rc = doc_view(e, doc, v);
+    if (rc) return rc;
+    uint64_t n = 0;
+    for (auto& sg : v.segs)
+        if (!sg.removed) n += sg.len;  // a marker counts 1 (Marker.cachedLength, mergeTree.ts:649)
+    if (len) *len = n;
+    return MTE_OK;
+}
+
 int mte_segments(mte_engine* e, uint32_t doc, mte_seg_row* rows, size_t cap, size_t* n) {
     DocView v;
     int rc = doc_view(e, doc, v);
@@ -1549,8 +1561,10 @@ struct DocBuild {
             *out = it->second;
             return MTE_OK;
         }
-        if (names.size() >= MTE_MAX_CLIENTS) return fail(MTE_E_UNSUPPORTED, "more than 64 clients in a document");
-        *out = (uint32_t)names.size();
+        // short ids >= MTE_MAX_CLIENTS are recorded (the op record holds 8 bits: later ones share 255);
+        // the engine reports such a document MTE_DOC_UNSUPPORTED at its first op from such a client,
+        // before any shared id could matter, and the rest of the batch replays normally
+        *out = (uint32_t)std::min<size_t>(names.size(), 255);
         names.push_back(name);
         ids[name] = *out;
         return MTE_OK;
@@ -1813,6 +1827,40 @@ static int load_chunk(DocBuild& db, const json::Value& tree, const std::u16strin
 // SnapshotV1 never emits it: universal segments carry no merge info (snapshotV1.ts:219-223).
 static const char* const kNonCollabName = "original";
 
+// One summary segment spec -> a LOAD_SEG-shaped record (SnapshotLoader.specToSegment,
+// snapshotLoader.ts:79-111): merge info gives client / seq / removedSeq / removedClient; a bare spec,
+// or merge info without client and seq, is NonCollab at the universal seq (*batchable: loadBody's
+// flushBatch test, :193-195).
+static int summary_seg(mte_builder* b, DocBuild& db, const json::Value& sp, mte_op& o, bool* info, bool* batchable) {
+    const json::Value* js = sp.kind == json::Value::Object ? sp.get(u"json") : nullptr;  // hasMergeInfo
+    if (int rc = load_spec(b, db, js ? *js : sp, o)) return rc;
+    std::string client = kNonCollabName;
+    bool hasClient = false, hasSeq = false;
+    if (js) {
+        const json::Value* c = sp.get(u"client");
+        if (c && c->kind == json::Value::String) {
+            client = json::to_utf8(c->str.data(), c->str.size());
+            hasClient = true;
+        }
+        hasSeq = num_field(sp, u"seq", &o.seq) != 0;
+    }
+    uint32_t cid;
+    if (int rc = db.short_id(client, &cid)) return rc;
+    o.client = (uint8_t)cid;
+    if (js && num_field(sp, u"removedSeq", &o.ref_seq)) {
+        o.flags |= MTE_F_LOAD_REMOVED;
+        const json::Value* rc = sp.get(u"removedClient");
+        std::string rn = rc && rc->kind == json::Value::String ? json::to_utf8(rc->str.data(), rc->str.size())
+                                                               : kNonCollabName;
+        uint32_t rid;
+        if (int e = db.short_id(rn, &rid)) return e;
+        o.pos1 = (int32_t)rid;
+    }
+    *info = js != nullptr;
+    *batchable = !hasClient && (!hasSeq || o.seq == 0);
+    return MTE_OK;
+}
+
 static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db) {
     if (!db.collab) return db.fail(MTE_E_ARG, "a summary is loaded by a collaborating client (observer name)");
     const json::Value* t = &summary;
@@ -1829,37 +1877,22 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
         for (const json::Value& sp : hs->items) {
             mte_op o{};
             o.type = MTE_OP_LOAD_SEG;
-            const json::Value* js = sp.kind == json::Value::Object ? sp.get(u"json") : nullptr;  // hasMergeInfo
-            if (int rc = load_spec(b, db, js ? *js : sp, o)) return rc;
-            std::string client = kNonCollabName;
-            if (js) {
-                mergeInfo = true;
-                const json::Value* c = sp.get(u"client");
-                if (c && c->kind == json::Value::String) client = json::to_utf8(c->str.data(), c->str.size());
-                num_field(sp, u"seq", &o.seq);
-            }
-            uint32_t cid;
-            if (int rc = db.short_id(client, &cid)) return rc;
-            o.client = (uint8_t)cid;
-            if (js && num_field(sp, u"removedSeq", &o.ref_seq)) {
-                o.flags |= MTE_F_LOAD_REMOVED;
-                const json::Value* rc = sp.get(u"removedClient");
-                std::string rn = rc && rc->kind == json::Value::String ? json::to_utf8(rc->str.data(), rc->str.size())
-                                                                       : kNonCollabName;
-                uint32_t rid;
-                if (int e = db.short_id(rn, &rid)) return e;
-                o.pos1 = (int32_t)rid;
-            }
+            bool info, batchable;
+            if (int rc = summary_seg(b, db, sp, o, &info, &batchable)) return rc;
+            mergeInfo |= info;
             db.ops.push_back(o);
         }
     }
     const size_t nHeader = db.ops.size() - first;
-    // loadBody (:150-216): later chunks appended at root.cachedLength, refSeq 0, NonCollab, seq 0
+    // loadBody (:150-216): nothing when the header holds every segment (:159-161; the shipAsserts on
+    // the lengths only log, :152-157, :176-182); otherwise every later chunk's segments in order
     const json::Value* ocm = md->get(u"orderedChunkMetadata");
-    if (ocm && ocm->kind == json::Value::Array && ocm->items.size() > 1) {
-        if (mergeInfo) return db.fail(MTE_E_UNSUPPORTED, "body chunks after a header with merge info");
-        uint32_t nc;
-        if (int rc = db.short_id(kNonCollabName, &nc)) return rc;
+    int32_t segCount = -1, totalSegs = -2;
+    num_field(header, u"segmentCount", &segCount);
+    num_field(*md, u"totalSegmentCount", &totalSegs);
+    std::vector<mte_op> body;
+    std::vector<uint8_t> bodyBatchable;
+    if (segCount != totalSegs && ocm && ocm->kind == json::Value::Array) {
         for (size_t i = 1; i < ocm->items.size(); i++) {
             const json::Value* id = ocm->items[i].kind == json::Value::Object ? ocm->items[i].get(u"id") : nullptr;
             if (!id || id->kind != json::Value::String) return db.fail(MTE_E_PARSE, "chunk id");
@@ -1868,16 +1901,25 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
             const json::Value* cs = ch.get(u"segments");
             if (!cs || cs->kind != json::Value::Array) continue;
             for (const json::Value& sp : cs->items) {
-                if (sp.kind == json::Value::Object && sp.get(u"json"))  // flushBatch never clears (:196-199)
-                    return db.fail(MTE_E_UNSUPPORTED, "merge-info segment in a body chunk");
                 mte_op o{};
-                o.type = MTE_OP_LOAD_SEG;
-                o.flags = MTE_F_LOAD_BODY;
-                if (int rc = load_spec(b, db, sp, o)) return rc;
-                if (o.b == 0) continue;  // blockInsert skips empty segments (mergeTree.ts:2196)
-                o.client = (uint8_t)nc;
-                db.ops.push_back(o);
+                bool info, batchable;
+                if (int rc = summary_seg(b, db, sp, o, &info, &batchable)) return rc;
+                mergeInfo |= info;
+                body.push_back(o);
+                bodyBatchable.push_back(batchable ? 1 : 0);
             }
+        }
+    }
+    // Without merge info every body segment is NonCollab at seq 0 and loadBody is ONE append at the
+    // document end: LOAD_SEG records whose tree shape the builder computes below. With merge info,
+    // the appends go through the insert walk on the device (LOAD_APPEND after LOAD_END), in the
+    // order loadBody issues them.
+    if (!mergeInfo) {
+        for (mte_op o : body) {
+            if (o.b == 0) continue;  // blockInsert skips empty segments (mergeTree.ts:2196)
+            o.type = MTE_OP_LOAD_SEG;
+            o.flags |= MTE_F_LOAD_BODY;
+            db.ops.push_back(o);
         }
     }
     // The loaded tree's shape (child counts per level, document order): reloadFromSegments packs the
@@ -1926,8 +1968,48 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
     end.msn = end.seq;
     num_field(*md, u"minSequenceNumber", &end.msn);
     db.ops.push_back(end);
+    if (mergeInfo && !body.empty()) {
+        // loadBody's appends (:184-213): a batchable segment joins `batch`; any other flushes the batch
+        // (append at root.cachedLength, NonCollab, seq 0) and is appended alone with its own client and
+        // seq. flushBatch never clears `batch` (:196-199): each later flush appends every earlier
+        // batched segment object again (MTE_F_APPEND_REPEAT) before the new ones.
+        std::vector<size_t> batch;
+        std::vector<uint8_t> linked(body.size(), 0);
+        auto emit = [&](size_t i, bool firstOfCall, uint32_t client, int32_t seq) {
+            if (body[i].b == 0) return;  // blockInsert skips empty segments: no walk, no position
+            mte_op o = body[i];
+            o.type = MTE_OP_LOAD_APPEND;
+            o.client = (uint8_t)client;
+            o.seq = seq;
+            o.flags = (uint16_t)(o.flags & (MTE_F_LOAD_MARKER | MTE_F_LOAD_REMOVED));
+            if (firstOfCall) o.flags |= MTE_F_APPEND_FIRST;
+            if (linked[i]) o.flags |= MTE_F_APPEND_REPEAT;
+            linked[i] = 1;
+            db.ops.push_back(o);
+        };
+        uint32_t nc;
+        if (int rc = db.short_id(kNonCollabName, &nc)) return rc;
+        auto flush = [&]() {
+            bool firstOfCall = true;
+            for (size_t i : batch) {
+                const size_t before = db.ops.size();
+                emit(i, firstOfCall, nc, 0);
+                firstOfCall &= db.ops.size() == before;
+            }
+        };
+        for (size_t i = 0; i < body.size(); i++) {
+            if (bodyBatchable[i]) {
+                batch.push_back(i);
+            } else {
+                flush();
+                emit(i, true, body[i].client, body[i].seq);
+            }
+        }
+        flush();
+    }
     // loadBodyAndCatchupOps (snapshotLoader.ts:55-77): one blob beyond the chunks holds catch-up
-    // messages (legacy summaries), applied after the load like any sequenced message
+    // messages (legacy summaries), applied after the load like any sequenced message; any other blob
+    // count is an error
     const json::Value* es = t->get(u"entries");
     size_t nChunks = ocm && ocm->kind == json::Value::Array ? ocm->items.size() : 1, nBlobs = 0;
     const json::Value* extra = nullptr;
@@ -1956,6 +2038,8 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
             return db.fail(MTE_E_PARSE, ex.what());
         }
         if (int rc = add_messages(b, msgs, db)) return rc;
+    } else if (nBlobs != nChunks) {
+        return db.fail(MTE_E_PARSE, "Unexpected blobs in snapshot");
     }
     return MTE_OK;
 }

@@ -18,7 +18,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", os.environ.get("MTE_LIB", ""), "libmte.so")
 PROF_NAMES = ["apply", "resolve", "insert_slot", "range", "zamboni", "scour", "heap", "find_seg", "map", "pack",
               "fetch", "lru", "text", "alloc", "ops", "total",
-              "n_resolve", "n_dirty", "n_scour", "n_scour_changed", "n_pack", "n_pop", "n_push", "n_split_blk"]
+              "n_resolve", "n_dirty", "n_scour", "n_scour_changed", "n_pack", "n_pop", "n_push", "n_split_blk",
+              "op_ins", "op_rem", "edit", "split", "zam_edit", "zam_msn", "res_blocks", "res_slot", "blen_dirty",
+              "scour_chain", "scour_write", "loop", "n_ins", "n_rem"]
+PROF_SLOTS = 40
 
 MTE_OP_INSERT, MTE_OP_REMOVE, MTE_OP_ANNOTATE, MTE_OP_INSERT_MARKER, MTE_OP_NOOP = 0, 1, 2, 3, 4
 MTE_F_END_OF_MSG, MTE_F_REWRITE = 1, 2
@@ -92,7 +95,7 @@ SUMMARY_DTYPE = np.dtype([("checksum", "<u8"), ("ops", "<u4"), ("length", "<u4")
 
 # Every symbol declared in include/mte.h (checked by tests/test_abi.py).
 EXPORTS = ["mte_abi_version", "mte_build_info", "mte_create", "mte_destroy", "mte_last_error", "mte_load",
-           "mte_replay", "mte_generate", "mte_generate_ids", "mte_export_batch", "mte_doc_status", "mte_text", "mte_segments",
+           "mte_replay", "mte_generate", "mte_generate_ids", "mte_export_batch", "mte_doc_status", "mte_text", "mte_length", "mte_segments",
            "mte_snapshot_v1", "mte_snapshot_shared_string", "mte_summaries", "mte_rccl_unique_id",
            "mte_rccl_comm_create", "mte_rccl_comm_destroy", "mte_gather_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
            "mte_builder_batch",
@@ -122,6 +125,7 @@ def lib():
         L.mte_export_batch.argtypes = [vp, ctypes.POINTER(mte_batch)]
         L.mte_doc_status.argtypes = [vp, u32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64)]
         L.mte_text.argtypes = [vp, u32, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+        L.mte_length.argtypes = [vp, u32, ctypes.POINTER(u64)]
         L.mte_segments_json.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.mte_snapshot_v1.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz), ctypes.POINTER(u32)]
         L.mte_snapshot_shared_string.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
@@ -288,6 +292,12 @@ class Engine:
         self._check(lib().mte_text(self._h, doc, buf, n.value, ctypes.byref(n)), "mte_text")
         return np.frombuffer(buf, dtype=np.uint16, count=n.value).tobytes().decode("utf-16-le", "surrogatepass")
 
+    def length(self, doc):
+        """Client.getLength(): the observer's visible length, markers counting 1."""
+        n = ctypes.c_uint64()
+        self._check(lib().mte_length(self._h, doc, ctypes.byref(n)), "mte_length")
+        return n.value
+
     def _str_call(self, fn, doc, *extra):
         n = ctypes.c_size_t()
         self._check(fn(self._h, doc, None, 0, ctypes.byref(n), *extra), fn.__name__)
@@ -355,9 +365,9 @@ class Engine:
 
     def profile(self):
         """Per-doc phase cycle counters (MTE_LIB=prof build), shape (n_docs, len(PROF_NAMES))."""
-        out = np.zeros((self.n_docs, len(PROF_NAMES)), dtype=np.uint64)
+        out = np.zeros((self.n_docs, PROF_SLOTS), dtype=np.uint64)
         self._check(lib().mte_profile(self._h, out.ctypes.data, out.size), "mte_profile")
-        return out
+        return out[:, : len(PROF_NAMES)]
 
     def set_option(self, key, value):
         """"force_hbm" (HBM-resident waves only), "pool_limit" (LDS leaf blocks per CU),
@@ -408,7 +418,7 @@ class MergeTreeClient:
         return self._run().text(0)
 
     def getLength(self):  # noqa: N802
-        return len(self.getText().encode("utf-16-le", "surrogatepass")) // 2
+        return self._run().length(0)
 
     def snapshot(self):
         return json.loads(self._run().snapshot_json(0))

@@ -76,6 +76,15 @@ enum {
     MTE_OP_LOAD_SEG = 5,
     MTE_OP_LOAD_END = 6,
     MTE_OP_LOAD_NODE = 7,
+    /* LOAD_APPEND: one segment of loadBody's appends (snapshotLoader.ts:166-213) for a summary with
+     *   merge info: insertSegments(pos, [seg], refSeq 0, client, seq) through the ordinary insert walk,
+     *   after LOAD_END. Fields as LOAD_SEG (a, b, props, MTE_F_LOAD_MARKER / _REMOVED: ref_seq, pos1),
+     *   client/seq = the append's. MTE_F_APPEND_FIRST: first segment of an append call, pos =
+     *   root.cachedLength; otherwise pos = the previous record's pos + its length. MTE_F_APPEND_REPEAT:
+     *   the segment object was appended before (flushBatch never clears its batch, :196-199): the
+     *   reference re-links that object if the walk finds pos -- one object in two places, which the
+     *   engine does not model (MTE_DOC_UNSUPPORTED) -- and skips it otherwise. */
+    MTE_OP_LOAD_APPEND = 8,
 };
 
 /* flags */
@@ -85,6 +94,8 @@ enum {
 #define MTE_F_LOAD_REMOVED 0x8u /* LOAD_SEG: removed (ref_seq = removedSeq, pos1 = removedClient) */
 #define MTE_F_LOAD_LEAF 0x10u   /* LOAD_SEG: first segment of a new leaf block */
 #define MTE_F_LOAD_BODY 0x20u   /* LOAD_SEG: appended from a body chunk */
+#define MTE_F_APPEND_FIRST 0x40u  /* LOAD_APPEND: first segment of an append call (pos = root.cachedLength) */
+#define MTE_F_APPEND_REPEAT 0x80u /* LOAD_APPEND: a segment object appended before (see MTE_OP_LOAD_APPEND) */
 
 typedef struct mte_op {
     int32_t seq;        /* sequenceNumber */
@@ -208,6 +219,9 @@ int mte_export_batch(mte_engine* e, mte_batch* out);
 int mte_doc_status(mte_engine* e, uint32_t doc, int32_t* code, int64_t* failing_seq);
 /* MergeTreeTextHelper.getText(currentSeq, observer) (textSegment.ts:154-172), UTF-16. */
 int mte_text(mte_engine* e, uint32_t doc, uint16_t* buf, size_t cap, size_t* len);
+/* Client.getLength() (client.ts:1057 -> MergeTree.getLength(currentSeq, observer), mergeTree.ts:1577-1584):
+ * the observer's visible length in UTF-16 units, a marker counting 1. */
+int mte_length(mte_engine* e, uint32_t doc, uint64_t* len);
 /* Final segment table (parity dump). rows may be NULL to query *n. */
 int mte_segments(mte_engine* e, uint32_t doc, mte_seg_row* rows, size_t cap, size_t* n);
 /* SnapshotV1.extractSync + emit (snapshotV1.ts:85-247): the ITree as JSON

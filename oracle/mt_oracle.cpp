@@ -26,6 +26,7 @@
 #include <sstream>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "../include/mte.h"
 #include "jsvalue.hpp"
@@ -981,24 +982,59 @@ class Doc {
         const int cur = num(md->o, u"sequenceNumber");
         const int minSeq = num(md->o, u"minSequenceNumber", &hasMin);
         mt.startCollaboration(0, hasMin ? minSeq : cur, cur);
-        // loadBody: every later chunk's segments, appended at root.cachedLength with refSeq 0
-        std::vector<Segment*> batch;
+        // loadBody (snapshotLoader.ts:150-216): nothing when the header holds every segment
+        // (:159-161; the shipAsserts on the lengths only log); otherwise every later chunk's segments
         JVP ocm = md->o.get(u"orderedChunkMetadata");
-        for (size_t i = 1; ocm && ocm->t == JV::Arr && i < ocm->a.size(); i++) {
-            JVP id = ocm->a[i]->t == JV::Obj ? ocm->a[i]->o.get(u"id") : nullptr;
-            if (!id || id->t != JV::Str) throw EngineError(MTE_DOC_UNSUPPORTED, "chunk id");
-            JVP ch = chunkAt(*t, id->s);
-            JVP cs = ch->o.get(u"segments");
-            if (!cs || cs->t != JV::Arr) continue;
-            for (auto& sp : cs->a) {
-                Segment* s = loadSpec(*sp);
-                // a merge-info body segment would hit flushBatch's never-cleared batch (:196-199)
-                if (!(s->clientId == NonCollabClient && s->seq == UniversalSequenceNumber))
-                    throw EngineError(MTE_DOC_UNSUPPORTED, "merge-info segment in a body chunk");
-                batch.push_back(s);
+        std::vector<Segment*> bodySegs;
+        bool hasCount = false, hasTotal = false;
+        const int segCount = num(header->o, u"segmentCount", &hasCount);
+        const int totalSegs = num(md->o, u"totalSegmentCount", &hasTotal);
+        if (!(hasCount && hasTotal && segCount == totalSegs)) {
+            for (size_t i = 1; ocm && ocm->t == JV::Arr && i < ocm->a.size(); i++) {
+                JVP id = ocm->a[i]->t == JV::Obj ? ocm->a[i]->o.get(u"id") : nullptr;
+                if (!id || id->t != JV::Str) throw EngineError(MTE_DOC_UNSUPPORTED, "chunk id");
+                JVP ch = chunkAt(*t, id->s);
+                JVP cs = ch->o.get(u"segments");
+                if (!cs || cs->t != JV::Arr) continue;
+                for (auto& sp : cs->a) bodySegs.push_back(loadSpec(*sp));
             }
         }
-        if (!batch.empty()) mt.insertSegments(mt.localLength(mt.root), batch, 0, NonCollabClient, 0);
+        // append(segments, cli, seq) = insertSegments(root.cachedLength, segments, refSeq 0, cli, seq):
+        // blockInsert walks each segment to insertPos and advances insertPos by its length. A segment
+        // object already in the tree (flushBatch never clears `batch`, :196-199) keeps its parent:
+        // when the walk fails it is skipped without error; when the walk finds pos the reference links
+        // the same object a second time -- a tree the engine does not model, so both report it as
+        // unsupported.
+        std::unordered_set<Segment*> linked;
+        auto append = [&](const std::vector<Segment*>& v, int cli, int seq) {
+            int insertPos = mt.localLength(mt.root);
+            for (Segment* sg : v) {
+                if (sg->len <= 0) continue;
+                if (linked.count(sg)) {
+                    if (mt.getLength(UniversalSequenceNumber, cli) >= insertPos)
+                        throw EngineError(MTE_DOC_UNSUPPORTED, "loadBody re-links a segment object");
+                    insertPos += sg->len;
+                    continue;
+                }
+                std::vector<Segment*> one{sg};
+                mt.insertSegments(insertPos, one, UniversalSequenceNumber, cli, seq);
+                linked.insert(sg);
+                insertPos += sg->len;
+            }
+        };
+        std::vector<Segment*> batch;
+        auto flushBatch = [&]() {
+            if (!batch.empty()) append(batch, NonCollabClient, UniversalSequenceNumber);
+        };
+        for (Segment* sg : bodySegs) {
+            if (sg->clientId == NonCollabClient && sg->seq == UniversalSequenceNumber) {
+                batch.push_back(sg);
+            } else {
+                flushBatch();
+                append({sg}, sg->clientId, sg->seq);
+            }
+        }
+        flushBatch();
         // loadBodyAndCatchupOps (snapshotLoader.ts:55-77): a blob beyond the chunks holds catch-up
         // messages, applied after the load (sequence.ts:499-527, processMergeTreeMsg -> applyMsg)
         JVP es = t->t == JV::Obj ? t->o.get(u"entries") : nullptr;
@@ -1015,6 +1051,7 @@ class Doc {
             }
             if (!isChunk) extra = e;
         }
+        if (nBlobs != nChunks + 1 && nBlobs != nChunks) throw EngineError(MTE_DOC_UNSUPPORTED, "Unexpected blobs in snapshot");
         if (nBlobs == nChunks + 1 && extra) {
             JVP v = extra->o.get(u"value");
             JVP c = v ? v->o.get(u"contents") : nullptr;
@@ -1072,6 +1109,7 @@ class Doc {
         std::vector<Node*> loadSegs;
         std::vector<Segment*> bodySegs;
         int bodyClient = NonCollabClient;
+        int appendPos = 0;
         for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1] && !status; i++) {
             const mte_op& op = b->ops[i];
             try {
@@ -1089,7 +1127,20 @@ class Doc {
                         bodySegs.clear();
                         continue;
                     }
-                    if (op.type != MTE_OP_LOAD_SEG) throw EngineError(MTE_DOC_UNSUPPORTED, "unknown record");
+                    if (op.type == MTE_OP_LOAD_APPEND) {  // loadBody's appends (loadSnapshot above)
+                        const int len = (op.flags & MTE_F_LOAD_MARKER) ? 1 : (int)op.b;
+                        if (op.flags & MTE_F_APPEND_FIRST) appendPos = mt.localLength(mt.root);
+                        const int pos = appendPos;
+                        appendPos += len;
+                        if (len == 0) continue;
+                        if (op.flags & MTE_F_APPEND_REPEAT) {
+                            if (mt.getLength(UniversalSequenceNumber, op.client) >= pos)
+                                throw EngineError(MTE_DOC_UNSUPPORTED, "loadBody re-links a segment object");
+                            continue;
+                        }
+                    } else if (op.type != MTE_OP_LOAD_SEG) {
+                        throw EngineError(MTE_DOC_UNSUPPORTED, "unknown record");
+                    }
                     Segment* s = mt.newSegment();
                     if (op.flags & MTE_F_LOAD_MARKER) {
                         s->marker = true;
@@ -1103,6 +1154,19 @@ class Doc {
                     if (op.flags & MTE_F_LOAD_BODY) {
                         bodySegs.push_back(s);
                         bodyClient = op.client;
+                        continue;
+                    }
+                    if (op.type == MTE_OP_LOAD_APPEND) {
+                        if (op.flags & MTE_F_LOAD_REMOVED) {
+                            if (op.pos1 < 0 || (size_t)op.pos1 >= names.size() ||
+                                getOrAddShortClientId(names[op.pos1]) != op.pos1)
+                                throw EngineError(MTE_DOC_UNSUPPORTED, "removed client id");
+                            s->removed = true;
+                            s->removedSeq = op.ref_seq;
+                            s->removedClientId = op.pos1;
+                        }
+                        std::vector<Segment*> one{s};
+                        mt.insertSegments(appendPos - s->len, one, UniversalSequenceNumber, op.client, op.seq);
                         continue;
                     }
                     s->seq = op.seq;

@@ -16,17 +16,25 @@ export declare class BatchedMergeEngine {
     load(docs: DocLog[]): void;
     generate(kind: 2 | 3 | 5, nDocs: number, nOps: number, nClients?: number, seed?: number): void;
     replay(): ReplayStats;
+    /** mte_replay on a worker thread (N-API async work); other calls on the engine throw meanwhile. */
+    replayAsync(): Promise<ReplayStats>;
     docStatus(doc: number): [number, number];
     getText(doc: number): string;
+    /** Client.getLength: the observer's visible length, markers counting 1. */
+    getLength(doc: number): number;
     snapshotV1(doc: number): ITree;
     summaries(): DocSummary[];
 }
 
-/** Client-shaped facade (merge-tree client.ts:42) for one document. */
+/** Client-shaped facade (merge-tree client.ts:42) for one document. Batch semantics: messages are
+ *  staged and replayed on the GPU when an output is next read (see index.js). */
 export declare class MergeTreeClient {
     constructor(observer?: string, options?: { device?: number; chunkSize?: number });
     load(summary: ITree | string): void;
     applyMsg(msg: ISequencedDocumentMessage): void;
+    applyMsgs(msgs: ISequencedDocumentMessage[]): void;
+    /** Replay the staged messages off the event loop. */
+    flush(): Promise<void>;
     getText(): string;
     getLength(): number;
     snapshot(): ITree;

@@ -39,9 +39,22 @@ class BatchedMergeEngine {
         addon.generate(this._engine, kind, nDocs, nOps, nClients, seed);
         this._docs = nDocs;
     }
-    replay() { return addon.replay(this._engine); }
-    docStatus(doc) { return addon.docStatus(this._engine, doc); }
-    getText(doc) { return addon.getText(this._engine, doc); }
+    replay() {
+        this._idle();
+        return addon.replay(this._engine);
+    }
+    /** mte_replay on a worker thread (N-API async work): the event loop keeps running. While it is
+     *  pending, every other call on this engine throws (the engine is not re-entrant). */
+    replayAsync() {
+        this._idle();
+        this._busy = true;
+        return addon.replayAsync(this._engine).finally(() => { this._busy = false; });
+    }
+    _idle() { if (this._busy) throw new Error("BatchedMergeEngine: a replayAsync() is still running"); }
+    /** Client.getLength() of a document: the observer's visible length, markers counting 1. */
+    getLength(doc) { this._idle(); return addon.getLength(this._engine, doc); }
+    docStatus(doc) { this._idle(); return addon.docStatus(this._engine, doc); }
+    getText(doc) { this._idle(); return addon.getText(this._engine, doc); }
     /** The ITree SnapshotV1.emit(serializer) returns: { entries: [...], id: null } */
     snapshotV1(doc) { return JSON.parse(addon.snapshotV1(this._engine, doc)); }
     /** 32-byte records {checksum u64, ops, length, segments, snapshotBytes, status, docId} */
@@ -60,7 +73,15 @@ class BatchedMergeEngine {
     }
 }
 
-/** Client-shaped facade for one document (client.ts:42): applyMsg, getText, getLength, snapshot. */
+/**
+ * Client-shaped facade for one document (client.ts:42): applyMsg, getText, getLength, snapshot.
+ *
+ * Batch semantics (documented contract): messages are STAGED by applyMsg/applyMsgs and replayed on
+ * the GPU, from the summary (or empty) state, the next time an output is read; reads without new
+ * messages reuse that replay. A replay is a kernel launch over the whole log, so read after a batch
+ * of messages (a catch-up or summarization step), not after every message: reading after each of n
+ * messages replays O(n^2) ops in total. Continuous per-message use belongs to the reference Client.
+ */
 class MergeTreeClient {
     constructor(observer = "__observer__", options = {}) {
         this.observer = observer;
@@ -73,20 +94,37 @@ class MergeTreeClient {
     /** Client.load / SnapshotLoader (client.ts:944-952): resume from a summary ITree before applyMsg. */
     load(summary) { this.summary = summary; this.messages = []; this._dirty = true; }
     applyMsg(msg) { this.messages.push(msg); this._dirty = true; }
+    /** Stage a batch of sequenced messages at once (one replay serves them all). */
+    applyMsgs(msgs) { for (const m of msgs) this.messages.push(m); this._dirty = true; }
+    _check() {
+        const [code, seq] = this._engine.docStatus(0);
+        if (code === DocStatus.InsertFailed) throw new Error(`MergeTree insert failed at seq ${seq}`);
+        if (code !== DocStatus.Ok) throw new Error(`replay failed (status ${code}) at seq ${seq}`);
+        this._dirty = false;
+    }
+    _stage() {
+        if (!this._engine) this._engine = new BatchedMergeEngine(this.options);
+        this._engine.load([{ observer: this.observer, messages: this.messages, summary: this.summary }]);
+    }
     _run() {
         if (this._dirty) {
-            if (!this._engine) this._engine = new BatchedMergeEngine(this.options);
-            this._engine.load([{ observer: this.observer, messages: this.messages, summary: this.summary }]);
+            this._stage();
             this._engine.replay();
-            const [code, seq] = this._engine.docStatus(0);
-            if (code === DocStatus.InsertFailed) throw new Error(`MergeTree insert failed at seq ${seq}`);
-            if (code !== DocStatus.Ok) throw new Error(`replay failed (status ${code}) at seq ${seq}`);
-            this._dirty = false;
+            this._check();
         }
         return this._engine;
     }
+    /** Replay the staged messages off the event loop; resolves when outputs can be read. */
+    async flush() {
+        if (this._dirty) {
+            this._stage();
+            await this._engine.replayAsync();
+            this._check();
+        }
+    }
     getText() { return this._run().getText(0); }
-    getLength() { return this.getText().length; }
+    /** Client.getLength (client.ts:1057): markers count 1, unlike getText().length. */
+    getLength() { return this._run().getLength(0); }
     snapshot() { return this._run().snapshotV1(0); }
 }
 

@@ -241,6 +241,86 @@ static napi_value js_replay(napi_env env, napi_callback_info info) {
     return o;
 }
 
+/* replayAsync(engine): Promise<{docs, ops, messages, failedDocs, kernelMs}> — mte_replay on a libuv
+ * worker thread (napi_create_async_work), so a long replay does not block the event loop. The engine
+ * is referenced until the work completes; the JS facade keeps calls on one engine from overlapping
+ * (mte.h: engine calls are not re-entrant). */
+typedef struct {
+    napi_async_work work;
+    napi_deferred deferred;
+    napi_ref engine_ref;
+    mte_engine* e;
+    mte_stats st;
+    int rc;
+    char err[512];
+} ReplayJob;
+
+static napi_value stats_object(napi_env env, const mte_stats* st) {
+    napi_value o;
+    if (napi_create_object(env, &o) != napi_ok) return NULL;
+    napi_set_named_property(env, o, "docs", make_f64(env, (double)st->docs));
+    napi_set_named_property(env, o, "ops", make_f64(env, (double)st->ops));
+    napi_set_named_property(env, o, "messages", make_f64(env, (double)st->messages));
+    napi_set_named_property(env, o, "failedDocs", make_f64(env, (double)st->failed_docs));
+    napi_set_named_property(env, o, "kernelMs", make_f64(env, st->kernel_ms));
+    return o;
+}
+
+static void replay_execute(napi_env env, void* data) {
+    (void)env;
+    ReplayJob* j = (ReplayJob*)data;
+    j->rc = mte_replay(j->e, &j->st);
+    if (j->rc) snprintf(j->err, sizeof j->err, "mte_replay failed (%d): %s", j->rc, mte_last_error(j->e));
+}
+
+static void replay_complete(napi_env env, napi_status status, void* data) {
+    ReplayJob* j = (ReplayJob*)data;
+    if (status != napi_ok && !j->rc) {
+        j->rc = MTE_E_STATE;
+        snprintf(j->err, sizeof j->err, "replayAsync: work cancelled");
+    }
+    if (j->rc) {
+        napi_value msg, err;
+        napi_create_string_utf8(env, j->err, NAPI_AUTO_LENGTH, &msg);
+        napi_create_error(env, NULL, msg, &err);
+        napi_reject_deferred(env, j->deferred, err);
+    } else {
+        napi_resolve_deferred(env, j->deferred, stats_object(env, &j->st));
+    }
+    napi_delete_reference(env, j->engine_ref);
+    napi_delete_async_work(env, j->work);
+    free(j);
+}
+
+static napi_value js_replay_async(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    if (!e) return throw_mte(env, "replayAsync", MTE_E_ARG, NULL);
+    ReplayJob* j = (ReplayJob*)calloc(1, sizeof *j);
+    j->e = e;
+    napi_value promise, name;
+    CHECK(env, napi_create_promise(env, &j->deferred, &promise));
+    CHECK(env, napi_create_reference(env, argv[0], 1, &j->engine_ref));
+    CHECK(env, napi_create_string_utf8(env, "mte_replay", NAPI_AUTO_LENGTH, &name));
+    CHECK(env, napi_create_async_work(env, NULL, name, replay_execute, replay_complete, j, &j->work));
+    CHECK(env, napi_queue_async_work(env, j->work));
+    return promise;
+}
+
+/* getLength(engine, doc): number — Client.getLength (markers count 1, mergeTree.ts:1577-1584) */
+static napi_value js_length(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    uint32_t d;
+    napi_get_value_uint32(env, argv[1], &d);
+    uint64_t n = 0;
+    int rc = mte_length(e, d, &n);
+    if (rc) return throw_mte(env, "mte_length", rc, mte_last_error(e));
+    return make_f64(env, (double)n);
+}
+
 /* docStatus(engine, doc): [code, failingSeq] */
 static napi_value js_doc_status(napi_env env, napi_callback_info info) {
     napi_value argv[2];
@@ -326,6 +406,8 @@ static napi_value init(napi_env env, napi_value exports) {
         {"load", 0, js_load, 0, 0, 0, napi_default, 0},
         {"generate", 0, js_generate, 0, 0, 0, napi_default, 0},
         {"replay", 0, js_replay, 0, 0, 0, napi_default, 0},
+        {"replayAsync", 0, js_replay_async, 0, 0, 0, napi_default, 0},
+        {"getLength", 0, js_length, 0, 0, 0, napi_default, 0},
         {"docStatus", 0, js_doc_status, 0, 0, 0, napi_default, 0},
         {"getText", 0, js_text, 0, 0, 0, napi_default, 0},
         {"snapshotV1", 0, js_snapshot, 0, 0, 0, napi_default, 0},

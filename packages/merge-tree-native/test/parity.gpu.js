@@ -23,9 +23,37 @@ const len0 = c2.getLength();
 c2.applyMsg(msg("w", 1, 0, { pos1: 3, seg: "XYZ", type: 0 }));
 assert.strictEqual(c2.getLength(), len0 + 3);
 assert.strictEqual(c2.getText().slice(3, 6), "XYZ");
+// Client.getLength counts a marker as 1 (mergeTree.ts:1577-1584): getText().length + markers
+const mk = JSON.parse(require("fs").readFileSync(__dirname + "/../../../tests/golden/v1/withMarkers.json", "utf8"));
+const c3 = new MergeTreeClient("catchup");
+c3.load(mk);
+let markers = 0;
+for (const ent of mk.entries[1].value.entries) {
+    for (const sg of JSON.parse(ent.value.contents).segments) if (sg.marker || (sg.json && sg.json.marker)) markers++;
+}
+assert.ok(markers > 0);
+assert.strictEqual(c3.getLength(), c3.getText().length + markers);
 const e = new BatchedMergeEngine();
 e.generate(2, 8, 500, 8, 3);
 const st = e.replay();
 assert.strictEqual(st.failedDocs, 0);
 const sums = e.summaries();
-console.log(JSON.stringify({ ops: st.ops, checksums: sums.map((s) => s.checksum.toString()) }));
+(async () => {
+    // replayAsync: the same replay on a worker thread while the event loop keeps turning
+    const big = new BatchedMergeEngine();
+    big.generate(2, 2048, 10000, 8, 9);
+    const syncSums = (big.replay(), big.summaries().map((s) => s.checksum.toString()));
+    let ticks = 0;
+    const timer = setInterval(() => { ticks++; }, 0);
+    const pending = big.replayAsync();
+    assert.throws(() => big.getText(0), /still running/);
+    const st2 = await pending;
+    clearInterval(timer);
+    assert.strictEqual(st2.failedDocs, 0);
+    assert.deepStrictEqual(big.summaries().map((s) => s.checksum.toString()), syncSums);
+    const c4 = new MergeTreeClient();
+    c4.applyMsgs(hello);
+    await c4.flush();
+    assert.strictEqual(c4.getText(), "hello world");
+    console.log(JSON.stringify({ ops: st.ops, checksums: sums.map((s) => s.checksum.toString()), async_ticks: ticks }));
+})().catch((err) => { console.error(err); process.exit(1); });

@@ -271,3 +271,83 @@ def test_gpu_legacy_summaries_reemit_v1(engine):
     for d, (kind, name) in enumerate(LEGACY):
         compare_doc(engine, batch, d, observer=OBS)
         assert json.loads(engine.snapshot_shared_string(d)) == json.loads(fixture(name))
+
+
+def collab_body_summaries():
+    """(summary, suffix) pairs whose summaries have BODY chunks holding merge-info segments: cut from
+    multi-writer logs and emitted with small chunk sizes, so loadBody's batching (and its never-cleared
+    flushBatch batch, snapshotLoader.ts:184-213) decides what the loaded tree holds."""
+    out = []
+    for seed in (3, 4, 5):
+        log = c1_farm_log(seed=seed, total_ops=700)
+        for k in (150, 333, 520):
+            o = OracleDoc("0")
+            o.apply_json(dumps(log[:k]))
+            for chunk in (12, 40, 97):
+                out.append((o.snapshot_json(chunk), log[k:]))
+    for lag in (2, 6):
+        s = TestString("fakeId")
+        for i in range(260):
+            if i % 5 == 4 and len(s.text) > 10:
+                s.remove_range(i % 7, i % 7 + 4, False)
+            else:
+                s.insert((i * 13) % (len(s.text) + 1), f"t{i}", False)
+            s.msgs[-1]["minimumSequenceNumber"] = max(0, s.seq - lag)
+        for k in (90, 200):
+            o = OracleDoc("0")
+            o.apply_json(dumps(s.msgs[:k]))
+            for chunk in (16, 60):
+                out.append((o.snapshot_json(chunk), s.msgs[k:]))
+    return out
+
+
+def _body_has_merge_info(summary):
+    tree = json.loads(summary)
+    for e in tree["entries"][1:]:
+        for sg in json.loads(e["value"]["contents"])["segments"]:
+            if isinstance(sg, dict) and "json" in sg:
+                return True
+    return False
+
+
+def test_collab_body_summaries_records_match_oracle_loader():
+    """The builder's LOAD_APPEND records, replayed by the oracle, give the same status, segment table
+    and SnapshotV1 as the oracle's own restatement of SnapshotLoader.loadBody on the JSON; successful
+    loads then catch up on the suffix identically."""
+    cases = collab_body_summaries()
+    b = mte.Builder()
+    for summ, suffix in cases:
+        b.add_doc_from_summary(summ, suffix, observer=OBS)
+    batch = b.batch()
+    outcomes = {}
+    for d, (summ, suffix) in enumerate(cases):
+        rec = OracleDoc(OBS)
+        rec.apply_batch(ctypes.addressof(batch), d)
+        ref = OracleDoc(OBS)
+        ref.load_summary(summ)
+        if ref.status()[0] == 0 and suffix:
+            ref.apply_json(dumps(suffix))
+        assert rec.status()[0] == ref.status()[0], (d, rec.status(), ref.status())
+        if ref.status()[0] == 0:
+            assert rec.segments_json() == ref.segments_json(), d
+            assert rec.snapshot_json() == ref.snapshot_json(), d
+        key = (ref.status()[0], _body_has_merge_info(summ))
+        outcomes[key] = outcomes.get(key, 0) + 1
+    # merge-info bodies that load and catch up, and the reference's two failure modes, all occur
+    assert outcomes.get((0, True), 0) >= 5, outcomes
+    assert sum(v for (st, mi), v in outcomes.items() if st != 0) >= 1, outcomes
+
+
+@pytest.mark.gpu
+def test_gpu_collab_body_summaries_match_oracle(engine):
+    from tests.gpu_helpers import compare_doc
+
+    cases = collab_body_summaries()
+    b = mte.Builder()
+    for summ, suffix in cases:
+        b.add_doc_from_summary(summ, suffix, observer=OBS)
+    batch = b.batch()
+    engine.load(batch)
+    engine.replay()
+    for d in range(len(cases)):
+        compare_doc(engine, batch, d, observer=OBS)

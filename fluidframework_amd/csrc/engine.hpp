@@ -2051,15 +2051,23 @@ struct Engine {
             fail(MTE_DOC_UNSUPPORTED, op.seq);
             return false;
         }
-        i32 pos;
-        if (op.flags & MTE_F_APPEND_FIRST) pos = get_length(st.curSeq, 0u);
-        else pos = (i32)stat_get(ST_APPEND);
+        // one length scan serves both questions: root.cachedLength (the observer's view) for the first
+        // segment of a call, and for a repeated object whether the walk finds pos (pos <= the length
+        // of the (refSeq 0, client) view)
+        const bool first = (op.flags & MTE_F_APPEND_FIRST) != 0, repeat = (op.flags & MTE_F_APPEND_REPEAT) != 0;
+        i32 pos = first ? 0 : (i32)stat_get(ST_APPEND);
+        i32 viewLen = 0;
+        for (u32 q = first ? 0u : 1u; q < (repeat ? 2u : 1u); q++) {
+            const i32 n = get_length(q ? 0 : st.curSeq, q ? (u32)op.client : 0u);
+            pos = q ? pos : n;
+            viewLen = n;
+        }
         sync();
         if (L == 0) STATS()[ST_APPEND] = (u32)(pos + (i32)rec.len);
         sync();
         if (rec.len == 0) return false;
-        if (op.flags & MTE_F_APPEND_REPEAT) {
-            if (resolve(pos, 0, op.client).ok) fail(MTE_DOC_UNSUPPORTED, op.seq);
+        if (repeat) {
+            if (pos <= viewLen) fail(MTE_DOC_UNSUPPORTED, op.seq);
             return false;
         }
         if (rm) {

@@ -5,8 +5,9 @@ import json
 import os
 import sys
 
-# the replay pass: LDS workgroups and HBM-resident waves, launched together on two streams
-KERNELS = ("k_lds<false>", "k_hbmq<false>")
+# the replay pass: solo workgroups, LDS workgroups and HBM-resident waves, launched together on three
+# streams
+KERNELS = ("k_solo<false>", "k_lds<false>", "k_hbmq<false>")
 
 
 def rows(pattern):
@@ -17,27 +18,35 @@ def rows(pattern):
     return out
 
 
-def main(tag, docs=4096, ops=10000, kind=2):
+def main(tag, config="C4"):
+    sys.path.insert(0, os.getcwd())
+    import bench
+    from fluidframework_amd.shard import plan_shard
+
+    c = bench.CONFIGS[config]
+    ids, counts = plan_shard(config, 1, 0, c["docs"], c["ops"])
+    docs, ops, kind = len(ids), int(counts.sum()), c["kind"]
     base = f"gpurun_out/prof_{tag}"
     stats = rows(f"{base}/trace/**/*kernel_stats.csv")
     trace = rows(f"{base}/trace/**/*kernel_trace.csv")
-    summary = {"tag": tag, "docs": docs, "ops": ops, "kind": kind, "kernels": {}}
+    summary = {"tag": tag, "config": config, "docs": docs, "ops": ops, "kind": kind, "kernels": {}}
     for r in stats:
         summary["kernels"][r["Name"]] = {k: r[k] for k in ("Calls", "TotalDurationNs", "AverageNs", "Percentage")}
     for k in KERNELS:
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace if k in r["Kernel_Name"]]
         if durs:
             summary[f"{k}_avg_ms_trace"] = sum(durs) / len(durs) / 1e6
-    # pass time: first start to last end of each (k_lds, k_hbmq) pair, in dispatch order
-    lds = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in trace if KERNELS[0] in r["Kernel_Name"])
-    hbq = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in trace if KERNELS[1] in r["Kernel_Name"])
-    if lds and len(lds) == len(hbq):
-        passes = [max(a[1], b[1]) - min(a[0], b[0]) for a, b in zip(lds, hbq)]
+    # pass time: first start to last end of the pass's kernels, in dispatch order
+    per = [sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in trace if k in r["Kernel_Name"])
+           for k in KERNELS]
+    per = [x for x in per if x]
+    if per and all(len(x) == len(per[0]) for x in per):
+        passes = [max(x[i][1] for x in per) - min(x[i][0] for x in per) for i in range(len(per[0]))]
         summary["replay_pass_avg_ms_trace"] = sum(passes) / len(passes) / 1e6
     for cname in ("FETCH_SIZE", "WRITE_SIZE"):
         pm = rows(f"{base}/pmc_{'fetch' if cname == 'FETCH_SIZE' else 'write'}/**/*counter_collection.csv")
-        # per pass: the counters of one k_lds dispatch plus one k_hbmq dispatch (rocprofv3 serialises
-        # dispatches while it collects counters)
+        # per pass: the counters of one dispatch of each pass kernel (rocprofv3 serialises dispatches
+        # while it collects counters, so k_lds then takes every document k_solo does not)
         tot = 0.0
         for k in KERNELS:
             vals = [float(r["Counter_Value"]) for r in pm if k in r["Kernel_Name"] and r["Counter_Name"] == cname]
@@ -55,7 +64,7 @@ def main(tag, docs=4096, ops=10000, kind=2):
         with open(p) as f, open(f"profiles/{tag}_kernel_stats.csv", "w") as g:
             g.write(f.read())
     if "hbm_bytes_per_launch" in summary:
-        with open("profiles/pmc_replay.json", "w") as f:
+        with open(f"profiles/pmc_replay_{config}.json", "w") as f:
             json.dump({"docs": docs, "ops": ops, "kind": kind, "source": f"profiles/{tag}_summary.json",
                        "hbm_bytes_per_launch": summary["hbm_bytes_per_launch"],
                        "note": "raw (FETCH_SIZE+WRITE_SIZE)*1024; gfx950 FETCH_SIZE calibration (x2) applies only to "
@@ -64,4 +73,4 @@ def main(tag, docs=4096, ops=10000, kind=2):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r02", sys.argv[2] if len(sys.argv) > 2 else "C4")

@@ -341,3 +341,46 @@ def test_one_document_view_of_a_batch(engine):
         assert int(s["status"][0]) == sts[0] == 0 and int(s["checksum"][0]) == cks[0]
     finally:
         e2.close()
+
+
+def test_reference_spec_pins_on_gpu(engine):
+    """The restated reference spec cases (mergeTree.annotate.spec.ts, mergeTree.insertingWalk.spec.ts,
+    properties.spec.ts; tests/test_oracle_specs.py) on the GPU: bit-exact vs the oracle and the
+    reference tests' literal expectations."""
+    from tests.test_oracle_specs import (ANNOTATE_CASES, MATCH_CASES, WALK_CASES, _ann_case, match_case_log,
+                                         walk_case_log)
+
+    logs, checks = [], []
+    for case in sorted(ANNOTATE_CASES):
+        steps, expected = ANNOTATE_CASES[case]
+        logs.append(_ann_case(steps))
+        checks.append(("props", expected))
+    for kind, where in WALK_CASES:
+        m, expected = walk_case_log(kind, where)
+        logs.append(m)
+        checks.append(("text", expected))
+    for a, b, match in MATCH_CASES:
+        logs.append(match_case_log(a, b))
+        checks.append(("live", ["xy", "z"] if match else ["x", "y", "z"]))
+    bld = mte.Builder()
+    for m in logs:
+        bld.add_doc(m)
+    batch = bld.batch()
+    engine.load(batch)
+    st = engine.replay()
+    assert st["failed_docs"] == 0
+    for d, (what, expected) in enumerate(checks):
+        compare_doc(engine, batch, d)
+        segs = json.loads(engine.segments_json(d))
+        live = [s for s in segs if "removedSeq" not in s]
+        if what == "text":
+            assert engine.text(d) == expected and engine.length(d) == len(expected)
+        elif what == "live":
+            assert [s.get("text") for s in live] == expected
+        else:
+            at = 0
+            for s in live:
+                if at <= 1 < at + s["len"]:
+                    assert s["text"] == "el" and json.loads(s["props"]) == expected
+                    break
+                at += s["len"]

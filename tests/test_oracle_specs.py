@@ -168,3 +168,163 @@ def test_c1_conflict_farm_replays_cleanly():
     a = replay(m, observer="0")
     b = replay(m, observer="0")
     assert a.text() == b.text() and a.snapshot_json() == b.snapshot_json()
+
+
+# ---------------------------------------------------------------------------------------------
+# mergeTree.annotate.spec.ts (:15-46 setup; the "collaborating" cases whose local ops end up sequenced)
+# as observer replays: "hello world!" below the MSN, a Tile marker at 3 by "remote", then the case's
+# annotates of [1, 5) in their sequenced order. Expected: the properties of the segment containing
+# position 1 ("el"), literal values from the cited assertions.
+def _annotate_base():
+    return [msg("init", 1, 0, ins(0, "hello world!"), 1),
+            msg("remote", 2, 1, ins(3, {"marker": {"refType": 1}}), 1)]
+
+
+def _ann_case(steps):
+    m = _annotate_base()
+    for i, (client, props, rewrite) in enumerate(steps):
+        c = ann(1, 5, props)
+        if rewrite:
+            c["combiningOp"] = {"name": "rewrite"}
+        m.append(msg(client, 3 + i, 2 + i, c, 1))
+    return m
+
+
+ANNOTATE_CASES = {
+    # :286-305 sequenced local
+    "sequenced_local": ([("local", {"propertySource": "local"}, False)], {"propertySource": "local"}),
+    # :307-341 sequenced local before remote
+    "sequenced_local_before_remote": ([("local", {"propertySource": "local"}, False),
+                                       ("remote", {"propertySource": "remote", "remoteProperty": 1}, False)],
+                                      {"propertySource": "remote", "remoteProperty": 1}),
+    # :343-434 three local changes, all acked in order
+    "three_local_changes": ([("local", {"propertySource": "local"}, False),
+                             ("local", {"propertySource": "local2", "secondSource": 1}, False),
+                             ("local", {"thirdSource": 1}, False)],
+                            {"propertySource": "local2", "secondSource": 1, "thirdSource": 1}),
+    # :436-483 two local changes with an interleaved remote (the second local op is sequenced last)
+    "two_local_interleaved_remote": ([("local", {"propertySource": "local"}, False),
+                                      ("remote", {"propertySource": "remote", "remoteOnly": 1,
+                                                  "secondSource": "remote"}, False),
+                                      ("local", {"secondSource": "local2"}, False)],
+                                     {"propertySource": "remote", "remoteOnly": 1, "secondSource": "local2"}),
+    # :542-579 remote before sequenced local
+    "remote_before_sequenced_local": ([("remote", {"propertySource": "remote", "remoteProperty": 1}, False),
+                                       ("local", {"propertySource": "local"}, False)],
+                                      {"propertySource": "local", "remoteProperty": 1}),
+    # :644-679 rewrite: sequenced local before remote
+    "rewrite_sequenced_local_before_remote": ([("local", {"propertySource": "local"}, True),
+                                               ("remote", {"propertySource": "remote", "remoteProperty": 1}, False)],
+                                              {"propertySource": "remote", "remoteProperty": 1}),
+    # :681-729 rewrite: two local changes with an interleaved remote
+    "rewrite_two_local_interleaved_remote": ([("local", {"propertySource": "local"}, True),
+                                              ("remote", {"propertySource": "remote", "remoteOnly": 1,
+                                                          "secondSource": "remote"}, False),
+                                              ("local", {"secondSource": "local2"}, True)],
+                                             {"secondSource": "local2"}),
+}
+
+
+def props_at(d, pos):
+    """Properties of the live segment containing visible position `pos` (getContainingSegment)."""
+    at = 0
+    for s in json.loads(d.segments_json()):
+        if "removedSeq" in s:
+            continue
+        if at <= pos < at + s["len"]:
+            return s, (json.loads(s["props"]) if s["props"] else None)
+        at += s["len"]
+    raise AssertionError("position beyond the text")
+
+
+@pytest.mark.parametrize("case", sorted(ANNOTATE_CASES))
+def test_annotate_spec_cases(case):
+    steps, expected = ANNOTATE_CASES[case]
+    d = replay(_ann_case(steps))
+    seg, props = props_at(d, 1)
+    assert seg["text"] == "el"
+    assert props == expected
+
+
+# mergeTree.insertingWalk.spec.ts:24-174 trees, :179-256 inserts of "a" at the beginning, end and
+# middle, with the expected strings. The trees are built by a sequenced writer ("w", MSN held at 0 so
+# the 7-child layer stays 7 children, as reloaded/inserted in the reference) and the insert comes from
+# another client that saw everything.
+def _walk_tree(kind):
+    m, seq, text = [], 0, ""
+
+    def add(c, who="w"):
+        nonlocal seq
+        seq += 1
+        m.append(msg(who, seq, seq - 1, c, 0))
+
+    if kind == "single_segment":
+        add(ins(0, "hello world"))
+        text = "hello world"
+        middle = round(len(text) / 2)
+    elif kind == "full_single_layer":  # MaxNodesInBlock - 1 = 7 children "0".."6"
+        for i in range(7):
+            add(ins(len(text), str(i)))
+            text += str(i)
+        middle = round(8 / 2)
+    else:  # "tree_with_removals": "0".."31", a quarter of the text removed from each end
+        for i in range(32):
+            add(ins(len(text), str(i)))
+            text += str(i)
+        r = round(len(text) / 4)
+        add(rem(0, r))
+        text = text[r:]
+        add(rem(len(text) - r, len(text)))
+        text = text[: len(text) - r]
+        middle = round(len(text) / 2)
+    return m, seq, text, middle
+
+
+WALK_CASES = [(k, w) for k in ("single_segment", "full_single_layer", "tree_with_removals")
+              for w in ("beginning", "end", "middle")]
+
+
+def walk_case_log(kind, where):
+    m, seq, text, middle = _walk_tree(kind)
+    pos = {"beginning": 0, "end": len(text), "middle": middle}[where]
+    m.append(msg("x", seq + 1, seq, ins(pos, "a"), 0))
+    return m, text[:pos] + "a" + text[pos:]
+
+
+@pytest.mark.parametrize("kind,where", WALK_CASES)
+def test_inserting_walk_spec(kind, where):
+    m, expected = walk_case_log(kind, where)
+    d = replay(m)
+    assert d.text() == expected
+    assert d.length() == len(expected)
+
+
+# properties.spec.ts:10-35 matchProperties cases, observed through zamboni and SnapshotV1 coalescing:
+# two adjacent segments with the case's property sets fall below the MSN; they merge into one
+# segment exactly when matchProperties holds (scourNode mergeTree.ts:1321-1336, snapshotV1.ts:196-202).
+MATCH_CASES = [
+    ({"a": "a"}, {"a": "a"}, True),
+    ({"a": "a"}, {"a": "b"}, False),
+    ({"a": "a", "1": 1}, {"a": "a", "1": 1}, True),
+    ({"a": "a", "1": 1}, {"a": "b", "1": 2}, False),
+    ({"a": "a"}, {"b": "a"}, False),
+    ({"a": "a"}, {"a": "a", "b": "b"}, False),
+    ({"c": {"a": "a"}}, {"c": {"a": "a"}}, True),
+    ({"c": {"a": "a"}}, {"c": {"a": "b"}}, False),
+]
+
+
+def match_case_log(a, b):
+    return [msg("w", 1, 0, ins(0, {"text": "x", "props": a}), 0),
+            msg("w", 2, 1, ins(1, {"text": "y", "props": b}), 0),
+            msg("v", 3, 2, ins(2, "z"), 2)]
+
+
+@pytest.mark.parametrize("i", range(len(MATCH_CASES)))
+def test_match_properties_spec(i):
+    a, b, match = MATCH_CASES[i]
+    d = replay(match_case_log(a, b))
+    live = [s for s in json.loads(d.segments_json()) if "removedSeq" not in s]
+    assert [s["text"] for s in live] == (["xy", "z"] if match else ["x", "y", "z"])
+    header = json.loads(json.loads(d.snapshot_json())["entries"][0]["value"]["contents"])
+    assert header["segmentCount"] == (2 if match else 3)

@@ -144,7 +144,11 @@ struct St {
     u32 adirty, gdirty;
 };
 
-template <bool LDSM, bool SOLO = false>
+// FULL = false: the instantiation for batches that use no property sets, no client id above 31 and no
+// '\n' in any payload (the host checks, mte_host.cpp batch_is_lean): property maps, the HBM half of
+// the overlap masks and TextSegment.canAppend's newline test compile out, which leaves the replay
+// loop fewer live registers. Same results on such batches (tests/test_gpu_c4.py).
+template <bool LDSM, bool SOLO = false, bool FULL = true>
 struct Engine {
     static_assert(LDSM || !SOLO, "the solo plan is LDS-resident");
     const Params& p;
@@ -429,7 +433,7 @@ struct Engine {
         const u32 rm = (meta >> 16) & 1u;  // F_REMOVED
         const u32 ins = eq1(meta & 0xffu, C) | le1((i32)q.y, R) | cz;
         u32 ovh;
-        if (C < 32) {
+        if (!FULL || C < 32) {
             ovh = (z >> C) & 1u;
         } else {  // clients 32..63: HBM half of the mask (rare)
             ovh = 0;
@@ -527,7 +531,7 @@ struct Engine {
             for (u32 s = 0; s < 8; s++) q[s] = VIS()[b * 8 + s];
 #endif
             u32 sv = 0;
-            if (C >= 32) {  // clients 32..63: the general predicate (HBM half of the overlap mask)
+            if (FULL && C >= 32) {  // clients 32..63: the general predicate (HBM half of the overlap mask)
 #pragma unroll
                 for (u32 s = 0; s < 8; s++)
                     sv += s < o.w ? vis_len(q[s], AUX()[b * 8 + s].z, b * 8 + s, R, C, cz) : 0u;
@@ -1176,6 +1180,7 @@ struct Engine {
     }
     MTE_DEV bool match_props(u32 a, u32 b) const {  // properties.ts:62-93
         if (a == b) return true;
+        if constexpr (!FULL) return false;  // a batch without properties: every map id is 0
         if (a == 0 || b == 0) return false;
         if (a >= map_cap || b >= map_cap) return false;
         const u32* ma = maps + (u64)a * MAP_WORDS;
@@ -1199,6 +1204,7 @@ struct Engine {
     // SegmentPropertiesManager.addProperties (segmentPropertiesManager.ts:35-111) on an immutable map:
     // returns a fresh map id. Executed by lane 0; result broadcast.
     MTE_DEV u32 build_map(u32 old, u32 propset, bool rewrite) {
+        if constexpr (!FULL) return 0;
         MTE_PROF(PF_MAP);
         u32 id = NONE;
         i32 err = 0;
@@ -1374,7 +1380,7 @@ struct Engine {
         if (!(mREM & ~mKEPT) && !(mSET & (mSET << 1))) return cnt;  // nothing dropped, nothing to merge
         MTE_COUNT(PN_SCOUR_CHANGED, 1);
         const u64 mTXT = wave_ballot(act && !(me.meta & F_MARKER));
-        const u64 mNL = has_nl ? wave_ballot(act && !(me.meta & F_MARKER) && ends_nl(me.toff, me.len)) : 0ull;
+        const u64 mNL = (FULL && has_nl) ? wave_ballot(act && !(me.meta & F_MARKER) && ends_nl(me.toff, me.len)) : 0ull;
         u32 nkeep = 0;
         u32 kSrc = 0, kLen = 0, kOff = 0, kCap = 0;  // lane i < nkeep: kept slot i
         Jobs jb;

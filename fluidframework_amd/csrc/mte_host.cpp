@@ -231,6 +231,9 @@ struct mte_engine {
     uint64_t slot_ops_cap = 65536;       // slots are sized for documents of at most this many ops
     uint32_t slot_blk_limit = 0;         // test knob: leaf blocks per slot (0 = from slot_ops_cap)
     // critical-path documents replayed by k_solo (a whole CU's LDS for one wave each)
+    bool lean_ok = false;                // batch_is_lean: the replay may run the FULL = false kernels
+    bool lean_opt = true;                // option "lean" (0 = always the FULL kernels)
+    bool last_lean = false;
     uint32_t solo_max = 16;              // at most this many (0 = off)
     uint64_t solo_min_ops = 20000;       // ... each at least this long
     uint32_t solo_div = 6;               // ... and at least 1/solo_div of the longest document
@@ -591,6 +594,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     const uint32_t nd = b->n_docs;
     std::vector<uint64_t> n_ops(nd), pay(nd), pi(nd), an(nd);
     std::vector<uint8_t> collab(nd), has_nl(nd, 0);
+    bool lean = true;
     for (uint32_t d = 0; d < nd; d++) {
         for (uint64_t q = b->doc_payload_offsets[d]; q < b->doc_payload_offsets[d + 1]; q++)
             if (b->payload[q] == (uint16_t)'\n') {
@@ -601,6 +605,8 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         pay[d] = b->doc_payload_offsets[d + 1] - b->doc_payload_offsets[d];
         count_doc_ops(e->hb, d, pi[d], an[d]);
         collab[d] = e->hb.client(d, 0).empty() ? 0 : 1;  // empty observer name => local, non-collab
+        lean = lean && !has_nl[d] && !pi[d] && !an[d] &&
+               e->hb.doc_client_offsets[d + 1] - e->hb.doc_client_offsets[d] <= 32;
         // a document with more than MTE_MAX_CLIENTS clients fails alone (MTE_DOC_UNSUPPORTED at its
         // first op from a client beyond the cap), never the batch
     }
@@ -615,6 +621,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     e->last_h2d_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     e->P.ops = e->d_ops.p;
     e->P.payload = e->d_payload.p;
+    e->lean_ok = lean;
     if ((rc = alloc_out_text(e))) return rc;
     return MTE_OK;
 }
@@ -636,6 +643,8 @@ static int run_kernel(mte_engine* e, bool gen) {
     if ((rc = alloc_slots(e))) return rc;  // options may have changed the wave plan
     uint32_t groups, hbm_waves, lds_active;
     const uint32_t n_solo = e->P.n_solo;
+    const bool full = gen || !(e->lean_ok && e->lean_opt);  // the generator always runs FULL
+    e->last_lean = !full;
     wave_plan(e, nd, groups, hbm_waves, &lds_active, n_solo);
     e->P.slot_hbm0 = groups * LDS_WAVES;
     e->P.lds_active = lds_active;
@@ -655,16 +664,16 @@ static int run_kernel(mte_engine* e, bool gen) {
     // they fill every CU's remaining wave slots; k_lds and k_hbmq drain one document queue
     if (n_solo) {
         HIP_TRY(e, hipStreamWaitEvent(e->stream3, e->ev0, 0));
-        HIP_TRY(e, launch_solo(e->P, gen, n_solo, e->stream3));
+        HIP_TRY(e, launch_solo(e->P, gen, full, n_solo, e->stream3));
         HIP_TRY(e, hipEventRecord(e->ev3, e->stream3));
     }
-    if (groups) HIP_TRY(e, launch_lds(e->P, gen, groups, e->stream));
+    if (groups) HIP_TRY(e, launch_lds(e->P, gen, full, groups, e->stream));
     // k_hbmq: one workgroup (wave) per document; those that find the queue drained exit at once
     if (hbm_waves && !groups) {
-        HIP_TRY(e, launch_hbmq(e->P, gen, nd, e->stream));
+        HIP_TRY(e, launch_hbmq(e->P, gen, full, nd, e->stream));
     } else if (hbm_waves) {
         HIP_TRY(e, hipStreamWaitEvent(e->stream2, e->ev0, 0));
-        HIP_TRY(e, launch_hbmq(e->P, gen, nd, e->stream2));
+        HIP_TRY(e, launch_hbmq(e->P, gen, full, nd, e->stream2));
         HIP_TRY(e, hipEventRecord(e->ev2, e->stream2));
         HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev2, 0));
     }
@@ -702,7 +711,7 @@ static int run_kernel(mte_engine* e, bool gen) {
         e->P.doc_list = e->d_list.p;
         e->P.n_list = (uint32_t)spill.size();
         HIP_TRY(e, hipEventRecord(e->ev0, e->stream));
-        HIP_TRY(e, launch_hbm(e->P, gen, (uint32_t)spill.size(), e->stream));
+        HIP_TRY(e, launch_hbm(e->P, gen, full, (uint32_t)spill.size(), e->stream));
         HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
         HIP_TRY(e, hipStreamSynchronize(e->stream));
         HIP_TRY(e, hipEventElapsedTime(&hbm_ms, e->ev0, e->ev1));
@@ -807,6 +816,8 @@ int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_o
     e->P.gen_seed = seed_base;
     e->P.gen_n_propsets = nps;
     e->gen_kind = kind;
+    // kinds 2 and 5 draw no properties and no '\n'; short ids stay below 1 + n_clients
+    e->lean_ok = kind != 3 && n_clients < 32;
     rc = run_kernel(e, true);
     if (rc) return rc;
     // client names: observer + writers in first-appearance (short id) order
@@ -1485,6 +1496,7 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "doc_id_base") e->doc_id_base = (uint64_t)std::max<int64_t>(0, value);  // next load
     else if (k == "solo_max") e->solo_max = (uint32_t)std::max<int64_t>(0, value);
     else if (k == "solo_min_ops") e->solo_min_ops = (uint64_t)std::max<int64_t>(1, value);
+    else if (k == "lean") e->lean_opt = value != 0;
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
 }
@@ -1501,6 +1513,7 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "slot_bytes") *value = (int64_t)e->P.slot_bytes;
     else if (k == "slots") *value = e->n_slots;
     else if (k == "solo") *value = e->last_solo;
+    else if (k == "lean") *value = e->last_lean;
     else return set_err(e, MTE_E_ARG, "unknown info key " + k);
     return MTE_OK;
 }

@@ -5,9 +5,9 @@
 #include "engine_types.hpp"
 
 namespace mte {
-hipError_t launch_lds(const Params& p, bool gen, u32 n_groups, hipStream_t s);
-hipError_t launch_solo(const Params& p, bool gen, u32 n_solo, hipStream_t s);
-hipError_t launch_hbmq(const Params& p, bool gen, u32 n_waves, hipStream_t s);
-hipError_t launch_hbm(const Params& p, bool gen, u32 n_docs, hipStream_t s);
+hipError_t launch_lds(const Params& p, bool gen, bool full, u32 n_groups, hipStream_t s);
+hipError_t launch_solo(const Params& p, bool gen, bool full, u32 n_solo, hipStream_t s);
+hipError_t launch_hbmq(const Params& p, bool gen, bool full, u32 n_waves, hipStream_t s);
+hipError_t launch_hbm(const Params& p, bool gen, bool full, u32 n_docs, hipStream_t s);
 hipError_t launch_wave_selftest(const u32* in, u32* out, u32 n_waves, hipStream_t s);
 }  // namespace mte

@@ -354,7 +354,7 @@ class Engine:
                                        ctypes.byref(rows), ctypes.byref(co)), "mte_run_info")
         out = {"spilled": sp.value, "continued": co.value, "lds_ms": a.value, "hbm_ms": b.value,
                "out_rows": rows.value}
-        for k in ("lds_groups", "hbm_waves", "hbm_docs", "slot_bytes", "slots", "solo"):
+        for k in ("lds_groups", "hbm_waves", "hbm_docs", "slot_bytes", "slots", "solo", "lean"):
             out[k] = self.get_info(k)
         return out
 
@@ -371,7 +371,8 @@ class Engine:
 
     def set_option(self, key, value):
         """"force_hbm" (HBM-resident waves only), "pool_limit" (LDS leaf blocks per CU),
-        "hbm_waves_per_cu" (HBM-resident waves beside each LDS workgroup), "slot_budget_mb"."""
+        "hbm_waves_per_cu" (HBM-resident waves beside each LDS workgroup), "slot_budget_mb",
+        "solo_max" / "solo_min_ops" (solo route), "lean" (0 = never the property-free kernels)."""
         self._check(lib().mte_set_option(self._h, key.encode(), int(value)), "mte_set_option")
 
     def last_kernel_ms(self):

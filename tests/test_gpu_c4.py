@@ -31,7 +31,7 @@ def test_scaled_c4_zipf_batch_matches_oracle(engine):
     st = engine.replay()
     assert st["failed_docs"] == 0 and st["ops"] == int(counts.sum())
     info = engine.run_info()
-    assert info["solo"] >= 1, info
+    assert info["solo"] >= 1 and info["lean"] == 1, info
     head = engine.doc_result(0)
     assert head["ops"] == 250_000 and head["mode"] == 3, head  # solo, stayed LDS-resident
     bad, _, _ = compare_batch_checksums(engine, batch)
@@ -71,6 +71,28 @@ def test_solo_off_matches_solo_on(engine):
     finally:
         engine.set_option("solo_max", 16)
     assert a.tolist() == b.tolist()
+
+
+@pytest.mark.parametrize("kind", [2, 3, 5])
+def test_lean_kernels_match_full_kernels(engine, kind):
+    """Batches without properties, '\\n' or client ids above 31 replay on the FULL = false kernels
+    (engine.hpp); forcing the FULL ones gives the same checksums. Kind 3 (properties) never runs lean."""
+    counts = zipf_op_counts(512, seed=5, lo=200, hi=40_000)
+    engine.generate(kind, 512, 0, n_clients=8, seed=11, ops_per_doc=counts)
+    engine.replay()
+    assert engine.run_info()["lean"] == (0 if kind == 3 else 1)
+    a = engine.summaries()["checksum"].copy()
+    engine.set_option("lean", 0)
+    try:
+        engine.replay()
+        assert engine.run_info()["lean"] == 0
+        b = engine.summaries()["checksum"].copy()
+    finally:
+        engine.set_option("lean", 1)
+    assert a.tolist() == b.tolist()
+    engine.generate(kind, 4, 0, n_clients=40, seed=11, ops_per_doc=[3000] * 4)  # ids up to 40
+    engine.replay()
+    assert engine.run_info()["lean"] == 0
 
 
 @pytest.mark.parametrize("kind", [2, 3, 5])

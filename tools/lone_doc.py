@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--force-hbm", type=int, default=0)
     ap.add_argument("--verify", type=int, default=1)
+    ap.add_argument("--opt", action="append", default=[], help="engine option key=value (repeatable)")
     a = ap.parse_args()
     e = mte.Engine(0)
     t0 = time.time()
@@ -30,6 +31,9 @@ def main():
     gen_s = time.time() - t0
     if a.force_hbm:
         e.set_option("force_hbm", 1)
+    for kv in a.opt:
+        k, v = kv.split("=")
+        e.set_option(k, int(v))
     res = {"kind": a.kind, "docs": a.docs, "ops": a.ops, "gen_s": round(gen_s, 2), "lib": os.environ.get("MTE_LIB", "")}
     for r in range(a.reps):
         st = e.replay()

@@ -649,6 +649,70 @@ struct Engine {
         return cum;
     }
 
+    // posFromRelativePos (mergeTree.ts:1943-1966) for the op's RELPOS record (include/mte.h): the
+    // marker is found by its builder tag (bits 16..31 of its refType word, aux.y) and
+    // getPosition(marker, R, C) (mergeTree.ts:1586-1603) is the visible length before it in document
+    // order. An unmapped tag, or a marker zamboni has dropped, fails the document (unsupported).
+    MTE_DEV bool marker_pos(u32 tag, i32 R, u32 C, i32 seq, i32& out) {
+        if (tag == 0 || tag > 0xFFFFu) {
+            fail(MTE_DOC_UNSUPPORTED, seq);
+            return false;
+        }
+        fence_ovl();
+        u32 k = NONE, s = 0;
+        for (u32 base = 0; base < st.n_lb; base += 8) {
+            const u32 kk = base + (L >> 3), sl = L & 7;
+            const uint4 o = kk < st.n_lb ? ORD()[kk] : make_uint4(NONE, 0, 0, 0);
+            const u32 idx = sidx(o.x, sl);
+            const bool hit = kk < st.n_lb && sl < o.w && (VIS()[idx].w & F_MARKER) != 0 && (AUX()[idx].y >> 16) == tag;
+            const u64 m = wave_ballot(hit);
+            if (m) {
+                const u32 l = (u32)__builtin_ctzll(m);
+                k = base + (l >> 3);
+                s = l & 7;
+                break;
+            }
+        }
+        if (k == NONE) {
+            fail(MTE_DOC_UNSUPPORTED, seq);
+            return false;
+        }
+        i32 cum = 0;
+        for (u32 base = 0; base < k; base += 64) {
+            const u32 kk = base + L;
+            const bool valid = kk < k;
+            const uint4 o = valid ? ORD()[kk] : make_uint4(0, 0, 0, 0);
+            cum += (i32)wave_sum(blen_all(o, valid, R, C));
+        }
+        const u32 blk = wave_first(ORD()[k].x);
+        const u32 idx = sidx(blk, L);
+        const u32 cz = C == 0 ? 1u : 0u;
+        const u32 v = L < s ? vis_len(VIS()[idx], AUX()[idx].z, idx, R, C, cz) : 0u;
+        out = cum + (i32)wave_sum(v);
+        return true;
+    }
+    MTE_DEV bool rel_positions(mte_op& op, u64 i, i32 R, u32 C) {
+        if (i <= p.docs[doc].op_begin) {
+            fail(MTE_DOC_UNSUPPORTED, op.seq);
+            return false;
+        }
+        const mte_op rr = read_op(p.ops + i - 1);
+        if (rr.type != MTE_OP_RELPOS) {
+            fail(MTE_DOC_UNSUPPORTED, op.seq);
+            return false;
+        }
+        i32 q;
+        if (rr.pos1) {
+            if (!marker_pos((u32)rr.pos1, R, C, op.seq, q)) return false;
+            op.pos1 = (rr.flags & MTE_F_REL_BEFORE1) ? q - rr.msn : q + 1 + rr.msn;  // Marker cachedLength 1
+        }
+        if (rr.a) {
+            if (!marker_pos((u32)rr.a, R, C, op.seq, q)) return false;
+            op.a = (rr.flags & MTE_F_REL_BEFORE2) ? q - (i32)rr.props : q + 1 + (i32)rr.props;
+        }
+        return true;
+    }
+
     // ---------------------------------------------------------------- allocation
     // Out of room: in LDS mode the document leaves the LDS plan (DOC_SPILL: its LDS state is
     // dropped and the host re-runs it HBM-resident); in HBM mode it is a capacity failure.
@@ -2084,9 +2148,10 @@ struct Engine {
         return true;
     }
 
-    MTE_DEV void apply(const mte_op& op) {
+    MTE_DEV void apply(const mte_op& op_in, u64 op_index) {
         MTE_PROF(PF_APPLY);
         MTE_COUNT(PF_OPS, 1);
+        mte_op op = op_in;
 #ifdef MTE_PROFILE
         const u64 t_op0 = __builtin_amdgcn_s_memtime();
         struct OpScope {
@@ -2108,6 +2173,11 @@ struct Engine {
         if (collab && op.type != MTE_OP_NOOP && !ld && !(st.curSeq < op.seq)) {
             fail(MTE_DOC_SEQ_ORDER, op.seq);
             return;
+        }
+        if constexpr (FULL) {  // relative positions need marker ids, i.e. properties
+            if (op.flags & MTE_F_REL) {
+                if (!rel_positions(op, op_index, R, C)) return;
+            }
         }
         bool edited = false;
         if (op.type <= MTE_OP_INSERT_MARKER || ld) {
@@ -2343,7 +2413,7 @@ struct Engine {
         // loops below carry no branch for them
         for (; i < e && !st.status; i++) {
             const mte_op op = read_op(p.ops + i);
-            if (op.type < MTE_OP_LOAD_SEG || op.type == MTE_OP_LOAD_APPEND) break;
+            if (op.type < MTE_OP_LOAD_SEG || op.type >= MTE_OP_LOAD_APPEND) break;
             if (!room()) return i;
             load_record(op, i);
         }
@@ -2373,12 +2443,12 @@ struct Engine {
                     MTE_PROF(PF_LOOP);
                     if (!room()) break;
                 }
-                apply(op);
+                apply(op, i);
             }
         } else {
             for (; i < e && !st.status; i++) {
                 mte_op op = p.ops[i];
-                apply(op);
+                apply(op, i);
             }
         }
         return i;
@@ -2507,7 +2577,7 @@ struct Engine {
             g.lastPos = op.pos1;
             g.rng = rng;
             if (L == 0) p.ops[op0 + step] = op;
-            apply(op);
+            apply(op, 0);
         }
         wave_sync();  // op records and payload visible before the replay kernel
         return true;

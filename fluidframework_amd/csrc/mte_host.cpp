@@ -24,6 +24,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/mte.h"
@@ -573,10 +574,11 @@ void mte_destroy(mte_engine* e) {
 
 const char* mte_last_error(const mte_engine* e) { return e ? e->err.c_str() : "null engine"; }
 
-static void count_doc_ops(const HostBatch& hb, uint32_t d, uint64_t& pi, uint64_t& an) {
+static void count_doc_ops(const HostBatch& hb, uint32_t d, uint64_t& pi, uint64_t& an, bool* rel = nullptr) {
     pi = an = 0;
     for (uint64_t i = hb.doc_op_offsets[d]; i < hb.doc_op_offsets[d + 1]; i++) {
         const mte_op& o = hb.ops[i];
+        if (rel && o.type == MTE_OP_RELPOS) *rel = true;
         if ((o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER || o.type == MTE_OP_LOAD_SEG ||
              o.type == MTE_OP_LOAD_APPEND) && o.props)
             pi++;
@@ -603,9 +605,10 @@ int mte_load(mte_engine* e, const mte_batch* b) {
             }
         n_ops[d] = b->doc_op_offsets[d + 1] - b->doc_op_offsets[d];
         pay[d] = b->doc_payload_offsets[d + 1] - b->doc_payload_offsets[d];
-        count_doc_ops(e->hb, d, pi[d], an[d]);
+        bool rel = false;
+        count_doc_ops(e->hb, d, pi[d], an[d], &rel);
         collab[d] = e->hb.client(d, 0).empty() ? 0 : 1;  // empty observer name => local, non-collab
-        lean = lean && !has_nl[d] && !pi[d] && !an[d] &&
+        lean = lean && !has_nl[d] && !pi[d] && !an[d] && !rel &&
                e->hb.doc_client_offsets[d + 1] - e->hb.doc_client_offsets[d] <= 32;
         // a document with more than MTE_MAX_CLIENTS clients fails alone (MTE_DOC_UNSUPPORTED at its
         // first op from a client beyond the cap), never the batch
@@ -923,7 +926,7 @@ struct DocView {
                 sv.rclient = c.collab ? (int32_t)((v.w >> 8) & 0xff) : -1;
                 sv.ovl = e->h_out_ovl[i];
                 sv.props = a.x ? (uint32_t)(i + 1) : 0u;
-                sv.reftype = sv.kind ? t.x : 0;
+                sv.reftype = sv.kind ? (t.x & 0xFFFFu) : 0;  // bits 16..31: the marker's tag
                 sv.text = sv.kind ? nullptr : txt + t.x;
                 segs.push_back(sv);
             }
@@ -1549,6 +1552,15 @@ static int num_field(const json::Value& o, const char16_t* k, int32_t* out) {
     return 1;
 }
 
+// Marker.getId (mergeTree.ts:690-695) of a segment's props: the "markerId" value when it is a
+// non-empty string (a truthy non-string id is left unmapped: relative positions naming it fail).
+static bool marker_id(const json::Value* props, std::u16string* id) {
+    const json::Value* v = props && props->kind == json::Value::Object ? props->get(u"markerId") : nullptr;
+    if (!v || v->kind != json::Value::String || v->str.empty()) return false;
+    *id = v->str;
+    return true;
+}
+
 // One document under construction: its records, payload and short-id table (observer = 0).
 struct DocBuild {
     std::vector<mte_op> ops;
@@ -1557,6 +1569,38 @@ struct DocBuild {
     std::unordered_map<std::string, uint32_t> ids;
     bool collab = false;
     std::string err;
+    // marker ids for relative positions (include/mte.h MTE_OP_RELPOS): id -> tag of the marker the
+    // reference maps it to; ids tied to two markers, and every id after an annotate that sets a
+    // "markerId" property, are ambiguous (blockUpdate re-maps live markers, mergeTree.ts:2748-2768)
+    std::unordered_map<std::u16string, uint32_t> mk_tag;
+    std::unordered_set<std::u16string> mk_amb;
+    bool mk_annot = false;
+    uint32_t n_tags = 0;
+    // mapIdToSegment (mergeTree.ts:1185-1187) for a marker record: its tag into bits 16..31 of the
+    // refType word *w
+    void map_marker(const std::u16string& id, uint32_t* w) {
+        if (mk_tag.count(id)) mk_amb.insert(id);
+        if (n_tags >= 0xFFFFu) {
+            mk_amb.insert(id);
+            return;
+        }
+        mk_tag[id] = ++n_tags;
+        *w = (*w & 0xFFFFu) | (n_tags << 16);
+    }
+    // posFromRelativePos's marker lookup (mergeTree.ts:1949-1951) -> tag, offset, before
+    uint32_t rel_tag(const json::Value& rp, int32_t* off, bool* before) const {
+        *off = 0;
+        *before = false;
+        if (rp.kind != json::Value::Object) return MTE_REL_UNMAPPED;
+        const json::Value* id = rp.get(u"id");
+        const json::Value* bf = rp.get(u"before");
+        *before = bf && json::truthy(bf);
+        num_field(rp, u"offset", off);
+        if (!id || id->kind != json::Value::String || id->str.empty() || mk_annot || mk_amb.count(id->str))
+            return MTE_REL_UNMAPPED;
+        auto it = mk_tag.find(id->str);
+        return it == mk_tag.end() ? MTE_REL_UNMAPPED : it->second;
+    }
     explicit DocBuild(const char* observer_name) {
         const std::string observer = observer_name ? observer_name : "";
         names.push_back(observer);
@@ -1634,9 +1678,10 @@ static int add_messages(mte_builder* b, const json::Value& doc, DocBuild& db) {
         size_t first = ops.size();
         for (const json::Value* c : members) {
             if (c->kind != json::Value::Object) continue;
-            if (c->get(u"relativePos1") || c->get(u"relativePos2") || c->get(u"register"))
-                return fail(MTE_E_UNSUPPORTED, "relative positions / registers are out of scope");
+            if (c->get(u"register")) return fail(MTE_E_UNSUPPORTED, "registers are out of scope");
             mte_op o = base;
+            std::u16string mkid;
+            bool mapMarker = false;
             int32_t t = -1;
             num_field(*c, u"type", &t);
             num_field(*c, u"pos1", &o.pos1);
@@ -1654,8 +1699,10 @@ static int add_messages(mte_builder* b, const json::Value& doc, DocBuild& db) {
                     const json::Value* mk = seg->get(u"marker");
                     int32_t rt = 0;
                     if (mk->kind == json::Value::Object) num_field(*mk, u"refType", &rt);
+                    if (rt < 0 || rt > 0xFFFF) return fail(MTE_E_UNSUPPORTED, "refType beyond 16 bits");
                     o.b = (uint32_t)rt;
                     props = seg->get(u"props");
+                    mapMarker = marker_id(props, &mkid);
                 } else if (seg->kind == json::Value::Object && seg->get(u"text") &&
                            seg->get(u"text")->kind == json::Value::String) {
                     const json::Value* tx = seg->get(u"text");
@@ -1689,6 +1736,38 @@ static int add_messages(mte_builder* b, const json::Value& doc, DocBuild& db) {
                 o.props = b->in->propset(props && props->kind == json::Value::Object ? *props : empty);
             } else {
                 continue;
+            }
+            // relativePos1 / relativePos2 where pos1 / pos2 is undefined (client.ts:493-510): a RELPOS
+            // record before the op (an insert uses only its start)
+            const json::Value* rp1 = c->get(u"relativePos1");
+            const json::Value* rp2 = c->get(u"relativePos2");
+            const bool r1 = rp1 && json::truthy(rp1) && !c->get(u"pos1");
+            const bool r2 = t != 0 && rp2 && json::truthy(rp2) && !c->get(u"pos2");
+            if (r1 || r2) {
+                mte_op r = base;
+                r.type = MTE_OP_RELPOS;
+                r.flags = 0;
+                r.props = 0;
+                r.msn = 0;
+                bool before = false;
+                int32_t off = 0;
+                if (r1) {
+                    r.pos1 = (int32_t)db.rel_tag(*rp1, &off, &before);
+                    r.msn = off;
+                    if (before) r.flags |= MTE_F_REL_BEFORE1;
+                }
+                if (r2) {
+                    r.a = (int32_t)db.rel_tag(*rp2, &off, &before);
+                    r.props = (uint32_t)off;
+                    if (before) r.flags |= MTE_F_REL_BEFORE2;
+                }
+                ops.push_back(r);
+                o.flags |= MTE_F_REL;
+            }
+            if (mapMarker) db.map_marker(mkid, &o.b);  // after the op's own position (insertSegments)
+            if (t == 2) {
+                const json::Value* ap = c->get(u"props");
+                if (ap && ap->kind == json::Value::Object && ap->get(u"markerId")) db.mk_annot = true;
             }
             ops.push_back(o);
         }
@@ -1725,7 +1804,8 @@ int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* t
 // Resume from a summary: SnapshotLoader (snapshotLoader.ts:38-216) as LOAD records (include/mte.h).
 
 // A segment spec (sequenceFactory.ts:31-37: string | {text, props} | {marker, props}) -> o.a/o.b/props.
-static int load_spec(mte_builder* b, DocBuild& db, const json::Value& seg, mte_op& o) {
+static int load_spec(mte_builder* b, DocBuild& db, const json::Value& seg, mte_op& o, std::u16string* mkid = nullptr,
+                     bool* hasId = nullptr) {
     const json::Value* props = nullptr;
     if (seg.kind == json::Value::String) {
         o.a = (int32_t)db.payload.size();
@@ -1735,10 +1815,12 @@ static int load_spec(mte_builder* b, DocBuild& db, const json::Value& seg, mte_o
         const json::Value* mk = seg.get(u"marker");
         int32_t rt = 0;
         if (mk->kind == json::Value::Object) num_field(*mk, u"refType", &rt);
+        if (rt < 0 || rt > 0xFFFF) return db.fail(MTE_E_UNSUPPORTED, "refType beyond 16 bits");
         o.a = rt;
         o.b = 1;
         o.flags |= MTE_F_LOAD_MARKER;
         props = seg.get(u"props");
+        if (mkid && hasId) *hasId = marker_id(props, mkid);
     } else if (seg.kind == json::Value::Object && seg.get(u"text") && seg.get(u"text")->kind == json::Value::String) {
         const json::Value* tx = seg.get(u"text");
         o.a = (int32_t)db.payload.size();
@@ -1844,9 +1926,14 @@ static const char* const kNonCollabName = "original";
 // snapshotLoader.ts:79-111): merge info gives client / seq / removedSeq / removedClient; a bare spec,
 // or merge info without client and seq, is NonCollab at the universal seq (*batchable: loadBody's
 // flushBatch test, :193-195).
-static int summary_seg(mte_builder* b, DocBuild& db, const json::Value& sp, mte_op& o, bool* info, bool* batchable) {
+struct MarkerId {  // a summary marker's Marker.getId, tagged when the record is emitted
+    bool has = false;
+    std::u16string id;
+};
+static int summary_seg(mte_builder* b, DocBuild& db, const json::Value& sp, mte_op& o, bool* info, bool* batchable,
+                       MarkerId* mid) {
     const json::Value* js = sp.kind == json::Value::Object ? sp.get(u"json") : nullptr;  // hasMergeInfo
-    if (int rc = load_spec(b, db, js ? *js : sp, o)) return rc;
+    if (int rc = load_spec(b, db, js ? *js : sp, o, &mid->id, &mid->has)) return rc;
     std::string client = kNonCollabName;
     bool hasClient = false, hasSeq = false;
     if (js) {
@@ -1891,8 +1978,15 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
             mte_op o{};
             o.type = MTE_OP_LOAD_SEG;
             bool info, batchable;
-            if (int rc = summary_seg(b, db, sp, o, &info, &batchable)) return rc;
+            MarkerId mid;
+            if (int rc = summary_seg(b, db, sp, o, &info, &batchable, &mid)) return rc;
             mergeInfo |= info;
+            // reloadFromSegments maps the live markers (blockUpdate -> addNodeReferences, mergeTree.ts:275-284)
+            if (mid.has && !(o.flags & MTE_F_LOAD_REMOVED)) {
+                uint32_t w = (uint32_t)o.a;
+                db.map_marker(mid.id, &w);
+                o.a = (int32_t)w;
+            }
             db.ops.push_back(o);
         }
     }
@@ -1905,6 +1999,7 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
     num_field(*md, u"totalSegmentCount", &totalSegs);
     std::vector<mte_op> body;
     std::vector<uint8_t> bodyBatchable;
+    std::vector<MarkerId> bodyIds;
     if (segCount != totalSegs && ocm && ocm->kind == json::Value::Array) {
         for (size_t i = 1; i < ocm->items.size(); i++) {
             const json::Value* id = ocm->items[i].kind == json::Value::Object ? ocm->items[i].get(u"id") : nullptr;
@@ -1916,10 +2011,12 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
             for (const json::Value& sp : cs->items) {
                 mte_op o{};
                 bool info, batchable;
-                if (int rc = summary_seg(b, db, sp, o, &info, &batchable)) return rc;
+                MarkerId mid;
+                if (int rc = summary_seg(b, db, sp, o, &info, &batchable, &mid)) return rc;
                 mergeInfo |= info;
                 body.push_back(o);
                 bodyBatchable.push_back(batchable ? 1 : 0);
+                bodyIds.push_back(std::move(mid));
             }
         }
     }
@@ -1927,11 +2024,20 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
     // document end: LOAD_SEG records whose tree shape the builder computes below. With merge info,
     // the appends go through the insert walk on the device (LOAD_APPEND after LOAD_END), in the
     // order loadBody issues them.
+    // The appended markers are mapped by insertSegments (blockInsert, mergeTree.ts:2199-2205).
+    auto tag_body = [&](size_t i, mte_op& o) {
+        if (!bodyIds[i].has) return;
+        uint32_t w = (uint32_t)o.a;
+        db.map_marker(bodyIds[i].id, &w);
+        o.a = (int32_t)w;
+    };
     if (!mergeInfo) {
-        for (mte_op o : body) {
+        for (size_t i = 0; i < body.size(); i++) {
+            mte_op o = body[i];
             if (o.b == 0) continue;  // blockInsert skips empty segments (mergeTree.ts:2196)
             o.type = MTE_OP_LOAD_SEG;
             o.flags |= MTE_F_LOAD_BODY;
+            tag_body(i, o);
             db.ops.push_back(o);
         }
     }
@@ -1997,6 +2103,7 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
             o.flags = (uint16_t)(o.flags & (MTE_F_LOAD_MARKER | MTE_F_LOAD_REMOVED));
             if (firstOfCall) o.flags |= MTE_F_APPEND_FIRST;
             if (linked[i]) o.flags |= MTE_F_APPEND_REPEAT;
+            else tag_body(i, o);  // a repeat is the same object: mapped already
             linked[i] = 1;
             db.ops.push_back(o);
         };

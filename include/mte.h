@@ -60,7 +60,7 @@ enum {
     MTE_OP_INSERT = 0,        /* insert text segment: a = payload offset, b = length */
     MTE_OP_REMOVE = 1,        /* remove [pos1, a) */
     MTE_OP_ANNOTATE = 2,      /* annotate [pos1, a) with prop set `props` */
-    MTE_OP_INSERT_MARKER = 3, /* insert Marker: b = refType, props = marker props */
+    MTE_OP_INSERT_MARKER = 3, /* insert Marker: b = refType | tag << 16 (MTE_OP_RELPOS), props = marker props */
     MTE_OP_NOOP = 4,          /* sequenced message with no merge-tree op (only seq/msn advance) */
     /* Resume from a summary (SnapshotLoader, snapshotLoader.ts:98-216); records precede the op log.
      * LOAD_SEG: one segment in document order (specToSegment :79-111): a = payload offset (text) or
@@ -85,7 +85,26 @@ enum {
      *   reference re-links that object if the walk finds pos -- one object in two places, which the
      *   engine does not model (MTE_DOC_UNSUPPORTED) -- and skips it otherwise. */
     MTE_OP_LOAD_APPEND = 8,
+    /* RELPOS: the relativePos1 / relativePos2 of the op record right after it (ops.ts:66-94), which
+     *   carries MTE_F_REL; Client.getValidOpRange (client.ts:493-510) takes a position from it only where
+     *   pos1 / pos2 is undefined. pos1 / a = the tag of the marker for position 1 / 2 (0 = the op's own
+     *   pos1 / pos2; MTE_REL_UNMAPPED = an id the builder cannot tie to one marker), msn / props (as
+     *   int32) = offset 1 / 2, MTE_F_REL_BEFORE1 / 2 = relativePos.before; seq, ref_seq, client = the
+     *   op's. posFromRelativePos (mergeTree.ts:1943-1966): pos = getPosition(marker) - offset when
+     *   before, getPosition(marker) + 1 + offset otherwise.
+     *   Marker tags: the builder numbers the markers whose props carry a truthy "markerId"
+     *   (Marker.getId, mergeTree.ts:690-695) 1, 2, ... per document in the order the reference maps
+     *   them (mapIdToSegment at insert, mergeTree.ts:2074-2078 / 2199-2205; live loaded markers,
+     *   addNodeReferences :275-284) and stores the tag in bits 16..31 of the marker's refType field
+     *   (INSERT_MARKER b, LOAD_SEG / LOAD_APPEND a); refType itself must fit 16 bits. An id is
+     *   MTE_REL_UNMAPPED when it was never mapped, was mapped to two markers (blockUpdate re-maps live
+     *   markers, :2748-2768, so the winner depends on block-update order), an annotate before the op
+     *   set a "markerId" property, or the marker count passed 65535. A document fails
+     *   MTE_DOC_UNSUPPORTED at an op whose marker is unmapped or no longer in the tree (zamboni
+     *   dropped it: the reference would walk its stale parent chain). */
+    MTE_OP_RELPOS = 9,
 };
+#define MTE_REL_UNMAPPED 0xFFFFFFFFu
 
 /* flags */
 #define MTE_F_END_OF_MSG 0x1u   /* last op of its ISequencedDocumentMessage: currentSeq=seq, setMinSeq(msn) */
@@ -96,6 +115,9 @@ enum {
 #define MTE_F_LOAD_BODY 0x20u   /* LOAD_SEG: appended from a body chunk */
 #define MTE_F_APPEND_FIRST 0x40u  /* LOAD_APPEND: first segment of an append call (pos = root.cachedLength) */
 #define MTE_F_APPEND_REPEAT 0x80u /* LOAD_APPEND: a segment object appended before (see MTE_OP_LOAD_APPEND) */
+#define MTE_F_REL 0x100u          /* op: positions from the MTE_OP_RELPOS record just before it */
+#define MTE_F_REL_BEFORE1 0x200u  /* RELPOS: relativePos1.before */
+#define MTE_F_REL_BEFORE2 0x400u  /* RELPOS: relativePos2.before */
 
 typedef struct mte_op {
     int32_t seq;        /* sequenceNumber */

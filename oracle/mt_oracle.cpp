@@ -762,6 +762,56 @@ class Doc {
     long long failingSeq = -1;
     std::string error;
     uint64_t opsApplied = 0;
+    // idToSegment (mergeTree.ts:1098, 1185-1187) by the builder's marker tag (include/mte.h
+    // MTE_OP_RELPOS): the builder leaves unmapped every id the reference could tie to two markers
+    std::unordered_map<uint32_t, Segment*> tagged;
+
+    // posFromRelativePos (mergeTree.ts:1943-1966) -> getPosition (:1586-1603). A marker no longer
+    // linked into the tree (zamboni dropped it; the reference would walk its stale parent chain) and
+    // an unmapped id are unsupported.
+    int markerPos(uint32_t tag, int refSeq, int clientId) {
+        auto it = tag && tag <= 0xFFFFu ? tagged.find(tag) : tagged.end();
+        if (it == tagged.end()) throw EngineError(MTE_DOC_UNSUPPORTED, "relative position: marker id not mapped");
+        return getPosition(it->second, refSeq, clientId);
+    }
+    int getPosition(Node* node, int refSeq, int clientId) {
+        for (Node* n = node; n != mt.root; n = n->parent) {
+            bool linked = false;
+            for (int ci = 0; n->parent && ci < n->parent->childCount; ci++) linked |= n->parent->children[ci] == n;
+            if (!linked) throw EngineError(MTE_DOC_UNSUPPORTED, "relative position: marker dropped from the tree");
+        }
+        int total = 0;
+        Block* parent = node->parent;
+        Node* prevParent = nullptr;
+        while (parent) {
+            for (int ci = 0; ci < parent->childCount; ci++) {
+                Node* child = parent->children[ci];
+                if ((prevParent && child == prevParent) || child == node) break;
+                total += mt.nodeLength(child, refSeq, clientId);
+            }
+            prevParent = parent;
+            parent = parent->parent;
+        }
+        return total;
+    }
+    // Client.getValidOpRange (client.ts:493-510): positions from the RELPOS record before the op
+    void relPositions(const mte_batch* b, uint64_t i, uint32_t d, mte_op& op) {
+        if (i == b->doc_op_offsets[d] || b->ops[i - 1].type != MTE_OP_RELPOS)
+            throw EngineError(MTE_DOC_UNSUPPORTED, "MTE_F_REL without a RELPOS record");
+        const mte_op& r = b->ops[i - 1];
+        if (r.pos1) {
+            const int q = markerPos((uint32_t)r.pos1, op.ref_seq, op.client);
+            op.pos1 = (r.flags & MTE_F_REL_BEFORE1) ? q - r.msn : q + 1 + r.msn;  // Marker cachedLength 1
+        }
+        if (r.a) {
+            const int q = markerPos((uint32_t)r.a, op.ref_seq, op.client);
+            op.a = (r.flags & MTE_F_REL_BEFORE2) ? q - (int32_t)r.props : q + 1 + (int32_t)r.props;
+        }
+    }
+    void tag(Segment* s, uint32_t word) {
+        s->refType = (int)(word & 0xFFFFu);
+        if (word >> 16) tagged[word >> 16] = s;
+    }
 
     explicit Doc(const char* observerName) {
         mt.longIds = &shortIds;
@@ -782,6 +832,33 @@ class Doc {
         return id;
     }
     std::string longId(int shortId) const { return shortId >= 0 ? shortIds[shortId] : "original"; }
+
+    // The JSON path's idToSegment, keyed by the id string itself (the record path above uses the
+    // builder's tags): mapped at insert and for live loaded markers; an id mapped to two markers, and
+    // any id after an annotate that sets "markerId", is ambiguous -- blockUpdate re-maps live markers
+    // (mergeTree.ts:2748-2768, 275-284) in an order this restatement does not model -- and a relative
+    // position naming it is unsupported, as in the builder (include/mte.h MTE_OP_RELPOS).
+    std::unordered_map<u16s, Segment*> idToSegment;
+    std::unordered_set<u16s> idAmbiguous;
+    bool idAnnotated = false;
+    void mapIdToSegment(Segment* s) {
+        if (!s->marker || !s->hasProps) return;
+        JVP v = s->props.get(u"markerId");
+        if (!v || v->t != JV::Str || v->s.empty()) return;
+        auto it = idToSegment.find(v->s);
+        if (it != idToSegment.end() && it->second != s) idAmbiguous.insert(v->s);
+        idToSegment[v->s] = s;
+    }
+    int posFromRelativePos(const JV& rp, int refSeq, int clientId) {  // mergeTree.ts:1943-1966
+        JVP id = rp.t == JV::Obj ? rp.o.get(u"id") : nullptr;
+        if (!id || id->t != JV::Str || id->s.empty() || idAnnotated || idAmbiguous.count(id->s) ||
+            !idToSegment.count(id->s))
+            throw EngineError(MTE_DOC_UNSUPPORTED, "relative position: marker id not mapped");
+        int pos = getPosition(idToSegment[id->s], refSeq, clientId);
+        JVP before = rp.o.get(u"before"), off = rp.o.get(u"offset");
+        const int o = off && off->t == JV::Num ? (int)off->n : 0;
+        return truthy(before.get()) ? pos - o : pos + 1 + o;
+    }
 
     Segment* makeSegment(const JV& spec) {  // SharedStringFactory.segmentFromSpec (sequenceFactory.ts:31-37)
         Segment* s = mt.newSegment();
@@ -819,27 +896,38 @@ class Doc {
 
     // Client.applyRemoteOp (client.ts:776-803) -> applyInsertOp/RemoveRange/AnnotateRange (:328-449)
     void applyRemoteOp(const JObj& op, int clientId, int refSeq, int seq) {
-        if (op.get(u"relativePos1") || op.get(u"relativePos2") || op.get(u"register"))
-            throw EngineError(MTE_DOC_UNSUPPORTED, "relative positions / registers are out of scope");
+        if (op.get(u"register")) throw EngineError(MTE_DOC_UNSUPPORTED, "registers are out of scope");
         int type = num(op, u"type");
         bool hasPos1 = false;
         int pos1 = num(op, u"pos1", &hasPos1);
         int pos2 = num(op, u"pos2");
+        // Client.getValidOpRange (client.ts:493-510)
+        auto relPositions = [&]() {
+            JVP rp1 = op.get(u"relativePos1"), rp2 = op.get(u"relativePos2");
+            if (!op.get(u"pos1") && rp1 && truthy(rp1.get())) pos1 = posFromRelativePos(*rp1, refSeq, clientId);
+            if (type != 0 && !op.get(u"pos2") && rp2 && truthy(rp2.get()))
+                pos2 = posFromRelativePos(*rp2, refSeq, clientId);
+        };
         switch (type) {
             case 0: {
                 JVP seg = op.get(u"seg");
                 if (!seg) return;
+                relPositions();
                 std::vector<Segment*> segs{makeSegment(*seg)};
+                mapIdToSegment(segs[0]);
                 mt.insertSegments(pos1, segs, refSeq, clientId, seq);
                 opsApplied++;
                 break;
             }
             case 1:
+                relPositions();
                 mt.markRangeRemoved(pos1, pos2, refSeq, clientId, seq);
                 opsApplied++;
                 break;
             case 2: {
+                relPositions();
                 JVP props = op.get(u"props");
+                if (props && props->t == JV::Obj && props->o.get(u"markerId")) idAnnotated = true;
                 JVP comb = op.get(u"combiningOp");
                 bool rewrite = false;
                 if (comb) {
@@ -978,6 +1066,8 @@ class Doc {
         if (hs && hs->t == JV::Arr)
             for (auto& sp : hs->a) segs.push_back(loadSpec(*sp));
         mt.reloadFromSegments(segs);
+        for (Node* n : segs)  // addNodeReferences maps the live markers (mergeTree.ts:275-284)
+            if (!((Segment*)n)->removed) mapIdToSegment((Segment*)n);
         bool hasMin = false;
         const int cur = num(md->o, u"sequenceNumber");
         const int minSeq = num(md->o, u"minSequenceNumber", &hasMin);
@@ -1017,6 +1107,7 @@ class Doc {
                     continue;
                 }
                 std::vector<Segment*> one{sg};
+                mapIdToSegment(sg);  // blockInsert (mergeTree.ts:2199-2205)
                 mt.insertSegments(insertPos, one, UniversalSequenceNumber, cli, seq);
                 linked.insert(sg);
                 insertPos += sg->len;
@@ -1111,12 +1202,12 @@ class Doc {
         int bodyClient = NonCollabClient;
         int appendPos = 0;
         for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1] && !status; i++) {
-            const mte_op& op = b->ops[i];
+            mte_op op = b->ops[i];
             try {
                 if (op.client >= names.size()) throw EngineError(MTE_DOC_UNSUPPORTED, "client id out of range");
                 int shortId = getOrAddShortClientId(names[op.client]);
                 if (shortId != op.client) throw EngineError(MTE_DOC_UNSUPPORTED, "client ids not in first-appearance order");
-                if (op.type >= MTE_OP_LOAD_SEG) {  // summary records (include/mte.h; loadSnapshot above)
+                if (op.type >= MTE_OP_LOAD_SEG && op.type != MTE_OP_RELPOS) {  // summary records (include/mte.h; loadSnapshot above)
                     if (op.type == MTE_OP_LOAD_NODE) continue;  // the engine's shape hint; rebuilt here
                     if (op.type == MTE_OP_LOAD_END) {
                         mt.reloadFromSegments(loadSegs);
@@ -1144,7 +1235,7 @@ class Doc {
                     Segment* s = mt.newSegment();
                     if (op.flags & MTE_F_LOAD_MARKER) {
                         s->marker = true;
-                        s->refType = op.a;
+                        tag(s, (uint32_t)op.a);
                         s->len = 1;
                     } else {
                         s->text.assign((const char16_t*)payload + op.a, op.b);
@@ -1184,6 +1275,7 @@ class Doc {
                 }
                 if (op.type != MTE_OP_NOOP && !(mt.cw.currentSeq < op.seq))
                     throw EngineError(MTE_DOC_SEQ_ORDER, "seq <= currentSeq");
+                if (op.flags & MTE_F_REL) relPositions(b, i, d, op);
                 switch (op.type) {
                     case MTE_OP_INSERT:
                     case MTE_OP_INSERT_MARKER: {
@@ -1193,7 +1285,7 @@ class Doc {
                             s->len = (int)op.b;
                         } else {
                             s->marker = true;
-                            s->refType = (int)op.b;
+                            tag(s, op.b);
                             s->len = 1;
                         }
                         if (op.props) MergeTree::addProperties(s, propset(b, op.props), false);

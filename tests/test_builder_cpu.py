@@ -90,4 +90,4 @@ def test_builder_groups_and_noops():
 def test_builder_rejects_out_of_scope():
     b = mte.Builder()
     with pytest.raises(mte.MteError):
-        b.add_doc([msg("a", 1, 0, {"relativePos1": {"id": "x"}, "seg": "q", "type": 0})])
+        b.add_doc([msg("a", 1, 0, {"register": "r", "seg": "q", "type": 0})])

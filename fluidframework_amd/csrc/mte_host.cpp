@@ -227,7 +227,10 @@ struct mte_engine {
     // options (mte_set_option)
     bool force_hbm = false;           // no LDS-resident waves: every document HBM-resident
     uint32_t pool_limit = 0;
-    uint32_t hbm_waves_per_cu = 8;    // HBM-resident waves (slots) per CU beside the LDS workgroup (2 per SIMD)
+#ifndef MTE_HBMQ_PER_CU
+#define MTE_HBMQ_PER_CU 8
+#endif
+    uint32_t hbm_waves_per_cu = MTE_HBMQ_PER_CU;  // HBM-resident waves (slots) per CU beside the LDS workgroup
     uint64_t slot_budget = 48ull << 30;  // HBM for per-wave slots
     uint64_t slot_ops_cap = 65536;       // slots are sized for documents of at most this many ops
     uint32_t slot_blk_limit = 0;         // test knob: leaf blocks per slot (0 = from slot_ops_cap)
@@ -1517,6 +1520,11 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "slots") *value = e->n_slots;
     else if (k == "solo") *value = e->last_solo;
     else if (k == "lean") *value = e->last_lean;
+    else if (k == "out_text") {  // UTF-16 units Engine::finish gathered (counters[6..7])
+        uint32_t ctr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (e->d_counters.p) HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
+        *value = (int64_t)(ctr[6] | ((uint64_t)ctr[7] << 32));
+    }
     else return set_err(e, MTE_E_ARG, "unknown info key " + k);
     return MTE_OK;
 }

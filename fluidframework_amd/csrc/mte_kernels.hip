@@ -15,8 +15,17 @@
 
 namespace mte {
 
+// Waves per SIMD the register allocation of k_lds / k_hbmq is sized for (512 VGPRs / n each): the
+// two kernels share every CU, LDS_WAVES / 4 LDS waves plus hbm_waves_per_cu / 4 HBM waves per SIMD.
+#ifndef MTE_LDS_WPE
+#define MTE_LDS_WPE 4
+#endif
+#ifndef MTE_HBMQ_WPE
+#define MTE_HBMQ_WPE 4
+#endif
+
 template <bool GEN, bool FULL>
-__global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(4))) void k_lds(Params p) {
+__global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(MTE_LDS_WPE))) void k_lds(Params p) {
     LdsPlan* lp = &g_plan;
     const u32 t = threadIdx.x, L = t & 63;
     const u32 w = wave_first(t >> 6);  // wave-uniform (the compiler cannot infer it from threadIdx)
@@ -171,7 +180,7 @@ MTE_DEV u32 acquire_hslot(const Params& p) {
 // rather than a persistent loop: with the engine inlined into a loop, hipcc 7.2 built a divergent
 // loop latch that came back with EXEC narrowed to one lane.)
 template <bool GEN, bool FULL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_hbmq(Params p) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_HBMQ_WPE))) void k_hbmq(Params p) {
     const u32 L = lane_id();
     u32 i = 0;
     if (L == 0) i = p.n_prio + atomicAdd(&p.counters[0], 1u);

@@ -15,8 +15,12 @@ ap.add_argument("--kind", type=int, default=2)
 ap.add_argument("--docs", type=int, default=2048)
 ap.add_argument("--ops", type=int, default=10000)
 ap.add_argument("--replays", type=int, default=1)
+ap.add_argument("--opt", action="append", default=[], help="engine option key=value (repeatable)")
 a = ap.parse_args()
 e = mte.Engine(0)
+for kv in a.opt:
+    k, v = kv.split("=")
+    e.set_option(k, int(v))
 if a.config:
     import bench
     from fluidframework_amd.shard import plan_shard
@@ -28,6 +32,9 @@ if a.config:
 else:
     e.generate(a.kind, a.docs, a.ops, n_clients=8, seed=3)
     meta = {"docs": a.docs, "ops": a.docs * a.ops, "kind": a.kind}
+times = []
 for _ in range(a.replays):
     st = e.replay()
+    times.append(round(st["kernel_ms"], 2))
+meta["kernel_ms_all"] = times
 print(json.dumps({**meta, **st, **e.run_info()}))

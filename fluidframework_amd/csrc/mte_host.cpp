@@ -1609,9 +1609,23 @@ struct DocBuild {
         auto it = mk_tag.find(id->str);
         return it == mk_tag.end() ? MTE_REL_UNMAPPED : it->second;
     }
+    // Windowed short ids: the engine's client field has MTE_MAX_CLIENTS values, the reference's
+    // short-id map grows without bound (client.ts:644-668; a container log gets a new clientId per
+    // reconnect). A client's id matters only while one of its ops is above minSeq: nodeLength
+    // (mergeTree.ts:1659-1699) compares client ids only for segments whose seq / removedSeq is above
+    // the op's refSeq >= minSeq (msn is the least refSeq of the quorum), and SnapshotV1 names clients
+    // only above minSeq. So a slot whose client's last op is at or below minSeq is reused; `names`
+    // holds each slot's last owner (the name every output above minSeq refers to). Concurrent
+    // overlapping removers are all above minSeq while their removal matters. An op whose refSeq is
+    // below minSeq after a reuse is reported unsupported (slot 255), as is a client with no free slot.
+    std::vector<int32_t> last_use;  // slot -> highest seq its owner used
+    int32_t cur_min = 0;            // minSeq as the engine will have it at the next record
+    bool loading = false;           // summary records: no reuse before LOAD_END
+    bool reused = false;
     explicit DocBuild(const char* observer_name) {
         const std::string observer = observer_name ? observer_name : "";
         names.push_back(observer);
+        last_use.push_back(INT32_MAX);  // the observer keeps slot 0
         ids[observer] = 0;
         collab = !observer.empty();
     }
@@ -1619,19 +1633,33 @@ struct DocBuild {
         err = m;
         return code;
     }
-    // getOrAddShortClientId (client.ts:644-668)
-    int short_id(const std::string& name, uint32_t* out) {
+    // getOrAddShortClientId (client.ts:644-668), windowed (above); `use` = the seq the id is used at
+    int short_id(const std::string& name, uint32_t* out, int32_t use = 0) {
         auto it = ids.find(name);
         if (it != ids.end()) {
             *out = it->second;
+            if (use > last_use[*out]) last_use[*out] = use;
             return MTE_OK;
         }
-        // short ids >= MTE_MAX_CLIENTS are recorded (the op record holds 8 bits: later ones share 255);
-        // the engine reports such a document MTE_DOC_UNSUPPORTED at its first op from such a client,
-        // before any shared id could matter, and the rest of the batch replays normally
-        *out = (uint32_t)std::min<size_t>(names.size(), 255);
-        names.push_back(name);
-        ids[name] = *out;
+        uint32_t slot = NONE;
+        if (names.size() < MTE_MAX_CLIENTS) {
+            slot = (uint32_t)names.size();
+            names.push_back(name);
+            last_use.push_back(use);
+        } else if (!loading) {
+            for (uint32_t q = 1; q < MTE_MAX_CLIENTS && slot == NONE; q++)
+                if (last_use[q] <= cur_min) slot = q;
+            if (slot != NONE) {
+                ids.erase(names[slot]);
+                names[slot] = name;
+                last_use[slot] = use;
+                reused = true;
+            }
+        }
+        // no slot free: the engine reports the document MTE_DOC_UNSUPPORTED at the first record
+        // naming this client (255), the rest of the batch replays normally
+        *out = slot == NONE ? 255u : slot;
+        if (slot != NONE) ids[name] = slot;
         return MTE_OK;
     }
     void commit(HostBatch& hb) {
@@ -1664,7 +1692,7 @@ static int add_messages(mte_builder* b, const json::Value& doc, DocBuild& db) {
         std::string name = (cid && cid->kind == json::Value::String) ? json::to_utf8(cid->str.data(), cid->str.size()) : "";
         if (!collab) name = "";
         uint32_t sid;
-        if (int rc = db.short_id(name, &sid)) return rc;
+        if (int rc = db.short_id(name, &sid, base.seq)) return rc;
         base.client = (uint8_t)sid;
         const json::Value* type = m.get(u"type");
         const json::Value* contents = m.get(u"contents");
@@ -1673,6 +1701,7 @@ static int add_messages(mte_builder* b, const json::Value& doc, DocBuild& db) {
                     contents->kind == json::Value::Object;
         if (isOp) {
             if (collab && sid == 0) return fail(MTE_E_UNSUPPORTED, "observer never submits ops (ack path)");
+            if (db.reused && base.ref_seq < db.cur_min) base.client = 255;  // refSeq below minSeq after a reuse
             int32_t t = -1;
             num_field(*contents, u"type", &t);
             if (t == 3) {
@@ -1785,6 +1814,7 @@ static int add_messages(mte_builder* b, const json::Value& doc, DocBuild& db) {
             ops.push_back(o);
         }
         ops.back().flags |= MTE_F_END_OF_MSG;
+        if (collab && base.msn > db.cur_min) db.cur_min = base.msn;  // setMinSeq after the message
     }
     return MTE_OK;
 }
@@ -1953,7 +1983,7 @@ static int summary_seg(mte_builder* b, DocBuild& db, const json::Value& sp, mte_
         hasSeq = num_field(sp, u"seq", &o.seq) != 0;
     }
     uint32_t cid;
-    if (int rc = db.short_id(client, &cid)) return rc;
+    if (int rc = db.short_id(client, &cid, o.seq)) return rc;
     o.client = (uint8_t)cid;
     if (js && num_field(sp, u"removedSeq", &o.ref_seq)) {
         o.flags |= MTE_F_LOAD_REMOVED;
@@ -1961,7 +1991,7 @@ static int summary_seg(mte_builder* b, DocBuild& db, const json::Value& sp, mte_
         std::string rn = rc && rc->kind == json::Value::String ? json::to_utf8(rc->str.data(), rc->str.size())
                                                                : kNonCollabName;
         uint32_t rid;
-        if (int e = db.short_id(rn, &rid)) return e;
+        if (int e = db.short_id(rn, &rid, o.ref_seq)) return e;
         o.pos1 = (int32_t)rid;
     }
     *info = js != nullptr;
@@ -1971,6 +2001,7 @@ static int summary_seg(mte_builder* b, DocBuild& db, const json::Value& sp, mte_
 
 static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db) {
     if (!db.collab) return db.fail(MTE_E_ARG, "a summary is loaded by a collaborating client (observer name)");
+    db.loading = true;  // no short-id reuse inside the load records
     const json::Value* t = &summary;
     const json::Value* content = tree_entry(summary, u"content");
     if (content && content->get(u"value")) t = content->get(u"value");  // SharedString summary (sequence.ts:413-438)
@@ -2135,6 +2166,8 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
         }
         flush();
     }
+    db.loading = false;
+    db.cur_min = std::max(db.cur_min, end.msn);  // startOrUpdateCollaboration(minSeq)
     // loadBodyAndCatchupOps (snapshotLoader.ts:55-77): one blob beyond the chunks holds catch-up
     // messages (legacy summaries), applied after the load like any sequenced message; any other blob
     // count is an error

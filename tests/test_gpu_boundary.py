@@ -14,23 +14,26 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "v1")
 
 
-def _log(n_writers, n=200):
+def _log(n_writers, n=200, window=True):
+    """window: msn follows the head (clients leave the collaboration window); otherwise msn stays 0."""
     out, L = [], 0
     for s in range(1, n + 1):
         w = f"w{(s - 1) % n_writers}"
+        msn = s - 1 if window else 0
         if L > 10 and s % 3 == 0:
-            out.append(msg(w, s, s - 1, rem(s % L, s % L + 2), s - 1))
+            out.append(msg(w, s, s - 1, rem(s % L, s % L + 2), msn))
             L -= 2
         else:
-            out.append(msg(w, s, s - 1, ins(s % (L + 1), f"{s % 10}"), s - 1))
+            out.append(msg(w, s, s - 1, ins(s % (L + 1), f"{s % 10}"), msn))
             L += 1
     return out
 
 
 def test_document_over_64_clients_fails_alone():
-    """A batch with one 70-writer document: mte_load succeeds, that document reports
-    MTE_DOC_UNSUPPORTED at the first op of its 64th writer (short id 64), the others replay exactly."""
-    logs = [_log(8), _log(70), _log(12)]
+    """A batch with one document of 70 writers all inside the collaboration window: mte_load
+    succeeds, that document reports MTE_DOC_UNSUPPORTED at the first op of its 64th writer (no slot
+    free), the others replay exactly (70 writers whose ops leave the window reuse slots)."""
+    logs = [_log(8), _log(70, window=False), _log(12), _log(70)]
     b = mte.Builder()
     for lg in logs:
         b.add_doc(lg)
@@ -43,7 +46,7 @@ def test_document_over_64_clients_fails_alone():
         code, seq = e.status(1)
         assert code == 4  # MTE_DOC_UNSUPPORTED
         assert seq == 64  # w63 is short id 64 (observer 0): its first message is seq 64
-        for d in (0, 2):
+        for d in (0, 2, 3):
             compare_doc(e, batch, d)
     finally:
         e.close()

@@ -1,0 +1,451 @@
+// SnapshotV1 emission on the device: SnapshotV1.extractSync + emit
+// (snapshotV1.ts:57-247, snapshotChunks.ts) over each document's final segments, which
+// Engine::finish gathered in document order (rows: vis / aux / overlap, the row's property map, the
+// text of every row). One wave per document:
+//   1. entries (extractSync, :170-228): removed segments at or below minSeq are elided; settled
+//      segments (seq <= minSeq, not removed) coalesce into the previous one when both are text,
+//      TextSegment.canAppend holds (no trailing '\n', either side <= 256 chars) and matchProperties
+//      holds; every other segment is a merge-info entry ({"json":…, seq/client above minSeq,
+//      removedSeq/removedClient});
+//   2. chunks (:108-168): entries fill a chunk until its length reaches `chunk` characters;
+//   3. bytes: the header blob (with headerMetadata) and body_i blobs, JSON exactly as
+//      JSON.stringify writes them (UTF-8; '"', '\\', control characters escaped, unpaired
+//      surrogates as \uXXXX; property objects in JS key order: array-index keys ascending, then
+//      insertion order).
+// The pass runs twice per list of documents: COUNT sizes every document's blobs (bytes, blob
+// count), the host lays the documents out in the output pool, WRITE fills them. Byte-oriented,
+// HBM-bound work: lanes encode 64 characters / copy 64 bytes per step, nothing is reshaped for MFMA.
+#include "wave_hip.hpp"
+#include "emit.h"
+
+namespace mte {
+using i64 = long long;
+
+namespace {
+
+struct Out {  // wave-uniform byte cursor; out == nullptr: count only
+    char* out;
+    u64 pos;
+};
+
+MTE_DEV void put_lit(Out& o, const char* s, u32 n) {
+    const u32 L = lane_id();
+    if (o.out)
+        for (u32 i = L; i < n; i += 64) o.out[o.pos + i] = s[i];
+    o.pos += n;
+}
+template <u32 N>
+MTE_DEV void put(Out& o, const char (&s)[N]) {
+    put_lit(o, s, N - 1);
+}
+MTE_DEV void put_bytes(Out& o, const char* src, u64 n) {
+    const u32 L = lane_id();
+    if (o.out)
+        for (u64 i = L; i < n; i += 64) o.out[o.pos + i] = src[i];
+    o.pos += n;
+}
+MTE_DEV void put_int(Out& o, i64 v) {  // Number::toString of an integer
+    const bool neg = v < 0;
+    u64 a = neg ? (u64)(-v) : (u64)v;
+    u32 nd = 1;
+    for (u64 t = a; t >= 10; t /= 10) nd++;
+    const u32 L = lane_id();
+    if (o.out) {
+        if (neg && L == 0) o.out[o.pos] = '-';
+        if (L < nd) {
+            u64 t = a;
+            for (u32 k = 0; k < nd - 1 - L; k++) t /= 10;
+            o.out[o.pos + (neg ? 1 : 0) + L] = (char)('0' + t % 10);
+        }
+    }
+    o.pos += nd + (neg ? 1 : 0);
+}
+
+MTE_DEV bool is_hi(u32 c) { return c >= 0xD800 && c < 0xDC00; }
+MTE_DEV bool is_lo(u32 c) { return c >= 0xDC00 && c < 0xE000; }
+
+// JSON string of n UTF-16 units (jsonlite.hpp quote, JSON.stringify's escaping), lane = unit
+MTE_DEV void put_quoted(Out& o, const u16* s, u64 n) {
+    const u32 L = lane_id();
+    if (o.out && L == 0) o.out[o.pos] = '"';
+    o.pos += 1;
+    static constexpr char hx[] = "0123456789abcdef";
+    for (u64 base = 0; base < n; base += 64) {
+        const u64 i = base + L;
+        const bool in = i < n;
+        const u32 c = in ? s[i] : 0u;
+        const u32 prev = in && i > 0 ? s[i - 1] : 0u;
+        const u32 next = in && i + 1 < n ? s[i + 1] : 0u;
+        u32 nb = 0;
+        if (in) {
+            if (c == '"' || c == '\\') nb = 2;
+            else if (c < 0x20) nb = (c == '\b' || c == '\f' || c == '\n' || c == '\r' || c == '\t') ? 2 : 6;
+            else if (is_hi(c)) nb = is_lo(next) ? 4 : 6;
+            else if (is_lo(c)) nb = is_hi(prev) ? 0 : 6;
+            else nb = c < 0x80 ? 1 : c < 0x800 ? 2 : 3;
+        }
+        const u32 incl = wave_scan_incl(nb);
+        if (o.out && nb) {
+            char* d = o.out + o.pos + (incl - nb);
+            if (c == '"' || c == '\\') {
+                d[0] = '\\';
+                d[1] = (char)c;
+            } else if (c < 0x20) {
+                if (nb == 2) {
+                    d[0] = '\\';
+                    d[1] = c == '\b' ? 'b' : c == '\f' ? 'f' : c == '\n' ? 'n' : c == '\r' ? 'r' : 't';
+                } else {
+                    d[0] = '\\'; d[1] = 'u'; d[2] = '0'; d[3] = '0';
+                    d[4] = hx[c >> 4]; d[5] = hx[c & 15];
+                }
+            } else if (nb == 6) {  // unpaired surrogate
+                d[0] = '\\'; d[1] = 'u';
+                d[2] = hx[(c >> 12) & 15]; d[3] = hx[(c >> 8) & 15]; d[4] = hx[(c >> 4) & 15]; d[5] = hx[c & 15];
+            } else if (nb == 4) {  // surrogate pair -> one 4-byte sequence
+                const u32 cp = 0x10000u + ((c - 0xD800u) << 10) + (next - 0xDC00u);
+                d[0] = (char)(0xF0 | (cp >> 18));
+                d[1] = (char)(0x80 | ((cp >> 12) & 0x3F));
+                d[2] = (char)(0x80 | ((cp >> 6) & 0x3F));
+                d[3] = (char)(0x80 | (cp & 0x3F));
+            } else if (nb == 1) {
+                d[0] = (char)c;
+            } else if (nb == 2) {
+                d[0] = (char)(0xC0 | (c >> 6));
+                d[1] = (char)(0x80 | (c & 0x3F));
+            } else {
+                d[0] = (char)(0xE0 | (c >> 12));
+                d[1] = (char)(0x80 | ((c >> 6) & 0x3F));
+                d[2] = (char)(0x80 | (c & 0x3F));
+            }
+        }
+        o.pos += wave_read(incl, 63);
+    }
+    if (o.out && L == 0) o.out[o.pos] = '"';
+    o.pos += 1;
+}
+
+struct Doc {
+    const EmitParams& p;
+    u32 d;
+    DocRes r;
+    u64 row0;  // first row in the output pool
+    MTE_DEV Doc(const EmitParams& pp, u32 dd) : p(pp), d(dd) {
+        r = p.res[d];
+        row0 = r.out_off;
+    }
+    MTE_DEV const u32* map(u64 row) const { return p.maps + row * MAP_WORDS; }
+    // matchProperties (properties.ts:62-93) on two rows' maps (host DocView::match_props)
+    MTE_DEV bool val_match(u32 a, u32 b) const {
+        if (a == b) return true;
+        if (p.val_flags[b] & 2u) {
+            const u32 j = p.val_objidx[b];
+            return j != NONE && ((p.val_objmatch[a] >> j) & 1ull);
+        }
+        return false;
+    }
+    MTE_DEV bool match(u64 ra, bool ha, u64 rb, bool hb) const {
+        if (!ha && !hb) return true;
+        if (!ha || !hb || !p.maps) return false;
+        const u32 *ma = map(ra), *mb = map(rb);
+        const u32 n = ma[0];
+        if (n != mb[0]) return false;
+        for (u32 i = 0; i < n; i++) {
+            bool found = false;
+            for (u32 q = 0; q < n; q++)
+                if (mb[1 + 2 * q] == ma[1 + 2 * i]) {
+                    if (!val_match(ma[2 + 2 * i], mb[2 + 2 * q])) return false;
+                    found = true;
+                }
+            if (!found) return false;
+        }
+        return true;
+    }
+    // {"k":v,...} in JS key order
+    MTE_DEV void put_props(Out& o, u64 row) const {
+        const u32* m = map(row);
+        const u32 n = m[0] < 7 ? m[0] : 7u;
+        u32 ord[7];
+        u32 k = 0;
+        // array-index keys ascending first (insertion sort of at most 7), then insertion order
+        for (u32 i = 0; i < n; i++) {
+            const u32 key = m[1 + 2 * i];
+            if (!p.key_is_index[key]) continue;
+            u32 j = k++;
+            while (j > 0 && p.key_index[m[1 + 2 * ord[j - 1]]] > p.key_index[key]) {
+                ord[j] = ord[j - 1];
+                j--;
+            }
+            ord[j] = i;
+        }
+        for (u32 i = 0; i < n; i++)
+            if (!p.key_is_index[m[1 + 2 * i]]) ord[k++] = i;
+        put(o, "{");
+        for (u32 q = 0; q < n; q++) {
+            if (q) put(o, ",");
+            const u32 key = m[1 + 2 * ord[q]], val = m[2 + 2 * ord[q]];
+            put_bytes(o, p.key_text + p.key_off[key], p.key_off[key + 1] - p.key_off[key]);
+            put(o, ":");
+            put_bytes(o, p.val_text + p.val_off[val], p.val_off[val + 1] - p.val_off[val]);
+        }
+        put(o, "}");
+    }
+    MTE_DEV void put_name(Out& o, u32 slot) const {  // getLongClientId, JSON-quoted
+        if (slot == NONE) {  // NonCollabClient
+            put(o, "\"original\"");
+            return;
+        }
+        const u64 i = (u64)p.name_base[d] + slot;
+        if (i >= p.name_base[d + 1]) {
+            put(o, "\"\"");
+            return;
+        }
+        put_bytes(o, p.names + p.name_off[i], p.name_off[i + 1] - p.name_off[i]);
+    }
+    MTE_DEV const u16* row_text(uint4 a) const { return p.text + r.text_off + a.y; }
+
+    // 1. entries: ent[row0 + k] = (first row, last row, length, kind) with kind 0 a settled text
+    // run, 1 a settled marker, 2 a merge-info segment; returns the entry count
+    MTE_DEV u32 build_entries() const {
+        const u32 L = lane_id(), n = r.n_segs;
+        const i32 minSeq = r.min_seq;
+        u32 ne = 0;
+        bool open = false, runText = false, runProps = false;
+        u32 runFirst = 0, runLast = 0, runLen = 0, runLast16 = 0;
+        auto close = [&]() {
+            if (open && L == 0) p.ent[row0 + ne] = make_uint4(runFirst, runLast, runLen, runText ? 0u : 1u);
+            ne += open ? 1u : 0u;
+            open = false;
+        };
+        for (u32 base = 0; base < n; base += 64) {
+            const u32 k = base + L;
+            uint4 v = make_uint4(0, 0, 0, 0), a = make_uint4(0, 0, 0, 0);
+            u32 last16 = 0;
+            if (k < n) {
+                v = p.vis[row0 + k];
+                a = p.aux[row0 + k];
+                if (!(v.w & F_MARKER) && v.x) last16 = row_text(a)[v.x - 1];
+            }
+            const u32 cnt = n - base < 64 ? n - base : 64u;
+            for (u32 j = 0; j < cnt; j++) {
+                const u32 len = wave_read(v.x, j), seq = wave_read(v.y, j), rseq = wave_read(v.z, j);
+                const u32 meta = wave_read(v.w, j), hasP = wave_read(a.x, j) != 0;
+                const bool removed = (meta & F_REMOVED) != 0, marker = (meta & F_MARKER) != 0;
+                const u32 row = base + j;
+                if (removed && (i32)rseq <= minSeq) continue;  // elided (:184-186)
+                if ((i32)seq <= minSeq && !removed) {
+                    if (open && runText && !marker && !(runLen && runLast16 == u'\n') &&
+                        (runLen <= 256 || len <= 256) && match(row0 + runFirst, runProps, row0 + row, hasP)) {
+                        runLast = row;  // clone + append (:197-202)
+                        runLen += len;
+                        if (len) runLast16 = wave_read(last16, j);
+                        continue;
+                    }
+                    close();
+                    open = true;
+                    runText = !marker;
+                    runProps = hasP;
+                    runFirst = runLast = row;
+                    runLen = len;
+                    runLast16 = wave_read(last16, j);
+                } else {
+                    close();
+                    if (L == 0) p.ent[row0 + ne] = make_uint4(row, row, len, 2u);
+                    ne++;
+                }
+            }
+        }
+        close();
+        return ne;
+    }
+
+    // the text of a settled run: its rows' text without the elided rows between them, gathered
+    // contiguously (in place when no elided text lies inside)
+    MTE_DEV const u16* run_text(uint4 e, u64& n) const {
+        const u32 L = lane_id();
+        const i32 minSeq = r.min_seq;
+        const uint4 a0 = p.aux[row0 + e.x];
+        const u16* first = row_text(a0);
+        bool contiguous = true;
+        for (u32 row = e.x + 1; row <= e.y && contiguous; row++) {
+            const uint4 v = p.vis[row0 + row];
+            contiguous = !((v.w & F_REMOVED) && (i32)v.z <= minSeq && !(v.w & F_MARKER) && v.x);
+        }
+        n = e.z;
+        if (contiguous) return first;
+        u16* dst = p.tscr + r.text_off + a0.y;
+        u64 at = 0;
+        for (u32 row = e.x; row <= e.y; row++) {
+            const uint4 v = p.vis[row0 + row];
+            if ((v.w & F_REMOVED) && (i32)v.z <= minSeq) continue;
+            const u16* src = row_text(p.aux[row0 + row]);
+            for (u32 i = L; i < v.x; i += 64) dst[at + i] = src[i];
+            at += v.x;
+        }
+        wave_sync();
+        return dst;
+    }
+    MTE_DEV void put_seg(Out& o, u32 row, const u16* txt, u64 n) const {  // Segment.toJSONObject
+        const uint4 v = p.vis[row0 + row], a = p.aux[row0 + row];
+        if (v.w & F_MARKER) {
+            put(o, "{\"marker\":{\"refType\":");
+            put_int(o, a.y & 0xFFFFu);
+            put(o, "}");
+            if (a.x) {
+                put(o, ",\"props\":");
+                put_props(o, row0 + row);
+            }
+            put(o, "}");
+        } else if (a.x) {
+            put(o, "{\"text\":");
+            put_quoted(o, txt, n);
+            put(o, ",\"props\":");
+            put_props(o, row0 + row);
+            put(o, "}");
+        } else {
+            put_quoted(o, txt, n);
+        }
+    }
+    MTE_DEV void put_entry(Out& o, uint4 e) const {
+        if (e.w == 0 || e.w == 1) {  // settled: coalesced text run or a marker
+            u64 n = 0;
+            const u16* t = e.w == 0 ? run_text(e, n) : nullptr;
+            put_seg(o, e.x, t, n);
+            return;
+        }
+        const uint4 v = p.vis[row0 + e.x], a = p.aux[row0 + e.x];
+        put(o, "{\"json\":");
+        put_seg(o, e.x, (v.w & F_MARKER) ? nullptr : row_text(a), (v.w & F_MARKER) ? 0 : v.x);
+        const bool collab = p.cfg[d].collab != 0;
+        if ((i32)v.y > r.min_seq) {
+            put(o, ",\"seq\":");
+            put_int(o, (i32)v.y);
+            put(o, ",\"client\":");
+            put_name(o, collab ? (v.w & 0xffu) : NONE);
+        }
+        if (v.w & F_REMOVED) {
+            put(o, ",\"removedSeq\":");
+            put_int(o, (i32)v.z);
+            put(o, ",\"removedClient\":");
+            put_name(o, collab ? ((v.w >> 8) & 0xffu) : NONE);
+        }
+        put(o, "}");
+    }
+
+    // 2 + 3: chunk plan and bytes; returns the byte count, blob starts into blob_off (WRITE)
+    MTE_DEV u64 emit(u32 ne, char* out, u64* blob_off, u32& nblobs) const {
+        const u32 L = lane_id();
+        const u32 chunk = p.chunk;
+        // chunk plan: count, total length, the header chunk's entries
+        u32 nch = 0, c0cnt = 0, c0len = 0;
+        u64 totalLen = 0;
+        {
+            u32 i = 0;
+            do {
+                u32 cnt = 0;
+                u64 len = 0;
+                while (len < chunk && i < ne) {
+                    len += p.ent[row0 + i].z;
+                    i++;
+                    cnt++;
+                }
+                if (nch == 0) {
+                    c0cnt = cnt;
+                    c0len = (u32)len;
+                }
+                nch++;
+                totalLen += len;
+            } while (i < ne);
+        }
+        nblobs = nch;
+        Out o{out, 0};
+        u32 i = 0;
+        for (u32 c = 0; c < nch; c++) {
+            if (blob_off && L == 0) blob_off[c] = o.pos;
+            // this chunk's entries
+            u32 cnt = 0;
+            u64 len = 0;
+            if (c == 0) {
+                cnt = c0cnt;
+                len = c0len;
+            } else {
+                for (u32 q = i; len < chunk && q < ne; q++) {
+                    len += p.ent[row0 + q].z;
+                    cnt++;
+                }
+            }
+            put(o, "{\"version\":\"1\",\"segmentCount\":");
+            put_int(o, cnt);
+            put(o, ",\"length\":");
+            put_int(o, (i64)len);
+            put(o, ",\"segments\":[");
+            for (u32 q = 0; q < cnt; q++) {
+                if (q) put(o, ",");
+                put_entry(o, p.ent[row0 + i + q]);
+            }
+            put(o, "],\"startIndex\":");
+            put_int(o, i);
+            if (c == 0) {
+                put(o, ",\"headerMetadata\":{\"minSequenceNumber\":");
+                put_int(o, r.min_seq);
+                put(o, ",\"sequenceNumber\":");
+                put_int(o, r.cur_seq);
+                put(o, ",\"orderedChunkMetadata\":[{\"id\":\"header\"}");
+                for (u32 b = 1; b < nch; b++) {
+                    put(o, ",{\"id\":\"body_");
+                    put_int(o, b - 1);
+                    put(o, "\"}");
+                }
+                put(o, "],\"totalLength\":");
+                put_int(o, (i64)totalLen);
+                put(o, ",\"totalSegmentCount\":");
+                put_int(o, ne);
+                put(o, "}");
+            }
+            put(o, "}");
+            i += cnt;
+        }
+        return o.pos;
+    }
+};
+
+}  // namespace
+
+// COUNT: entries, bytes and blob count of every listed document (status 0 only)
+__global__ __launch_bounds__(64) void k_emit_count(EmitParams p) {
+    const u32 i = blockIdx.x;
+    if (i >= p.n_list) return;
+    const u32 d = p.list[i];
+    Doc doc(p, d);
+    u32 ne = 0, nb = 0;
+    u64 bytes = 0;
+    if (doc.r.status == 0) {
+        ne = doc.build_entries();
+        wave_sync();  // entries written by lane 0, read by every lane
+        bytes = doc.emit(ne, nullptr, nullptr, nb);
+    }
+    if (lane_id() == 0) {
+        p.n_ent[d] = ne;
+        p.size[d] = bytes;
+        p.nblobs[d] = nb;
+    }
+}
+
+// WRITE: the blobs of every listed document at out + out_off[d], blob starts at blob_off + blob_base[d]
+__global__ __launch_bounds__(64) void k_emit_write(EmitParams p) {
+    const u32 i = blockIdx.x;
+    if (i >= p.n_list) return;
+    const u32 d = p.list[i];
+    Doc doc(p, d);
+    if (doc.r.status != 0 || p.size[d] == 0) return;
+    u32 nb = 0;
+    doc.emit(p.n_ent[d], p.out + p.out_off[d], p.blob_off + p.blob_base[d], nb);
+}
+
+hipError_t launch_emit(const EmitParams& p, bool write, hipStream_t s) {
+    if (p.n_list == 0) return hipSuccess;
+    void* args[] = {(void*)&p};
+    return hipLaunchKernel(write ? (const void*)k_emit_write : (const void*)k_emit_count, dim3(p.n_list), dim3(64),
+                           args, 0, s);
+}
+
+}  // namespace mte

@@ -29,6 +29,7 @@
 
 #include "../../include/mte.h"
 #include "../../include/mte_diag.h"
+#include "emit.h"
 #include "engine_types.hpp"
 #include "jsonlite.hpp"
 #include "mte_kernels.h"
@@ -250,6 +251,29 @@ struct mte_engine {
     uint32_t last_solo = 0;
     double last_solo_ms = 0;
     uint32_t n_groups = 256;
+    // SnapshotV1 emission on the device (emit.hip): property / name tables, scratch, and two output
+    // pools -- round 0 (every document but the solo ones) runs while the critical path is still
+    // replaying, round 1 (solo and host-re-run documents) after it
+    bool emit_opt = true;     // option "emit"
+    bool emit_tables = false; // tables uploaded for the current batch
+    DevBuf<char> d_key_text, d_val_text, d_names;
+    DevBuf<uint64_t> d_key_off, d_val_off, d_name_off, d_name_base, d_emit_size, d_out_off, d_blob_base;
+    DevBuf<unsigned char> d_key_is_index;
+    DevBuf<uint32_t> d_key_index, d_n_ent, d_nblobs, d_emit_list[2];
+    DevBuf<uint4> d_ent;
+    DevBuf<uint16_t> d_tscr;
+    struct EmitPool {
+        DevBuf<char> out;
+        DevBuf<uint64_t> blob_off;
+        uint64_t used = 0, blobs = 0;
+        std::vector<char> h;
+        std::vector<uint64_t> h_blob_off;
+    } pool[2];
+    std::vector<uint64_t> h_emit_size, h_out_off, h_blob_base;
+    std::vector<uint32_t> h_nblobs;
+    std::vector<uint8_t> emit_pool_of;  // per document: its pool, 255 = not emitted (failed / emission off)
+    bool emit_downloaded = false;
+    double last_emit_ms = 0;
     // downloaded final state
     std::vector<uint32_t> h_maps;
     std::vector<uint4> h_out_vis, h_out_aux;
@@ -593,6 +617,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     if (!e || !b) return MTE_E_ARG;
     HIP_TRY(e, hipSetDevice(e->device));
     e->hb.copy_from(b);
+    e->emit_tables = false;
     e->generated = false;
     e->host_ops_valid = true;
     e->replayed = e->downloaded = false;
@@ -639,6 +664,124 @@ static void doc_hbm_caps(uint64_t n, DocCfg& c, uint64_t& bytes) {
     bytes = HbmLayout::of(c.hb_blk, c.hb_ord, c.hb_in, c.hb_heap).bytes;
 }
 
+extern "C++" {
+template <class T>
+static hipError_t grow(DevBuf<T>& b, size_t n) {  // grow-only device buffer (contents not kept)
+    if (b.p && b.n >= n) return hipSuccess;
+    return b.alloc(std::max<size_t>(n, 1));
+}
+}
+
+// Property texts (interned JSON), key order data and every document's client names (JSON-quoted
+// UTF-8, by slot) for the emission kernels; once per loaded / generated batch.
+static int emit_tables(mte_engine* e) {
+    if (e->emit_tables) return MTE_OK;
+    const HostBatch& hb = e->hb;
+    const uint32_t nd = e->P.n_docs;
+    std::vector<char> names;
+    std::vector<uint64_t> off{0}, base;
+    for (uint32_t d = 0; d < nd; d++) {
+        base.push_back(off.size() - 1);
+        const uint32_t nc = hb.doc_client_offsets.size() > d + 1 ? hb.doc_client_offsets[d + 1] - hb.doc_client_offsets[d] : 0;
+        for (uint32_t c = 0; c < nc; c++) {
+            const std::string n = hb.client(d, c);
+            std::u16string u;
+            json::decode_utf8(n.data(), n.size(), u);
+            std::string q;
+            json::quote(q, u);
+            names.insert(names.end(), q.begin(), q.end());
+            off.push_back(names.size());
+        }
+    }
+    base.push_back(off.size() - 1);
+    std::vector<char> kt(hb.key_text.begin(), hb.key_text.end()), vt(hb.val_text.begin(), hb.val_text.end());
+    int rc;
+    if ((rc = upload(e, e->d_names, names)) || (rc = upload(e, e->d_name_off, off)) || (rc = upload(e, e->d_name_base, base)) ||
+        (rc = upload(e, e->d_key_text, kt)) || (rc = upload(e, e->d_key_off, hb.key_offsets)) ||
+        (rc = upload(e, e->d_val_text, vt)) || (rc = upload(e, e->d_val_off, hb.val_offsets)) ||
+        (rc = upload(e, e->d_key_is_index, e->key_is_index)) || (rc = upload(e, e->d_key_index, e->key_index)))
+        return rc;
+    HIP_TRY(e, grow(e->d_ent, e->P.out_cap));
+    HIP_TRY(e, grow(e->d_tscr, e->P.out_text_cap));
+    HIP_TRY(e, grow(e->d_n_ent, nd));
+    HIP_TRY(e, grow(e->d_nblobs, nd));
+    HIP_TRY(e, grow(e->d_emit_size, nd));
+    HIP_TRY(e, grow(e->d_out_off, nd));
+    HIP_TRY(e, grow(e->d_blob_base, nd));
+    e->h_emit_size.assign(nd, 0);
+    e->h_nblobs.assign(nd, 0);
+    e->h_out_off.assign(nd, 0);
+    e->h_blob_base.assign(nd, 0);
+    e->emit_tables = true;
+    return MTE_OK;
+}
+
+static EmitParams emit_params(mte_engine* e) {
+    EmitParams P{};
+    P.chunk = e->chunk;
+    P.res = e->d_res.p;
+    P.cfg = e->d_cfg.p;
+    P.vis = e->d_out_vis.p;
+    P.aux = e->d_out_aux.p;
+    P.maps = e->P.out_maps;
+    P.text = e->d_out_text.p;
+    P.key_text = e->d_key_text.p;
+    P.key_off = e->d_key_off.p;
+    P.key_is_index = e->d_key_is_index.p;
+    P.key_index = e->d_key_index.p;
+    P.val_text = e->d_val_text.p;
+    P.val_off = e->d_val_off.p;
+    P.val_flags = e->d_val_flags.p;
+    P.val_objidx = e->d_val_objidx.p;
+    P.val_objmatch = e->d_val_objmatch.p;
+    P.names = e->d_names.p;
+    P.name_off = e->d_name_off.p;
+    P.name_base = e->d_name_base.p;
+    P.ent = e->d_ent.p;
+    P.tscr = e->d_tscr.p;
+    P.n_ent = e->d_n_ent.p;
+    P.size = e->d_emit_size.p;
+    P.nblobs = e->d_nblobs.p;
+    P.out_off = e->d_out_off.p;
+    P.blob_base = e->d_blob_base.p;
+    return P;
+}
+
+// SnapshotV1 bytes of the listed documents into pool k on stream s: COUNT, lay the documents out,
+// WRITE. Returns with s drained (the host needs the sizes between the two kernels).
+static int emit_list(mte_engine* e, int k, const std::vector<uint32_t>& list, hipStream_t s) {
+    auto& pl = e->pool[k];
+    pl.used = pl.blobs = 0;
+    if (list.empty()) return MTE_OK;
+    const uint32_t nd = e->P.n_docs;
+    HIP_TRY(e, grow(e->d_emit_list[k], list.size()));
+    HIP_TRY(e, hipMemcpyAsync(e->d_emit_list[k].p, list.data(), list.size() * 4, hipMemcpyHostToDevice, s));
+    EmitParams P = emit_params(e);
+    P.list = e->d_emit_list[k].p;
+    P.n_list = (uint32_t)list.size();
+    HIP_TRY(e, launch_emit(P, false, s));
+    HIP_TRY(e, hipMemcpyAsync(e->h_emit_size.data(), e->d_emit_size.p, nd * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(e, hipMemcpyAsync(e->h_nblobs.data(), e->d_nblobs.p, nd * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(e, hipStreamSynchronize(s));
+    for (uint32_t d : list) {
+        if (!e->h_emit_size[d]) continue;
+        e->h_out_off[d] = pl.used;
+        pl.used += e->h_emit_size[d];
+        e->h_blob_base[d] = pl.blobs;
+        pl.blobs += e->h_nblobs[d];
+        e->emit_pool_of[d] = (uint8_t)k;
+    }
+    HIP_TRY(e, grow(pl.out, pl.used));
+    HIP_TRY(e, grow(pl.blob_off, pl.blobs));
+    HIP_TRY(e, hipMemcpyAsync(e->d_out_off.p, e->h_out_off.data(), nd * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(e, hipMemcpyAsync(e->d_blob_base.p, e->h_blob_base.data(), nd * 8, hipMemcpyHostToDevice, s));
+    P.out = pl.out.p;
+    P.blob_off = pl.blob_off.p;
+    HIP_TRY(e, launch_emit(P, true, s));
+    HIP_TRY(e, hipStreamSynchronize(s));
+    return MTE_OK;
+}
+
 static int run_kernel(mte_engine* e, bool gen) {
     HIP_TRY(e, hipSetDevice(e->device));
     const uint32_t nd = e->P.n_docs;
@@ -682,6 +825,17 @@ static int run_kernel(mte_engine* e, bool gen) {
         HIP_TRY(e, launch_hbmq(e->P, gen, full, nd, e->stream2));
         HIP_TRY(e, hipEventRecord(e->ev2, e->stream2));
         HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev2, 0));
+    }
+    const bool emit = !gen && e->emit_opt;
+    e->emit_downloaded = false;
+    int erc;
+    if (emit) {
+        if ((erc = emit_tables(e))) return erc;
+        e->emit_pool_of.assign(nd, 255);
+        // round 0: every document but the solo ones, while k_solo still replays the critical path
+        // (the documents the host re-runs are still DOC_SPILL here: COUNT skips them)
+        std::vector<uint32_t> bulk(e->order.begin() + std::min<uint32_t>(n_solo, nd), e->order.end());
+        if ((erc = emit_list(e, 0, bulk, e->stream))) return erc;
     }
     if (n_solo) HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev3, 0));
     HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
@@ -727,6 +881,18 @@ static int run_kernel(mte_engine* e, bool gen) {
     e->last_lds_ms = lds_ms;
     e->last_hbm_ms = hbm_ms;
     e->last_kernel_ms = (double)lds_ms + hbm_ms;
+    e->last_emit_ms = 0;
+    if (emit) {  // round 1: the solo documents and those the host re-ran
+        std::vector<uint32_t> rest(e->order.begin(), e->order.begin() + std::min<uint32_t>(n_solo, nd));
+        rest.insert(rest.end(), spill.begin(), spill.end());
+        HIP_TRY(e, hipEventRecord(e->ev0, e->stream));
+        if ((erc = emit_list(e, 1, rest, e->stream))) return erc;
+        HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
+        HIP_TRY(e, hipEventSynchronize(e->ev1));
+        float ms = 0;
+        HIP_TRY(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+        e->last_emit_ms = ms;
+    }
     e->res.resize(nd);
     HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nd * sizeof(DocRes), hipMemcpyDeviceToHost));
     e->replayed = true;
@@ -822,6 +988,7 @@ int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_o
     e->P.gen_seed = seed_base;
     e->P.gen_n_propsets = nps;
     e->gen_kind = kind;
+    e->emit_tables = false;  // names are known after the generator ran
     // kinds 2 and 5 draw no properties and no '\n'; short ids stay below 1 + n_clients
     e->lean_ok = kind != 3 && n_clients < 32;
     rc = run_kernel(e, true);
@@ -1008,100 +1175,6 @@ struct DocView {
             if (text) json::quote(o, *text); else json::quote(o, (const char16_t*)s.text, s.len);
         }
     }
-    // SnapshotV1.extractSync + emit (snapshotV1.ts:57-247)
-    std::vector<std::string> snapshot_blobs(uint32_t chunk) const {
-        const DocRes& r = e->res[d];
-        const int32_t minSeq = r.min_seq, curSeq = r.cur_seq;
-        std::vector<std::string> sj;
-        std::vector<uint32_t> sl;
-        const SegView* prev = nullptr;
-        std::u16string prevText;  // coalesced text of `prev`
-        uint32_t prevLen = 0;
-        auto push_prev = [&]() {
-            if (!prev) return;
-            std::string j;
-            seg_json(j, *prev, &prevText);
-            sj.push_back(std::move(j));
-            sl.push_back(prevLen);
-        };
-        for (const SegView& s : segs) {
-            if (s.removed && s.rseq <= minSeq) continue;  // elided (:184-186)
-            if (s.seq <= minSeq && !s.removed) {
-                if (!prev) {
-                    prev = &s;
-                    prevText.assign((const char16_t*)s.text, s.kind ? 0 : s.len);
-                    prevLen = s.len;
-                } else if (prev->kind == 0 && s.kind == 0 && !(prevLen && prevText.back() == u'\n') &&
-                           (prevLen <= 256 || s.len <= 256) && match_props(prev->props, s.props)) {
-                    prevText.append((const char16_t*)s.text, s.len);  // clone + append (:197-202)
-                    prevLen += s.len;
-                } else {
-                    push_prev();
-                    prev = &s;
-                    prevText.assign((const char16_t*)s.text, s.kind ? 0 : s.len);
-                    prevLen = s.len;
-                }
-            } else {
-                push_prev();
-                prev = nullptr;
-                std::string raw = "{\"json\":";
-                seg_json(raw, s, nullptr);
-                if (s.seq > minSeq) {
-                    raw += ",\"seq\":" + json::number(s.seq) + ",\"client\":";
-                    std::string c = long_id(s.client);
-                    std::u16string cu;
-                    json::decode_utf8(c.data(), c.size(), cu);
-                    json::quote(raw, cu);
-                }
-                if (s.removed) {
-                    raw += ",\"removedSeq\":" + json::number(s.rseq) + ",\"removedClient\":";
-                    std::string c = long_id(s.rclient);
-                    std::u16string cu;
-                    json::decode_utf8(c.data(), c.size(), cu);
-                    json::quote(raw, cu);
-                }
-                raw += "}";
-                sj.push_back(std::move(raw));
-                sl.push_back(s.len);
-            }
-        }
-        push_prev();
-        struct Chunk {
-            size_t start, count;
-            uint64_t length;
-        };
-        std::vector<Chunk> chunks;
-        size_t total = 0;
-        uint64_t totalLen = 0;
-        do {
-            Chunk c{total, 0, 0};
-            while (c.length < chunk && c.start + c.count < sj.size()) c.length += sl[c.start + c.count++];
-            chunks.push_back(c);
-            total += c.count;
-            totalLen += c.length;
-        } while (total < sj.size());
-        std::vector<std::string> blobs;
-        for (size_t i = 0; i < chunks.size(); i++) {
-            const Chunk& c = chunks[i];
-            std::string o = "{\"version\":\"1\",\"segmentCount\":" + std::to_string(c.count) +
-                            ",\"length\":" + std::to_string(c.length) + ",\"segments\":[";
-            for (size_t q = 0; q < c.count; q++) {
-                if (q) o.push_back(',');
-                o += sj[c.start + q];
-            }
-            o += "],\"startIndex\":" + std::to_string(c.start);
-            if (i == 0) {
-                o += ",\"headerMetadata\":{\"minSequenceNumber\":" + json::number(minSeq) +
-                     ",\"sequenceNumber\":" + json::number(curSeq) + ",\"orderedChunkMetadata\":[{\"id\":\"header\"}";
-                for (size_t b = 1; b < chunks.size(); b++) o += ",{\"id\":\"body_" + std::to_string(b - 1) + "\"}";
-                o += "],\"totalLength\":" + std::to_string(totalLen) + ",\"totalSegmentCount\":" +
-                     std::to_string(total) + "}";
-            }
-            o += "}";
-            blobs.push_back(std::move(o));
-        }
-        return blobs;
-    }
     std::u16string text() const {
         std::u16string t;
         for (auto& s : segs)
@@ -1250,6 +1323,35 @@ int mte_segments_json(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t
 // SharedSegmentSequence.snapshotCore (sequence.ts:413-438): the interval-collection blob "header"
 // (MapKernel.serialize of no collections: "{}"; interval ops are outside the path) and the merge-tree
 // ITree as "content".
+// The SnapshotV1 blobs the device wrote (emit.hip), downloaded once per replay on first use.
+static int ensure_emit_download(mte_engine* e) {
+    if (e->emit_downloaded) return MTE_OK;
+    HIP_TRY(e, hipSetDevice(e->device));
+    for (auto& pl : e->pool) {
+        pl.h.resize(pl.used);
+        pl.h_blob_off.resize(pl.blobs);
+        if (pl.used) HIP_TRY(e, hipMemcpy(pl.h.data(), pl.out.p, pl.used, hipMemcpyDeviceToHost));
+        if (pl.blobs) HIP_TRY(e, hipMemcpy(pl.h_blob_off.data(), pl.blob_off.p, pl.blobs * 8, hipMemcpyDeviceToHost));
+    }
+    e->emit_downloaded = true;
+    return MTE_OK;
+}
+// Document d's blobs as (pointer, length); MTE_E_STATE when it has none (failed, or emission off).
+static int doc_blobs(mte_engine* e, uint32_t d, std::vector<std::pair<const char*, size_t>>& out) {
+    out.clear();
+    int rc = ensure_emit_download(e);
+    if (rc) return rc;
+    if (d >= e->emit_pool_of.size() || e->emit_pool_of[d] == 255)
+        return set_err(e, MTE_E_STATE, "no SnapshotV1 for this document (replay failed, or option emit is 0)");
+    const auto& pl = e->pool[e->emit_pool_of[d]];
+    const uint64_t o = e->h_out_off[d], n = e->h_emit_size[d], b0 = e->h_blob_base[d], nb = e->h_nblobs[d];
+    for (uint64_t b = 0; b < nb; b++) {
+        const uint64_t s0 = pl.h_blob_off[b0 + b], s1 = b + 1 < nb ? pl.h_blob_off[b0 + b + 1] : n;
+        out.emplace_back(pl.h.data() + o + s0, (size_t)(s1 - s0));
+    }
+    return MTE_OK;
+}
+
 int mte_snapshot_shared_string(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len) {
     size_t n = 0;
     int rc = mte_snapshot_v1(e, doc, nullptr, 0, &n, nullptr);
@@ -1267,17 +1369,18 @@ int mte_snapshot_shared_string(mte_engine* e, uint32_t doc, char* buf, size_t ca
 }
 
 int mte_snapshot_v1(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len, uint32_t* n_blobs) {
-    DocView v;
-    int rc = doc_view(e, doc, v);
+    if (!e) return MTE_E_ARG;
+    if (doc >= e->P.n_docs) return set_err(e, MTE_E_RANGE, "doc index out of range");
+    std::vector<std::pair<const char*, size_t>> blobs;
+    int rc = doc_blobs(e, doc, blobs);
     if (rc) return rc;
-    auto blobs = v.snapshot_blobs(e->chunk);
     std::string o = "{\"entries\":[";
     for (size_t i = 0; i < blobs.size(); i++) {
         if (i) o += ",";
         std::string path = i == 0 ? "header" : "body_" + std::to_string(i - 1);
         o += "{\"mode\":\"100644\",\"path\":\"" + path + "\",\"type\":\"Blob\",\"value\":{\"contents\":";
         std::u16string bu;
-        json::decode_utf8(blobs[i].data(), blobs[i].size(), bu);
+        json::decode_utf8(blobs[i].first, blobs[i].second, bu);
         json::quote(o, bu);
         o += ",\"encoding\":\"utf-8\"}}";
     }
@@ -1296,8 +1399,10 @@ int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap) {
     if (rc) return rc;
     const uint32_t nd = e->P.n_docs;
     if (cap < nd) return MTE_E_RANGE;
+    if ((rc = ensure_emit_download(e))) return rc;
     std::atomic<uint32_t> next{0};
     auto work = [&]() {
+        std::vector<std::pair<const char*, size_t>> blobs;
         for (uint32_t d; (d = next.fetch_add(1)) < nd;) {
             DocView v;
             v.e = e;
@@ -1307,11 +1412,16 @@ int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap) {
             std::string t8 = json::to_utf8(t.data(), t.size());
             uint64_t h = fnv1a(0xcbf29ce484222325ull, t8.data(), t8.size());
             uint32_t sb = 0;
-            for (auto& b : v.snapshot_blobs(e->chunk)) {
-                uint8_t z = 0;
-                h = fnv1a(h, &z, 1);
-                h = fnv1a(h, b.data(), b.size());
-                sb += (uint32_t)b.size();
+            if (e->res[d].status == 0 && e->emit_pool_of.size() > d && e->emit_pool_of[d] != 255) {
+                const auto& pl = e->pool[e->emit_pool_of[d]];
+                const uint64_t o = e->h_out_off[d], n = e->h_emit_size[d], b0 = e->h_blob_base[d], nb = e->h_nblobs[d];
+                for (uint64_t b = 0; b < nb; b++) {
+                    const uint64_t s0 = pl.h_blob_off[b0 + b], s1 = b + 1 < nb ? pl.h_blob_off[b0 + b + 1] : n;
+                    uint8_t z = 0;
+                    h = fnv1a(h, &z, 1);
+                    h = fnv1a(h, pl.h.data() + o + s0, s1 - s0);
+                }
+                sb = (uint32_t)n;
             }
             mte_doc_summary& s = out[d];
             s.checksum = h;
@@ -1503,6 +1613,7 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "solo_max") e->solo_max = (uint32_t)std::max<int64_t>(0, value);
     else if (k == "solo_min_ops") e->solo_min_ops = (uint64_t)std::max<int64_t>(1, value);
     else if (k == "lean") e->lean_opt = value != 0;
+    else if (k == "emit") e->emit_opt = value != 0;  // SnapshotV1 emission on the device after replay
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
 }
@@ -1520,6 +1631,7 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "slots") *value = e->n_slots;
     else if (k == "solo") *value = e->last_solo;
     else if (k == "lean") *value = e->last_lean;
+    else if (k == "emit_us") *value = (int64_t)(e->last_emit_ms * 1000.0);  // emission after the replay pass
     else if (k == "out_text") {  // UTF-16 units Engine::finish gathered (counters[6..7])
         uint32_t ctr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (e->d_counters.p) HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));

@@ -1,0 +1,71 @@
+"""GPU: SnapshotV1 emission on the device (emit.hip) -- JSON escaping (quotes, backslashes, control
+characters, non-ASCII, surrogate pairs split across segments, lone surrogates), coalesced runs across
+elided segments, property objects in JS key order, merge-info entries with client names, chunking --
+byte-identical to the oracle's SnapshotV1 (snapshotV1.ts:57-247 restated)."""
+import ctypes
+import json
+
+import pytest
+
+from fluidframework_amd import mte
+from oracle import OracleDoc
+from tests.gpu_helpers import compare_doc
+from tests.oplog import ann, ins, msg, rem
+
+TEXTS = ['a"b\\c', "\u0001\t\n\b\f\r", "é漢字", "\ud83d", "\ude00", "x\ud800y", "\udfff", "ok", "\U0001F600z"]
+
+
+def escape_log(collab):
+    out, seq, L = [], 0, 0
+    for i, t in enumerate(TEXTS * 3):
+        seq += 1
+        w = f"w{i % 3}" if collab else "local"
+        out.append(msg(w, seq, seq - 1, ins(L, t), max(0, seq - 4) if collab else 0))
+        L += len(t.encode("utf-16-le", "surrogatepass")) // 2
+    seq += 1
+    out.append(msg("w0" if collab else "local", seq, seq - 1, ann(0, 6, {"b": 1, "7": True, "2": "s", "a": None}),
+                   max(0, seq - 4) if collab else 0))
+    seq += 1
+    out.append(msg("w1" if collab else "local", seq, seq - 1, rem(3, 9), max(0, seq - 4) if collab else 0))
+    return out
+
+
+def test_escape_logs_records_match_json():
+    """CPU: the builder carries lone surrogates and escapes through (oracle record path = JSON path)."""
+    log = escape_log(True)
+    b = mte.Builder()
+    b.add_doc(json.dumps(log))
+    batch = b.batch()
+    obs = "__observer__"
+    a, z = OracleDoc(obs), OracleDoc(obs)
+    a.apply_json(json.dumps(log))
+    z.apply_batch(ctypes.addressof(batch), 0)
+    assert a.status()[0] == z.status()[0] == 0
+    assert a.snapshot_json() == z.snapshot_json()
+    snap = a.snapshot_json()
+    assert "\\\\ud800" in snap and "\U0001F600" in snap  # a lone surrogate stays escaped, a split pair joins
+
+
+@pytest.mark.gpu
+def test_emission_escapes_and_runs():
+    logs = [escape_log(False), escape_log(True)]
+    b = mte.Builder()
+    b.add_doc(json.dumps(logs[0]), observer="")  # ensure_ascii: lone surrogates travel as \\uXXXX
+    b.add_doc(json.dumps(logs[1]))
+    batch = b.batch()
+    e = mte.Engine(0)
+    try:
+        e.load(batch)
+        e.replay()
+        compare_doc(e, batch, 0, observer=None)
+        compare_doc(e, batch, 1)
+        e.set_option("emit", 0)
+        e.replay()
+        with pytest.raises(mte.MteError):
+            e.snapshot_json(0)
+        e.set_option("emit", 1)
+        e.replay()
+        compare_doc(e, batch, 1)
+        assert e.get_info("emit_us") >= 0
+    finally:
+        e.close()

@@ -196,7 +196,8 @@ def run(args):
     snap_bytes = int(summ["snapshot_bytes"].sum())
 
     # roofline of the replay pass: algorithmic bytes per launch / HIP-event pass time
-    alg_bytes = n_ops_rank * (OP_RECORD_B + LEAF_BLOCK_B) + payload_chars  # 1 B/char ASCII payload
+    # + the SnapshotV1 bytes the pass emits (emit.hip, inside the timed step)
+    alg_bytes = n_ops_rank * (OP_RECORD_B + LEAF_BLOCK_B) + payload_chars + snap_bytes  # 1 B/char ASCII payload
     kernel_ms = sum(kms) / len(kms)
     achieved = alg_bytes / (kernel_ms / 1000.0) / 1e9
     traffic = None
@@ -268,7 +269,7 @@ def run(args):
                        "ops_per_step": total_ops, "clients": args.clients, "parallelism": f"doc-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "replay pass: mte::k_solo + mte::k_lds + mte::k_hbmq (concurrent streams)",
+                         "kernel": "replay pass: mte::k_solo + mte::k_lds + mte::k_hbmq (concurrent streams) + SnapshotV1 emission (mte::k_emit_count/k_emit_write, overlapped with k_solo)",
                          "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "extra": {"ops_per_step_rank0": ops_applied, "longest_doc_ops": int(counts.max()),

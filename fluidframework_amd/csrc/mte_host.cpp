@@ -828,10 +828,11 @@ static int run_kernel(mte_engine* e, bool gen) {
     }
     const bool emit = !gen && e->emit_opt;
     e->emit_downloaded = false;
+    e->emit_pool_of.assign(nd, 255);
+    e->pool[0].used = e->pool[0].blobs = e->pool[1].used = e->pool[1].blobs = 0;
     int erc;
     if (emit) {
         if ((erc = emit_tables(e))) return erc;
-        e->emit_pool_of.assign(nd, 255);
         // round 0: every document but the solo ones, while k_solo still replays the critical path
         // (the documents the host re-runs are still DOC_SPILL here: COUNT skips them)
         std::vector<uint32_t> bulk(e->order.begin() + std::min<uint32_t>(n_solo, nd), e->order.end());

@@ -9,7 +9,6 @@ import pytest
 
 from fluidframework_amd import mte
 from oracle import OracleDoc
-from tests.gpu_helpers import compare_doc
 from tests.oplog import ann, ins, msg, rem
 
 TEXTS = ['a"b\\c', "\u0001\t\n\b\f\r", "é漢字", "\ud83d", "\ude00", "x\ud800y", "\udfff", "ok", "\U0001F600z"]
@@ -48,24 +47,31 @@ def test_escape_logs_records_match_json():
 
 @pytest.mark.gpu
 def test_emission_escapes_and_runs():
-    logs = [escape_log(False), escape_log(True)]
+    """(Local, non-collaborative emission is pinned byte-for-byte by the reference's v1 fixtures,
+    test_gpu_parity.py::test_v1_golden_fixtures_on_gpu.)"""
     b = mte.Builder()
-    b.add_doc(json.dumps(logs[0]), observer="")  # ensure_ascii: lone surrogates travel as \\uXXXX
-    b.add_doc(json.dumps(logs[1]))
+    b.add_doc(json.dumps(escape_log(True)))  # ensure_ascii: lone surrogates travel as \\uXXXX
+    b.add_doc(json.dumps(escape_log(True)[:-1]))
     batch = b.batch()
     e = mte.Engine(0)
     try:
         e.load(batch)
         e.replay()
-        compare_doc(e, batch, 0, observer=None)
-        compare_doc(e, batch, 1)
+        for d in range(2):  # text() is not compared: lone surrogates have no UTF-8 form to compare by
+            o = OracleDoc()
+            o.apply_batch(ctypes.addressof(batch), d)
+            assert e.status(d)[0] == o.status()[0] == 0
+            assert e.segments_json(d) == o.segments_json()
+            assert e.snapshot_json(d) == o.snapshot_json(), d
         e.set_option("emit", 0)
         e.replay()
         with pytest.raises(mte.MteError):
             e.snapshot_json(0)
         e.set_option("emit", 1)
         e.replay()
-        compare_doc(e, batch, 1)
+        o = OracleDoc()
+        o.apply_batch(ctypes.addressof(batch), 1)
+        assert e.snapshot_json(1) == o.snapshot_json()
         assert e.get_info("emit_us") >= 0
     finally:
         e.close()

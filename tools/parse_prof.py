@@ -7,7 +7,7 @@ import sys
 
 # the replay pass: solo workgroups, LDS workgroups and HBM-resident waves, launched together on three
 # streams
-KERNELS = ("k_solo<false>", "k_lds<false>", "k_hbmq<false>")
+KERNELS = ("k_solo<false", "k_lds<false", "k_hbmq<false", "k_emit_count", "k_emit_write")
 
 
 def rows(pattern):
@@ -36,23 +36,32 @@ def main(tag, config="C4"):
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace if k in r["Kernel_Name"]]
         if durs:
             summary[f"{k}_avg_ms_trace"] = sum(durs) / len(durs) / 1e6
-    # pass time: first start to last end of the pass's kernels, in dispatch order
-    per = [sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in trace if k in r["Kernel_Name"])
-           for k in KERNELS]
-    per = [x for x in per if x]
-    if per and all(len(x) == len(per[0]) for x in per):
-        passes = [max(x[i][1] for x in per) - min(x[i][0] for x in per) for i in range(len(per[0]))]
+    # pass time: from the pass's first kernel start to its last kernel end; passes are told apart by
+    # the dispatches of their first kernel (k_solo when the batch has critical-path documents)
+    evts = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in trace
+                  if any(k in r["Kernel_Name"] for k in KERNELS))
+    anchor = "k_solo<false" if any("k_solo<false" in e[2] for e in evts) else "k_lds<false"
+    starts = [e[0] for e in evts if anchor in e[2]]
+    passes = []
+    for i, a in enumerate(starts):
+        lo = a - 50_000_000  # the other streams' first kernels start within 50 ms of the anchor
+        hi = starts[i + 1] - 50_000_000 if i + 1 < len(starts) else float("inf")
+        win = [e for e in evts if lo <= e[0] < hi]
+        passes.append(max(e[1] for e in win) - min(e[0] for e in win))
+    if passes:
         summary["replay_pass_avg_ms_trace"] = sum(passes) / len(passes) / 1e6
     for cname in ("FETCH_SIZE", "WRITE_SIZE"):
         pm = rows(f"{base}/pmc_{'fetch' if cname == 'FETCH_SIZE' else 'write'}/**/*counter_collection.csv")
-        # per pass: the counters of one dispatch of each pass kernel (rocprofv3 serialises dispatches
-        # while it collects counters, so k_lds then takes every document k_solo does not)
+        # per pass: every dispatch of the pass kernels / the number of passes (rocprofv3 serialises
+        # dispatches while it collects counters, so k_lds then takes every document k_solo does not;
+        # the emission kernels run twice per pass)
+        n_pass = len({r["Dispatch_Id"] for r in pm if anchor in r["Kernel_Name"] and r["Counter_Name"] == cname})
         tot = 0.0
         for k in KERNELS:
             vals = [float(r["Counter_Value"]) for r in pm if k in r["Kernel_Name"] and r["Counter_Name"] == cname]
-            if vals:
-                summary[f"{cname}_kib_{k}"] = sum(vals) / len(vals)
-                tot += sum(vals) / len(vals)
+            if vals and n_pass:
+                summary[f"{cname}_kib_{k}"] = sum(vals) / n_pass
+                tot += sum(vals) / n_pass
         if tot:
             summary[cname + "_kib_per_launch"] = tot
     if "FETCH_SIZE_kib_per_launch" in summary and "WRITE_SIZE_kib_per_launch" in summary:

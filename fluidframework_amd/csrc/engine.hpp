@@ -512,8 +512,26 @@ struct Engine {
         const u32 cz = C == 0 ? 1u : 0u;
         const bool fast = !valid | (cz != 0) | ((i32)o.z <= R);
         u32 v = valid ? o.y : 0u;
-        if (wave_ballot(!fast)) {
+        const u64 dm = wave_ballot(!fast);
+        if (dm) {
             MTE_PROF(PF_BLEN_DIRTY);
+#ifndef MTE_OLD_BLEN
+            if (!(dm & (dm - 1))) {
+                // one dirty block (the common case): lane = slot, one conflict-free LDS read per lane
+                // instead of every lane reading 8 slots of its own block (the 128-B block stride
+                // puts all 64 lanes on 2 bank groups)
+                const u32 j = (u32)__builtin_ctzll(dm);
+                const u32 bj = wave_read(o.x, j), cj = wave_read(o.w, j);
+                const u32 bb = bj < blk_cap() ? bj : 0u;
+                const u32 s = L & 7u;
+                const u32 idx = bb * 8 + s;
+                const uint4 q1 = VIS()[idx];
+                const u32 z1 = AUX()[idx].z;
+                const u32 sv1 = (L < 8 && s < cj) ? vis_len(q1, z1, idx, R, C, cz) : 0u;
+                const u32 tot = wave_read(group8_scan(sv1), 7);
+                return L == j ? tot : v;
+            }
+#endif
             const u32 b = o.x < blk_cap() ? o.x : 0u;
             uint4 q[8];
 #ifdef MTE_MASK_BLEN

@@ -39,11 +39,19 @@ enum ProfSlot : u32 {
     PF_SCOUR_CHAIN, PF_SCOUR_WRITE, PF_LOOP, PN_INS, PN_REM
 };
 #ifdef MTE_PROFILE
+// MTE_PROF_ONLY=<slot>: time that one phase only (every s_memtime scope and counter atomic perturbs
+// a lone wave, so a full phase profile overstates the small phases); the op count stays on
+#ifdef MTE_PROF_ONLY
+#define MTE_PON(slot) ((slot) == MTE_PROF_ONLY)
+#else
+#define MTE_PON(slot) true
+#endif
 // counters accumulate straight into the per-document HBM record (fire-and-forget atomics: no
 // registers held across the engine, which runs at its 128-VGPR bound)
-#define MTE_COUNT(slot, n)                                    \
-    do {                                                      \
-        if (lane_id() == 0) atomicAdd(prof + (slot), (u64)(n)); \
+#define MTE_COUNT(slot, n)                                                          \
+    do {                                                                            \
+        if (MTE_PON(slot) || (slot) == PF_OPS)                                      \
+            if (lane_id() == 0) atomicAdd(prof + (slot), (u64)(n));                 \
     } while (0)
 #else
 #define MTE_COUNT(slot, n) \
@@ -51,16 +59,20 @@ enum ProfSlot : u32 {
     } while (0)
 #endif
 #ifdef MTE_PROFILE
-struct ProfScope {
+template <bool ON>
+struct ProfScopeT {
     u64* acc;
     u64 t0;
-    MTE_DEV ProfScope(u64* a) : acc(a), t0(__builtin_amdgcn_s_memtime()) {}
-    MTE_DEV ~ProfScope() {
-        const u64 dt = __builtin_amdgcn_s_memtime() - t0;
-        if (lane_id() == 0) atomicAdd(acc, dt);
+    MTE_DEV ProfScopeT(u64* a) : acc(a), t0(ON ? __builtin_amdgcn_s_memtime() : 0) {}
+    MTE_DEV ~ProfScopeT() {
+        if (ON) {
+            const u64 dt = __builtin_amdgcn_s_memtime() - t0;
+            if (lane_id() == 0) atomicAdd(acc, dt);
+        }
     }
 };
-#define MTE_PROF(slot) ProfScope _prof_scope_##slot(prof + (slot))
+typedef ProfScopeT<true> ProfScope;
+#define MTE_PROF(slot) ProfScopeT<MTE_PON(slot)> _prof_scope_##slot(prof + (slot))
 #elif defined(MTE_MARKERS)
 // static code-size analysis (tools/asm_regions.py): phase scopes as assembly comments
 template <u32 S>
@@ -610,7 +622,7 @@ struct Engine {
         fence_ovl();
         i32 cum = 0;
 #ifdef MTE_PROFILE
-        ProfScope _rb(prof + PF_RES_BLOCKS);
+        MTE_PROF(PF_RES_BLOCKS);
 #endif
         for (u32 base = 0; base < st.n_lb; base += 64) {
             const u32 k = base + L;
@@ -633,6 +645,34 @@ struct Engine {
             cum += (i32)wave_read(incl, 63);
         }
         if (!f.ok) return f;
+        resolve_slot(f, pos, R, C);
+        return f;
+    }
+    // The block of `pos` from one block scan already held per lane (lane = doc-order index, n_lb <= 64:
+    // o, its visible length v and the inclusive prefix incl), then the slot inside it. The block's child
+    // count is re-read (a split since the scan may have added a slot; block splits invalidate the scan).
+    MTE_DEV Found resolve_pre(uint4 o, u32 v, u32 incl, i32 pos, i32 R, u32 C) {
+        Found f;
+        f.ok = false;
+        f.k = 0;
+        f.blk = NONE;
+        f.cnt = 0;
+        f.slot = -1;
+        f.r = 0;
+        f.cum = 0;
+        fence_ovl();
+        const u64 hit = wave_ballot(L < st.n_lb && (i32)incl >= pos);
+        if (!hit) return f;
+        const u32 j = (u32)__builtin_ctzll(hit);
+        f.ok = true;
+        f.k = j;
+        f.blk = wave_read(o.x, j);
+        f.cnt = U(ORD()[j].w);
+        f.cum = (i32)wave_read(incl - v, j);
+        resolve_slot(f, pos, R, C);
+        return f;
+    }
+    MTE_DEV void resolve_slot(Found& f, i32 pos, i32 R, u32 C) {
         MTE_PROF(PF_RES_SLOT);
         // inside the block: first slot with r < vislen, or a zero-visible slot at r == 0 that wins breakTie
         const u32 s = L;
@@ -652,7 +692,6 @@ struct Engine {
             f.slot = (i32)l2;
             f.r = wave_read(r, l2);
         }
-        return f;
     }
 
     MTE_DEV i32 get_length(i32 R, u32 C) {  // MergeTree.getLength (mergeTree.ts:1577-1579)
@@ -1467,7 +1506,7 @@ struct Engine {
         u32 kSrc = 0, kLen = 0, kOff = 0, kCap = 0;  // lane i < nkeep: kept slot i
         Jobs jb;
 #ifdef MTE_PROFILE
-        u64 _tc0 = __builtin_amdgcn_s_memtime();
+        u64 _tc0 = MTE_PON(PF_SCOUR_CHAIN) ? __builtin_amdgcn_s_memtime() : 0;
 #endif
         for (u32 attempt = 0; attempt < 2; attempt++) {
             nkeep = 0;
@@ -1558,8 +1597,8 @@ struct Engine {
             if (act) me = load(blk, L);
         }
 #ifdef MTE_PROFILE
-        if (L == 0) atomicAdd(prof + PF_SCOUR_CHAIN, __builtin_amdgcn_s_memtime() - _tc0);
-        ProfScope _sw(prof + PF_SCOUR_WRITE);
+        if (MTE_PON(PF_SCOUR_CHAIN) && L == 0) atomicAdd(prof + PF_SCOUR_CHAIN, __builtin_amdgcn_s_memtime() - _tc0);
+        MTE_PROF(PF_SCOUR_WRITE);
 #endif
         if (jb.n) run_jobs(jb);
         Seg out = load(blk, L < nkeep ? kSrc : 0u);  // the kept slots, re-read (not yet overwritten)
@@ -1790,13 +1829,27 @@ struct Engine {
         const u32 nphase = ins ? 2u : 3u;
         Found known;  // insert after a split: the insertion point follows from the split (below)
         known.ok = false;
+        // remove / annotate: ONE block scan serves both boundaries and the mark pass while the block
+        // layout it saw holds (a boundary split that splits its block 8 -> 4+4 changes n_lb: the later
+        // phases scan again); blocks keep their visible lengths across a boundary split
+        uint4 po = make_uint4(0, 0, 0, 0);
+        u32 pv = 0, pincl = 0, pn = NONE;
+        if (!ins && st.n_lb <= 64) {
+            fence_ovl();
+            const bool valid = L < st.n_lb;
+            po = valid ? ORD()[L] : make_uint4(0, 0, 0, 0);
+            pv = blen_all(po, valid, R, C);
+            pincl = wave_scan_incl(pv);
+            pn = st.n_lb;
+        }
         for (u32 ph = 0; ph < nphase; ph++) {
             if (!ins && ph == 2) {
-                range_op(type == MTE_OP_REMOVE, p1, p2, R, C, seq, propset, rewrite);
+                range_op(type == MTE_OP_REMOVE, p1, p2, R, C, seq, propset, rewrite, pn == st.n_lb, pv, pincl);
                 return st.status == 0;
             }
             const bool place = ins && ph == 1;
-            const Found f = known.ok ? known : resolve(ph == 1 && !ins ? p2 : p1, R, C);
+            const i32 pos = ph == 1 && !ins ? p2 : p1;
+            const Found f = known.ok ? known : (pn == st.n_lb ? resolve_pre(po, pv, pincl, pos, R, C) : resolve(pos, R, C));
             if (!f.ok) {
                 if (ins) {
                     fail(MTE_DOC_INSERT_FAILED, seq);
@@ -1879,7 +1932,9 @@ struct Engine {
 
     // markRangeRemoved / annotateRange mark pass (nodeMap, mergeTree.ts:2903-2965): positions are
     // those of the (R, C) view before the op; blocks overlapping [p1, p2) are processed in order.
-    MTE_DEV void range_op(bool remove, i32 p1, i32 p2, i32 R, u32 C, i32 seq, u32 propset, bool rewrite) {
+    // pre: the block scan of edit() is still valid (n_lb <= 64, one chunk): pv / pincl per lane.
+    MTE_DEV void range_op(bool remove, i32 p1, i32 p2, i32 R, u32 C, i32 seq, u32 propset, bool rewrite, bool pre,
+                          u32 pv, u32 pincl) {
         MTE_PROF(PF_RANGE);
         fence_ovl();
         i32 cum = 0;
@@ -1888,8 +1943,8 @@ struct Engine {
             const u32 k = base + L;
             const bool valid = k < st.n_lb;
             uint4 o = valid ? ORD()[k] : make_uint4(0, 0, 0, 0);
-            const u32 v = blen_all(o, valid, R, C);
-            const u32 incl = wave_scan_incl(v);
+            const u32 v = pre ? pv : blen_all(o, valid, R, C);
+            const u32 incl = pre ? pincl : wave_scan_incl(v);
             const i32 cb = cum + (i32)(incl - v);
             u64 hm = wave_ballot(valid && v > 0 && cb < p2 && cb + (i32)v > p1);
             cum += (i32)wave_read(incl, 63);
@@ -2171,10 +2226,12 @@ struct Engine {
         MTE_COUNT(PF_OPS, 1);
         mte_op op = op_in;
 #ifdef MTE_PROFILE
-        const u64 t_op0 = __builtin_amdgcn_s_memtime();
+        const u64 t_op0 = (MTE_PON(PF_OP_INS) || MTE_PON(PF_OP_REM)) ? __builtin_amdgcn_s_memtime() : 0;
         struct OpScope {
             u64* acc; u64 t0; u32 L;
-            MTE_DEV ~OpScope() { if (L == 0) atomicAdd(acc, __builtin_amdgcn_s_memtime() - t0); }
+            MTE_DEV ~OpScope() {
+                if ((MTE_PON(PF_OP_INS) || MTE_PON(PF_OP_REM)) && L == 0) atomicAdd(acc, __builtin_amdgcn_s_memtime() - t0);
+            }
         } _op_scope{prof + (op.type == MTE_OP_REMOVE ? PF_OP_REM : PF_OP_INS), t_op0, L};
         MTE_COUNT(op.type == MTE_OP_REMOVE ? PN_REM : PN_INS, 1);
 #endif
@@ -2238,7 +2295,7 @@ struct Engine {
             }
             if (run) {
 #ifdef MTE_PROFILE
-                ProfScope _zs(prof + (z == 0 ? PF_ZAM_EDIT : PF_ZAM_MSN));
+                ProfScopeT<MTE_PON(PF_ZAM_EDIT) || MTE_PON(PF_ZAM_MSN)> _zs(prof + (z == 0 ? PF_ZAM_EDIT : PF_ZAM_MSN));
 #endif
                 zamboni();
             }
@@ -2424,7 +2481,7 @@ struct Engine {
     // continues HBM-resident from there) or on a failure (st.status).
     MTE_DEV u64 replay_run(u64 i) {
 #ifdef MTE_PROFILE
-        ProfScope _total(prof + PF_TOTAL);
+        MTE_PROF(PF_TOTAL);
 #endif
         const u64 e = p.docs[doc].op_end;
         // summary records (resume from a summary) precede the op log: a cold prefix loop, so the op

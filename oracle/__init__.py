@@ -42,6 +42,8 @@ def lib():
             getattr(L, f).argtypes = [vp]
         L.orc_snapshot_json.restype = vp
         L.orc_snapshot_json.argtypes = [vp, u32]
+        L.orc_snapshot_legacy_json.restype = vp
+        L.orc_snapshot_legacy_json.argtypes = [vp, u32, cp]
         L.orc_checksum.restype = u64
         L.orc_checksum.argtypes = [vp, u32]
         L.orc_ops_applied.restype = u64
@@ -128,6 +130,10 @@ class OracleDoc:
 
     def snapshot_json(self, chunk=10000):
         return _take(lib().orc_snapshot_json(self._h, chunk))
+
+    def snapshot_legacy_json(self, chunk=10000, catch_up_name="catchupOps"):
+        """SnapshotLegacy ITree (snapshotlegacy.ts): header, body, catch-up messages blob."""
+        return _take(lib().orc_snapshot_legacy_json(self._h, chunk, catch_up_name.encode()))
 
     def checksum(self, chunk=10000):
         return lib().orc_checksum(self._h, chunk)

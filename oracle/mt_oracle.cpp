@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <atomic>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <optional>
@@ -218,6 +219,10 @@ class MergeTree {
     std::deque<Segment> segPool;
     std::deque<Block> blockPool;
     std::vector<std::string>* longIds = nullptr;  // getLongClientId
+    // mergeTreeDeltaCallback (mergeTree.ts:1981-1987, 2592-2598, 2705-2711): operation (0 insert,
+    // 1 remove, 2 annotate) and the delta segments in walk order, each with its propertyDeltas keys
+    typedef std::vector<std::pair<Segment*, std::vector<u16s>>> Deltas;
+    std::function<void(int, Deltas&)> onDelta;
 
     MergeTree() { root = makeBlock(0); }
 
@@ -508,6 +513,11 @@ class MergeTree {
     void insertSegments(int pos, std::vector<Segment*>& segs, int refSeq, int clientId, int seq) {
         ensureIntervalBoundary(pos, refSeq, clientId);
         blockInsert(pos, refSeq, clientId, seq, segs);
+        if (onDelta) {
+            Deltas d;
+            for (Segment* x : segs) d.emplace_back(x, std::vector<u16s>());
+            onDelta(0, d);
+        }
         if (cw.collaborating && seq != UnassignedSequenceNumber) zamboniSegments();
     }
 
@@ -537,6 +547,7 @@ class MergeTree {
     void markRangeRemoved(int start, int end, int refSeq, int clientId, int seq) {
         ensureIntervalBoundary(start, refSeq, clientId);
         ensureIntervalBoundary(end, refSeq, clientId);
+        Deltas removed;
         auto markRemoved = [&](Segment* s, int, int, int) {
             if (s->removed) {
                 if (s->removedSeq == UnassignedSequenceNumber) {
@@ -549,6 +560,7 @@ class MergeTree {
                 s->removed = true;
                 s->removedClientId = clientId;
                 s->removedSeq = seq;
+                removed.emplace_back(s, std::vector<u16s>());  // removedSegments (:2639)
             }
             if (cw.collaborating) {
                 if (!(s->removedSeq == UnassignedSequenceNumber && clientId == cw.clientId)) addToLRUSet(s, seq);
@@ -556,11 +568,14 @@ class MergeTree {
             return true;
         };
         nodeMap(root, 0, refSeq, clientId, start, end, markRemoved);
+        if (onDelta) onDelta(1, removed);
         if (cw.collaborating && seq != UnassignedSequenceNumber) zamboniSegments();
     }
 
     // SegmentPropertiesManager.addProperties (segmentPropertiesManager.ts:35-111), remote / non-collab
-    static void addProperties(Segment* s, const JObj& newProps, bool rewrite) {
+    // Returns the keys of the propertyDeltas it builds, in their insertion order.
+    static std::vector<u16s> addProperties(Segment* s, const JObj& newProps, bool rewrite) {
+        std::vector<u16s> deltas;
         if (!s->hasProps) {
             s->hasProps = true;
             s->props = JObj();
@@ -568,26 +583,33 @@ class MergeTree {
         if (rewrite) {
             for (auto& k : s->props.keys()) {
                 JVP nv = newProps.get(k);
-                if (!truthy(nv.get())) s->props.del(k);
+                if (!truthy(nv.get())) {
+                    s->props.del(k);
+                    deltas.push_back(k);
+                }
             }
         }
         for (auto& k : newProps.keys()) {
             JVP nv = newProps.get(k);
+            if (std::find(deltas.begin(), deltas.end(), k) == deltas.end()) deltas.push_back(k);
             if (nv->t == JV::Null) s->props.del(k);
             else s->props.set(k, nv);
         }
+        return deltas;
     }
 
     // mergeTree.ts:2565-2605
     void annotateRange(int start, int end, const JObj& props, bool rewrite, int refSeq, int clientId, int seq) {
         ensureIntervalBoundary(start, refSeq, clientId);
         ensureIntervalBoundary(end, refSeq, clientId);
+        Deltas annotated;
         auto annotate = [&](Segment* s, int, int, int) {
-            addProperties(s, props, rewrite);
+            annotated.emplace_back(s, addProperties(s, props, rewrite));
             if (cw.collaborating && seq != UnassignedSequenceNumber) addToLRUSet(s, seq);
             return true;
         };
         nodeMap(root, 0, refSeq, clientId, start, end, annotate);
+        if (onDelta) onDelta(2, annotated);
         if (cw.collaborating && seq != UnassignedSequenceNumber) zamboniSegments();
     }
 
@@ -766,6 +788,82 @@ class Doc {
     // MTE_OP_RELPOS): the builder leaves unmapped every id the reference could tie to two markers
     std::unordered_map<uint32_t, Segment*> tagged;
 
+    // ---- legacy snapshot catch-up messages (SharedSegmentSequence.processMergeTreeMsg,
+    // sequence.ts:597-634, with newMergeTreeSnapshotFormat unset): every op message is stashed in
+    // messagesSinceMSNChange; one whose refSeq is not seq - 1 is stashed with refSeq = seq - 1 and its
+    // contents rebuilt from its sequenceDelta events (createOpsFromDelta, sequence.ts:58-100).
+    std::vector<JVP> catchup;
+    bool transforming = false;
+    std::vector<JVP> xops;  // ops built from the current message's delta events
+    static JVP jnum(double x) {
+        JVP v = std::make_shared<JV>();
+        v->t = JV::Num;
+        v->n = x;
+        return v;
+    }
+    static JVP jobj() {
+        JVP v = std::make_shared<JV>();
+        v->t = JV::Obj;
+        return v;
+    }
+    // SequenceDeltaEvent.ranges (sequenceDeltaEvent.ts:26-46): delta segments in document order, each
+    // at client.getPosition(segment) = getPosition(segment, currentSeq, local client) -- the op is
+    // not yet in currentSeq, so its own inserts count 0 and its own removals still count
+    void deltaOps(int op, MergeTree::Deltas& d) {
+        if (!transforming) return;
+        for (auto& e : d) {
+            Segment* seg = e.first;
+            const int pos = seg->parent ? getPosition(seg, mt.cw.currentSeq, mt.cw.clientId) : -1;
+            const double len = seg->len;
+            JVP last = xops.empty() ? nullptr : xops.back();
+            if (op == 0) {  // createInsertOp(pos, segment.clone().toJSONObject())
+                std::string sj;
+                segment_json(sj, seg);
+                JVP o = jobj();
+                o->o.set(u"pos1", jnum(pos));
+                o->o.set(u"seg", parse(sj.data(), sj.size()));
+                o->o.set(u"type", jnum(0));
+                xops.push_back(o);
+            } else if (op == 1) {  // lastRem?.pos1 === r.position ? lastRem.pos2 += len : createRemoveRangeOp
+                JVP p1 = last ? last->o.get(u"pos1") : nullptr;
+                if (p1 && p1->t == JV::Num && p1->n == pos) {
+                    JVP p2 = last->o.get(u"pos2");
+                    last->o.set(u"pos2", jnum(p2 && p2->t == JV::Num ? p2->n + len : NAN));
+                } else {
+                    JVP o = jobj();
+                    o->o.set(u"pos1", jnum(pos));
+                    o->o.set(u"pos2", jnum(pos + len));
+                    o->o.set(u"type", jnum(1));
+                    xops.push_back(o);
+                }
+            } else {  // props[key] = segment.properties[key] ?? null over the propertyDeltas keys
+                JVP props = jobj();
+                for (auto& k : e.second) {
+                    JVP v = seg->hasProps ? seg->props.get(k) : nullptr;
+                    props->o.set(k, v ? v : std::make_shared<JV>());
+                }
+                JVP p2 = last ? last->o.get(u"pos2") : nullptr;
+                JVP lp = last ? last->o.get(u"props") : nullptr;
+                if (p2 && p2->t == JV::Num && p2->n == pos && match_values(lp.get(), props.get())) {
+                    last->o.set(u"pos2", jnum(p2->n + len));
+                } else {
+                    JVP o = jobj();
+                    o->o.set(u"pos1", jnum(pos));
+                    o->o.set(u"pos2", jnum(pos + len));
+                    o->o.set(u"props", props);
+                    o->o.set(u"type", jnum(2));
+                    xops.push_back(o);
+                }
+            }
+        }
+    }
+    // processMinSequenceNumberChanged (sequence.ts:640-650)
+    void trimCatchup(int minSeq) {
+        size_t i = 0;
+        while (i < catchup.size() && num(catchup[i]->o, u"sequenceNumber") <= minSeq) i++;
+        if (i) catchup.erase(catchup.begin(), catchup.begin() + i);
+    }
+
     // posFromRelativePos (mergeTree.ts:1943-1966) -> getPosition (:1586-1603). A marker no longer
     // linked into the tree (zamboni dropped it; the reference would walk its stale parent chain) and
     // an unmapped id are unsupported.
@@ -820,6 +918,7 @@ class Doc {
             collab = true;
             getOrAddShortClientId(observer);
             mt.startCollaboration(0, 0, 0);
+            mt.onDelta = [this](int op, MergeTree::Deltas& d) { deltaOps(op, d); };
         }
     }
 
@@ -967,7 +1066,30 @@ class Doc {
                 if (clientName == observer) throw EngineError(MTE_DOC_UNSUPPORTED, "observer never submits ops");
                 if (!(mt.cw.currentSeq < seq)) throw EngineError(MTE_DOC_SEQ_ORDER, "seq <= currentSeq");
                 JVP contents = m.get(u"contents");
+                transforming = refSeq != seq - 1;
+                xops.clear();
                 if (contents && contents->t == JV::Obj) applyRemoteOp(contents->o, shortId, refSeq, seq);
+                transforming = false;
+                updateSeqNumbers(msn, seq);
+                JVP stash = std::make_shared<JV>(msg);
+                if (refSeq != seq - 1) {
+                    stash->o.set(u"referenceSequenceNumber", jnum(seq - 1));
+                    if (xops.size() == 1) {
+                        stash->o.set(u"contents", xops[0]);
+                    } else {  // createGroupOp(...ops)
+                        JVP g = jobj(), arr = std::make_shared<JV>();
+                        arr->t = JV::Arr;
+                        arr->a = xops;
+                        g->o.set(u"ops", arr);
+                        g->o.set(u"type", jnum(3));
+                        stash->o.set(u"contents", g);
+                    }
+                }
+                xops.clear();
+                catchup.push_back(stash);
+                // "Do GC every once in a while" (sequence.ts:628-632)
+                if (catchup.size() > 20 && num(catchup[20]->o, u"sequenceNumber") < msn) trimCatchup(msn);
+                return;
             }
             updateSeqNumbers(msn, seq);
         } catch (EngineError& e) {
@@ -1616,6 +1738,114 @@ class Doc {
         return o;
     }
 
+    // SnapshotLegacy.extractSync (snapshotlegacy.ts:184-238) + emit (:103-182) through
+    // serializeAsMinSupportedVersion (snapshotChunks.ts:75-111): the view at minSeq (segments inserted
+    // at or below minSeq and not removed at or below it) coalesced, a header chunk of at least
+    // chunkSize characters, one body chunk with the rest, and the catch-up messages above minSeq
+    // (sequence.ts:584-595: messagesSinceMSNChange trimmed, minimumSequenceNumber set to minSeq).
+    // Returns (path, contents) in tree-entry order.
+    std::vector<std::pair<std::string, std::string>> snapshotLegacyBlobs(uint32_t chunkSize, const std::string& catchName) {
+        const int minSeq = mt.cw.minSeq;
+        std::vector<std::string> segJson;
+        std::vector<long long> segLen;
+        std::unique_ptr<Segment> prevClone;
+        Segment* prev = nullptr;
+        auto pushSeg = [&](Segment* x) {
+            std::string j;
+            segment_json(j, x);
+            segJson.push_back(j);
+            segLen.push_back(x->len);
+        };
+        auto f = [&](Segment* x) {
+            if (x->seq != UnassignedSequenceNumber && x->seq <= minSeq &&
+                (!x->removed || x->removedSeq == UnassignedSequenceNumber || x->removedSeq > minSeq)) {
+                if (prev && canAppend(prev, x) && matchProperties(prev, x)) {
+                    auto c = std::make_unique<Segment>(*prev);
+                    c->text += x->text;
+                    c->len = (int)c->text.size();
+                    prevClone = std::move(c);
+                    prev = prevClone.get();
+                } else {
+                    if (prev) pushSeg(prev);
+                    prevClone.reset();
+                    prev = x;
+                }
+            }
+            return true;
+        };
+        mt.walkAllSegments(mt.root, f);
+        if (prev) pushSeg(prev);
+        long long total = 0;  // segmentsTotalLength, fixed up to the segments' sum (:228-236)
+        for (long long l : segLen) total += l;
+        const size_t n = segJson.size();
+        // getSeqLengthSegs (:73-98)
+        auto chunk = [&](long long approx, size_t start, size_t& count, long long& length) {
+            count = 0;
+            length = 0;
+            while (length < approx && start + count < n) length += segLen[start + count++];
+        };
+        auto chunkJson = [&](size_t start, size_t count, long long length, bool header) {
+            std::string o = "{\"chunkStartSegmentIndex\":" + std::to_string(start) +
+                            ",\"chunkSegmentCount\":" + std::to_string(count) +
+                            ",\"chunkLengthChars\":" + std::to_string(length) +
+                            ",\"totalLengthChars\":" + std::to_string(total) +
+                            ",\"totalSegmentCount\":" + std::to_string(n) +
+                            ",\"chunkSequenceNumber\":" + js_number(minSeq) + ",\"segmentTexts\":[";
+            for (size_t i = 0; i < count; i++) {
+                if (i) o += ",";
+                o += segJson[start + i];
+            }
+            o += "]";
+            if (header) {  // buildHeaderMetadataForLegecyChunk (snapshotChunks.ts:178-199)
+                o += ",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}";
+                if (length < total) o += ",{\"id\":\"body\"}";
+                o += "],\"sequenceNumber\":" + js_number(minSeq) + ",\"totalLength\":" + std::to_string(total) +
+                     ",\"totalSegmentCount\":" + std::to_string(n) + "}";
+            }
+            o += "}";
+            return o;
+        };
+        std::vector<std::pair<std::string, std::string>> blobs;
+        size_t c1 = 0;
+        long long l1 = 0;
+        chunk(chunkSize, 0, c1, l1);
+        blobs.emplace_back("header", chunkJson(0, c1, l1, true));
+        if (c1 < n) {
+            size_t c2 = 0;
+            long long l2 = 0;
+            chunk(total, c1, c2, l2);
+            blobs.emplace_back("body", chunkJson(c1, c2, l2, false));
+        }
+        std::string cu = "[";
+        bool first = true;
+        for (auto& m : catchup) {
+            if (num(m->o, u"sequenceNumber") <= minSeq) continue;
+            JV c = *m;
+            c.o.set(u"minimumSequenceNumber", jnum(minSeq));
+            if (!first) cu += ",";
+            first = false;
+            js_stringify(cu, c);
+        }
+        cu += "]";
+        blobs.emplace_back(catchName, cu);
+        return blobs;
+    }
+    std::string snapshotLegacyTree(uint32_t chunkSize, const std::string& catchName) {
+        std::string o = "{\"entries\":[";
+        bool firstE = true;
+        for (auto& b : snapshotLegacyBlobs(chunkSize, catchName)) {
+            if (!firstE) o += ",";
+            firstE = false;
+            o += "{\"mode\":\"100644\",\"path\":";
+            js_quote(o, utf8_to_u16(b.first.data(), b.first.size()));
+            o += ",\"type\":\"Blob\",\"value\":{\"contents\":";
+            js_quote(o, utf8_to_u16(b.second.data(), b.second.size()));
+            o += ",\"encoding\":\"utf-8\"}}";
+        }
+        o += "],\"id\":null}";
+        return o;
+    }
+
     uint64_t checksum(uint32_t chunkSize) {
         uint64_t h = 0xcbf29ce484222325ull;
         std::string t = u16_to_utf8(text());
@@ -1729,6 +1959,11 @@ char* orc_text(Doc* d) { return dupstr(orc::u16_to_utf8(d->text())); }
 char* orc_segments_json(Doc* d) { return dupstr(d->segmentsJson()); }
 char* orc_snapshot_json(Doc* d, uint32_t chunk) { return dupstr(d->snapshotTree(chunk ? chunk : 10000)); }
 uint64_t orc_checksum(Doc* d, uint32_t chunk) { return d->checksum(chunk ? chunk : 10000); }
+// Legacy-format merge-tree summary (SnapshotLegacy, the format the reference emits unless
+// newMergeTreeSnapshotFormat is set): the ITree JSON, catch-up blob named catch_name.
+char* orc_snapshot_legacy_json(Doc* d, uint32_t chunk, const char* catch_name) {
+    return dupstr(d->snapshotLegacyTree(chunk ? chunk : 10000, catch_name && *catch_name ? catch_name : "catchupOps"));
+}
 uint64_t orc_ops_applied(Doc* d) { return d->opsApplied; }
 
 int orc_status(Doc* d, char* msg, size_t cap, long long* failing_seq) {

@@ -60,3 +60,28 @@ def test_snapshot_v1_fixture(name):
     assert [p for p, _ in got] == [p for p, _ in want]
     for (p, g), (_, w) in zip(got, want):
         assert g == w, f"blob {p} differs"
+
+
+# generateSharedStrings.ts:14-22: "legacy" writes the catch-up blob under the option's name,
+# "legacyWithCatchUp" under the default "catchupOps"; both with the legacy (default) snapshot format
+LEGACY_CATCHUP = {"legacy": "randomNameForCatchUpOps", "legacyWithCatchUp": "catchupOps"}
+
+
+def legacy_fixture_blobs(version, name):
+    with open(os.path.join(os.path.dirname(__file__), "golden", version, name + ".json")) as f:
+        tree = json.load(f)
+    content = [e for e in tree["entries"] if e["path"] == "content"][0]
+    return [(e["path"], e["value"]["contents"]) for e in content["value"]["entries"]]
+
+
+@pytest.mark.parametrize("version", sorted(LEGACY_CATCHUP))
+@pytest.mark.parametrize("name", ["headerOnly", "headerAndBody", "largeBody", "withMarkers", "withAnnotations"])
+def test_snapshot_legacy_fixture(version, name):
+    """SnapshotLegacy (snapshotlegacy.ts:103-238) bytes of the same documents equal the legacy fixtures."""
+    d = build_doc(name)
+    tree = json.loads(d.snapshot_legacy_json(catch_up_name=LEGACY_CATCHUP[version]))
+    got = [(e["path"], e["value"]["contents"]) for e in tree["entries"]]
+    want = legacy_fixture_blobs(version, name)
+    assert [p for p, _ in got] == [p for p, _ in want]
+    for (p, g), (_, w) in zip(got, want):
+        assert g == w, f"blob {p} differs"

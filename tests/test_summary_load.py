@@ -351,3 +351,54 @@ def test_gpu_collab_body_summaries_match_oracle(engine):
     engine.replay()
     for d in range(len(cases)):
         compare_doc(engine, batch, d, observer=OBS)
+
+
+# Legacy-format EMISSION (SnapshotLegacy, snapshotlegacy.ts:103-238; sequence.ts:584-634). The header /
+# body bytes are pinned by the ten legacy fixtures (tests/test_oracle_fixtures.py); the catch-up blob has
+# no reference fixture with messages in it (parity unpinned), so it is checked by a round trip: a
+# catch-up client loading the legacy summary (header/body = the view at minSeq, then the catch-up
+# messages, rewritten to refSeq = seq - 1 with positions from their delta events) must see the text
+# of the document it was cut from. (Later ops concurrent with the rewritten messages may legitimately
+# diverge: the rewrite linearises them, which is why the reference moved to SnapshotV1.)
+def test_oracle_legacy_catchup_round_trip():
+    n = 0
+    for seed in range(1, 7):
+        log = c1_farm_log(seed=seed, total_ops=600)
+        for k in range(37, 600, 61):
+            o = OracleDoc("0")
+            o.apply_json(dumps(log[:k]))
+            assert o.status()[0] == 0
+            legacy = json.loads(o.snapshot_legacy_json())
+            blobs = {e["path"]: e["value"]["contents"] for e in legacy["entries"]}
+            catch = json.loads(blobs["catchupOps"])
+            min_seq = json.loads(blobs["header"])["chunkSequenceNumber"]
+            assert all(m["sequenceNumber"] > min_seq and m["minimumSequenceNumber"] == min_seq for m in catch)
+            assert all(m["referenceSequenceNumber"] == m["sequenceNumber"] - 1 for m in catch)
+            n += len(catch)
+            r = oracle_catchup(json.dumps(legacy), None, observer="reloader")
+            assert r.status()[0] == 0, r.status()
+            assert r.text() == o.text(), (seed, k)
+    assert n > 100  # the rewrite path is exercised
+
+
+def test_oracle_legacy_catchup_untransformed_continues():
+    """One writer with refSeq = seq - 1 (no rewrite) and the MSN trailing by 3: the catch-up messages are
+    stashed as received, and a client loading the legacy summary stays identical through the rest of the log."""
+    s = TestString("fakeId")
+    for i in range(300):
+        if i % 5 == 4 and len(s.text) > 10:
+            s.remove_range(i % 7, i % 7 + 4, False)
+        else:
+            s.insert((i * 13) % (len(s.text) + 1), f"t{i}", False)
+        s.msgs[-1]["minimumSequenceNumber"] = max(0, s.seq - 3)
+    for k in (50, 200, 299):
+        o = OracleDoc("0")
+        o.apply_json(dumps(s.msgs[:k]))
+        legacy = o.snapshot_legacy_json()
+        catch = json.loads({e["path"]: e["value"]["contents"] for e in json.loads(legacy)["entries"]}["catchupOps"])
+        assert [m["sequenceNumber"] for m in catch] == [k - 2, k - 1, k]
+        want = [dict(m, minimumSequenceNumber=k - 3) for m in s.msgs[k - 3:k]]
+        assert catch == want
+        r = oracle_catchup(legacy, s.msgs[k:], observer="reloader")
+        o.apply_json(dumps(s.msgs[k:]))
+        assert r.text() == o.text() == s.text

@@ -10,6 +10,7 @@ struct EmitParams {
     const u32* list;
     u32 n_list;
     u32 chunk;                 // SnapshotV1 chunk size in characters (10000)
+    u32 legacy;                // 1: SnapshotLegacy header / body chunks (snapshotlegacy.ts) instead of SnapshotV1
     const DocRes* res;
     const DocCfg* cfg;
     const uint4* vis;          // rows: (len, seq, removedSeq, client | removedClient << 8 | flags)

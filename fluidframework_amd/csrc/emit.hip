@@ -12,6 +12,11 @@
 //      JSON.stringify writes them (UTF-8; '"', '\\', control characters escaped, unpaired
 //      surrogates as \uXXXX; property objects in JS key order: array-index keys ascending, then
 //      insertion order).
+// Legacy format (EmitParams::legacy, SnapshotLegacy.extractSync + emit, snapshotlegacy.ts:103-238): the
+// entries are the view at minSeq only (segments inserted at or below minSeq and not removed at or
+// below it, coalesced the same way; the others are skipped without breaking a run), a header chunk of
+// at least `chunk` characters and ONE body chunk with the rest, in MergeTreeChunkLegacy JSON
+// (serializeAsMinSupportedVersion, snapshotChunks.ts:75-111). The catch-up blob is the host's.
 // The pass runs twice per list of documents: COUNT sizes every document's blobs (bytes, blob
 // count), the host lays the documents out in the output pool, WRITE fills them. Byte-oriented,
 // HBM-bound work: lanes encode 64 characters / copy 64 bytes per step, nothing is reshaped for MFMA.
@@ -232,7 +237,8 @@ struct Doc {
                 const bool removed = (meta & F_REMOVED) != 0, marker = (meta & F_MARKER) != 0;
                 const u32 row = base + j;
                 if (removed && (i32)rseq <= minSeq) continue;  // elided (:184-186)
-                if ((i32)seq <= minSeq && !removed) {
+                if (p.legacy && (i32)seq > minSeq) continue;   // not in the view at minSeq (legacy :195-196)
+                if ((i32)seq <= minSeq && (!removed || p.legacy)) {
                     if (open && runText && !marker && !(runLen && runLast16 == u'\n') &&
                         (runLen <= 256 || len <= 256) && match(row0 + runFirst, runProps, row0 + row, hasP)) {
                         runLast = row;  // clone + append (:197-202)
@@ -258,6 +264,11 @@ struct Doc {
         return ne;
     }
 
+    // a row inside a run's row span that is not part of it: elided (removed at or below minSeq) or,
+    // in the legacy view, inserted above minSeq
+    MTE_DEV bool skipped(uint4 v) const {
+        return ((v.w & F_REMOVED) && (i32)v.z <= r.min_seq) || (p.legacy && (i32)v.y > r.min_seq);
+    }
     // the text of a settled run: its rows' text without the elided rows between them, gathered
     // contiguously (in place when no elided text lies inside)
     MTE_DEV const u16* run_text(uint4 e, u64& n) const {
@@ -268,7 +279,7 @@ struct Doc {
         bool contiguous = true;
         for (u32 row = e.x + 1; row <= e.y && contiguous; row++) {
             const uint4 v = p.vis[row0 + row];
-            contiguous = !((v.w & F_REMOVED) && (i32)v.z <= minSeq && !(v.w & F_MARKER) && v.x);
+            contiguous = !(skipped(v) && !(v.w & F_MARKER) && v.x);
         }
         n = e.z;
         if (contiguous) return first;
@@ -276,7 +287,7 @@ struct Doc {
         u64 at = 0;
         for (u32 row = e.x; row <= e.y; row++) {
             const uint4 v = p.vis[row0 + row];
-            if ((v.w & F_REMOVED) && (i32)v.z <= minSeq) continue;
+            if (skipped(v)) continue;
             const u16* src = row_text(p.aux[row0 + row]);
             for (u32 i = L; i < v.x; i += 64) dst[at + i] = src[i];
             at += v.x;
@@ -331,8 +342,60 @@ struct Doc {
         put(o, "}");
     }
 
+    // SnapshotLegacy.emit (snapshotlegacy.ts:103-182): getSeqLengthSegs for the header (>= chunk
+    // characters) and one body with the rest; MergeTreeChunkLegacy keys in object-literal order,
+    // headerMetadata (buildHeaderMetadataForLegecyChunk, snapshotChunks.ts:178-199) on the header only,
+    // chunkMinSequenceNumber undefined (omitted)
+    MTE_DEV u64 emit_legacy(u32 ne, char* out, u64* blob_off, u32& nblobs) const {
+        const u32 L = lane_id();
+        u64 total = 0;
+        for (u32 q = 0; q < ne; q++) total += p.ent[row0 + q].z;
+        u32 c1 = 0;
+        u64 l1 = 0;
+        while (l1 < p.chunk && c1 < ne) l1 += p.ent[row0 + c1++].z;
+        nblobs = c1 < ne ? 2u : 1u;
+        Out o{out, 0};
+        for (u32 c = 0; c < nblobs; c++) {
+            if (blob_off && L == 0) blob_off[c] = o.pos;
+            const u32 start = c ? c1 : 0u, cnt = c ? ne - c1 : c1;
+            const u64 len = c ? total - l1 : l1;
+            put(o, "{\"chunkStartSegmentIndex\":");
+            put_int(o, start);
+            put(o, ",\"chunkSegmentCount\":");
+            put_int(o, cnt);
+            put(o, ",\"chunkLengthChars\":");
+            put_int(o, (i64)len);
+            put(o, ",\"totalLengthChars\":");
+            put_int(o, (i64)total);
+            put(o, ",\"totalSegmentCount\":");
+            put_int(o, ne);
+            put(o, ",\"chunkSequenceNumber\":");
+            put_int(o, r.min_seq);
+            put(o, ",\"segmentTexts\":[");
+            for (u32 q = 0; q < cnt; q++) {
+                if (q) put(o, ",");
+                put_entry(o, p.ent[row0 + start + q]);
+            }
+            put(o, "]");
+            if (c == 0) {
+                put(o, ",\"headerMetadata\":{\"orderedChunkMetadata\":[{\"id\":\"header\"}");
+                if (l1 < total) put(o, ",{\"id\":\"body\"}");
+                put(o, "],\"sequenceNumber\":");
+                put_int(o, r.min_seq);
+                put(o, ",\"totalLength\":");
+                put_int(o, (i64)total);
+                put(o, ",\"totalSegmentCount\":");
+                put_int(o, ne);
+                put(o, "}");
+            }
+            put(o, "}");
+        }
+        return o.pos;
+    }
+
     // 2 + 3: chunk plan and bytes; returns the byte count, blob starts into blob_off (WRITE)
     MTE_DEV u64 emit(u32 ne, char* out, u64* blob_off, u32& nblobs) const {
+        if (p.legacy) return emit_legacy(ne, out, blob_off, nblobs);
         const u32 L = lane_id();
         const u32 chunk = p.chunk;
         // chunk plan: count, total length, the header chunk's entries

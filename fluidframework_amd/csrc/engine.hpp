@@ -271,6 +271,7 @@ struct Engine {
         wave = 0;
     }
 
+    static constexpr u32 ST_CUOP = 7;  // doc-relative index of the MTE_F_CATCHUP op being applied
     // per-document counters kept in memory (few updates; spares scalar registers)
     MTE_DEV void stat_add(u32 i, u32 v) {
         if (L == 0) atomicAdd(&STATS()[i], v);
@@ -768,6 +769,38 @@ struct Engine {
             op.a = (rr.flags & MTE_F_REL_BEFORE2) ? q - (i32)rr.props : q + 1 + (i32)rr.props;
         }
         return true;
+    }
+
+    // ---------------------------------------------------------------- legacy catch-up delta ranges
+    // SnapshotLegacy's catch-up rewrite (sequence.ts:597-634) rebuilds an MTE_F_CATCHUP message's
+    // contents from its sequenceDelta ranges: each delta segment at client.getPosition(segment)
+    // (sequenceDeltaEvent.ts:26-46 -> mergeTree.ts:1586-1603), the local (observer) view, in which
+    // nodeLength is the segment's length unless removed -- the op itself included.
+    MTE_DEV i32 obs_prefix(u32 k, u32 blk, u32 s) {
+        sync();
+        u32 cum = 0;
+        for (u32 base = 0; base < k; base += 64) {
+            const u32 kk = base + L;
+            cum += wave_sum(kk < k ? ORD()[kk].y : 0u);
+        }
+        const uint4 q = VIS()[sidx(blk, L)];
+        cum += wave_sum(L < s && L < 8 ? obs_len(q.x, q.w) : 0u);
+        return (i32)cum;
+    }
+    MTE_DEV void cu_record(u32 kind, i32 pos, u32 len, u32 nmap, u32 omap) {
+        const u32 n = stat_get(ST_CU), op = stat_get(ST_CUOP);
+        const DocCfg& c = p.docs[doc];
+        if (n >= c.cu_cap || !p.cu_rec) {
+            fail(MTE_DOC_CAPACITY, st.curSeq);
+            return;
+        }
+        if (L == 0) {
+            uint4* r = p.cu_rec + (c.cu_off + n) * 2;
+            r[0] = make_uint4(op, (u32)pos, len, kind);
+            r[1] = make_uint4(nmap, omap, 0, 0);
+            STATS()[ST_CU] = n + 1;
+        }
+        sync();
     }
 
     // ---------------------------------------------------------------- allocation
@@ -1823,7 +1856,7 @@ struct Engine {
     // (ensureIntervalBoundary), then place the new segment. Remove / annotate
     // (mergeTree.ts:2565-2719): split at p1 and p2, then mark the range. The phases share ONE
     // resolve and ONE insert_slot call site. Returns false when nothing was edited (empty insert).
-    MTE_DEV bool edit(u32 type, i32 p1, i32 p2, i32 R, u32 C, i32 seq, Seg rec, u32 propset, bool rewrite) {
+    MTE_DEV bool edit(u32 type, i32 p1, i32 p2, i32 R, u32 C, i32 seq, Seg rec, u32 propset, bool rewrite, bool cu) {
         MTE_PROF(PF_EDIT);
         const bool ins = type == MTE_OP_INSERT || type == MTE_OP_INSERT_MARKER;
         const u32 nphase = ins ? 2u : 3u;
@@ -1834,7 +1867,11 @@ struct Engine {
         // phases scan again); blocks keep their visible lengths across a boundary split
         uint4 po = make_uint4(0, 0, 0, 0);
         u32 pv = 0, pincl = 0, pn = NONE;
+#ifdef MTE_NO_FUSE
+        if (false) {
+#else
         if (!ins && st.n_lb <= 64) {
+#endif
             fence_ovl();
             const bool valid = L < st.n_lb;
             po = valid ? ORD()[L] : make_uint4(0, 0, 0, 0);
@@ -1844,7 +1881,7 @@ struct Engine {
         }
         for (u32 ph = 0; ph < nphase; ph++) {
             if (!ins && ph == 2) {
-                range_op(type == MTE_OP_REMOVE, p1, p2, R, C, seq, propset, rewrite, pn == st.n_lb, pv, pincl);
+                range_op(type == MTE_OP_REMOVE, p1, p2, R, C, seq, propset, rewrite, pn == st.n_lb, pv, pincl, cu);
                 return st.status == 0;
             }
             const bool place = ins && ph == 1;
@@ -1925,6 +1962,13 @@ struct Engine {
                     known.slot = (i32)s - 3;
                 }
             }
+            if (place && cu) {  // the inserted segment's delta range
+                const u32 kb = b == f.blk ? f.k : f.k + 1;
+                const u32 cntb = U(ORD()[kb].w);
+                const u64 m = wave_ballot(L < cntb && L < 8 && AUX()[sidx(b, L)].w == rec.sid);
+                cu_record(0, obs_prefix(kb, b, m ? (u32)__builtin_ctzll(m) : 0u), rec.len, 0, 0);
+                if (st.status) return false;
+            }
             if (place && collab && seq > st.minSeq) add_lru(b, rec.sid, seq);
         }
         return st.status == 0;
@@ -1934,7 +1978,7 @@ struct Engine {
     // those of the (R, C) view before the op; blocks overlapping [p1, p2) are processed in order.
     // pre: the block scan of edit() is still valid (n_lb <= 64, one chunk): pv / pincl per lane.
     MTE_DEV void range_op(bool remove, i32 p1, i32 p2, i32 R, u32 C, i32 seq, u32 propset, bool rewrite, bool pre,
-                          u32 pv, u32 pincl) {
+                          u32 pv, u32 pincl, bool cu) {
         MTE_PROF(PF_RANGE);
         fence_ovl();
         i32 cum = 0;
@@ -1996,6 +2040,13 @@ struct Engine {
                         if (gone && seq > (i32)ob.z) ob.z = (u32)seq;
                         ORD()[kj] = ob;
                     }
+                    if (cu) {  // removedSegments (mergeTree.ts:2639): the segments this op removed
+                        for (u64 fm = wave_ballot(fresh != 0); fm && !st.status; fm &= fm - 1) {
+                            const u32 sl = (u32)__builtin_ctzll(fm);
+                            cu_record(1, obs_prefix(kj, blk, sl), wave_read(fresh, sl), 0, 0);
+                        }
+                        if (st.status) return;
+                    }
                 } else {
                     const u32 props = mark ? AUX()[idx].x : 0u;
                     u64 pending = mm;
@@ -2014,6 +2065,15 @@ struct Engine {
                         const bool same = mark && props == old && ((pending >> L) & 1ull);
                         if (same) AUX()[idx].x = nid;
                         pending &= ~wave_ballot(same);
+                    }
+                    if (cu) {  // deltaSegments with their propertyDeltas (maps before / after)
+                        for (u64 am = mm; am && !st.status; am &= am - 1) {
+                            const u32 sl = (u32)__builtin_ctzll(am);
+                            sync();
+                            const u32 nmap = U(AUX()[sidx(blk, sl)].x);
+                            cu_record(2, obs_prefix(kj, blk, sl), wave_read(q.x, sl), nmap, wave_read(props, sl));
+                        }
+                        if (st.status) return;
                     }
                 }
                 sync();
@@ -2272,7 +2332,13 @@ struct Engine {
             rec.toff = (mk && !ld) ? op.b : (u32)op.a;
             rec.tcap = 0;
             rec.sid = 0;
-            edited = edit(type, p1, op.a, R, C, seq, rec, op.props, (op.flags & MTE_F_REWRITE) != 0);
+            const bool cu = (op.flags & MTE_F_CATCHUP) != 0 && !ld;
+            if (cu) {
+                sync();
+                if (L == 0) STATS()[ST_CUOP] = (u32)(op_index - p.docs[doc].op_begin);
+                sync();
+            }
+            edited = edit(type, p1, op.a, R, C, seq, rec, op.props, (op.flags & MTE_F_REWRITE) != 0, cu);
             if (!ld) stat_add(ST_OPS, 1);
             if (st.status) return;
         }
@@ -2426,7 +2492,7 @@ struct Engine {
             }
         }
         const u32 fseq = stat_get(ST_FAILSEQ), ops = stat_get(ST_OPS), msgs = stat_get(ST_MSGS);
-        const u32 ngc = stat_get(ST_GC), maxlb = stat_get(ST_MAXLB);
+        const u32 ngc = stat_get(ST_GC), maxlb = stat_get(ST_MAXLB), ncu = stat_get(ST_CU);
         if (L == 0) {
             DocRes& o = p.res[doc];
             o.status = st.status;
@@ -2447,6 +2513,7 @@ struct Engine {
             o.n_segs = nseg;
             o.text_off = toff;
             o.max_lb = maxlb;
+            o.cu_n = ncu;
             o.mode = SOLO ? 3u : (LDSM ? 0u : (continued ? 2u : 1u));
         }
     }

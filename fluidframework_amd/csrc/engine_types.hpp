@@ -51,7 +51,7 @@ struct WaveRegion {
     u16 hint[256];              // LRU heap: segment id (mod 256) -> leaf block
     u32 stats[8];               // per-document counters (engine.hpp ST_*)
 };
-constexpr u32 ST_OPS = 0, ST_MSGS = 1, ST_GC = 2, ST_MAXLB = 3, ST_FAILSEQ = 4, ST_APPEND = 5, ST_WORDS = 8;
+constexpr u32 ST_OPS = 0, ST_MSGS = 1, ST_GC = 2, ST_MAXLB = 3, ST_FAILSEQ = 4, ST_APPEND = 5, ST_CU = 6, ST_WORDS = 8;
 constexpr u32 POOL_HDR = 80;  // 16-word allocation bitmap + pool_avail
 constexpr u32 POOL_BLOCKS = ((LDS_BYTES - LDS_WAVES * (u32)sizeof(WaveRegion) - POOL_HDR - 16) / (8 * 32 + 4 + 1)) & ~3u;
 
@@ -105,6 +105,9 @@ struct DocCfg {
     u64 ovl_off;       // per segment id: removedClientOverlap mask (u64)
     u64 map_off;
     u64 hb_off;        // byte offset of this doc's HBM-resident state (HBM mode only)
+    u64 cu_off;        // first catch-up delta record (Params::cu_rec, 2 x uint4 each) of this doc
+    u32 cu_cap;        // catch-up delta records it may write (MTE_F_CATCHUP ops)
+    u32 cu_pad;
     u32 payload_len;
     u32 arena_cap;
     u32 seg_cap;       // segment ids available
@@ -138,6 +141,7 @@ struct DocRes {
     u32 mode;        // 0 LDS-resident, 1 HBM-resident, 2 continued HBM-resident, 3 solo LDS-resident
     u32 spill_why;   // why the LDS pass gave the doc up (engine.hpp St::spillWhy)
     u32 text_off;    // first unit of this doc's gathered final text in the output text pool
+    u32 cu_n;        // catch-up delta records written (Engine::cu_record)
 };
 
 // internal status: the LDS-resident replay ran out of room (leaf-block pool, interior nodes, heap
@@ -188,6 +192,8 @@ struct Params {
     u32 solo_blk, solo_ord, solo_in, solo_heap;  // capacities of a solo slot (hbm_caps of its longest doc)
     u32 pool_limit;           // test knob: LDS leaf blocks usable per CU (0 = all)
     u64* prof;                // MTE_PROFILE builds: per doc PROF_SLOTS cycle counters
+    uint4* cu_rec;            // catch-up delta records: (op index in the doc, position, length, kind),
+                              // (map after, map before, 0, 0); kind 0 insert, 1 remove, 2 annotate
     // synthetic workload generator
     u32* gen_first_seen;      // per doc: 64 entries, writer index for each short id (1..)
     u32 gen_kind;

@@ -52,6 +52,11 @@ struct HostBatch {
     std::vector<uint32_t> doc_client_offsets{0};
     std::vector<uint64_t> client_name_offsets{0};
     std::string client_names;
+    // legacy catch-up messages (include/mte.h mte_batch.msg_*)
+    std::vector<uint64_t> doc_msg_offsets{0};
+    std::vector<uint64_t> msg_first_op;
+    std::vector<uint64_t> msg_text_offsets{0};
+    std::string msg_text;
 
     uint32_t n_docs() const { return (uint32_t)doc_op_offsets.size() - 1; }
     void view(mte_batch* b) const {
@@ -73,6 +78,11 @@ struct HostBatch {
         b->doc_client_offsets = doc_client_offsets.data();
         b->client_name_offsets = client_name_offsets.data();
         b->client_names = client_names.data();
+        const bool msgs = doc_msg_offsets.size() == (size_t)n_docs() + 1;  // generated batches keep none
+        b->doc_msg_offsets = msgs ? doc_msg_offsets.data() : nullptr;
+        b->msg_first_op = msgs ? msg_first_op.data() : nullptr;
+        b->msg_text_offsets = msgs ? msg_text_offsets.data() : nullptr;
+        b->msg_text = msgs ? msg_text.data() : nullptr;
     }
     void copy_from(const mte_batch* b) {
         const uint32_t n = b->n_docs;
@@ -93,6 +103,21 @@ struct HostBatch {
         uint32_t nn = doc_client_offsets[n];
         client_name_offsets.assign(b->client_name_offsets, b->client_name_offsets + nn + 1);
         client_names.assign(b->client_names, b->client_name_offsets[nn]);
+        if (b->doc_msg_offsets && b->msg_first_op && b->msg_text_offsets && b->msg_text) {
+            doc_msg_offsets.assign(b->doc_msg_offsets, b->doc_msg_offsets + n + 1);
+            const uint64_t nm = doc_msg_offsets[n];
+            msg_first_op.assign(b->msg_first_op, b->msg_first_op + nm);
+            msg_text_offsets.assign(b->msg_text_offsets, b->msg_text_offsets + nm + 1);
+            msg_text.assign(b->msg_text, b->msg_text_offsets[nm]);
+        } else {
+            doc_msg_offsets.assign(n + 1, 0);
+            msg_first_op.clear();
+            msg_text_offsets.assign(1, 0);
+            msg_text.clear();
+        }
+    }
+    std::string message(uint64_t i) const {
+        return msg_text.substr(msg_text_offsets[i], msg_text_offsets[i + 1] - msg_text_offsets[i]);
     }
     std::string key(uint32_t k) const { return key_text.substr(key_offsets[k], key_offsets[k + 1] - key_offsets[k]); }
     std::string val(uint32_t v) const { return val_text.substr(val_offsets[v], val_offsets[v + 1] - val_offsets[v]); }
@@ -255,6 +280,9 @@ struct mte_engine {
     // pools -- round 0 (every document but the solo ones) runs while the critical path is still
     // replaying, round 1 (solo and host-re-run documents) after it
     bool emit_opt = true;     // option "emit"
+    bool legacy = false;      // snapshot_format 1 (mte_config / option "snapshot_format"): SnapshotLegacy
+    bool emitted_legacy = false;  // format of the last emission
+    DevBuf<uint4> d_cu;       // catch-up delta records (Params::cu_rec)
     bool emit_tables = false; // tables uploaded for the current batch
     DevBuf<char> d_key_text, d_val_text, d_names;
     DevBuf<uint64_t> d_key_off, d_val_off, d_name_off, d_name_base, d_emit_size, d_out_off, d_blob_base;
@@ -565,6 +593,7 @@ int mte_create(const mte_config* cfg, mte_engine** out) {
     if (cfg) {
         e->device = cfg->device;
         if (cfg->chunk_size) e->chunk = cfg->chunk_size;
+        e->legacy = cfg->snapshot_format == 1;
     }
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= e->device) {
@@ -645,6 +674,29 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     int rc;
     if ((rc = layout_and_alloc(e, n_ops, pay, pi, an, collab, has_nl, 0, b->doc_op_offsets, b->doc_payload_offsets)))
         return rc;
+    // catch-up delta records (legacy summaries): an insert has one range, a remove / annotate at most
+    // one per character of its range (every delta segment is visible in the op's view), or at most
+    // every segment when a position is relative
+    uint64_t cu = 0;
+    for (uint32_t d = 0; d < nd; d++) {
+        DocCfg& c = e->cfg[d];
+        uint64_t cap = 0;
+        for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
+            const mte_op& o = b->ops[i];
+            if (!(o.flags & MTE_F_CATCHUP)) continue;
+            if (o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER) cap += 1;
+            else if (o.flags & MTE_F_REL) cap += c.seg_cap;
+            else cap += (uint64_t)std::max<int64_t>(0, (int64_t)o.a - (int64_t)o.pos1);
+        }
+        c.cu_off = cu;
+        c.cu_cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFF0ull);
+        cu += c.cu_cap;
+    }
+    if (cu) {
+        HIP_TRY(e, e->d_cu.alloc(2 * cu));
+        if ((rc = upload(e, e->d_cfg, e->cfg))) return rc;
+    }
+    e->P.cu_rec = cu ? e->d_cu.p : nullptr;
     if ((rc = upload(e, e->d_ops, e->hb.ops))) return rc;
     if ((rc = upload(e, e->d_payload, e->hb.payload))) return rc;
     if ((rc = upload_props(e))) return rc;
@@ -719,6 +771,7 @@ static int emit_tables(mte_engine* e) {
 static EmitParams emit_params(mte_engine* e) {
     EmitParams P{};
     P.chunk = e->chunk;
+    P.legacy = e->legacy ? 1u : 0u;
     P.res = e->d_res.p;
     P.cfg = e->d_cfg.p;
     P.vis = e->d_out_vis.p;
@@ -827,6 +880,7 @@ static int run_kernel(mte_engine* e, bool gen) {
         HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev2, 0));
     }
     const bool emit = !gen && e->emit_opt;
+    e->emitted_legacy = e->legacy;
     e->emit_downloaded = false;
     e->emit_pool_of.assign(nd, 255);
     e->pool[0].used = e->pool[0].blobs = e->pool[1].used = e->pool[1].blobs = 0;
@@ -1353,12 +1407,21 @@ static int doc_blobs(mte_engine* e, uint32_t d, std::vector<std::pair<const char
     return MTE_OK;
 }
 
+static int legacy_tree(mte_engine* e, uint32_t doc, const char* catch_up_name, std::string& o);
+
 int mte_snapshot_shared_string(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len) {
+    if (!e) return MTE_E_ARG;
     size_t n = 0;
-    int rc = mte_snapshot_v1(e, doc, nullptr, 0, &n, nullptr);
-    if (rc) return rc;
-    std::string inner(n, '\0');
-    if ((rc = mte_snapshot_v1(e, doc, &inner[0], n, &n, nullptr))) return rc;
+    int rc;
+    std::string inner;
+    if (e->emitted_legacy) {
+        if (doc >= e->P.n_docs) return set_err(e, MTE_E_RANGE, "doc index out of range");
+        if ((rc = legacy_tree(e, doc, nullptr, inner))) return rc;
+    } else {
+        if ((rc = mte_snapshot_v1(e, doc, nullptr, 0, &n, nullptr))) return rc;
+        inner.assign(n, '\0');
+        if ((rc = mte_snapshot_v1(e, doc, &inner[0], n, &n, nullptr))) return rc;
+    }
     std::string o = "{\"entries\":[{\"mode\":\"100644\",\"path\":\"header\",\"type\":\"Blob\",\"value\":"
                     "{\"contents\":\"{}\",\"encoding\":\"utf-8\"}},{\"mode\":\"040000\",\"path\":\"content\","
                     "\"type\":\"Tree\",\"value\":" + inner + "}],\"id\":null}";
@@ -1372,6 +1435,7 @@ int mte_snapshot_shared_string(mte_engine* e, uint32_t doc, char* buf, size_t ca
 int mte_snapshot_v1(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len, uint32_t* n_blobs) {
     if (!e) return MTE_E_ARG;
     if (doc >= e->P.n_docs) return set_err(e, MTE_E_RANGE, "doc index out of range");
+    if (e->emitted_legacy) return set_err(e, MTE_E_STATE, "the last replay emitted SnapshotLegacy (snapshot_format 1)");
     std::vector<std::pair<const char*, size_t>> blobs;
     int rc = doc_blobs(e, doc, blobs);
     if (rc) return rc;
@@ -1387,6 +1451,254 @@ int mte_snapshot_v1(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* 
     }
     o += "],\"id\":null}";
     if (n_blobs) *n_blobs = (uint32_t)blobs.size();
+    if (len) *len = o.size();
+    if (!buf) return MTE_OK;
+    if (cap < o.size()) return MTE_E_RANGE;
+    memcpy(buf, o.data(), o.size());
+    return MTE_OK;
+}
+
+// ---- SnapshotLegacy catch-up messages (sequence.ts:584-650) -------------------------------------
+static int num_field(const json::Value& o, const char16_t* k, int32_t* out);
+static void set_member(json::Value& o, const char16_t* k, json::Value v) {
+    for (auto& m : o.members)
+        if (m.first == k) {
+            m.second = std::move(v);
+            return;
+        }
+    o.members.emplace_back(k, std::move(v));
+}
+static json::Value jobj() {
+    json::Value v;
+    v.kind = json::Value::Object;
+    return v;
+}
+static json::Value jnumv(double x) {
+    json::Value v;
+    v.kind = json::Value::Number;
+    v.num = x;
+    return v;
+}
+// one property map of document d from the device (MAP_WORDS words: count, then (key, value) ids)
+static int read_map(mte_engine* e, uint32_t d, uint32_t id, std::vector<std::pair<uint32_t, uint32_t>>& kv) {
+    kv.clear();
+    if (id == 0) return MTE_OK;
+    if (id >= e->cfg[d].map_cap) return set_err(e, MTE_E_STATE, "catch-up: property map id out of range");
+    uint32_t w[MAP_WORDS];
+    HIP_TRY(e, hipMemcpy(w, e->d_maps.p + (e->cfg[d].map_off + id) * MAP_WORDS, sizeof w, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < std::min<uint32_t>(w[0], MTE_MAX_PROPS); i++) kv.emplace_back(w[1 + 2 * i], w[2 + 2 * i]);
+    return MTE_OK;
+}
+static json::Value parse_text(const std::string& t) { return json::parse(t.data(), t.size()); }
+// propertyDeltas keys of an annotate (segmentPropertiesManager.ts:65-106): with rewrite, the segment's
+// keys (Object.keys order) whose new value is falsy or absent, then the op's keys; each key mapped to
+// the segment's value after the op, or null (createOpsFromDelta, sequence.ts:62-81)
+static int annotate_props(mte_engine* e, uint32_t d, const mte_op& op, uint32_t nmap, uint32_t omap, json::Value& props) {
+    const HostBatch& hb = e->hb;
+    std::vector<std::pair<uint32_t, uint32_t>> nk, ok;
+    int rc;
+    if ((rc = read_map(e, d, nmap, nk)) || (rc = read_map(e, d, omap, ok))) return rc;
+    std::vector<uint32_t> keys;
+    const mte_propset ps = op.props < hb.propsets.size() ? hb.propsets[op.props] : mte_propset{0, 0};
+    auto in_new = [&](uint32_t k, uint32_t* v) {
+        for (uint32_t q = 0; q < ps.count; q++)
+            if (hb.prop_keys[ps.first + q] == k) {
+                *v = hb.prop_vals[ps.first + q];
+                return true;
+            }
+        return false;
+    };
+    if (op.flags & MTE_F_REWRITE) {
+        std::vector<size_t> idx(ok.size());
+        for (size_t i = 0; i < ok.size(); i++) idx[i] = i;
+        std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {  // JS own-key order
+            const uint32_t ka = ok[a].first, kb = ok[b].first;
+            const bool ia = e->key_is_index[ka], ib = e->key_is_index[kb];
+            if (ia != ib) return ia;
+            return ia && e->key_index[ka] < e->key_index[kb];
+        });
+        for (size_t i : idx) {
+            uint32_t v = 0;
+            if (!in_new(ok[i].first, &v) || (e->val_flags[v] & 1u)) keys.push_back(ok[i].first);
+        }
+    }
+    for (uint32_t q = 0; q < ps.count; q++) {
+        const uint32_t k = hb.prop_keys[ps.first + q];
+        if (std::find(keys.begin(), keys.end(), k) == keys.end()) keys.push_back(k);
+    }
+    props = jobj();
+    for (uint32_t k : keys) {
+        json::Value kv = parse_text(hb.key(k));
+        json::Value val;  // null
+        for (auto& p : nk)
+            if (p.first == k) val = parse_text(hb.val(p.second));
+        set_member(props, kv.str.c_str(), std::move(val));
+    }
+    return MTE_OK;
+}
+// segment.clone().toJSONObject() of an insert op's segment (textSegment.ts:48-54, mergeTree.ts:652-656)
+static json::Value insert_seg_json(const mte_engine* e, uint32_t d, const mte_op& op) {
+    const HostBatch& hb = e->hb;
+    json::Value props = jobj();
+    if (op.props && op.props < hb.propsets.size()) {
+        const mte_propset ps = hb.propsets[op.props];
+        for (uint32_t q = 0; q < ps.count; q++) {
+            const uint32_t v = hb.prop_vals[ps.first + q];
+            if (v == 0) continue;  // null deletes
+            json::Value kv = parse_text(hb.key(hb.prop_keys[ps.first + q]));
+            set_member(props, kv.str.c_str(), parse_text(hb.val(v)));
+        }
+    }
+    json::Value seg;
+    if (op.type == MTE_OP_INSERT_MARKER) {
+        seg = jobj();
+        json::Value mk = jobj();
+        set_member(mk, u"refType", jnumv((double)(op.b & 0xFFFFu)));
+        set_member(seg, u"marker", std::move(mk));
+        if (op.props) set_member(seg, u"props", std::move(props));
+        return seg;
+    }
+    json::Value text;
+    text.kind = json::Value::String;
+    const uint64_t p0 = hb.doc_payload_offsets[d] + (uint64_t)op.a;
+    text.str.assign((const char16_t*)hb.payload.data() + p0, op.b);
+    if (!op.props) return text;
+    seg = jobj();
+    set_member(seg, u"text", std::move(text));
+    set_member(seg, u"props", std::move(props));
+    return seg;
+}
+// The catch-up blob of document d: JSON.stringify(messagesSinceMSNChange) at snapshot time.
+static int catch_up_json(mte_engine* e, uint32_t d, std::string& out) {
+    const HostBatch& hb = e->hb;
+    const DocRes& r = e->res[d];
+    const int32_t minSeq = r.min_seq;
+    const uint64_t m0 = hb.doc_msg_offsets[d], m1 = hb.doc_msg_offsets[d + 1];
+    const uint64_t op0 = hb.doc_op_offsets[d], nops = hb.doc_op_offsets[d + 1] - op0;
+    // every applied op above minSeq must have its message (generated logs have none)
+    uint64_t need = 0, have = 0;
+    for (uint64_t i = 0; i < nops; i++) {
+        const mte_op& o = hb.ops[op0 + i];
+        if ((o.flags & MTE_F_END_OF_MSG) && o.seq > minSeq && o.type <= MTE_OP_INSERT_MARKER) need++;
+    }
+    std::vector<uint4> rec(2 * (size_t)r.cu_n);
+    if (r.cu_n) HIP_TRY(e, hipMemcpy(rec.data(), e->d_cu.p + 2 * e->cfg[d].cu_off, rec.size() * sizeof(uint4), hipMemcpyDeviceToHost));
+    out = "[";
+    size_t ri = 0;
+    bool first = true;
+    for (uint64_t i = m0; i < m1; i++) {
+        json::Value m;
+        try {
+            m = parse_text(hb.message(i));
+        } catch (std::exception& ex) {
+            return set_err(e, MTE_E_PARSE, ex.what());
+        }
+        int32_t seq = 0, ref = 0;
+        num_field(m, u"sequenceNumber", &seq);
+        num_field(m, u"referenceSequenceNumber", &ref);
+        const uint64_t f0 = hb.msg_first_op[i], f1 = i + 1 < m1 ? hb.msg_first_op[i + 1] : nops;
+        while (ri < r.cu_n && rec[2 * ri].x < f0) ri++;
+        if (seq <= minSeq) continue;
+        have++;
+        if (ref != seq - 1) {  // stashMessage = {...message, referenceSequenceNumber, contents}
+            std::vector<json::Value> ops;
+            for (; ri < r.cu_n && rec[2 * ri].x < f1; ri++) {
+                const uint4 a = rec[2 * ri], b = rec[2 * ri + 1];
+                const mte_op& op = hb.ops[op0 + a.x];
+                const double pos = (double)(int32_t)a.y, len = (double)a.z;
+                json::Value* last = ops.empty() ? nullptr : &ops.back();
+                if (a.w == 0) {  // createInsertOp(r.position, segment.clone().toJSONObject())
+                    json::Value o = jobj();
+                    set_member(o, u"pos1", jnumv(pos));
+                    set_member(o, u"seg", insert_seg_json(e, d, op));
+                    set_member(o, u"type", jnumv(0));
+                    ops.push_back(std::move(o));
+                } else if (a.w == 1) {  // lastRem?.pos1 === r.position ? lastRem.pos2 += len : a new remove
+                    const json::Value* p1 = last ? last->get(u"pos1") : nullptr;
+                    if (p1 && p1->kind == json::Value::Number && p1->num == pos) {
+                        const json::Value* p2 = last->get(u"pos2");
+                        set_member(*last, u"pos2", jnumv(p2 && p2->kind == json::Value::Number ? p2->num + len : NAN));
+                    } else {
+                        json::Value o = jobj();
+                        set_member(o, u"pos1", jnumv(pos));
+                        set_member(o, u"pos2", jnumv(pos + len));
+                        set_member(o, u"type", jnumv(1));
+                        ops.push_back(std::move(o));
+                    }
+                } else {  // annotate: extend the last one when adjacent with matching props
+                    json::Value props;
+                    int rc = annotate_props(e, d, op, b.x, b.y, props);
+                    if (rc) return rc;
+                    const json::Value* p2 = last ? last->get(u"pos2") : nullptr;
+                    const json::Value* lp = last ? last->get(u"props") : nullptr;
+                    if (p2 && p2->kind == json::Value::Number && p2->num == pos && json::match_properties(lp, &props)) {
+                        set_member(*last, u"pos2", jnumv(p2->num + len));
+                    } else {
+                        json::Value o = jobj();
+                        set_member(o, u"pos1", jnumv(pos));
+                        set_member(o, u"pos2", jnumv(pos + len));
+                        set_member(o, u"props", std::move(props));
+                        set_member(o, u"type", jnumv(2));
+                        ops.push_back(std::move(o));
+                    }
+                }
+            }
+            set_member(m, u"referenceSequenceNumber", jnumv(seq - 1));
+            if (ops.size() == 1) {
+                set_member(m, u"contents", std::move(ops[0]));
+            } else {  // createGroupOp(...ops)
+                json::Value g = jobj(), arr;
+                arr.kind = json::Value::Array;
+                arr.items = std::move(ops);
+                set_member(g, u"ops", std::move(arr));
+                set_member(g, u"type", jnumv(3));
+                set_member(m, u"contents", std::move(g));
+            }
+        }
+        set_member(m, u"minimumSequenceNumber", jnumv(minSeq));  // sequence.ts:590
+        if (!first) out += ",";
+        first = false;
+        json::stringify(out, m);
+    }
+    out += "]";
+    if (have < need)
+        return set_err(e, MTE_E_UNSUPPORTED, "legacy catch-up: ops above minSeq without their message JSON (generated log)");
+    return MTE_OK;
+}
+static int legacy_tree(mte_engine* e, uint32_t doc, const char* catch_up_name, std::string& o) {
+    if (!e->emitted_legacy) return set_err(e, MTE_E_STATE, "replay with snapshot_format 1 for SnapshotLegacy");
+    std::vector<std::pair<const char*, size_t>> blobs;
+    int rc = doc_blobs(e, doc, blobs);
+    if (rc || (rc = ensure_download(e))) return rc;
+    std::string cu;
+    if ((rc = catch_up_json(e, doc, cu))) return rc;
+    const std::string cname = catch_up_name && *catch_up_name ? catch_up_name : "catchupOps";
+    o = "{\"entries\":[";
+    auto entry = [&](const std::string& path, const char* p, size_t n) {
+        o += "{\"mode\":\"100644\",\"path\":";
+        std::u16string pu;
+        json::decode_utf8(path.data(), path.size(), pu);
+        json::quote(o, pu);
+        o += ",\"type\":\"Blob\",\"value\":{\"contents\":";
+        std::u16string bu;
+        json::decode_utf8(p, n, bu);
+        json::quote(o, bu);
+        o += ",\"encoding\":\"utf-8\"}}";
+    };
+    for (size_t i = 0; i < blobs.size(); i++) {
+        entry(i == 0 ? "header" : "body", blobs[i].first, blobs[i].second);
+        o += ",";
+    }
+    entry(cname, cu.data(), cu.size());
+    o += "],\"id\":null}";
+    return MTE_OK;
+}
+int mte_snapshot_legacy(mte_engine* e, uint32_t doc, const char* catch_up_name, char* buf, size_t cap, size_t* len) {
+    if (!e) return MTE_E_ARG;
+    if (doc >= e->P.n_docs) return set_err(e, MTE_E_RANGE, "doc index out of range");
+    std::string o;
+    int rc = legacy_tree(e, doc, catch_up_name, o);
+    if (rc) return rc;
     if (len) *len = o.size();
     if (!buf) return MTE_OK;
     if (cap < o.size()) return MTE_E_RANGE;
@@ -1615,6 +1927,7 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "solo_min_ops") e->solo_min_ops = (uint64_t)std::max<int64_t>(1, value);
     else if (k == "lean") e->lean_opt = value != 0;
     else if (k == "emit") e->emit_opt = value != 0;  // SnapshotV1 emission on the device after replay
+    else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
 }
@@ -1731,6 +2044,19 @@ struct DocBuild {
     // holds each slot's last owner (the name every output above minSeq refers to). Concurrent
     // overlapping removers are all above minSeq while their removal matters. An op whose refSeq is
     // below minSeq after a reuse is reported unsupported (slot 255), as is a client with no free slot.
+    // messagesSinceMSNChange (sequence.ts:597-650): op messages above the running minSeq, as
+    // JSON.stringify(JSON.parse(message)), with the index of their first op record; the ones left at
+    // commit are the legacy summary's catch-up messages
+    struct Msg {
+        int32_t seq;
+        bool rewrite;  // refSeq != seq - 1: the legacy summary rewrites it from its delta ranges
+        uint64_t first_op;
+        std::string text;
+    };
+    std::deque<Msg> stash;
+    void trim_stash() {
+        while (!stash.empty() && stash.front().seq <= cur_min) stash.pop_front();
+    }
     std::vector<int32_t> last_use;  // slot -> highest seq its owner used
     int32_t cur_min = 0;            // minSeq as the engine will have it at the next record
     bool loading = false;           // summary records: no reuse before LOAD_END
@@ -1776,6 +2102,17 @@ struct DocBuild {
         return MTE_OK;
     }
     void commit(HostBatch& hb) {
+        trim_stash();
+        for (size_t i = 0; i < stash.size(); i++) {
+            const uint64_t end = i + 1 < stash.size() ? stash[i + 1].first_op : ops.size();
+            if (stash[i].rewrite)
+                for (uint64_t q = stash[i].first_op; q < end && q < ops.size(); q++)
+                    if (ops[q].type <= MTE_OP_INSERT_MARKER) ops[q].flags |= MTE_F_CATCHUP;
+            hb.msg_first_op.push_back(stash[i].first_op);
+            hb.msg_text += stash[i].text;
+            hb.msg_text_offsets.push_back(hb.msg_text.size());
+        }
+        hb.doc_msg_offsets.push_back(hb.msg_first_op.size());
         hb.ops.insert(hb.ops.end(), ops.begin(), ops.end());
         hb.doc_op_offsets.push_back(hb.ops.size());
         hb.payload.insert(hb.payload.end(), payload.begin(), payload.end());
@@ -1928,6 +2265,10 @@ static int add_messages(mte_builder* b, const json::Value& doc, DocBuild& db) {
         }
         ops.back().flags |= MTE_F_END_OF_MSG;
         if (collab && base.msn > db.cur_min) db.cur_min = base.msn;  // setMinSeq after the message
+        if (collab && type && type->kind == json::Value::String && type->str == u"op") {
+            db.stash.push_back(DocBuild::Msg{base.seq, base.ref_seq != base.seq - 1, (uint64_t)first, json::stringify(m)});
+            if (db.stash.size() > 64) db.trim_stash();
+        }
     }
     return MTE_OK;
 }

@@ -72,11 +72,16 @@ class mte_batch(ctypes.Structure):
         ("doc_client_offsets", ctypes.POINTER(ctypes.c_uint32)),
         ("client_name_offsets", ctypes.POINTER(ctypes.c_uint64)),
         ("client_names", ctypes.c_void_p),
+        ("doc_msg_offsets", ctypes.POINTER(ctypes.c_uint64)),
+        ("msg_first_op", ctypes.POINTER(ctypes.c_uint64)),
+        ("msg_text_offsets", ctypes.POINTER(ctypes.c_uint64)),
+        ("msg_text", ctypes.c_void_p),
     ]
 
 
 class mte_config(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int32), ("chunk_size", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 6)]
+    _fields_ = [("device", ctypes.c_int32), ("chunk_size", ctypes.c_uint32), ("snapshot_format", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32 * 5)]
 
 
 class mte_stats(ctypes.Structure):
@@ -96,7 +101,7 @@ SUMMARY_DTYPE = np.dtype([("checksum", "<u8"), ("ops", "<u4"), ("length", "<u4")
 # Every symbol declared in include/mte.h (checked by tests/test_abi.py).
 EXPORTS = ["mte_abi_version", "mte_build_info", "mte_create", "mte_destroy", "mte_last_error", "mte_load",
            "mte_replay", "mte_generate", "mte_generate_ids", "mte_export_batch", "mte_doc_status", "mte_text", "mte_length", "mte_segments",
-           "mte_snapshot_v1", "mte_snapshot_shared_string", "mte_summaries", "mte_rccl_unique_id",
+           "mte_snapshot_v1", "mte_snapshot_legacy", "mte_snapshot_shared_string", "mte_summaries", "mte_rccl_unique_id",
            "mte_rccl_comm_create", "mte_rccl_comm_destroy", "mte_gather_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
            "mte_builder_batch",
            "mte_builder_error", "mte_builder_destroy"]
@@ -129,6 +134,7 @@ def lib():
         L.mte_segments_json.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.mte_snapshot_v1.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz), ctypes.POINTER(u32)]
         L.mte_snapshot_shared_string.argtypes = [vp, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+        L.mte_snapshot_legacy.argtypes = [vp, u32, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.mte_summaries.argtypes = [vp, ctypes.c_void_p, sz]
         L.mte_rccl_unique_id.argtypes = [ctypes.c_void_p]
         L.mte_rccl_comm_create.argtypes = [vp, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
@@ -232,8 +238,10 @@ def batch_ops(b):
 class Engine:
     """One engine per GPU: loads/generates batches, replays them with the HIP kernel."""
 
-    def __init__(self, device=0, chunk_size=10000):
-        cfg = mte_config(device=device, chunk_size=chunk_size)
+    def __init__(self, device=0, chunk_size=10000, snapshot_format=0):
+        """snapshot_format 0: SnapshotV1 (newMergeTreeSnapshotFormat); 1: SnapshotLegacy (the reference's
+        default, client.ts:930-941)."""
+        cfg = mte_config(device=device, chunk_size=chunk_size, snapshot_format=snapshot_format)
         h = ctypes.c_void_p()
         rc = lib().mte_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc:
@@ -311,6 +319,15 @@ class Engine:
     def snapshot_json(self, doc):
         nb = ctypes.c_uint32()
         return self._str_call(lib().mte_snapshot_v1, doc, ctypes.byref(nb))
+
+    def snapshot_legacy(self, doc, catch_up_name="catchupOps"):
+        """SnapshotLegacy ITree (header, body, catch-up messages) after a snapshot_format 1 replay."""
+        n = ctypes.c_size_t()
+        name = catch_up_name.encode()
+        self._check(lib().mte_snapshot_legacy(self._h, doc, name, None, 0, ctypes.byref(n)), "mte_snapshot_legacy")
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._check(lib().mte_snapshot_legacy(self._h, doc, name, buf, n.value + 1, ctypes.byref(n)), "mte_snapshot_legacy")
+        return buf.raw[: n.value].decode("utf-8")
 
     def snapshot_shared_string(self, doc):
         """SharedString summary tree: {"header": intervals "{}", "content": SnapshotV1 tree}."""

@@ -118,6 +118,8 @@ enum {
 #define MTE_F_REL 0x100u          /* op: positions from the MTE_OP_RELPOS record just before it */
 #define MTE_F_REL_BEFORE1 0x200u  /* RELPOS: relativePos1.before */
 #define MTE_F_REL_BEFORE2 0x400u  /* RELPOS: relativePos2.before */
+#define MTE_F_CATCHUP 0x800u      /* op of a catch-up message the legacy summary rewrites (refSeq != seq - 1,
+                                     sequence.ts:603-625): the engine records its delta ranges */
 
 typedef struct mte_op {
     int32_t seq;        /* sequenceNumber */
@@ -161,6 +163,13 @@ typedef struct mte_batch {
     const uint32_t* doc_client_offsets;   /* n_docs+1 prefix offsets into client_name_offsets */
     const uint64_t* client_name_offsets;  /* (total names)+1 byte offsets into client_names */
     const char* client_names;             /* UTF-8 */
+    /* SnapshotLegacy catch-up messages (messagesSinceMSNChange, sequence.ts:597-650): per doc the op
+     * messages above its log's final MSN, JSON.stringify(JSON.parse(message)) text, and the
+     * doc-relative index of each one's first op record. All NULL: none kept. */
+    const uint64_t* doc_msg_offsets;      /* n_docs+1 prefix offsets into msg_first_op / msg_text_offsets */
+    const uint64_t* msg_first_op;
+    const uint64_t* msg_text_offsets;     /* (total msgs)+1 byte offsets into msg_text */
+    const char* msg_text;
 } mte_batch;
 
 /* ---- engine ------------------------------------------------------------------------------ */
@@ -169,7 +178,9 @@ typedef struct mte_engine mte_engine;
 typedef struct mte_config {
     int32_t device;             /* HIP device ordinal */
     uint32_t chunk_size;        /* SnapshotV1 chunk size (snapshotV1.ts:40); 0 => 10000 */
-    uint32_t reserved[6];
+    uint32_t snapshot_format;   /* 0: SnapshotV1 (runtime option newMergeTreeSnapshotFormat: true);
+                                   1: SnapshotLegacy (the reference's default, client.ts:930-941) */
+    uint32_t reserved[5];
 } mte_config;
 
 typedef struct mte_stats {
@@ -251,8 +262,17 @@ int mte_segments(mte_engine* e, uint32_t doc, mte_seg_row* rows, size_t cap, siz
  * buf may be NULL to query *len. */
 int mte_snapshot_v1(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len, uint32_t* n_blobs);
 /* SharedSegmentSequence.snapshotCore (sequence.ts:413-438): the SharedString summary tree, "header"
- * (interval collections: "{}") + "content" (the tree of mte_snapshot_v1). buf may be NULL. */
+ * (interval collections: "{}") + "content" (the tree of mte_snapshot_v1, or of mte_snapshot_legacy
+ * after a replay with snapshot_format 1). buf may be NULL. */
 int mte_snapshot_shared_string(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* len);
+/* SnapshotLegacy.extractSync + emit (snapshotlegacy.ts:103-238) after a replay with snapshot_format 1:
+ * the ITree JSON {"entries":[header, body?, <catch_up_name>]} -- the view at minSeq in
+ * MergeTreeChunkLegacy chunks (serializeAsMinSupportedVersion, snapshotChunks.ts:75-111) and the
+ * catch-up messages above minSeq (sequence.ts:584-634: minimumSequenceNumber set to minSeq; a message
+ * whose refSeq is not seq - 1 rewritten to refSeq seq - 1 with contents rebuilt from its delta
+ * ranges, createOpsFromDelta sequence.ts:58-100). catch_up_name NULL => "catchupOps". buf may be NULL.
+ * MTE_E_UNSUPPORTED when the document has ops above minSeq but no message JSON (generated logs). */
+int mte_snapshot_legacy(mte_engine* e, uint32_t doc, const char* catch_up_name, char* buf, size_t cap, size_t* len);
 /* Per-doc summaries for all docs of the batch (checksum over text + snapshot blobs). */
 int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap);
 

@@ -12,7 +12,7 @@ export interface DocSummary {
 export interface DocLog { observer?: string; messages: ISequencedDocumentMessage[]; summary?: ITree | string; }
 
 export declare class BatchedMergeEngine {
-    constructor(options?: { device?: number; chunkSize?: number });
+    constructor(options?: { device?: number; chunkSize?: number; newMergeTreeSnapshotFormat?: boolean });
     load(docs: DocLog[]): void;
     generate(kind: 2 | 3 | 5, nDocs: number, nOps: number, nClients?: number, seed?: number): void;
     replay(): ReplayStats;
@@ -23,6 +23,8 @@ export declare class BatchedMergeEngine {
     /** Client.getLength: the observer's visible length, markers counting 1. */
     getLength(doc: number): number;
     snapshotV1(doc: number): ITree;
+    /** After a replay with newMergeTreeSnapshotFormat: false. */
+    snapshotLegacy(doc: number, catchUpBlobName?: string): ITree;
     summaries(): DocSummary[];
 }
 

@@ -16,7 +16,9 @@ class BatchedMergeEngine {
     constructor(options = {}) {
         this.device = options.device || 0;
         this.chunkSize = options.chunkSize || 10000;  // SnapshotV1.chunkSize (snapshotV1.ts:40)
-        this._engine = addon.createEngine(this.device, this.chunkSize);
+        // newMergeTreeSnapshotFormat (client.ts:930-941): true (default here) SnapshotV1, false SnapshotLegacy
+        this.legacyFormat = options.newMergeTreeSnapshotFormat === false;
+        this._engine = addon.createEngine(this.device, this.chunkSize, this.legacyFormat ? 1 : 0);
         this._docs = 0;
     }
     /** Stage per-document logs: docs = [{ observer, messages: ISequencedDocumentMessage[], summary? }]
@@ -57,6 +59,10 @@ class BatchedMergeEngine {
     getText(doc) { this._idle(); return addon.getText(this._engine, doc); }
     /** The ITree SnapshotV1.emit(serializer) returns: { entries: [...], id: null } */
     snapshotV1(doc) { return JSON.parse(addon.snapshotV1(this._engine, doc)); }
+    /** SnapshotLegacy ITree (snapshotlegacy.ts:103-182): header, body, catch-up messages */
+    snapshotLegacy(doc, catchUpBlobName = "catchupOps") {
+        return JSON.parse(addon.snapshotLegacy(this._engine, doc, catchUpBlobName));
+    }
     /** 32-byte records {checksum u64, ops, length, segments, snapshotBytes, status, docId} */
     summaries() {
         const buf = addon.summaries(this._engine, this._docs);
@@ -125,7 +131,12 @@ class MergeTreeClient {
     getText() { return this._run().getText(0); }
     /** Client.getLength (client.ts:1057): markers count 1, unlike getText().length. */
     getLength() { return this._run().getLength(0); }
-    snapshot() { return this._run().snapshotV1(0); }
+    /** Client.snapshot (client.ts:907-942): SnapshotV1, or SnapshotLegacy with its catch-up messages
+     *  when the options say newMergeTreeSnapshotFormat: false. */
+    snapshot() {
+        const e = this._run();
+        return e.legacyFormat ? e.snapshotLegacy(0, this.options.catchUpBlobName) : e.snapshotV1(0);
+    }
 }
 
 module.exports = {

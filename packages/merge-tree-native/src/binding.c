@@ -84,15 +84,19 @@ static napi_value js_build_info(napi_env env, napi_callback_info info) {
     return r;
 }
 
-/* createEngine(device, chunkSize): External — new Client(...) for a whole batch */
+/* createEngine(device, chunkSize, snapshotFormat): External — new Client(...) for a whole batch;
+ * snapshotFormat 1 = SnapshotLegacy (the reference's default, client.ts:930-941) */
 static napi_value js_create_engine(napi_env env, napi_callback_info info) {
-    napi_value argv[2];
+    napi_value argv[3];
     mte_config cfg;
     memset(&cfg, 0, sizeof cfg);
-    if (get_args(env, info, 2, argv)) {
+    size_t argc = 3;
+    napi_get_cb_info(env, info, &argc, argv, NULL, NULL);
+    if (argc >= 2) {
         napi_get_value_int32(env, argv[0], &cfg.device);
         napi_get_value_uint32(env, argv[1], &cfg.chunk_size);
     }
+    if (argc >= 3) napi_get_value_uint32(env, argv[2], &cfg.snapshot_format);
     mte_engine* e = NULL;
     int rc = mte_create(&cfg, &e);
     if (rc) return throw_mte(env, "mte_create", rc, "no HIP device (MI355X/gfx950 required; no CPU fallback)");
@@ -378,6 +382,33 @@ static napi_value js_snapshot(napi_env env, napi_callback_info info) {
     return s;
 }
 
+/* snapshotLegacy(engine, doc, catchUpBlobName): string — the SnapshotLegacy.emit ITree as JSON */
+static napi_value js_snapshot_legacy(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    size_t argc = 3;
+    napi_get_cb_info(env, info, &argc, argv, NULL, NULL);
+    if (argc < 2) {
+        napi_throw_type_error(env, NULL, "snapshotLegacy(engine, doc, catchUpBlobName?)");
+        return NULL;
+    }
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    uint32_t d;
+    napi_get_value_uint32(env, argv[1], &d);
+    char name[256] = "catchupOps";
+    size_t nl = 0;
+    if (argc >= 3) napi_get_value_string_utf8(env, argv[2], name, sizeof name, &nl);
+    size_t n = 0;
+    int rc = mte_snapshot_legacy(e, d, name, NULL, 0, &n);
+    if (rc) return throw_mte(env, "mte_snapshot_legacy", rc, mte_last_error(e));
+    char* buf = (char*)malloc(n + 1);
+    rc = mte_snapshot_legacy(e, d, name, buf, n + 1, &n);
+    napi_value s;
+    if (!rc) napi_create_string_utf8(env, buf, n, &s);
+    free(buf);
+    if (rc) return throw_mte(env, "mte_snapshot_legacy", rc, mte_last_error(e));
+    return s;
+}
+
 /* summaries(engine, nDocs): Buffer of 32-byte mte_doc_summary records */
 static napi_value js_summaries(napi_env env, napi_callback_info info) {
     napi_value argv[2];
@@ -411,6 +442,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"docStatus", 0, js_doc_status, 0, 0, 0, napi_default, 0},
         {"getText", 0, js_text, 0, 0, 0, napi_default, 0},
         {"snapshotV1", 0, js_snapshot, 0, 0, 0, napi_default, 0},
+        {"snapshotLegacy", 0, js_snapshot_legacy, 0, 0, 0, napi_default, 0},
         {"summaries", 0, js_summaries, 0, 0, 0, napi_default, 0},
     };
     napi_define_properties(env, exports, sizeof props / sizeof props[0], props);

@@ -33,6 +33,13 @@ for (const ent of mk.entries[1].value.entries) {
 }
 assert.ok(markers > 0);
 assert.strictEqual(c3.getLength(), c3.getText().length + markers);
+// newMergeTreeSnapshotFormat: false -> SnapshotLegacy (client.ts:930-941): the reference's legacy fixture
+const legacyFix = JSON.parse(require("fs").readFileSync(__dirname + "/../../../tests/golden/legacyWithCatchUp/headerOnly.json", "utf8"));
+const lc = new MergeTreeClient("", { newMergeTreeSnapshotFormat: false });
+for (let i = 0; i < 1250; i++) lc.applyMsg(msg("", i + 1, i, { pos1: 0, seg: `text${i}`, type: 0 }));
+const lt = lc.snapshot();
+assert.deepStrictEqual(lt.entries.map((x) => [x.path, x.value.contents]),
+    legacyFix.entries[1].value.entries.map((x) => [x.path, x.value.contents]));
 const e = new BatchedMergeEngine();
 e.generate(2, 8, 500, 8, 3);
 const st = e.replay();

@@ -426,6 +426,12 @@ struct Engine {
         return x == BM_NOPAR ? NONE : x;
     }
     MTE_DEV u32 bscour(u32 b) const { return b < blk_cap() ? U(BMETA()[b]) >> 30 : SC_UNDEF; }
+    // the whole metadata word (parent | needsScour), for a read-modify-write with one read
+    MTE_DEV u32 bmeta_u(u32 b) const { return b < blk_cap() ? U(BMETA()[b]) : (BM_NOPAR | (SC_UNDEF << 30)); }
+    MTE_DEV static u32 par_of_word(u32 w) { return (w & BM_PAR) == BM_NOPAR ? NONE : (w & BM_PAR); }
+    MTE_DEV void set_bscour_w(u32 b, u32 w, u32 sc) const {  // w: the block's current metadata word
+        if (L == 0 && b < blk_cap()) BMETA()[b] = (w & BM_PAR) | (sc << 30);
+    }
     MTE_DEV void set_bpar_lane(u32 b, u32 par) const {  // per-lane write
         if (b < blk_cap()) BMETA()[b] = (BMETA()[b] & ~BM_PAR) | (par == NONE ? BM_NOPAR : (par & BM_PAR));
     }
@@ -989,19 +995,32 @@ struct Engine {
         return NONE;
     }
     // Current leaf block of segment `sid` (the LRU heap entry's segment.parent), NONE if unlinked.
-    MTE_DEV bool find_seg(u32 sid, u32& k, u32& blk, u32& cnt) {
+    MTE_DEV bool find_seg(u32 sid, u32& k, u32& blk, u32& cnt, u32& bm) {
         MTE_PROF(PF_FIND_SEG);
-        {  // the block recorded at push time (kept current by splits and packs)
+        {  // the block recorded at push time (kept current by splits and packs): its slots, its
+           // metadata word and the doc-order entry holding it are independent reads
             const u32 hb = hint_get(sid);
-            const u32 kk = ord_find(hb);
+            const u32 hs = AUX()[sidx(hb, L)].w;
+            const u32 hw = BMETA()[hb < blk_cap() ? hb : 0u];
+            u32 kk = NONE, c = 0;
+            for (u32 base = 0; base < st.n_lb; base += 64) {
+                const u32 idx = base + L;
+                const uint4 o = idx < st.n_lb ? ORD()[idx] : make_uint4(NONE, 0, 0, 0);
+                const u64 m = wave_ballot(idx < st.n_lb && o.x == hb);
+                if (m) {
+                    const u32 j = (u32)__builtin_ctzll(m);
+                    kk = base + j;
+                    c = wave_read(o.w, j);
+                    break;
+                }
+            }
             if (kk != NONE) {
-                const uint4 o = ORD()[kk];
-                const u32 c = wave_first(o.w);
-                const u64 m = wave_ballot((L < c) & (L < 8) & (AUX()[sidx(hb, L)].w == sid));
+                const u64 m = wave_ballot((L < c) & (L < 8) & (hs == sid));
                 if (m) {
                     k = kk;
                     blk = hb;
                     cnt = c;
+                    bm = U(hw);
                     return true;
                 }
             }
@@ -1016,6 +1035,7 @@ struct Engine {
                 k = base + (l >> 3);
                 blk = wave_read(o.x, l);
                 cnt = wave_read(o.w, l);
+                bm = bmeta_u(blk);
                 return true;
             }
         }
@@ -1114,13 +1134,14 @@ struct Engine {
         const bool mv = L >= j && L < cnt;
         Seg t;
         if (mv) t = load(blk, L);
+        const uint4 ok = ORD()[k];  // read beside the slots (the stores below do not touch it)
         sync();
         if (mv) store(blk, L + 1, t);
         if (L == 0) store(blk, j, rec);
         const u32 nc = cnt + 1;
         if (nc < 8) {
             if (L == 0) {
-                uint4 o = ORD()[k];
+                uint4 o = ok;
                 o.w = nc;
                 if (fresh) {
                     o.y += obs_len(rec.len, rec.meta);
@@ -1312,10 +1333,10 @@ struct Engine {
     MTE_DEV void add_lru(u32 blk, u32 sid, i32 seq) {
         MTE_PROF(PF_LRU);
         if (!collab || blk == NONE) return;
-        u32 sc = bscour(blk);
-        if (sc != SC_TRUE && seq > st.curSeq) {
+        const u32 w = bmeta_u(blk);
+        if ((w >> 30) != SC_TRUE && seq > st.curSeq) {
             sync();
-            set_bscour(blk, SC_TRUE);
+            set_bscour_w(blk, w, SC_TRUE);
             sync();
             heap_push(sid, seq, blk);
         }
@@ -1492,6 +1513,9 @@ struct Engine {
     // jobs (sources are never destinations of the same batch, see scour()).
     MTE_DEV void run_jobs(const Jobs& jb) {
         MTE_PROF(PF_TEXT);
+#ifdef MTE_NO_TEXT  // timing experiment only (wrong text): the cost of the scour's text copies
+        return;
+#endif
         const u32 jl = L < jb.n ? jb.len : 0u;
         const u32 jinc = wave_scan_incl(jl);
         const u32 total = wave_read(jinc, 63);
@@ -1808,19 +1832,19 @@ struct Engine {
         for (int i = 0; i < 2 && !st.status; i++) {
             if (st.heapSize == 0 || st.heapTop > st.minSeq) break;
             uint2 e = heap_pop();
-            u32 k, blk, cnt;
-            if (!find_seg(e.x, k, blk, cnt)) continue;  // segment no longer linked
-            if (bscour(blk) == SC_FALSE) continue;
+            u32 k, blk, cnt, bm;
+            if (!find_seg(e.x, k, blk, cnt, bm)) continue;  // segment no longer linked
+            if ((bm >> 30) == SC_FALSE) continue;
             bool packing = false;
             u32 par = NONE, m = 0, kids = NONE, k0 = 0, cnts = 0, idx = 0;
             for (;;) {
                 const u32 nc = scour(k, blk, cnt);
                 if (st.status) return;
                 if (!packing) {
-                    set_bscour(blk, SC_FALSE);
+                    set_bscour_w(blk, bm, SC_FALSE);  // scour leaves the metadata word alone
                     sync();
                     if (!(nc < cnt && nc < 4 && st.height > 1)) break;
-                    par = bpar(blk);
+                    par = par_of_word(bm);
                     if (par == NONE || par >= in_cap() || incnt_u(par) > 8 || incnt_u(par) == 0) {
                         fail(MTE_DOC_CAPACITY, st.curSeq);
                         return;
@@ -2004,6 +2028,7 @@ struct Engine {
                 const u32 idx = sidx(blk, s);
                 uint4 q = VIS()[idx];
                 const u32 z = AUX()[idx].z;
+                const uint4 obk = ORD()[kj];  // read beside the slots (marking does not touch it)
                 const bool in = s < cnt && s < 8;
                 const u32 sv = in ? vis_len(q, z, idx, R, C, C == 0 ? 1u : 0u) : 0u;
                 const u32 si = group8_scan(sv);
@@ -2035,7 +2060,7 @@ struct Engine {
                     if (C >= 32 && wave_ballot(mark && !fresh)) st.gdirty = 1;
                     const u32 gone = wave_read(group8_scan(fresh), 7);
                     if (L == 0) {
-                        uint4 ob = ORD()[kj];
+                        uint4 ob = obk;
                         ob.y -= gone;
                         if (gone && seq > (i32)ob.z) ob.z = (u32)seq;
                         ORD()[kj] = ob;

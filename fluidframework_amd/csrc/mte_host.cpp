@@ -694,7 +694,10 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     }
     if (cu) {
         HIP_TRY(e, e->d_cu.alloc(2 * cu));
-        if ((rc = upload(e, e->d_cfg, e->cfg))) return rc;
+        // same size: copy into the buffer the kernels' Params::docs already points at (upload would
+        // reallocate it and leave that pointer dangling)
+        HIP_TRY(e, hipMemcpyAsync(e->d_cfg.p, e->cfg.data(), e->cfg.size() * sizeof(DocCfg), hipMemcpyHostToDevice,
+                                  e->stream));
     }
     e->P.cu_rec = cu ? e->d_cu.p : nullptr;
     if ((rc = upload(e, e->d_ops, e->hb.ops))) return rc;
@@ -1577,7 +1580,7 @@ static int catch_up_json(mte_engine* e, uint32_t d, std::string& out) {
     const uint64_t op0 = hb.doc_op_offsets[d], nops = hb.doc_op_offsets[d + 1] - op0;
     // every applied op above minSeq must have its message (generated logs have none)
     uint64_t need = 0, have = 0;
-    for (uint64_t i = 0; i < nops; i++) {
+    for (uint64_t i = 0; e->cfg[d].collab && i < nops; i++) {  // local (non-collaborative) edits are not messages
         const mte_op& o = hb.ops[op0 + i];
         if ((o.flags & MTE_F_END_OF_MSG) && o.seq > minSeq && o.type <= MTE_OP_INSERT_MARKER) need++;
     }

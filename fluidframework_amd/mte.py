@@ -357,10 +357,10 @@ class Engine:
 
     DOC_RESULT_FIELDS = ["status", "failing_seq", "ops", "msgs", "min_seq", "cur_seq", "height", "n_lb",
                          "arena_sel", "arena_top", "map_next", "seg_next", "heap_size", "n_gc", "out_off", "n_segs",
-                         "max_lb", "mode", "spill_why", "text_off"]
+                         "max_lb", "mode", "spill_why", "text_off", "cu_n"]
 
     def doc_result(self, doc):
-        buf = (ctypes.c_int32 * 20)()
+        buf = (ctypes.c_int32 * 21)()
         self._check(lib().mte_doc_result(self._h, doc, buf, ctypes.sizeof(buf)), "mte_doc_result")
         return dict(zip(self.DOC_RESULT_FIELDS, list(buf)))
 

@@ -209,15 +209,16 @@ struct Doc {
     MTE_DEV const u16* row_text(uint4 a) const { return p.text + r.text_off + a.y; }
 
     // 1. entries: ent[row0 + k] = (first row, last row, length, kind) with kind 0 a settled text
-    // run, 1 a settled marker, 2 a merge-info segment; returns the entry count
+    // run, 1 a settled marker, 2 a merge-info segment, 3 a settled PermutationSegment run (its
+    // canAppend: two unallocated runs always append, permutationvector.ts:88-94); returns the count
     MTE_DEV u32 build_entries() const {
         const u32 L = lane_id(), n = r.n_segs;
         const i32 minSeq = r.min_seq;
         u32 ne = 0;
-        bool open = false, runText = false, runProps = false;
+        bool open = false, runText = false, runProps = false, runPerm = false;
         u32 runFirst = 0, runLast = 0, runLen = 0, runLast16 = 0;
         auto close = [&]() {
-            if (open && L == 0) p.ent[row0 + ne] = make_uint4(runFirst, runLast, runLen, runText ? 0u : 1u);
+            if (open && L == 0) p.ent[row0 + ne] = make_uint4(runFirst, runLast, runLen, runPerm ? 3u : runText ? 0u : 1u);
             ne += open ? 1u : 0u;
             open = false;
         };
@@ -228,19 +229,21 @@ struct Doc {
             if (k < n) {
                 v = p.vis[row0 + k];
                 a = p.aux[row0 + k];
-                if (!(v.w & F_MARKER) && v.x) last16 = row_text(a)[v.x - 1];
+                if (!(v.w & (F_MARKER | F_PERM)) && v.x) last16 = row_text(a)[v.x - 1];
             }
             const u32 cnt = n - base < 64 ? n - base : 64u;
             for (u32 j = 0; j < cnt; j++) {
                 const u32 len = wave_read(v.x, j), seq = wave_read(v.y, j), rseq = wave_read(v.z, j);
                 const u32 meta = wave_read(v.w, j), hasP = wave_read(a.x, j) != 0;
-                const bool removed = (meta & F_REMOVED) != 0, marker = (meta & F_MARKER) != 0;
+                const bool removed = (meta & F_REMOVED) != 0, marker = (meta & F_MARKER) != 0, perm = (meta & F_PERM) != 0;
                 const u32 row = base + j;
                 if (removed && (i32)rseq <= minSeq) continue;  // elided (:184-186)
                 if (p.legacy && (i32)seq > minSeq) continue;   // not in the view at minSeq (legacy :195-196)
                 if ((i32)seq <= minSeq && (!removed || p.legacy)) {
-                    if (open && runText && !marker && !(runLen && runLast16 == u'\n') &&
-                        (runLen <= 256 || len <= 256) && match(row0 + runFirst, runProps, row0 + row, hasP)) {
+                    if (open && (runPerm ? perm
+                                         : runText && !marker && !perm && !(runLen && runLast16 == u'\n') &&
+                                               (runLen <= 256 || len <= 256)) &&
+                        match(row0 + runFirst, runProps, row0 + row, hasP)) {
                         runLast = row;  // clone + append (:197-202)
                         runLen += len;
                         if (len) runLast16 = wave_read(last16, j);
@@ -248,7 +251,8 @@ struct Doc {
                     }
                     close();
                     open = true;
-                    runText = !marker;
+                    runText = !marker && !perm;
+                    runPerm = perm;
                     runProps = hasP;
                     runFirst = runLast = row;
                     runLen = len;
@@ -297,6 +301,12 @@ struct Doc {
     }
     MTE_DEV void put_seg(Out& o, u32 row, const u16* txt, u64 n) const {  // Segment.toJSONObject
         const uint4 v = p.vis[row0 + row], a = p.aux[row0 + row];
+        if (v.w & F_PERM) {  // PermutationSegment.toJSONObject (permutationvector.ts:75-77): [length, start]
+            put(o, "[");
+            put_int(o, (i64)n);
+            put(o, ",-2147483648]");  // Handle.unallocated: an observer never allocates handles
+            return;
+        }
         if (v.w & F_MARKER) {
             put(o, "{\"marker\":{\"refType\":");
             put_int(o, a.y & 0xFFFFu);
@@ -317,15 +327,16 @@ struct Doc {
         }
     }
     MTE_DEV void put_entry(Out& o, uint4 e) const {
-        if (e.w == 0 || e.w == 1) {  // settled: coalesced text run or a marker
-            u64 n = 0;
+        if (e.w == 0 || e.w == 1 || e.w == 3) {  // settled: coalesced text / permutation run or a marker
+            u64 n = e.w == 3 ? e.z : 0;
             const u16* t = e.w == 0 ? run_text(e, n) : nullptr;
             put_seg(o, e.x, t, n);
             return;
         }
         const uint4 v = p.vis[row0 + e.x], a = p.aux[row0 + e.x];
+        const bool notext = (v.w & (F_MARKER | F_PERM)) != 0;
         put(o, "{\"json\":");
-        put_seg(o, e.x, (v.w & F_MARKER) ? nullptr : row_text(a), (v.w & F_MARKER) ? 0 : v.x);
+        put_seg(o, e.x, notext ? nullptr : row_text(a), (v.w & F_MARKER) ? 0 : v.x);
         const bool collab = p.cfg[d].collab != 0;
         if ((i32)v.y > r.min_seq) {
             put(o, ",\"seq\":");

@@ -1557,7 +1557,10 @@ struct Engine {
         MTE_COUNT(PN_SCOUR, 1);
         if (!(mREM & ~mKEPT) && !(mSET & (mSET << 1))) return cnt;  // nothing dropped, nothing to merge
         MTE_COUNT(PN_SCOUR_CHANGED, 1);
-        const u64 mTXT = wave_ballot(act && !(me.meta & F_MARKER));
+        const u64 mTXT = wave_ballot(act && !(me.meta & (F_MARKER | F_PERM)));
+        // PermutationSegment runs (FULL batches only): canAppend holds between two unallocated runs
+        // (permutationvector.ts:88-94; an observer never allocates handles), no granularity, no text
+        const u64 mPERM = FULL ? wave_ballot(act && (me.meta & F_PERM)) : 0ull;
         const u64 mNL = (FULL && has_nl) ? wave_ballot(act && !(me.meta & F_MARKER) && ends_nl(me.toff, me.len)) : 0ull;
         u32 nkeep = 0;
         u32 kSrc = 0, kLen = 0, kOff = 0, kCap = 0;  // lane i < nkeep: kept slot i
@@ -1574,7 +1577,7 @@ struct Engine {
             // pMat: leading chars of the head's text already in memory; [pMat, pLen) are pending
             // in-place append jobs of this batch (a copy of the head must not read them)
             u32 pLen = 0, pOff = 0, pCap = 0, pProps = 0, pMat = 0;
-            bool pText = false, pNL = false, pFresh = false;
+            bool pText = false, pNL = false, pFresh = false, pPerm = false;
             for (u32 s = 0; s < cnt; s++) {
                 const u64 bit = 1ull << s;
                 bool keep = true;
@@ -1584,10 +1587,13 @@ struct Engine {
                 } else if (mSET & bit) {
                     const u32 len = wave_read(me.len, s), props = wave_read(me.props, s);
                     const u32 toff = wave_read(me.toff, s), tcap = wave_read(me.tcap, s);
-                    const bool ok = prev >= 0 && pText && !pNL && (mTXT & bit) &&
-                                    (pLen <= (u32)GRANULARITY || len <= (u32)GRANULARITY) && match_props(pProps, props);
-                    if (ok) {  // TextSegment.append (textSegment.ts:74-85)
-                        if ((pOff & ARENA_BIT) && pLen + len <= pCap) {
+                    const bool ok = prev >= 0 && match_props(pProps, props) &&
+                                    (pPerm ? (mPERM & bit) != 0
+                                           : pText && !pNL && (mTXT & bit) &&
+                                                 (pLen <= (u32)GRANULARITY || len <= (u32)GRANULARITY));
+                    if (ok) {  // TextSegment.append (textSegment.ts:74-85) / PermutationSegment.append
+                        if (pPerm) {
+                        } else if ((pOff & ARENA_BIT) && pLen + len <= pCap) {
                             job_add(jb, pOff + pLen, toff, len);
                         } else if (pOff + pLen == toff && pMat == pLen) {  // text already contiguous
                             if (pOff & ARENA_BIT) pCap = toff + tcap - pOff;
@@ -1624,6 +1630,7 @@ struct Engine {
                         pCap = tcap;
                         pProps = props;
                         pText = (mTXT & bit) != 0;
+                        pPerm = (mPERM & bit) != 0;
                         pNL = pText && (mNL & bit);
                         pFresh = false;
                     }
@@ -2347,14 +2354,14 @@ struct Engine {
             rec.len = mk ? 1u : op.b;
             rec.seq = seq;
             rec.rseq = 0;
-            rec.meta = (C & 0xff) | (mk ? F_MARKER : 0u);
+            rec.meta = (C & 0xff) | (mk ? F_MARKER : 0u) | ((FULL && !ld && (op.flags & MTE_F_PERM)) ? F_PERM : 0u);
             u32 type = op.type;
             i32 p1 = op.pos1;
             if (ld && !load_append_pos(op, rec, p1)) return;  // skipped (a repeated object) or failed
             type = ld ? (mk ? (u32)MTE_OP_INSERT_MARKER : (u32)MTE_OP_INSERT) : type;
             rec.props = (ins && op.props) ? build_map(0, op.props, false) : 0u;
             if (st.status) return;
-            rec.toff = (mk && !ld) ? op.b : (u32)op.a;
+            rec.toff = (mk && !ld) ? op.b : ((rec.meta & F_PERM) ? 0u : (u32)op.a);
             rec.tcap = 0;
             rec.sid = 0;
             const bool cu = (op.flags & MTE_F_CATCHUP) != 0 && !ld;
@@ -2440,7 +2447,7 @@ struct Engine {
         const u32 c = o.w > 8 ? 8u : o.w;
         for (u32 s = 0; s < c; s++) {
             const uint4 v = VIS()[o.x * 8 + s];
-            t += (v.w & F_MARKER) ? 0u : v.x;
+            t += (v.w & (F_MARKER | F_PERM)) ? 0u : v.x;
         }
         return t;
     }
@@ -2483,7 +2490,7 @@ struct Engine {
                 u32 tat = trun + tincl - bt;
                 for (u32 s = 0; s < c; s++) {
                     uint4 v = VIS()[o.x * 8 + s], a = AUX()[o.x * 8 + s];
-                    if (!(v.w & F_MARKER)) {  // wave-divergent copy, 8 units in flight per lane
+                    if (!(v.w & (F_MARKER | F_PERM))) {  // wave-divergent copy, 8 units in flight per lane
                         const u16* __restrict__ src = text_ptr(a.y);
                         u16* __restrict__ dst = tdst + tat;
                         for (u32 i = 0; i < v.x; i += 8) {

@@ -20,6 +20,7 @@ constexpr u32 SC_UNDEF = 0, SC_TRUE = 1, SC_FALSE = 2;   // needsScour tri-state
 constexpr u32 F_REMOVED = 1u << 16, F_MARKER = 1u << 17;  // slot meta flags
 constexpr u32 F_OVL = 1u << 18;    // removedClientOverlap non-empty: clients 0..31 in aux.z (dead tcap)
 constexpr u32 F_OVLHI = 1u << 19;  // ... and clients 32..63 in the HBM mask by segment id
+constexpr u32 F_PERM = 1u << 20;   // PermutationSegment run (SharedMatrix row / col vector): no text
 constexpr u32 MAP_WORDS = 16;                            // [0]=count, then 7 (key,val) pairs
 constexpr i32 GRANULARITY = 256;                         // TextSegmentGranularity (mergeTree.ts:1059)
 

@@ -634,7 +634,7 @@ static void count_doc_ops(const HostBatch& hb, uint32_t d, uint64_t& pi, uint64_
     pi = an = 0;
     for (uint64_t i = hb.doc_op_offsets[d]; i < hb.doc_op_offsets[d + 1]; i++) {
         const mte_op& o = hb.ops[i];
-        if (rel && o.type == MTE_OP_RELPOS) *rel = true;
+        if (rel && (o.type == MTE_OP_RELPOS || (o.flags & MTE_F_PERM))) *rel = true;  // FULL kernels only
         if ((o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER || o.type == MTE_OP_LOAD_SEG ||
              o.type == MTE_OP_LOAD_APPEND) && o.props)
             pi++;
@@ -1119,7 +1119,7 @@ static int ensure_download(mte_engine* e) {
 
 namespace {
 struct SegView {
-    uint32_t kind;  // 0 text, 1 marker
+    uint32_t kind;  // 0 text, 1 marker, 2 permutation run
     uint32_t len;
     int32_t seq, client, rseq, rclient;
     bool removed;
@@ -1145,7 +1145,7 @@ struct DocView {
                 uint4 a = e->h_out_aux[i];
                 uint2 t = make_uint2(a.y, a.z);
                 SegView sv;
-                sv.kind = (v.w & F_MARKER) ? 1 : 0;
+                sv.kind = (v.w & F_MARKER) ? 1 : (v.w & F_PERM) ? 2 : 0;
                 sv.len = v.x;
                 sv.seq = (int32_t)v.y;
                 sv.removed = (v.w & F_REMOVED) != 0;
@@ -1154,7 +1154,7 @@ struct DocView {
                 sv.rclient = c.collab ? (int32_t)((v.w >> 8) & 0xff) : -1;
                 sv.ovl = e->h_out_ovl[i];
                 sv.props = a.x ? (uint32_t)(i + 1) : 0u;
-                sv.reftype = sv.kind ? (t.x & 0xFFFFu) : 0;  // bits 16..31: the marker's tag
+                sv.reftype = sv.kind == 1 ? (t.x & 0xFFFFu) : 0;  // bits 16..31: the marker's tag
                 sv.text = sv.kind ? nullptr : txt + t.x;
                 segs.push_back(sv);
             }
@@ -1329,8 +1329,9 @@ int mte_segments_json(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t
         const SegView& s = v.segs[i];
         if (i) o += ",";
         o += "{\"kind\":";
-        o += s.kind ? "\"M\"" : "\"T\"";
-        if (s.kind) o += ",\"refType\":" + std::to_string(s.reftype);
+        o += s.kind == 1 ? "\"M\"" : s.kind == 2 ? "\"P\"" : "\"T\"";
+        if (s.kind == 1) o += ",\"refType\":" + std::to_string(s.reftype);
+        else if (s.kind == 2) o += ",\"start\":" + std::to_string(INT32_MIN);
         else {
             o += ",\"text\":";
             json::quote(o, (const char16_t*)s.text, s.len);
@@ -1454,6 +1455,33 @@ int mte_snapshot_v1(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* 
     }
     o += "],\"id\":null}";
     if (n_blobs) *n_blobs = (uint32_t)blobs.size();
+    if (len) *len = o.size();
+    if (!buf) return MTE_OK;
+    if (cap < o.size()) return MTE_E_RANGE;
+    memcpy(buf, o.data(), o.size());
+    return MTE_OK;
+}
+
+// SharedMatrix.snapshotCore (matrix.ts:405-430) over PermutationVector.snapshot (permutationvector.ts:260-273).
+int mte_snapshot_matrix(mte_engine* e, uint32_t rows_doc, uint32_t cols_doc, char* buf, size_t cap, size_t* len) {
+    if (!e) return MTE_E_ARG;
+    std::string o = "{\"entries\":[";
+    const uint32_t docs[2] = {rows_doc, cols_doc};
+    for (int i = 0; i < 2; i++) {
+        size_t n = 0;
+        int rc = mte_snapshot_v1(e, docs[i], nullptr, 0, &n, nullptr);
+        if (rc) return rc;
+        std::string seg(n, '\0');
+        if ((rc = mte_snapshot_v1(e, docs[i], &seg[0], n, &n, nullptr))) return rc;
+        o += std::string("{\"mode\":\"040000\",\"path\":\"") + (i ? "cols" : "rows") + "\",\"type\":\"Tree\",\"value\":";
+        // the handle table: [1] (its free-list head) until a cell op allocates a handle
+        o += "{\"entries\":[{\"mode\":\"040000\",\"path\":\"segments\",\"type\":\"Tree\",\"value\":" + seg +
+             "},{\"mode\":\"100644\",\"path\":\"handleTable\",\"type\":\"Blob\",\"value\":"
+             "{\"contents\":\"[1]\",\"encoding\":\"utf-8\"}}],\"id\":null}},";
+    }
+    // cells: [cells.snapshot(), pending.snapshot()] of two empty SparseArray2D ([undefined] each)
+    o += "{\"mode\":\"100644\",\"path\":\"cells\",\"type\":\"Blob\",\"value\":{\"contents\":\"[[null],[null]]\","
+         "\"encoding\":\"utf-8\"}}],\"id\":null}";
     if (len) *len = o.size();
     if (!buf) return MTE_OK;
     if (cap < o.size()) return MTE_E_RANGE;
@@ -2005,6 +2033,7 @@ struct DocBuild {
     std::vector<std::string> names;
     std::unordered_map<std::string, uint32_t> ids;
     bool collab = false;
+    bool perm = false;  // a SharedMatrix row / col vector: PermutationSegment specs
     std::string err;
     // marker ids for relative positions (include/mte.h MTE_OP_RELPOS): id -> tag of the marker the
     // reference maps it to; ids tied to two markers, and every id after an annotate that sets a
@@ -2179,7 +2208,15 @@ static int add_messages(mte_builder* b, const json::Value& doc, DocBuild& db) {
                 const json::Value* seg = c->get(u"seg");
                 if (!seg) continue;
                 const json::Value* props = nullptr;
-                if (seg->kind == json::Value::String) {
+                if (db.perm) {  // PermutationSegment.fromJSONObject (permutationvector.ts:41-44): [length, start]
+                    if (seg->kind != json::Value::Array || seg->items.empty() || seg->items[0].kind != json::Value::Number ||
+                        seg->items[0].num < 0 || seg->items[0].num > 0x7FFFFFFF)
+                        return fail(MTE_E_UNSUPPORTED, "not a PermutationSegment spec");
+                    o.type = MTE_OP_INSERT;
+                    o.flags |= MTE_F_PERM;  // handles reset on insert (onDelta, :302-309)
+                    o.a = 0;
+                    o.b = (uint32_t)seg->items[0].num;
+                } else if (seg->kind == json::Value::String) {
                     o.type = MTE_OP_INSERT;
                     o.a = (int32_t)payload.size();
                     o.b = (uint32_t)seg->str.size();
@@ -2889,6 +2926,52 @@ int mte_builder_add_container_log(mte_builder* b, const char* observer_name, con
 
 const char* mte_builder_doc_path(const mte_builder* b, uint32_t doc) {
     return b && doc < b->paths.size() ? b->paths[doc].c_str() : nullptr;
+}
+
+// SharedMatrix.processCore (matrix.ts:548-560): rows then cols, each PermutationVector fed the
+// messages that target it; cell ops allocate handles (not modelled).
+int mte_builder_add_matrix_log(mte_builder* b, const char* observer_name, const char* text, size_t len) {
+    if (!b || !text) return MTE_E_ARG;
+    json::Value log;
+    try {
+        log = json::parse(text, len);
+    } catch (std::exception& ex) {
+        b->err = ex.what();
+        return MTE_E_PARSE;
+    }
+    if (log.kind != json::Value::Array) {
+        b->err = "matrix log must be a JSON array of messages";
+        return MTE_E_PARSE;
+    }
+    json::Value part[2];
+    part[0].kind = part[1].kind = json::Value::Array;
+    for (const json::Value& m : log.items) {
+        const json::Value* c = m.kind == json::Value::Object ? m.get(u"contents") : nullptr;
+        const json::Value* t = c && c->kind == json::Value::Object ? c->get(u"target") : nullptr;
+        if (!t) {
+            if (c && c->kind == json::Value::Object) {
+                b->err = "SharedMatrix cell ops allocate row / col handles (getAllocatedHandle): out of scope";
+                return MTE_E_UNSUPPORTED;
+            }
+            continue;
+        }
+        if (t->kind == json::Value::String && t->str == u"rows") part[0].items.push_back(m);
+        else if (t->kind == json::Value::String && t->str == u"cols") part[1].items.push_back(m);
+    }
+    std::vector<std::unique_ptr<DocBuild>> dbs;
+    for (int i = 0; i < 2; i++) {
+        dbs.emplace_back(new DocBuild(observer_name));
+        dbs.back()->perm = true;
+        if (int rc = add_messages(b, part[i], *dbs.back())) {
+            b->err = dbs.back()->err;
+            return rc;
+        }
+    }
+    for (int i = 0; i < 2; i++) {
+        dbs[i]->commit(b->hb);
+        b->paths.emplace_back(i ? "cols" : "rows");
+    }
+    return MTE_OK;
 }
 
 int mte_builder_batch(mte_builder* b, mte_batch* out) {

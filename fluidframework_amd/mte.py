@@ -103,6 +103,7 @@ EXPORTS = ["mte_abi_version", "mte_build_info", "mte_create", "mte_destroy", "mt
            "mte_replay", "mte_generate", "mte_generate_ids", "mte_export_batch", "mte_doc_status", "mte_text", "mte_length", "mte_segments",
            "mte_snapshot_v1", "mte_snapshot_legacy", "mte_snapshot_shared_string", "mte_summaries", "mte_rccl_unique_id",
            "mte_rccl_comm_create", "mte_rccl_comm_destroy", "mte_gather_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
+           "mte_builder_add_matrix_log", "mte_snapshot_matrix",
            "mte_builder_batch",
            "mte_builder_error", "mte_builder_destroy"]
 
@@ -154,6 +155,8 @@ def lib():
         L.mte_builder_add_doc.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
         L.mte_builder_add_doc_from_summary.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, sz]
         L.mte_builder_add_container_log.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_uint32)]
+        L.mte_builder_add_matrix_log.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
+        L.mte_snapshot_matrix.argtypes = [vp, u32, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.mte_builder_doc_path.argtypes = [vp, ctypes.c_uint32]
         L.mte_builder_doc_path.restype = ctypes.c_char_p
         L.mte_builder_batch.argtypes = [vp, ctypes.POINTER(mte_batch)]
@@ -213,6 +216,18 @@ class Builder:
             raise MteError(f"mte_builder_add_container_log: {rc}: {lib().mte_builder_error(self._h).decode()}")
         first = self.n_docs() - n.value
         return [lib().mte_builder_doc_path(self._h, first + i).decode() for i in range(n.value)]
+
+    def add_matrix_log(self, messages, observer="readonly"):
+        """SharedMatrix messages -> two documents, the rows then the cols PermutationVector
+        (matrix.ts:548-560). Returns their indices (rows, cols)."""
+        t = messages if isinstance(messages, (str, bytes)) else json.dumps(messages, separators=(",", ":"),
+                                                                            ensure_ascii=False)
+        t = t.encode() if isinstance(t, str) else t
+        rc = lib().mte_builder_add_matrix_log(self._h, observer.encode(), t, len(t))
+        if rc:
+            raise MteError(f"mte_builder_add_matrix_log: {rc}: {lib().mte_builder_error(self._h).decode()}")
+        n = self.n_docs()
+        return n - 2, n - 1
 
     def n_docs(self):
         b = mte_batch()
@@ -327,6 +342,15 @@ class Engine:
         self._check(lib().mte_snapshot_legacy(self._h, doc, name, None, 0, ctypes.byref(n)), "mte_snapshot_legacy")
         buf = ctypes.create_string_buffer(n.value + 1)
         self._check(lib().mte_snapshot_legacy(self._h, doc, name, buf, n.value + 1, ctypes.byref(n)), "mte_snapshot_legacy")
+        return buf.raw[: n.value].decode("utf-8")
+
+    def snapshot_matrix(self, rows_doc, cols_doc):
+        """SharedMatrix summary tree (matrix.ts:405-430) of a rows / cols document pair."""
+        n = ctypes.c_size_t()
+        self._check(lib().mte_snapshot_matrix(self._h, rows_doc, cols_doc, None, 0, ctypes.byref(n)), "mte_snapshot_matrix")
+        buf = ctypes.create_string_buffer(n.value + 1)
+        self._check(lib().mte_snapshot_matrix(self._h, rows_doc, cols_doc, buf, n.value + 1, ctypes.byref(n)),
+                    "mte_snapshot_matrix")
         return buf.raw[: n.value].decode("utf-8")
 
     def snapshot_shared_string(self, doc):

@@ -118,6 +118,8 @@ enum {
 #define MTE_F_REL 0x100u          /* op: positions from the MTE_OP_RELPOS record just before it */
 #define MTE_F_REL_BEFORE1 0x200u  /* RELPOS: relativePos1.before */
 #define MTE_F_REL_BEFORE2 0x400u  /* RELPOS: relativePos2.before */
+#define MTE_F_PERM 0x1000u        /* INSERT: a PermutationSegment of a SharedMatrix row / col vector
+                                     (permutationvector.ts:37-127): b = length, no text, handles unallocated */
 #define MTE_F_CATCHUP 0x800u      /* op of a catch-up message the legacy summary rewrites (refSeq != seq - 1,
                                      sequence.ts:603-625): the engine records its delta ranges */
 
@@ -203,7 +205,7 @@ typedef struct mte_doc_summary {   /* 32-B record gathered across ranks (SURVEY 
 } mte_doc_summary;
 
 typedef struct mte_seg_row {       /* parity dump row (walkAllSegments order, mergeTree.ts:2969) */
-    uint32_t kind;                 /* 0 text, 1 marker */
+    uint32_t kind;                 /* 0 text, 1 marker, 2 permutation run */
     uint32_t len;
     int32_t seq;
     int32_t client;                /* short id (-1 local, -2 non-collab) */
@@ -273,6 +275,10 @@ int mte_snapshot_shared_string(mte_engine* e, uint32_t doc, char* buf, size_t ca
  * ranges, createOpsFromDelta sequence.ts:58-100). catch_up_name NULL => "catchupOps". buf may be NULL.
  * MTE_E_UNSUPPORTED when the document has ops above minSeq but no message JSON (generated logs). */
 int mte_snapshot_legacy(mte_engine* e, uint32_t doc, const char* catch_up_name, char* buf, size_t cap, size_t* len);
+/* SharedMatrix.snapshotCore (matrix.ts:405-430) of a rows / cols document pair from
+ * mte_builder_add_matrix_log: each PermutationVector.snapshot (permutationvector.ts:260-273: SnapshotV1
+ * under "segments" + the "handleTable" blob) and the "cells" blob. buf may be NULL. */
+int mte_snapshot_matrix(mte_engine* e, uint32_t rows_doc, uint32_t cols_doc, char* buf, size_t cap, size_t* len);
 /* Per-doc summaries for all docs of the batch (checksum over text + snapshot blobs). */
 int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap);
 
@@ -312,6 +318,12 @@ int mte_builder_add_doc_from_summary(mte_builder* b, const char* observer_name, 
 int mte_builder_add_container_log(mte_builder* b, const char* observer_name, const char* json, size_t len,
                                   uint32_t* n_docs);
 const char* mte_builder_doc_path(const mte_builder* b, uint32_t doc);
+/* SharedMatrix op log (matrix.ts:548-560): a JSON array of its sequenced messages becomes TWO documents,
+ * the rows then the cols PermutationVector (permutationvector.ts:129-146; paths "rows", "cols"), each
+ * fed the messages whose contents.target names it. Segments are PermutationSegment runs
+ * ([length, start] specs). Cell ("set") ops allocate handles and split runs
+ * (getAllocatedHandle, permutationvector.ts:174-193): MTE_E_UNSUPPORTED. */
+int mte_builder_add_matrix_log(mte_builder* b, const char* observer_name, const char* json, size_t len);
 int mte_builder_batch(mte_builder* b, mte_batch* out);   /* view valid until destroy */
 const char* mte_builder_error(const mte_builder* b);
 void mte_builder_destroy(mte_builder* b);

@@ -42,6 +42,9 @@ def lib():
             getattr(L, f).argtypes = [vp]
         L.orc_snapshot_json.restype = vp
         L.orc_snapshot_json.argtypes = [vp, u32]
+        L.orc_apply_matrix_json.argtypes = [vp, cp, ctypes.c_size_t, cp]
+        L.orc_snapshot_vector_json.restype = vp
+        L.orc_snapshot_vector_json.argtypes = [vp, u32]
         L.orc_snapshot_legacy_json.restype = vp
         L.orc_snapshot_legacy_json.argtypes = [vp, u32, cp]
         L.orc_checksum.restype = u64
@@ -130,6 +133,15 @@ class OracleDoc:
 
     def snapshot_json(self, chunk=10000):
         return _take(lib().orc_snapshot_json(self._h, chunk))
+
+    def apply_matrix_json(self, text, target):
+        """SharedMatrix messages (matrix.ts:548-560): this doc is its `target` ("rows" / "cols") vector."""
+        b = text.encode() if isinstance(text, str) else text
+        return lib().orc_apply_matrix_json(self._h, b, len(b), target.encode())
+
+    def snapshot_vector_json(self, chunk=10000):
+        """PermutationVector.snapshot (permutationvector.ts:260-273)."""
+        return _take(lib().orc_snapshot_vector_json(self._h, chunk))
 
     def snapshot_legacy_json(self, chunk=10000, catch_up_name="catchupOps"):
         """SnapshotLegacy ITree (snapshotlegacy.ts): header, body, catch-up messages blob."""

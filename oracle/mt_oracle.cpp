@@ -59,8 +59,11 @@ struct Node {
 };
 
 // BaseSegment / TextSegment / Marker (mergeTree.ts:429-798, textSegment.ts:16-111)
+constexpr int HandleUnallocated = INT32_MIN;  // Handle.unallocated (matrix/src/handletable.ts:11)
 struct Segment : Node {
     bool marker = false;
+    bool perm = false;                            // PermutationSegment (matrix/src/permutationvector.ts:37-127)
+    int start = HandleUnallocated;                // its first row/col handle
     int refType = 0;
     u16s text;
     int len = 0;                                  // cachedLength
@@ -186,10 +189,22 @@ static bool matchProperties(const Segment* a, const Segment* b) {
     return match_values(a->hasProps ? &av : nullptr, b->hasProps ? &bv : nullptr);
 }
 
+// TextSegment.append / PermutationSegment.append (textSegment.ts:74-85, permutationvector.ts:96-102)
+static void appendSeg(Segment* prev, const Segment* s) {
+    if (prev->perm) {
+        prev->len += s->len;
+        return;
+    }
+    prev->text += s->text;
+    prev->len = (int)prev->text.size();
+}
 // textSegment.ts:63-68
 static bool canAppend(const Segment* prev, const Segment* seg) {
     if (prev->marker) return false;  // Marker.canAppend (mergeTree.ts:793-795)
-    return !(prev->text.size() && prev->text.back() == u'\n') && !seg->marker &&
+    if (prev->perm)                  // PermutationSegment.canAppend (permutationvector.ts:88-94): handle runs
+        return seg->perm && (prev->start == HandleUnallocated ? seg->start == HandleUnallocated
+                                                               : seg->start == prev->start + prev->len);
+    return !(prev->text.size() && prev->text.back() == u'\n') && !seg->marker && !seg->perm &&
            (prev->len <= TextSegmentGranularity || seg->len <= TextSegmentGranularity);
 }
 
@@ -332,10 +347,17 @@ class MergeTree {
     Segment* splitAt(Segment* s, int pos) {
         if (!(pos > 0) || s->marker) return nullptr;
         Segment* r = newSegment();
-        r->text = s->text.substr(pos);
-        s->text = s->text.substr(0, pos);
-        s->len = (int)s->text.size();
-        r->len = (int)r->text.size();
+        if (s->perm) {  // PermutationSegment.createSplitSegmentAt (permutationvector.ts:104-115)
+            r->perm = true;
+            r->len = s->len - pos;
+            r->start = s->start == HandleUnallocated ? HandleUnallocated : s->start + pos;
+            s->len = pos;
+        } else {
+            r->text = s->text.substr(pos);
+            s->text = s->text.substr(0, pos);
+            s->len = (int)s->text.size();
+            r->len = (int)r->text.size();
+        }
         if (s->hasProps) { r->hasProps = true; r->props = s->props; }  // segmentPropertiesManager.ts:113-128
         r->parent = s->parent;
         r->removedClientId = s->removedClientId;
@@ -633,8 +655,7 @@ class MergeTree {
             } else if (s->seq <= cw.minSeq) {
                 bool ok = prev && canAppend(prev, s) && matchProperties(prev, s) && localNetLength(s) > 0;
                 if (ok) {
-                    prev->text += s->text;  // TextSegment.append (textSegment.ts:74-85)
-                    prev->len = (int)prev->text.size();
+                    appendSeg(prev, s);  // TextSegment.append (textSegment.ts:74-85)
                     s->parent = nullptr;
                 } else {
                     hold.push_back(s);
@@ -751,6 +772,10 @@ static void props_json(std::string& o, const JObj& p) {
     js_stringify(o, v);
 }
 static void segment_json(std::string& o, const Segment* s) {
+    if (s->perm) {  // PermutationSegment.toJSONObject (permutationvector.ts:75-77): [length, start]
+        o += "[" + js_number(s->len) + "," + js_number(s->start) + "]";
+        return;
+    }
     if (s->marker) {
         o += "{\"marker\":{\"refType\":" + js_number(s->refType) + "}";
         if (s->hasProps) { o += ",\"props\":"; props_json(o, s->props); }
@@ -959,8 +984,19 @@ class Doc {
         return truthy(before.get()) ? pos - o : pos + 1 + o;
     }
 
+    // a SharedMatrix row / col vector (PermutationVector, permutationvector.ts:129-146) instead of a
+    // SharedString: specs are PermutationSegment JSON
+    bool permutation = false;
     Segment* makeSegment(const JV& spec) {  // SharedStringFactory.segmentFromSpec (sequenceFactory.ts:31-37)
         Segment* s = mt.newSegment();
+        if (permutation) {  // PermutationSegment.fromJSONObject (permutationvector.ts:41-44): [length, start]
+            if (spec.t != JV::Arr || spec.a.empty() || !spec.a[0] || spec.a[0]->t != JV::Num)
+                throw EngineError(MTE_DOC_UNSUPPORTED, "not a PermutationSegment spec");
+            s->perm = true;
+            s->len = (int)spec.a[0]->n;
+            s->start = HandleUnallocated;  // onDelta resets every inserted segment's handles (:302-309)
+            return s;
+        }
         if (spec.t == JV::Str) {
             s->text = spec.s;
             s->len = (int)s->text.size();
@@ -1402,7 +1438,10 @@ class Doc {
                     case MTE_OP_INSERT:
                     case MTE_OP_INSERT_MARKER: {
                         Segment* s = mt.newSegment();
-                        if (op.type == MTE_OP_INSERT) {
+                        if (op.type == MTE_OP_INSERT && (op.flags & MTE_F_PERM)) {  // permutation run, handles unallocated
+                            s->perm = true;
+                            s->len = (int)op.b;
+                        } else if (op.type == MTE_OP_INSERT) {
                             s->text.assign((const char16_t*)payload + op.a, op.b);
                             s->len = (int)op.b;
                         } else {
@@ -1596,8 +1635,9 @@ class Doc {
             if (!first) o += ",";
             first = false;
             o += "{\"kind\":";
-            o += s->marker ? "\"M\"" : "\"T\"";
+            o += s->marker ? "\"M\"" : s->perm ? "\"P\"" : "\"T\"";
             if (s->marker) o += ",\"refType\":" + std::to_string(s->refType);
+            else if (s->perm) o += ",\"start\":" + std::to_string(s->start);
             else { o += ",\"text\":"; js_quote(o, s->text); }
             o += ",\"len\":" + std::to_string(s->len) + ",\"seq\":" + std::to_string(s->seq) + ",\"client\":";
             js_quote(o, utf8_to_u16(longId(s->clientId).data(), longId(s->clientId).size()));
@@ -1652,8 +1692,7 @@ class Doc {
                     prev = s;
                 } else if (canAppend(prev, s) && matchProperties(prev, s)) {
                     auto c = std::make_unique<Segment>(*prev);
-                    c->text += s->text;
-                    c->len = (int)c->text.size();
+                    appendSeg(c.get(), s);
                     prevClone = std::move(c);
                     prev = prevClone.get();
                 } else {
@@ -1761,8 +1800,7 @@ class Doc {
                 (!x->removed || x->removedSeq == UnassignedSequenceNumber || x->removedSeq > minSeq)) {
                 if (prev && canAppend(prev, x) && matchProperties(prev, x)) {
                     auto c = std::make_unique<Segment>(*prev);
-                    c->text += x->text;
-                    c->len = (int)c->text.size();
+                    appendSeg(c.get(), x);
                     prevClone = std::move(c);
                     prev = prevClone.get();
                 } else {
@@ -1891,6 +1929,45 @@ int orc_apply_json(Doc* d, const char* json, size_t len) {
         return -1;
     }
     return d->status;
+}
+
+// SharedMatrix.processCore (matrix.ts:548-560) for one of its PermutationVectors: the messages whose
+// contents target it go to its applyMsg; cell ops ("set", no target) allocate row / col handles
+// (getAllocatedHandle, permutationvector.ts:174-193), which this restatement does not model.
+int orc_apply_matrix_json(Doc* d, const char* json, size_t len, const char* target) {
+    d->permutation = true;
+    try {
+        orc::JVP v = orc::parse(json, len);
+        const orc::u16s tgt = orc::utf8_to_u16(target, strlen(target));
+        for (auto& m : v->a) {
+            if (d->status) break;
+            orc::JVP c = m->t == orc::JV::Obj ? m->o.get(u"contents") : nullptr;
+            orc::JVP t = c && c->t == orc::JV::Obj ? c->o.get(u"target") : nullptr;
+            if (!t) {
+                if (c && c->t == orc::JV::Obj) {
+                    d->status = MTE_DOC_UNSUPPORTED;
+                    d->error = "matrix cell ops (handle allocation) are out of scope";
+                    break;
+                }
+                continue;
+            }
+            if (t->t == orc::JV::Str && t->s == tgt) d->applyMsg(*m);
+        }
+    } catch (std::exception& e) {
+        d->status = MTE_DOC_UNSUPPORTED;
+        d->error = e.what();
+        return -1;
+    }
+    return d->status;
+}
+// PermutationVector.snapshot (permutationvector.ts:260-273): the merge-tree SnapshotV1 under
+// "segments" and the handle table ([1] until a handle is allocated) as a blob.
+char* orc_snapshot_vector_json(Doc* d, uint32_t chunk) {
+    std::string o = "{\"entries\":[{\"mode\":\"040000\",\"path\":\"segments\",\"type\":\"Tree\",\"value\":" +
+                    d->snapshotTree(chunk ? chunk : 10000) +
+                    "},{\"mode\":\"100644\",\"path\":\"handleTable\",\"type\":\"Blob\",\"value\":"
+                    "{\"contents\":\"[1]\",\"encoding\":\"utf-8\"}}],\"id\":null}";
+    return dupstr(o);
 }
 
 // Resume from a summary ITree JSON (SnapshotLoader); the doc must be fresh (observer set).

@@ -9,7 +9,9 @@ export interface DocSummary {
     snapshotBytes: number; status: number; docId: number;
 }
 /** summary: a SnapshotV1 ITree to resume from (SnapshotLoader); messages then are the catch-up suffix. */
-export interface DocLog { observer?: string; messages: ISequencedDocumentMessage[]; summary?: ITree | string; }
+export interface DocLog { observer?: string; messages?: ISequencedDocumentMessage[]; summary?: ITree | string;
+    /** SharedMatrix messages: this entry loads as two documents, the rows then the cols vector */
+    matrix?: ISequencedDocumentMessage[]; }
 
 export declare class BatchedMergeEngine {
     constructor(options?: { device?: number; chunkSize?: number; newMergeTreeSnapshotFormat?: boolean });
@@ -23,6 +25,8 @@ export declare class BatchedMergeEngine {
     /** Client.getLength: the observer's visible length, markers counting 1. */
     getLength(doc: number): number;
     snapshotV1(doc: number): ITree;
+    /** A { matrix } entry of load() adds two documents: its rows then its cols PermutationVector. */
+    snapshotMatrix(rowsDoc: number, colsDoc: number): ITree;
     /** After a replay with newMergeTreeSnapshotFormat: false. */
     snapshotLegacy(doc: number, catchUpBlobName?: string): ITree;
     summaries(): DocSummary[];

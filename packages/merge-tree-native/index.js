@@ -27,7 +27,9 @@ class BatchedMergeEngine {
         const b = addon.createBuilder();
         for (const d of docs) {
             const obs = d.observer === undefined ? "__observer__" : d.observer;
-            if (d.summary !== undefined) {
+            if (d.matrix !== undefined) {  // SharedMatrix messages: two documents, rows then cols
+                addon.builderAddMatrixLog(b, obs, JSON.stringify(d.matrix));
+            } else if (d.summary !== undefined) {
                 const s = typeof d.summary === "string" ? d.summary : JSON.stringify(d.summary);
                 addon.builderAddDocFromSummary(b, obs, s, d.messages ? JSON.stringify(d.messages) : null);
             } else {
@@ -35,7 +37,7 @@ class BatchedMergeEngine {
             }
         }
         addon.load(this._engine, b);
-        this._docs = docs.length;
+        this._docs = addon.builderDocCount(b);
     }
     generate(kind, nDocs, nOps, nClients = 8, seed = 0) {
         addon.generate(this._engine, kind, nDocs, nOps, nClients, seed);
@@ -59,6 +61,8 @@ class BatchedMergeEngine {
     getText(doc) { this._idle(); return addon.getText(this._engine, doc); }
     /** The ITree SnapshotV1.emit(serializer) returns: { entries: [...], id: null } */
     snapshotV1(doc) { return JSON.parse(addon.snapshotV1(this._engine, doc)); }
+    /** SharedMatrix summary of a { matrix } document pair (its rows and cols PermutationVectors) */
+    snapshotMatrix(rowsDoc, colsDoc) { return JSON.parse(addon.snapshotMatrix(this._engine, rowsDoc, colsDoc)); }
     /** SnapshotLegacy ITree (snapshotlegacy.ts:103-182): header, body, catch-up messages */
     snapshotLegacy(doc, catchUpBlobName = "catchupOps") {
         return JSON.parse(addon.snapshotLegacy(this._engine, doc, catchUpBlobName));
@@ -144,4 +148,5 @@ module.exports = {
     abiVersion: addon.abiVersion, buildInfo: addon.buildInfo,
     createBuilder: addon.createBuilder, builderAddDoc: addon.builderAddDoc, builderDocCount: addon.builderDocCount,
     builderAddDocFromSummary: addon.builderAddDocFromSummary, builderAddContainerLog: addon.builderAddContainerLog,
+    builderAddMatrixLog: addon.builderAddMatrixLog,
 };

@@ -187,6 +187,45 @@ static napi_value js_builder_add_container_log(napi_env env, napi_callback_info 
     return arr;
 }
 
+/* builderAddMatrixLog(builder, observerName, matrixMessagesJson): void — two documents, the rows then
+ * the cols PermutationVector of a SharedMatrix (matrix.ts:548-560) */
+static napi_value js_builder_add_matrix_log(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) {
+        napi_throw_type_error(env, NULL, "builderAddMatrixLog(builder, observer, json)");
+        return NULL;
+    }
+    mte_builder* b = (mte_builder*)get_external(env, argv[0]);
+    size_t len = 0;
+    char* obs = get_string(env, argv[1], NULL);
+    char* json = get_string(env, argv[2], &len);
+    int rc = (b && obs && json) ? mte_builder_add_matrix_log(b, obs, json, len) : MTE_E_ARG;
+    free(obs);
+    free(json);
+    if (rc) return throw_mte(env, "mte_builder_add_matrix_log", rc, b ? mte_builder_error(b) : NULL);
+    return NULL;
+}
+
+/* snapshotMatrix(engine, rowsDoc, colsDoc): string — SharedMatrix.snapshotCore (matrix.ts:405-430) */
+static napi_value js_snapshot_matrix(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    uint32_t r, c;
+    napi_get_value_uint32(env, argv[1], &r);
+    napi_get_value_uint32(env, argv[2], &c);
+    size_t n = 0;
+    int rc = mte_snapshot_matrix(e, r, c, NULL, 0, &n);
+    if (rc) return throw_mte(env, "mte_snapshot_matrix", rc, mte_last_error(e));
+    char* buf = (char*)malloc(n + 1);
+    rc = mte_snapshot_matrix(e, r, c, buf, n + 1, &n);
+    napi_value sv;
+    if (!rc) napi_create_string_utf8(env, buf, n, &sv);
+    free(buf);
+    if (rc) return throw_mte(env, "mte_snapshot_matrix", rc, mte_last_error(e));
+    return sv;
+}
+
 /* builderDocCount(builder): number */
 static napi_value js_builder_doc_count(napi_env env, napi_callback_info info) {
     napi_value argv[1];
@@ -433,6 +472,8 @@ static napi_value init(napi_env env, napi_value exports) {
         {"builderAddDoc", 0, js_builder_add_doc, 0, 0, 0, napi_default, 0},
         {"builderAddDocFromSummary", 0, js_builder_add_doc_from_summary, 0, 0, 0, napi_default, 0},
         {"builderAddContainerLog", 0, js_builder_add_container_log, 0, 0, 0, napi_default, 0},
+        {"builderAddMatrixLog", 0, js_builder_add_matrix_log, 0, 0, 0, napi_default, 0},
+        {"snapshotMatrix", 0, js_snapshot_matrix, 0, 0, 0, napi_default, 0},
         {"builderDocCount", 0, js_builder_doc_count, 0, 0, 0, napi_default, 0},
         {"load", 0, js_load, 0, 0, 0, napi_default, 0},
         {"generate", 0, js_generate, 0, 0, 0, napi_default, 0},

@@ -22,4 +22,10 @@ m.builderAddDocFromSummary(b, "catchup", summary, null);
 assert.strictEqual(m.builderDocCount(b), 4);
 assert.throws(() => m.builderAddDocFromSummary(b, "catchup", "{\"entries\":[]}", null), /mte_builder_add_doc_from_summary/);
 assert.deepStrictEqual(m.builderAddContainerLog(b, "readonly", "[]"), []);
+// a SharedMatrix log: rows and cols vectors (two documents); cell ops are out of scope
+const splice = (t, p, n) => ({ target: t, pos1: p, seg: [n, -2147483648], type: 0 });
+m.builderAddMatrixLog(b, "readonly", JSON.stringify([msg("a", 1, 0, splice("rows", 0, 3)), msg("a", 2, 1, splice("cols", 0, 2))]));
+assert.strictEqual(m.builderDocCount(b), 6);
+assert.throws(() => m.builderAddMatrixLog(b, "readonly", JSON.stringify([msg("a", 1, 0, { type: 2, row: 0, col: 0, value: 1 })])),
+    /mte_builder_add_matrix_log/);
 console.log("exports ok");

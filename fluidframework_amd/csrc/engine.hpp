@@ -160,8 +160,12 @@ struct St {
 // '\n' in any payload (the host checks, mte_host.cpp batch_is_lean): property maps, the HBM half of
 // the overlap masks and TextSegment.canAppend's newline test compile out, which leaves the replay
 // loop fewer live registers. Same results on such batches (tests/test_gpu_c4.py).
-template <bool LDSM, bool SOLO = false, bool FULL = true>
+// LVL 0: the lean instantiation (FULL = false); 1: FULL; 2: FULL + EXT, the extensions few batches use
+// -- legacy catch-up delta records (MTE_F_CATCHUP) and SharedMatrix permutation runs (MTE_F_PERM) --
+// kept out of the FULL kernels so they cost those no registers.
+template <bool LDSM, bool SOLO = false, int LVL = 1>
 struct Engine {
+    static constexpr bool FULL = LVL >= 1, EXT = LVL >= 2;
     static_assert(LDSM || !SOLO, "the solo plan is LDS-resident");
     const Params& p;
     u32 doc;
@@ -658,7 +662,7 @@ struct Engine {
     // The block of `pos` from one block scan already held per lane (lane = doc-order index, n_lb <= 64:
     // o, its visible length v and the inclusive prefix incl), then the slot inside it. The block's child
     // count is re-read (a split since the scan may have added a slot; block splits invalidate the scan).
-    MTE_DEV Found resolve_pre(uint4 o, u32 v, u32 incl, i32 pos, i32 R, u32 C) {
+    MTE_DEV Found resolve_pre(u32 v, u32 incl, i32 pos, i32 R, u32 C) {
         Found f;
         f.ok = false;
         f.k = 0;
@@ -673,8 +677,9 @@ struct Engine {
         const u32 j = (u32)__builtin_ctzll(hit);
         f.ok = true;
         f.k = j;
-        f.blk = wave_read(o.x, j);
-        f.cnt = U(ORD()[j].w);
+        const uint4 oj = ord_u(j);  // the block id, and its child count after any split since the scan
+        f.blk = oj.x;
+        f.cnt = oj.w;
         f.cum = (i32)wave_read(incl - v, j);
         resolve_slot(f, pos, R, C);
         return f;
@@ -1134,21 +1139,22 @@ struct Engine {
         const bool mv = L >= j && L < cnt;
         Seg t;
         if (mv) t = load(blk, L);
-        const uint4 ok = ORD()[k];  // read beside the slots (the stores below do not touch it)
+        const u32 oky = ORD()[k].y, okz = ORD()[k].z;  // read beside the slots (the stores do not touch them)
         sync();
         if (mv) store(blk, L + 1, t);
         if (L == 0) store(blk, j, rec);
         const u32 nc = cnt + 1;
         if (nc < 8) {
             if (L == 0) {
-                uint4 o = ok;
-                o.w = nc;
+                u32 y = oky, z = okz;
                 if (fresh) {
-                    o.y += obs_len(rec.len, rec.meta);
-                    i32 hi = seq_hi(rec.seq, rec.rseq, rec.meta);
-                    if (hi > (i32)o.z) o.z = (u32)hi;
+                    y += obs_len(rec.len, rec.meta);
+                    const i32 hi = seq_hi(rec.seq, rec.rseq, rec.meta);
+                    if (hi > (i32)z) z = (u32)hi;
                 }
-                ORD()[k] = o;
+                ORD()[k].y = y;
+                ORD()[k].z = z;
+                ORD()[k].w = nc;
             }
             sync();
             return blk;
@@ -1560,7 +1566,7 @@ struct Engine {
         const u64 mTXT = wave_ballot(act && !(me.meta & (F_MARKER | F_PERM)));
         // PermutationSegment runs (FULL batches only): canAppend holds between two unallocated runs
         // (permutationvector.ts:88-94; an observer never allocates handles), no granularity, no text
-        const u64 mPERM = FULL ? wave_ballot(act && (me.meta & F_PERM)) : 0ull;
+        const u64 mPERM = EXT ? wave_ballot(act && (me.meta & F_PERM)) : 0ull;
         const u64 mNL = (FULL && has_nl) ? wave_ballot(act && !(me.meta & F_MARKER) && ends_nl(me.toff, me.len)) : 0ull;
         u32 nkeep = 0;
         u32 kSrc = 0, kLen = 0, kOff = 0, kCap = 0;  // lane i < nkeep: kept slot i
@@ -1896,7 +1902,6 @@ struct Engine {
         // remove / annotate: ONE block scan serves both boundaries and the mark pass while the block
         // layout it saw holds (a boundary split that splits its block 8 -> 4+4 changes n_lb: the later
         // phases scan again); blocks keep their visible lengths across a boundary split
-        uint4 po = make_uint4(0, 0, 0, 0);
         u32 pv = 0, pincl = 0, pn = NONE;
 #ifdef MTE_NO_FUSE
         if (false) {
@@ -1905,7 +1910,7 @@ struct Engine {
 #endif
             fence_ovl();
             const bool valid = L < st.n_lb;
-            po = valid ? ORD()[L] : make_uint4(0, 0, 0, 0);
+            const uint4 po = valid ? ORD()[L] : make_uint4(0, 0, 0, 0);
             pv = blen_all(po, valid, R, C);
             pincl = wave_scan_incl(pv);
             pn = st.n_lb;
@@ -1917,7 +1922,7 @@ struct Engine {
             }
             const bool place = ins && ph == 1;
             const i32 pos = ph == 1 && !ins ? p2 : p1;
-            const Found f = known.ok ? known : (pn == st.n_lb ? resolve_pre(po, pv, pincl, pos, R, C) : resolve(pos, R, C));
+            const Found f = known.ok ? known : (pn == st.n_lb ? resolve_pre(pv, pincl, pos, R, C) : resolve(pos, R, C));
             if (!f.ok) {
                 if (ins) {
                     fail(MTE_DOC_INSERT_FAILED, seq);
@@ -1993,7 +1998,7 @@ struct Engine {
                     known.slot = (i32)s - 3;
                 }
             }
-            if (place && cu) {  // the inserted segment's delta range
+            if (EXT && place && cu) {  // the inserted segment's delta range
                 const u32 kb = b == f.blk ? f.k : f.k + 1;
                 const u32 cntb = U(ORD()[kb].w);
                 const u64 m = wave_ballot(L < cntb && L < 8 && AUX()[sidx(b, L)].w == rec.sid);
@@ -2035,7 +2040,7 @@ struct Engine {
                 const u32 idx = sidx(blk, s);
                 uint4 q = VIS()[idx];
                 const u32 z = AUX()[idx].z;
-                const uint4 obk = ORD()[kj];  // read beside the slots (marking does not touch it)
+                const u32 oby = remove ? ORD()[kj].y : 0u, obz = remove ? ORD()[kj].z : 0u;  // beside the slots
                 const bool in = s < cnt && s < 8;
                 const u32 sv = in ? vis_len(q, z, idx, R, C, C == 0 ? 1u : 0u) : 0u;
                 const u32 si = group8_scan(sv);
@@ -2067,12 +2072,10 @@ struct Engine {
                     if (C >= 32 && wave_ballot(mark && !fresh)) st.gdirty = 1;
                     const u32 gone = wave_read(group8_scan(fresh), 7);
                     if (L == 0) {
-                        uint4 ob = obk;
-                        ob.y -= gone;
-                        if (gone && seq > (i32)ob.z) ob.z = (u32)seq;
-                        ORD()[kj] = ob;
+                        ORD()[kj].y = oby - gone;
+                        if (gone && seq > (i32)obz) ORD()[kj].z = (u32)seq;
                     }
-                    if (cu) {  // removedSegments (mergeTree.ts:2639): the segments this op removed
+                    if (EXT && cu) {  // removedSegments (mergeTree.ts:2639): the segments this op removed
                         for (u64 fm = wave_ballot(fresh != 0); fm && !st.status; fm &= fm - 1) {
                             const u32 sl = (u32)__builtin_ctzll(fm);
                             cu_record(1, obs_prefix(kj, blk, sl), wave_read(fresh, sl), 0, 0);
@@ -2098,7 +2101,7 @@ struct Engine {
                         if (same) AUX()[idx].x = nid;
                         pending &= ~wave_ballot(same);
                     }
-                    if (cu) {  // deltaSegments with their propertyDeltas (maps before / after)
+                    if (EXT && cu) {  // deltaSegments with their propertyDeltas (maps before / after)
                         for (u64 am = mm; am && !st.status; am &= am - 1) {
                             const u32 sl = (u32)__builtin_ctzll(am);
                             sync();
@@ -2354,7 +2357,7 @@ struct Engine {
             rec.len = mk ? 1u : op.b;
             rec.seq = seq;
             rec.rseq = 0;
-            rec.meta = (C & 0xff) | (mk ? F_MARKER : 0u) | ((FULL && !ld && (op.flags & MTE_F_PERM)) ? F_PERM : 0u);
+            rec.meta = (C & 0xff) | (mk ? F_MARKER : 0u) | ((EXT && !ld && (op.flags & MTE_F_PERM)) ? F_PERM : 0u);
             u32 type = op.type;
             i32 p1 = op.pos1;
             if (ld && !load_append_pos(op, rec, p1)) return;  // skipped (a repeated object) or failed
@@ -2364,7 +2367,7 @@ struct Engine {
             rec.toff = (mk && !ld) ? op.b : ((rec.meta & F_PERM) ? 0u : (u32)op.a);
             rec.tcap = 0;
             rec.sid = 0;
-            const bool cu = (op.flags & MTE_F_CATCHUP) != 0 && !ld;
+            const bool cu = EXT && (op.flags & MTE_F_CATCHUP) != 0 && !ld;  // EXT batches only
             if (cu) {
                 sync();
                 if (L == 0) STATS()[ST_CUOP] = (u32)(op_index - p.docs[doc].op_begin);

@@ -218,7 +218,13 @@ struct mte_engine {
     uint32_t chunk = 10000;
     hipStream_t stream = nullptr, stream2 = nullptr;  // stream2: the HBM-resident waves (k_hbmq)
     hipStream_t stream3 = nullptr;                    // stream3: the solo workgroups (k_solo)
+    // option solo_isolate: CU-masked streams, the solo workgroups on n_solo CUs of their own and every
+    // other kernel of the pass on the rest (no HBM-resident or emission wave beside a critical path)
+    bool solo_isolate = false;
+    uint32_t iso_n = 0;
+    hipStream_t iso_rest = nullptr, iso_rest2 = nullptr, iso_solo = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
+    hipEvent_t ev_s0 = nullptr, ev_s1 = nullptr;  // timing of the solo workgroups (critical path)
     std::string err;
     HostBatch hb;
     bool generated = false;    // ops/payload live on the device; host copy filled on demand
@@ -262,6 +268,7 @@ struct mte_engine {
     uint32_t slot_blk_limit = 0;         // test knob: leaf blocks per slot (0 = from slot_ops_cap)
     // critical-path documents replayed by k_solo (a whole CU's LDS for one wave each)
     bool lean_ok = false;                // batch_is_lean: the replay may run the FULL = false kernels
+    bool ext_needed = false;             // catch-up records or permutation runs: the EXT kernels (level 2)
     bool lean_opt = true;                // option "lean" (0 = always the FULL kernels)
     bool last_lean = false;
     uint32_t solo_max = 16;              // at most this many (0 = off)
@@ -607,6 +614,8 @@ int mte_create(const mte_config* cfg, mte_engine** out) {
     HIP_TRY(e.get(), hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
     HIP_TRY(e.get(), hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking));
     HIP_TRY(e.get(), hipEventCreateWithFlags(&e->ev3, hipEventDisableTiming));
+    HIP_TRY(e.get(), hipEventCreate(&e->ev_s0));
+    HIP_TRY(e.get(), hipEventCreate(&e->ev_s1));
     HIP_TRY(e.get(), hipEventCreateWithFlags(&e->ev2, hipEventDisableTiming));
     HIP_TRY(e.get(), hipEventCreate(&e->ev0));
     HIP_TRY(e.get(), hipEventCreate(&e->ev1));
@@ -622,7 +631,11 @@ void mte_destroy(mte_engine* e) {
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->ev2) (void)hipEventDestroy(e->ev2);
     if (e->ev3) (void)hipEventDestroy(e->ev3);
+    if (e->ev_s0) (void)hipEventDestroy(e->ev_s0);
+    if (e->ev_s1) (void)hipEventDestroy(e->ev_s1);
     if (e->stream3) (void)hipStreamDestroy(e->stream3);
+    for (hipStream_t s : {e->iso_rest, e->iso_rest2, e->iso_solo})
+        if (s) (void)hipStreamDestroy(s);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -634,7 +647,7 @@ static void count_doc_ops(const HostBatch& hb, uint32_t d, uint64_t& pi, uint64_
     pi = an = 0;
     for (uint64_t i = hb.doc_op_offsets[d]; i < hb.doc_op_offsets[d + 1]; i++) {
         const mte_op& o = hb.ops[i];
-        if (rel && (o.type == MTE_OP_RELPOS || (o.flags & MTE_F_PERM))) *rel = true;  // FULL kernels only
+        if (rel && o.type == MTE_OP_RELPOS) *rel = true;  // FULL kernels only
         if ((o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER || o.type == MTE_OP_LOAD_SEG ||
              o.type == MTE_OP_LOAD_APPEND) && o.props)
             pi++;
@@ -653,7 +666,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     const uint32_t nd = b->n_docs;
     std::vector<uint64_t> n_ops(nd), pay(nd), pi(nd), an(nd);
     std::vector<uint8_t> collab(nd), has_nl(nd, 0);
-    bool lean = true;
+    bool lean = true, ext = false;
     for (uint32_t d = 0; d < nd; d++) {
         for (uint64_t q = b->doc_payload_offsets[d]; q < b->doc_payload_offsets[d + 1]; q++)
             if (b->payload[q] == (uint16_t)'\n') {
@@ -664,6 +677,8 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         pay[d] = b->doc_payload_offsets[d + 1] - b->doc_payload_offsets[d];
         bool rel = false;
         count_doc_ops(e->hb, d, pi[d], an[d], &rel);
+        for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1] && !ext; i++)
+            ext = (b->ops[i].flags & (MTE_F_PERM | MTE_F_CATCHUP)) != 0;
         collab[d] = e->hb.client(d, 0).empty() ? 0 : 1;  // empty observer name => local, non-collab
         lean = lean && !has_nl[d] && !pi[d] && !an[d] && !rel &&
                e->hb.doc_client_offsets[d + 1] - e->hb.doc_client_offsets[d] <= 32;
@@ -707,7 +722,8 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     e->last_h2d_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     e->P.ops = e->d_ops.p;
     e->P.payload = e->d_payload.p;
-    e->lean_ok = lean;
+    e->lean_ok = lean && !ext;
+    e->ext_needed = ext;
     if ((rc = alloc_out_text(e))) return rc;
     return MTE_OK;
 }
@@ -848,8 +864,9 @@ static int run_kernel(mte_engine* e, bool gen) {
     if ((rc = alloc_slots(e))) return rc;  // options may have changed the wave plan
     uint32_t groups, hbm_waves, lds_active;
     const uint32_t n_solo = e->P.n_solo;
-    const bool full = gen || !(e->lean_ok && e->lean_opt);  // the generator always runs FULL
-    e->last_lean = !full;
+    // engine level (engine.hpp): the generator always runs FULL
+    const int full = gen ? 1 : e->ext_needed ? 2 : (e->lean_ok && e->lean_opt) ? 0 : 1;
+    e->last_lean = full == 0;
     wave_plan(e, nd, groups, hbm_waves, &lds_active, n_solo);
     e->P.slot_hbm0 = groups * LDS_WAVES;
     e->P.lds_active = lds_active;
@@ -858,29 +875,53 @@ static int run_kernel(mte_engine* e, bool gen) {
         while (e->P.n_prio < nd && e->cfg[e->order[e->P.n_prio]].prio) e->P.n_prio++;
     e->P.n_prio = std::max(e->P.n_prio, n_solo);  // k_lds / k_hbmq start after the solo documents
     e->P.n_hslots = hbm_waves;
-    HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 8 * sizeof(uint32_t), e->stream));
-    HIP_TRY(e, hipMemsetAsync(e->d_slot_bits.p, 0, e->d_slot_bits.n * sizeof(uint32_t), e->stream));
-    HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, e->d_prof.n * sizeof(uint64_t), e->stream));  // profiling build
-    HIP_TRY(e, hipEventRecord(e->ev0, e->stream));
+    // the streams of this pass (CU-masked when isolating the solo workgroups)
+    hipStream_t s_main = e->stream, s_hbmq = e->stream2, s_solo = e->stream3;
+    if (e->solo_isolate && n_solo && n_solo < e->n_groups) {
+        if (e->iso_n != n_solo) {
+            for (hipStream_t* sp : {&e->iso_rest, &e->iso_rest2, &e->iso_solo})
+                if (*sp) {
+                    (void)hipStreamDestroy(*sp);
+                    *sp = nullptr;
+                }
+            const uint32_t words = (e->n_groups + 31) / 32;
+            std::vector<uint32_t> solo(words, 0), rest(words, 0);
+            for (uint32_t c = 0; c < e->n_groups; c++) (c < n_solo ? solo : rest)[c / 32] |= 1u << (c % 32);
+            HIP_TRY(e, hipExtStreamCreateWithCUMask(&e->iso_rest, words, rest.data()));
+            HIP_TRY(e, hipExtStreamCreateWithCUMask(&e->iso_rest2, words, rest.data()));
+            HIP_TRY(e, hipExtStreamCreateWithCUMask(&e->iso_solo, words, solo.data()));
+            e->iso_n = n_solo;
+        }
+        HIP_TRY(e, hipStreamSynchronize(e->stream));  // earlier uploads on the unmasked stream
+        s_main = e->iso_rest;
+        s_hbmq = e->iso_rest2;
+        s_solo = e->iso_solo;
+    }
+    HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 8 * sizeof(uint32_t), s_main));
+    HIP_TRY(e, hipMemsetAsync(e->d_slot_bits.p, 0, e->d_slot_bits.n * sizeof(uint32_t), s_main));
+    HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, e->d_prof.n * sizeof(uint64_t), s_main));  // profiling build
+    HIP_TRY(e, hipEventRecord(e->ev0, s_main));
     std::vector<uint32_t> spill;
     float lds_ms = 0, hbm_ms = 0;
     // pass 1: the solo workgroups first (third stream: each takes a CU), then the LDS workgroups
     // (one per remaining CU, all of its LDS), then the HBM-resident waves on the second stream so
     // they fill every CU's remaining wave slots; k_lds and k_hbmq drain one document queue
     if (n_solo) {
-        HIP_TRY(e, hipStreamWaitEvent(e->stream3, e->ev0, 0));
-        HIP_TRY(e, launch_solo(e->P, gen, full, n_solo, e->stream3));
-        HIP_TRY(e, hipEventRecord(e->ev3, e->stream3));
+        HIP_TRY(e, hipStreamWaitEvent(s_solo, e->ev0, 0));
+        HIP_TRY(e, hipEventRecord(e->ev_s0, s_solo));
+        HIP_TRY(e, launch_solo(e->P, gen, full, n_solo, s_solo));
+        HIP_TRY(e, hipEventRecord(e->ev_s1, s_solo));
+        HIP_TRY(e, hipEventRecord(e->ev3, s_solo));
     }
-    if (groups) HIP_TRY(e, launch_lds(e->P, gen, full, groups, e->stream));
+    if (groups) HIP_TRY(e, launch_lds(e->P, gen, full, groups, s_main));
     // k_hbmq: one workgroup (wave) per document; those that find the queue drained exit at once
     if (hbm_waves && !groups) {
-        HIP_TRY(e, launch_hbmq(e->P, gen, full, nd, e->stream));
+        HIP_TRY(e, launch_hbmq(e->P, gen, full, nd, s_main));
     } else if (hbm_waves) {
-        HIP_TRY(e, hipStreamWaitEvent(e->stream2, e->ev0, 0));
-        HIP_TRY(e, launch_hbmq(e->P, gen, full, nd, e->stream2));
-        HIP_TRY(e, hipEventRecord(e->ev2, e->stream2));
-        HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev2, 0));
+        HIP_TRY(e, hipStreamWaitEvent(s_hbmq, e->ev0, 0));
+        HIP_TRY(e, launch_hbmq(e->P, gen, full, nd, s_hbmq));
+        HIP_TRY(e, hipEventRecord(e->ev2, s_hbmq));
+        HIP_TRY(e, hipStreamWaitEvent(s_main, e->ev2, 0));
     }
     const bool emit = !gen && e->emit_opt;
     e->emitted_legacy = e->legacy;
@@ -893,11 +934,11 @@ static int run_kernel(mte_engine* e, bool gen) {
         // round 0: every document but the solo ones, while k_solo still replays the critical path
         // (the documents the host re-runs are still DOC_SPILL here: COUNT skips them)
         std::vector<uint32_t> bulk(e->order.begin() + std::min<uint32_t>(n_solo, nd), e->order.end());
-        if ((erc = emit_list(e, 0, bulk, e->stream))) return erc;
+        if ((erc = emit_list(e, 0, bulk, s_main))) return erc;
     }
-    if (n_solo) HIP_TRY(e, hipStreamWaitEvent(e->stream, e->ev3, 0));
-    HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
-    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    if (n_solo) HIP_TRY(e, hipStreamWaitEvent(s_main, e->ev3, 0));
+    HIP_TRY(e, hipEventRecord(e->ev1, s_main));
+    HIP_TRY(e, hipStreamSynchronize(s_main));
     HIP_TRY(e, hipEventElapsedTime(&lds_ms, e->ev0, e->ev1));
     e->res.resize(nd);
     HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nd * sizeof(DocRes), hipMemcpyDeviceToHost));
@@ -911,6 +952,11 @@ static int run_kernel(mte_engine* e, bool gen) {
     e->last_hbm_waves = hbm_waves;
     e->last_lds_groups = groups;
     e->last_solo = n_solo;
+    e->last_solo_ms = 0;
+    if (n_solo) {
+        float sm = 0;
+        if (hipEventElapsedTime(&sm, e->ev_s0, e->ev_s1) == hipSuccess) e->last_solo_ms = sm;
+    }
     e->last_spilled = (uint32_t)spill.size();
     if (!spill.empty()) {
         // second pass: the spilled documents, HBM-resident, one wave each, longest first
@@ -1049,6 +1095,7 @@ int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_o
     e->emit_tables = false;  // names are known after the generator ran
     // kinds 2 and 5 draw no properties and no '\n'; short ids stay below 1 + n_clients
     e->lean_ok = kind != 3 && n_clients < 32;
+    e->ext_needed = false;
     rc = run_kernel(e, true);
     if (rc) return rc;
     // client names: observer + writers in first-appearance (short id) order
@@ -1959,6 +2006,7 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "lean") e->lean_opt = value != 0;
     else if (k == "emit") e->emit_opt = value != 0;  // SnapshotV1 emission on the device after replay
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
+    else if (k == "solo_isolate") e->solo_isolate = value != 0;
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
 }
@@ -1975,6 +2023,7 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "slot_bytes") *value = (int64_t)e->P.slot_bytes;
     else if (k == "slots") *value = e->n_slots;
     else if (k == "solo") *value = e->last_solo;
+    else if (k == "solo_us") *value = (int64_t)(e->last_solo_ms * 1000.0);  // the solo workgroups' pass (critical path)
     else if (k == "lean") *value = e->last_lean;
     else if (k == "emit_us") *value = (int64_t)(e->last_emit_ms * 1000.0);  // emission after the replay pass
     else if (k == "out_text") {  // UTF-16 units Engine::finish gathered (counters[6..7])

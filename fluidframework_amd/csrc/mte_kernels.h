@@ -1,13 +1,14 @@
-// Kernel launchers (mte_kernels.hip) used by the host side (mte_host.cpp).
+// Kernel launchers (mte_kernels.hip) used by the host side (mte_host.cpp). full: the engine level
+// (0 lean, 1 FULL, 2 FULL + EXT; engine.hpp).
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include "engine_types.hpp"
 
 namespace mte {
-hipError_t launch_lds(const Params& p, bool gen, bool full, u32 n_groups, hipStream_t s);
-hipError_t launch_solo(const Params& p, bool gen, bool full, u32 n_solo, hipStream_t s);
-hipError_t launch_hbmq(const Params& p, bool gen, bool full, u32 n_waves, hipStream_t s);
-hipError_t launch_hbm(const Params& p, bool gen, bool full, u32 n_docs, hipStream_t s);
+hipError_t launch_lds(const Params& p, bool gen, int full, u32 n_groups, hipStream_t s);
+hipError_t launch_solo(const Params& p, bool gen, int full, u32 n_solo, hipStream_t s);
+hipError_t launch_hbmq(const Params& p, bool gen, int full, u32 n_waves, hipStream_t s);
+hipError_t launch_hbm(const Params& p, bool gen, int full, u32 n_docs, hipStream_t s);
 hipError_t launch_wave_selftest(const u32* in, u32* out, u32 n_waves, hipStream_t s);
 }  // namespace mte

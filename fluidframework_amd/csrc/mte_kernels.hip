@@ -24,7 +24,7 @@ namespace mte {
 #define MTE_HBMQ_WPE 4
 #endif
 
-template <bool GEN, bool FULL>
+template <bool GEN, int LVL>
 __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(MTE_LDS_WPE))) void k_lds(Params p) {
     LdsPlan* lp = &g_plan;
     const u32 t = threadIdx.x, L = t & 63;
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
         const u32 d = p.doc_list[i];
         const bool prio = p.docs[d].prio != 0;
         if (prio) __builtin_amdgcn_s_setprio(3);  // the critical path issues first on its SIMD
-        Engine<true, false, FULL> e(p, d);
+        Engine<true, false, LVL> e(p, d);
         e.bind_lds(w);
         GenState g;
         bool done;
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
             e.mark_spilled();  // slots too small to hold the LDS block ids (test knob): host re-run
         } else if (!done && e.st.status == 0) {
             // the LDS plan ran out of room between two ops: continue HBM-resident, same wave
-            Engine<false, false, FULL> h(p, d);
+            Engine<false, false, LVL> h(p, d);
             h.continued = true;
             h.bind_slot(blockIdx.x * LDS_WAVES + w);
             h.adopt(e);
@@ -97,13 +97,13 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
 // workgroup each, owning all of a CU's LDS (SoloPlan), at the highest wave priority. The replay
 // latency of the longest document bounds a Zipf batch, so it gets the plan with the
 // most room and no LDS-pool sharing; it continues HBM-resident only if it outgrows even that.
-template <bool GEN, bool FULL>
+template <bool GEN, int LVL>
 __global__ __launch_bounds__(64) void k_solo(Params p) {
     const u32 i = blockIdx.x;
     if (i >= p.n_solo) return;
     const u32 d = p.doc_list[i];
     __builtin_amdgcn_s_setprio(3);
-    Engine<true, true, FULL> e(p, d);
+    Engine<true, true, LVL> e(p, d);
     e.bind_lds(0);
     GenState g;
     bool done;
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(64) void k_solo(Params p) {
     if (e.st.status == DOC_SPILL) {
         e.mark_spilled();
     } else if (!done && e.st.status == 0) {
-        Engine<false, false, FULL> h(p, d);
+        Engine<false, false, LVL> h(p, d);
         h.continued = true;
         h.bind_solo_slot(i);
         h.adopt(e);
@@ -179,7 +179,7 @@ MTE_DEV u32 acquire_hslot(const Params& p) {
 // the LDS waves leave idle while they wait on LDS/ALU latency chains. (One document per workgroup
 // rather than a persistent loop: with the engine inlined into a loop, hipcc 7.2 built a divergent
 // loop latch that came back with EXEC narrowed to one lane.)
-template <bool GEN, bool FULL>
+template <bool GEN, int LVL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_HBMQ_WPE))) void k_hbmq(Params p) {
     const u32 L = lane_id();
     u32 i = 0;
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_HBMQ_WPE
     if (i >= p.n_list) return;
     const u32 d = p.doc_list[i];
     const u32 slot = acquire_hslot(p);
-    Engine<false, false, FULL> e(p, d);
+    Engine<false, false, LVL> e(p, d);
     e.bind_slot(p.slot_hbm0 + slot);
     e.reset_stats();
     e.init();
@@ -207,10 +207,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_HBMQ_WPE
     if (L == 0) atomicAnd(&p.slot_bits[slot >> 5], ~(1u << (slot & 31)));
 }
 
-template <bool GEN, bool FULL>
+template <bool GEN, int LVL>
 __global__ __launch_bounds__(64) void k_hbm(Params p) {
     const u32 d = p.doc_list[blockIdx.x];
-    Engine<false, false, FULL> e(p, d);
+    Engine<false, false, LVL> e(p, d);
     e.bind_hbm();
     e.init();
     if (GEN) {
@@ -237,45 +237,48 @@ __global__ __launch_bounds__(64) void k_wave_selftest(const u32* in, u32* out) {
 }
 
 // Kernel instantiations: the generator always runs the FULL engine (its C3 kind uses properties);
-// a replay runs the lean one (FULL = false) when the host found the batch free of the optional
-// features (mte_host.cpp batch_is_lean).
-#define MTE_PICK(K, gen, full) ((gen) ? (const void*)K<true, true> : (full) ? (const void*)K<false, true> : (const void*)K<false, false>)
+// a replay runs the lean one (level 0) when the host found the batch free of the optional features,
+// the EXT one (level 2) when it carries catch-up records or permutation runs, else FULL (level 1)
+// (mte_host.cpp mte_load).
+#define MTE_PICK(K, gen, lvl)                                                                           \
+    ((gen) ? (const void*)K<true, 1> : (lvl) >= 2 ? (const void*)K<false, 2> : (lvl) == 1 ? (const void*)K<false, 1> \
+                                                                               : (const void*)K<false, 0>)
 
 template <class Plan>
 static hipError_t lds_attr(const void* k) {
     return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Plan));
 }
 
-hipError_t launch_lds(const Params& p, bool gen, bool full, u32 n_groups, hipStream_t s) {
+hipError_t launch_lds(const Params& p, bool gen, int full, u32 n_groups, hipStream_t s) {
     // the LdsPlan is dynamic LDS: a static 160 KiB declaration makes the compiler size registers
     // for the 2 waves/SIMD that LDS allows, while k_lds is kept to <= 128 VGPRs so k_hbmq waves fit
     // beside it (2 + 2 per SIMD)
     static const hipError_t attr = [] {
-        hipError_t r = lds_attr<LdsPlan>((const void*)k_lds<true, true>);
-        if (r == hipSuccess) r = lds_attr<LdsPlan>((const void*)k_lds<false, true>);
-        if (r == hipSuccess) r = lds_attr<LdsPlan>((const void*)k_lds<false, false>);
+        hipError_t r = lds_attr<LdsPlan>((const void*)k_lds<true, 1>);
+        for (const void* k : {(const void*)k_lds<false, 0>, (const void*)k_lds<false, 1>, (const void*)k_lds<false, 2>})
+            if (r == hipSuccess) r = lds_attr<LdsPlan>(k);
         return r;
     }();
     if (attr != hipSuccess) return attr;
     void* args[] = {(void*)&p};
     return hipLaunchKernel(MTE_PICK(k_lds, gen, full), dim3(n_groups), dim3(64 * LDS_WAVES), args, sizeof(LdsPlan), s);
 }
-hipError_t launch_solo(const Params& p, bool gen, bool full, u32 n_solo, hipStream_t s) {
+hipError_t launch_solo(const Params& p, bool gen, int full, u32 n_solo, hipStream_t s) {
     static const hipError_t attr = [] {
-        hipError_t r = lds_attr<SoloPlan>((const void*)k_solo<true, true>);
-        if (r == hipSuccess) r = lds_attr<SoloPlan>((const void*)k_solo<false, true>);
-        if (r == hipSuccess) r = lds_attr<SoloPlan>((const void*)k_solo<false, false>);
+        hipError_t r = lds_attr<SoloPlan>((const void*)k_solo<true, 1>);
+        for (const void* k : {(const void*)k_solo<false, 0>, (const void*)k_solo<false, 1>, (const void*)k_solo<false, 2>})
+            if (r == hipSuccess) r = lds_attr<SoloPlan>(k);
         return r;
     }();
     if (attr != hipSuccess) return attr;
     void* args[] = {(void*)&p};
     return hipLaunchKernel(MTE_PICK(k_solo, gen, full), dim3(n_solo), dim3(64), args, sizeof(SoloPlan), s);
 }
-hipError_t launch_hbm(const Params& p, bool gen, bool full, u32 n_docs, hipStream_t s) {
+hipError_t launch_hbm(const Params& p, bool gen, int full, u32 n_docs, hipStream_t s) {
     void* args[] = {(void*)&p};
     return hipLaunchKernel(MTE_PICK(k_hbm, gen, full), dim3(n_docs), dim3(64), args, 0, s);
 }
-hipError_t launch_hbmq(const Params& p, bool gen, bool full, u32 n_waves, hipStream_t s) {  // n_waves >= docs left
+hipError_t launch_hbmq(const Params& p, bool gen, int full, u32 n_waves, hipStream_t s) {  // n_waves >= docs left
     void* args[] = {(void*)&p};
     return hipLaunchKernel(MTE_PICK(k_hbmq, gen, full), dim3(n_waves), dim3(64), args, 0, s);
 }

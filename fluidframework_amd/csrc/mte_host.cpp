@@ -218,11 +218,6 @@ struct mte_engine {
     uint32_t chunk = 10000;
     hipStream_t stream = nullptr, stream2 = nullptr;  // stream2: the HBM-resident waves (k_hbmq)
     hipStream_t stream3 = nullptr;                    // stream3: the solo workgroups (k_solo)
-    // option solo_isolate: CU-masked streams, the solo workgroups on n_solo CUs of their own and every
-    // other kernel of the pass on the rest (no HBM-resident or emission wave beside a critical path)
-    bool solo_isolate = false;
-    uint32_t iso_n = 0;
-    hipStream_t iso_rest = nullptr, iso_rest2 = nullptr, iso_solo = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
     hipEvent_t ev_s0 = nullptr, ev_s1 = nullptr;  // timing of the solo workgroups (critical path)
     std::string err;
@@ -634,8 +629,6 @@ void mte_destroy(mte_engine* e) {
     if (e->ev_s0) (void)hipEventDestroy(e->ev_s0);
     if (e->ev_s1) (void)hipEventDestroy(e->ev_s1);
     if (e->stream3) (void)hipStreamDestroy(e->stream3);
-    for (hipStream_t s : {e->iso_rest, e->iso_rest2, e->iso_solo})
-        if (s) (void)hipStreamDestroy(s);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -875,28 +868,10 @@ static int run_kernel(mte_engine* e, bool gen) {
         while (e->P.n_prio < nd && e->cfg[e->order[e->P.n_prio]].prio) e->P.n_prio++;
     e->P.n_prio = std::max(e->P.n_prio, n_solo);  // k_lds / k_hbmq start after the solo documents
     e->P.n_hslots = hbm_waves;
-    // the streams of this pass (CU-masked when isolating the solo workgroups)
+    // the streams of this pass (an A/B with CU-masked streams, hipExtStreamCreateWithCUMask, that kept
+    // the solo workgroups' CUs to themselves measured the C4 pass 8 % SLOWER -- 9.07 s vs 8.38 s, the
+    // solo workgroups themselves included -- and hung at teardown: not used)
     hipStream_t s_main = e->stream, s_hbmq = e->stream2, s_solo = e->stream3;
-    if (e->solo_isolate && n_solo && n_solo < e->n_groups) {
-        if (e->iso_n != n_solo) {
-            for (hipStream_t* sp : {&e->iso_rest, &e->iso_rest2, &e->iso_solo})
-                if (*sp) {
-                    (void)hipStreamDestroy(*sp);
-                    *sp = nullptr;
-                }
-            const uint32_t words = (e->n_groups + 31) / 32;
-            std::vector<uint32_t> solo(words, 0), rest(words, 0);
-            for (uint32_t c = 0; c < e->n_groups; c++) (c < n_solo ? solo : rest)[c / 32] |= 1u << (c % 32);
-            HIP_TRY(e, hipExtStreamCreateWithCUMask(&e->iso_rest, words, rest.data()));
-            HIP_TRY(e, hipExtStreamCreateWithCUMask(&e->iso_rest2, words, rest.data()));
-            HIP_TRY(e, hipExtStreamCreateWithCUMask(&e->iso_solo, words, solo.data()));
-            e->iso_n = n_solo;
-        }
-        HIP_TRY(e, hipStreamSynchronize(e->stream));  // earlier uploads on the unmasked stream
-        s_main = e->iso_rest;
-        s_hbmq = e->iso_rest2;
-        s_solo = e->iso_solo;
-    }
     HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 8 * sizeof(uint32_t), s_main));
     HIP_TRY(e, hipMemsetAsync(e->d_slot_bits.p, 0, e->d_slot_bits.n * sizeof(uint32_t), s_main));
     HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, e->d_prof.n * sizeof(uint64_t), s_main));  // profiling build
@@ -2006,7 +1981,6 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "lean") e->lean_opt = value != 0;
     else if (k == "emit") e->emit_opt = value != 0;  // SnapshotV1 emission on the device after replay
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
-    else if (k == "solo_isolate") e->solo_isolate = value != 0;
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
 }

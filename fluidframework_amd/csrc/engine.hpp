@@ -36,7 +36,7 @@ enum ProfSlot : u32 {
     PN_RESOLVE, PN_DIRTY, PN_SCOUR, PN_SCOUR_CHANGED, PN_PACK, PN_POP, PN_PUSH, PN_SPLIT_BLK,
     // finer scopes
     PF_OP_INS, PF_OP_REM, PF_EDIT, PF_SPLIT, PF_ZAM_EDIT, PF_ZAM_MSN, PF_RES_BLOCKS, PF_RES_SLOT, PF_BLEN_DIRTY,
-    PF_SCOUR_CHAIN, PF_SCOUR_WRITE, PF_LOOP, PN_INS, PN_REM
+    PF_SCOUR_CHAIN, PF_SCOUR_WRITE, PF_LOOP, PN_INS, PN_REM, PF_APRE, PF_APOST
 };
 #ifdef MTE_PROFILE
 // MTE_PROF_ONLY=<slot>: time that one phase only (every s_memtime scope and counter atomic perturbs
@@ -2330,6 +2330,9 @@ struct Engine {
         } _op_scope{prof + (op.type == MTE_OP_REMOVE ? PF_OP_REM : PF_OP_INS), t_op0, L};
         MTE_COUNT(op.type == MTE_OP_REMOVE ? PN_REM : PN_INS, 1);
 #endif
+#ifdef MTE_PROFILE
+        u64 t_pre = MTE_PON(PF_APRE) ? __builtin_amdgcn_s_memtime() : 0;
+#endif
         // a loadBody append of a summary load (include/mte.h MTE_OP_LOAD_APPEND) shares the insert
         // path: insertSegments(pos, [seg], refSeq 0, client, seq) with the segment's own merge info
         const bool ld = op.type == MTE_OP_LOAD_APPEND;
@@ -2373,10 +2376,16 @@ struct Engine {
                 if (L == 0) STATS()[ST_CUOP] = (u32)(op_index - p.docs[doc].op_begin);
                 sync();
             }
+#ifdef MTE_PROFILE
+            if (MTE_PON(PF_APRE) && L == 0) atomicAdd(prof + PF_APRE, __builtin_amdgcn_s_memtime() - t_pre);
+#endif
             edited = edit(type, p1, op.a, R, C, seq, rec, op.props, (op.flags & MTE_F_REWRITE) != 0, cu);
             if (!ld) stat_add(ST_OPS, 1);
             if (st.status) return;
         }
+#ifdef MTE_PROFILE
+        MTE_PROF(PF_APOST);
+#endif
         for (u32 z = 0; z < 2; z++) {
             bool run = edited;
             if (z == 1) {

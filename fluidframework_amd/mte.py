@@ -20,7 +20,7 @@ PROF_NAMES = ["apply", "resolve", "insert_slot", "range", "zamboni", "scour", "h
               "fetch", "lru", "text", "alloc", "ops", "total",
               "n_resolve", "n_dirty", "n_scour", "n_scour_changed", "n_pack", "n_pop", "n_push", "n_split_blk",
               "op_ins", "op_rem", "edit", "split", "zam_edit", "zam_msn", "res_blocks", "res_slot", "blen_dirty",
-              "scour_chain", "scour_write", "loop", "n_ins", "n_rem"]
+              "scour_chain", "scour_write", "loop", "n_ins", "n_rem", "apply_pre", "apply_post"]
 PROF_SLOTS = 40
 
 MTE_OP_INSERT, MTE_OP_REMOVE, MTE_OP_ANNOTATE, MTE_OP_INSERT_MARKER, MTE_OP_NOOP = 0, 1, 2, 3, 4

@@ -9,7 +9,7 @@ NAMES = ["apply", "resolve", "insert_slot", "range", "zamboni", "scour", "heap",
          "fetch", "lru", "text", "alloc", "ops", "total"]
 path = sys.argv[1]
 kernel = sys.argv[2] if len(sys.argv) > 2 else "k_lds<false>"
-mangled = {"k_lds<false>": "_ZN3mte5k_ldsILb0EEEvNS_6ParamsE", "k_solo<false>": "_ZN3mte6k_soloILb0EEEvNS_6ParamsE", "k_hbmq<false>": "_ZN3mte6k_hbmqILb0EEEvNS_6ParamsE"}[kernel]
+mangled = {"k_lds<false>": "_ZN3mte5k_ldsILb0ELi0EEEvNS_6ParamsE", "k_solo<false>": "_ZN3mte6k_soloILb0ELi0EEEvNS_6ParamsE", "k_hbmq<false>": "_ZN3mte6k_hbmqILb0ELi0EEEvNS_6ParamsE"}[kernel]
 lines = open(path).read().split("\n")
 start = next(i for i, l in enumerate(lines) if l.startswith(mangled + ":"))
 end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i] and i > start)
@@ -37,5 +37,5 @@ for l in lines[start:end + 1]:
 print(f"{kernel}: {total} instructions")
 for s in sorted(incl, key=lambda x: -incl[x]):
     k = kinds.get(s, Counter())
-    print(f"{NAMES[s] if s < len(NAMES) else s:12s} incl {incl[s]:6d} excl {excl[s]:6d}  "
+    print(f"{NAMES[s] if s < len(NAMES) else str(s):12s} incl {incl[s]:6d} excl {excl[s]:6d}  "
           + " ".join(f"{a}{b}" for a, b in sorted(k.items(), key=lambda x: -x[1])[:5]))

@@ -304,7 +304,7 @@ struct Engine {
         m_in_par = (u32*)(b + l.in_par);
         m_heap = (uint2*)(b + l.heap);
         m_scratch = (u32*)(b + l.scratch);
-        m_stats = m_scratch + 32;
+        m_stats = m_scratch + 64;
         m_hint = (u32*)(b + l.hint);
         m_blk_cap = cb;
         m_ord_cap = co;
@@ -662,7 +662,25 @@ struct Engine {
     // The block of `pos` from one block scan already held per lane (lane = doc-order index, n_lb <= 64:
     // o, its visible length v and the inclusive prefix incl), then the slot inside it. The block's child
     // count is re-read (a split since the scan may have added a slot; block splits invalidate the scan).
+    // The fused scan's per-lane block lengths: kept in registers by k_solo (no register budget), in the
+    // wave's scratch words by the budgeted kernels, whose registers it would otherwise hold across the
+    // split phases (lean k_lds: 42 -> 67 spilled VGPRs in registers)
+    static constexpr bool PRE_REGS = SOLO;
+    MTE_DEV void pre_put(u32 v) {
+        if constexpr (!PRE_REGS) {
+            sync();
+            SCRATCH()[L] = v;
+            sync();
+        }
+    }
+    MTE_DEV void pre_get(u32& v, u32& incl) {
+        if constexpr (!PRE_REGS) {
+            v = SCRATCH()[L];
+            incl = wave_scan_incl(v);
+        }
+    }
     MTE_DEV Found resolve_pre(u32 v, u32 incl, i32 pos, i32 R, u32 C) {
+        pre_get(v, incl);
         Found f;
         f.ok = false;
         f.k = 0;
@@ -1914,6 +1932,10 @@ struct Engine {
             pv = blen_all(po, valid, R, C);
             pincl = wave_scan_incl(pv);
             pn = st.n_lb;
+            if constexpr (!PRE_REGS) {
+                pre_put(pv);
+                pv = pincl = 0;  // not live across the phases
+            }
         }
         for (u32 ph = 0; ph < nphase; ph++) {
             if (!ins && ph == 2) {
@@ -2023,6 +2045,7 @@ struct Engine {
             const u32 k = base + L;
             const bool valid = k < st.n_lb;
             uint4 o = valid ? ORD()[k] : make_uint4(0, 0, 0, 0);
+            if (pre) pre_get(pv, pincl);
             const u32 v = pre ? pv : blen_all(o, valid, R, C);
             const u32 incl = pre ? pincl : wave_scan_incl(v);
             const i32 cb = cum + (i32)(incl - v);

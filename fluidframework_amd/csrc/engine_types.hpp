@@ -246,8 +246,8 @@ struct HbmLayout {
         o += a16((u64)in * 4);
         l.heap = o;
         o += a16((u64)(heap + 1) * 8);
-        l.scratch = o;
-        o += 64 * 4;
+        l.scratch = o;  // 64 words of per-lane scratch, then the per-document counters (stats)
+        o += 128 * 4;
         l.hint = o;
         o += HBM_HINTS * 4;
         l.bytes = o;

@@ -2652,6 +2652,9 @@ struct Engine {
                     MTE_PROF(PF_LOOP);
                     if (!room()) break;
                 }
+#ifdef MTE_UNIFORMIZE  // experiment: re-assert the state's uniformity every op
+                uniformize();
+#endif
                 apply(op, i);
             }
         } else {

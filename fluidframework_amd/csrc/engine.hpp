@@ -2145,31 +2145,6 @@ struct Engine {
         }
     }
 
-    // Re-assert that the replay state is wave-uniform (readfirstlane): the compiler's divergence
-    // analysis cannot see that values loaded from LDS at uniform addresses are uniform, and once a
-    // state word is considered divergent every branch on it becomes an exec-mask branch.
-    MTE_DEV void uniformize() {
-        st.root = U(st.root);
-        st.height = U(st.height);
-        st.n_lb = U(st.n_lb);
-        st.minSeq = (i32)U((u32)st.minSeq);
-        st.curSeq = (i32)U((u32)st.curSeq);
-        st.heapSize = U(st.heapSize);
-        st.heapTop = (i32)U((u32)st.heapTop);
-        st.segNext = U(st.segNext);
-        st.arenaTop = U(st.arenaTop);
-        st.arenaSel = U(st.arenaSel);
-        st.mapNext = U(st.mapNext);
-        st.lbFree = U(st.lbFree);
-        st.lbBump = U(st.lbBump);
-        st.inFree = U(st.inFree);
-        st.inBump = U(st.inBump);
-        st.inUsed = U(st.inUsed);
-        st.status = (i32)U((u32)st.status);
-        st.adirty = U(st.adirty);
-        st.gdirty = U(st.gdirty);
-    }
-
     // ---------------------------------------------------------------- resume from a summary
     // SnapshotLoader (snapshotLoader.ts:113-216) as records (include/mte.h MTE_OP_LOAD_*), applied
     // outside the op path (replay_run dispatches them). LOAD_SEG fills the leaf blocks in document
@@ -2652,9 +2627,6 @@ struct Engine {
                     MTE_PROF(PF_LOOP);
                     if (!room()) break;
                 }
-#ifdef MTE_UNIFORMIZE  // experiment: re-assert the state's uniformity every op
-                uniformize();
-#endif
                 apply(op, i);
             }
         } else {

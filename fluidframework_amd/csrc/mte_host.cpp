@@ -2451,16 +2451,55 @@ static int legacy_to_v1(const std::u16string& path, json::Value& c) {
     return MTE_OK;
 }
 
-// storage.read(path) + SnapshotV1.processChunk (snapshotV1.ts:249-270) for a utf-8 blob
+// An ITree blob's text (IBlob { contents, encoding: "utf-8" | "base64" }): what storage.read(path) +
+// fromBase64ToUtf8 give the loader (snapshotV1.ts:255,267; snapshotLoader.ts:225). Base64 as Node's
+// Buffer.from(s, "base64") reads it: standard or url-safe alphabet, whitespace skipped, '=' ends the
+// data. Returns 0, or -1 for a missing blob, -2 for an unknown encoding, -3 for a bad character.
+static int blob_utf8(const json::Value* v, std::string& out) {
+    const json::Value* c = v && v->kind == json::Value::Object ? v->get(u"contents") : nullptr;
+    const json::Value* enc = v && v->kind == json::Value::Object ? v->get(u"encoding") : nullptr;
+    if (!c || c->kind != json::Value::String) return -1;
+    if (!enc || (enc->kind == json::Value::String && enc->str == u"utf-8")) {
+        out = json::to_utf8(c->str.data(), c->str.size());
+        return 0;
+    }
+    if (!(enc->kind == json::Value::String && enc->str == u"base64")) return -2;
+    out.clear();
+    u32 acc = 0, nb = 0;
+    for (char16_t ch : c->str) {
+        int d;
+        if (ch >= u'A' && ch <= u'Z') d = ch - u'A';
+        else if (ch >= u'a' && ch <= u'z') d = ch - u'a' + 26;
+        else if (ch >= u'0' && ch <= u'9') d = ch - u'0' + 52;
+        else if (ch == u'+' || ch == u'-') d = 62;
+        else if (ch == u'/' || ch == u'_') d = 63;
+        else if (ch == u'=') break;
+        else if (ch == u' ' || ch == u'\n' || ch == u'\r' || ch == u'\t') continue;
+        else return -3;
+        acc = (acc << 6) | (u32)d;
+        nb += 6;
+        if (nb >= 8) {
+            nb -= 8;
+            out.push_back((char)((acc >> nb) & 0xff));
+        }
+    }
+    return 0;
+}
+static int blob_text(DocBuild& db, const json::Value* v, std::string& out, const char* missing) {
+    switch (blob_utf8(v, out)) {
+        case 0: return MTE_OK;
+        case -1: return db.fail(MTE_E_PARSE, missing);
+        case -2: return db.fail(MTE_E_UNSUPPORTED, "blob encoding other than utf-8 / base64");
+        default: return db.fail(MTE_E_PARSE, "bad base64 blob contents");
+    }
+}
+
+// storage.read(path) + SnapshotV1.processChunk (snapshotV1.ts:249-270)
 static int load_chunk(DocBuild& db, const json::Value& tree, const std::u16string& path, json::Value* out) {
     const json::Value* e = tree_entry(tree, path.c_str());
     const json::Value* v = e ? e->get(u"value") : nullptr;
-    const json::Value* c = v && v->kind == json::Value::Object ? v->get(u"contents") : nullptr;
-    const json::Value* enc = v && v->kind == json::Value::Object ? v->get(u"encoding") : nullptr;
-    if (!c || c->kind != json::Value::String) return db.fail(MTE_E_PARSE, "summary blob missing");
-    if (enc && !(enc->kind == json::Value::String && enc->str == u"utf-8"))
-        return db.fail(MTE_E_UNSUPPORTED, "only utf-8 blob contents are supported");
-    const std::string text = json::to_utf8(c->str.data(), c->str.size());
+    std::string text;
+    if (int rc = blob_text(db, v, text, "summary blob missing")) return rc;
     try {
         *out = json::parse(text.data(), text.size());
     } catch (std::exception& ex) {
@@ -2705,10 +2744,8 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
         if (!isChunk) extra = &e;
     }
     if (nBlobs == nChunks + 1 && extra) {
-        const json::Value* v = extra->get(u"value");
-        const json::Value* c = v ? v->get(u"contents") : nullptr;
-        if (!c || c->kind != json::Value::String) return db.fail(MTE_E_PARSE, "catch-up ops blob");
-        const std::string text = json::to_utf8(c->str.data(), c->str.size());
+        std::string text;
+        if (int rc = blob_text(db, extra->get(u"value"), text, "catch-up ops blob")) return rc;
         json::Value msgs;
         try {
             msgs = json::parse(text.data(), text.size());
@@ -2783,10 +2820,10 @@ static void attach_trees(const json::Value& attach, const std::string& id, std::
             if (t->str == u"Tree") {
                 q.emplace_back(full + "/" + u8(p->str), v);
             } else if (t->str == u"Blob" && p->str == u".attributes") {
-                const json::Value* c = v->get(u"contents");
-                if (!c || c->kind != json::Value::String) continue;
+                std::string at_text;
+                if (blob_utf8(v, at_text)) continue;
                 try {
-                    json::Value a = json::parse(u8(c->str).c_str(), u8(c->str).size());
+                    json::Value a = json::parse(at_text.c_str(), at_text.size());
                     const json::Value* at = a.get(u"type");
                     if (at && at->kind == json::Value::String && at->str == kSharedStringType) put(full, tree);
                 } catch (std::exception&) {

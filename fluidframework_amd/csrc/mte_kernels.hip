@@ -23,6 +23,11 @@ namespace mte {
 #ifndef MTE_HBMQ_WPE
 #define MTE_HBMQ_WPE 4
 #endif
+// k_solo owns its CU's LDS, so one wave per SIMD is all it ever has: the hint lets the scheduler
+// trade registers for latency hiding instead of aiming at an occupancy it can never reach.
+#ifndef MTE_SOLO_WPE
+#define MTE_SOLO_WPE 1
+#endif
 
 template <bool GEN, int LVL>
 __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(MTE_LDS_WPE))) void k_lds(Params p) {
@@ -98,7 +103,7 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
 // latency of the longest document bounds a Zipf batch, so it gets the plan with the
 // most room and no LDS-pool sharing; it continues HBM-resident only if it outgrows even that.
 template <bool GEN, int LVL>
-__global__ __launch_bounds__(64) void k_solo(Params p) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_SOLO_WPE, MTE_SOLO_WPE))) void k_solo(Params p) {
     const u32 i = blockIdx.x;
     if (i >= p.n_solo) return;
     const u32 d = p.doc_list[i];

@@ -305,8 +305,11 @@ int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* j
 /* Catch-up from a summary: SharedSegmentSequence.load + SnapshotLoader.initialize
  * (sequence.ts:593-633, snapshotLoader.ts:38-216) then applyMsg for the op-log suffix.
  * summary: the ITree JSON of mte_snapshot_v1 ({"entries":[header, body_0, ...]}) or a SharedString
- * tree holding it under "content"; blob contents utf-8. ops may be NULL (no suffix).
- * MTE_E_UNSUPPORTED for legacy (non-"1") chunks and for body chunks next to merge-info segments. */
+ * tree holding it under "content", or a SnapshotLegacy tree (chunks converted by toLatestVersion,
+ * snapshotChunks.ts:135-176; its catch-up ops blob applied after the load). Blobs are IBlob
+ * { contents, encoding }: "utf-8", or "base64" as storage returns them (fromBase64ToUtf8,
+ * snapshotV1.ts:267). ops may be NULL (no suffix). MTE_E_UNSUPPORTED for chunk versions other than
+ * "1" / legacy and for other blob encodings; MTE_E_PARSE for malformed JSON or base64. */
 int mte_builder_add_doc_from_summary(mte_builder* b, const char* observer_name, const char* summary,
                                      size_t summary_len, const char* ops, size_t ops_len);
 /* Container-level op log (clientReplayTool.ts:113-192,258-347 over FileDeltaStorageService's

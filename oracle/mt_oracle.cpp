@@ -1167,15 +1167,38 @@ class Doc {
         }
         return nullptr;
     }
-    // storage.read(path) + SnapshotV1.processChunk (snapshotV1.ts:249-270) for a utf-8 blob
+    // An ITree blob's text: storage.read(path) + fromBase64ToUtf8 (snapshotV1.ts:255,267,
+    // snapshotLoader.ts:225) for { contents, encoding: "utf-8" | "base64" }; base64 read as Node's
+    // Buffer.from(s, "base64") does (both alphabets, whitespace skipped, '=' ends the data).
+    static std::string blobText(JVP v, const char* missing) {
+        JVP c = v && v->t == JV::Obj ? v->o.get(u"contents") : nullptr;
+        JVP enc = v && v->t == JV::Obj ? v->o.get(u"encoding") : nullptr;
+        if (!c || c->t != JV::Str) throw EngineError(MTE_DOC_UNSUPPORTED, missing);
+        if (!enc || (enc->t == JV::Str && enc->s == u"utf-8")) return u16_to_utf8(c->s);
+        if (!(enc->t == JV::Str && enc->s == u"base64")) throw EngineError(MTE_DOC_UNSUPPORTED, "blob encoding");
+        static const std::string A = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+        std::string out;
+        unsigned acc = 0, nb = 0;
+        for (char16_t ch : c->s) {
+            if (ch == u'=') break;
+            if (ch == u' ' || ch == u'\n' || ch == u'\r' || ch == u'\t') continue;
+            const char16_t cc = ch == u'-' ? u'+' : (ch == u'_' ? u'/' : ch);
+            const size_t d = cc < 128 ? A.find((char)cc) : std::string::npos;
+            if (d == std::string::npos) throw EngineError(MTE_DOC_UNSUPPORTED, "bad base64 blob");
+            acc = (acc << 6) | (unsigned)d;
+            nb += 6;
+            if (nb >= 8) {
+                nb -= 8;
+                out.push_back((char)((acc >> nb) & 0xff));
+            }
+        }
+        return out;
+    }
+    // storage.read(path) + SnapshotV1.processChunk (snapshotV1.ts:249-270)
     static JVP chunkAt(const JV& tree, const u16s& path) {  // (legacy chunks converted to v1)
         JVP e = treeEntry(tree, path);
         JVP v = e ? e->o.get(u"value") : nullptr;
-        JVP c = v && v->t == JV::Obj ? v->o.get(u"contents") : nullptr;
-        JVP enc = v && v->t == JV::Obj ? v->o.get(u"encoding") : nullptr;
-        if (!c || c->t != JV::Str) throw EngineError(MTE_DOC_UNSUPPORTED, "summary blob missing");
-        if (enc && !(enc->t == JV::Str && enc->s == u"utf-8")) throw EngineError(MTE_DOC_UNSUPPORTED, "blob encoding");
-        std::string s = u16_to_utf8(c->s);
+        std::string s = blobText(v, "summary blob missing");
         JVP ch = parse(s.data(), s.size());
         JVP ver = ch->t == JV::Obj ? ch->o.get(u"version") : nullptr;
         if (!ver && ch->t == JV::Obj && ch->o.get(u"segmentTexts")) {  // toLatestVersion (snapshotChunks.ts:135-176)
@@ -1302,10 +1325,7 @@ class Doc {
         }
         if (nBlobs != nChunks + 1 && nBlobs != nChunks) throw EngineError(MTE_DOC_UNSUPPORTED, "Unexpected blobs in snapshot");
         if (nBlobs == nChunks + 1 && extra) {
-            JVP v = extra->o.get(u"value");
-            JVP c = v ? v->o.get(u"contents") : nullptr;
-            if (!c || c->t != JV::Str) throw EngineError(MTE_DOC_UNSUPPORTED, "catch-up ops blob");
-            std::string txt = u16_to_utf8(c->s);
+            std::string txt = blobText(extra->o.get(u"value"), "catch-up ops blob");
             JVP msgs = parse(txt.data(), txt.size());
             if (msgs->t == JV::Arr)
                 for (auto& m : msgs->a) applyMsg(*m);

@@ -165,6 +165,58 @@ def test_summary_errors():
         b.add_doc_from_summary(fixture("headerOnly"), observer="")  # loading needs a collaborating client
 
 
+def base64_blobs(summary, wrap=False):
+    """The same ITree with every blob as { contents: base64(utf-8 bytes), encoding: "base64" } -- the
+    form storage hands the loader (snapshotV1.ts:255,267 fromBase64ToUtf8); wrap=True breaks the
+    base64 text into 76-column lines as MIME encoders do."""
+    import base64
+
+    def walk(t):
+        for e in t["entries"]:
+            v = e["value"]
+            if e["type"] == "Tree":
+                walk(v)
+            else:
+                b = base64.b64encode(v["contents"].encode("utf-8")).decode("ascii")
+                if wrap:
+                    b = "\n".join(b[i:i + 76] for i in range(0, len(b), 76))
+                e["value"] = {"contents": b, "encoding": "base64"}
+    tree = json.loads(summary)
+    walk(tree)
+    return json.dumps(tree)
+
+
+def test_base64_blobs_load_like_utf8():
+    """Every v1 and legacy fixture (incl. the catch-up ops blobs) and the collaborative summaries load
+    identically from base64 blobs, in the oracle and in the builder's records."""
+    cases = [(fixture(n), None) for n in FIXTURES] + collab_summaries()
+    cases += [(legacy_fixture(k, n), None) for k, n in LEGACY]
+    b = mte.Builder()
+    for i, (summ, suffix) in enumerate(cases):
+        b.add_doc_from_summary(base64_blobs(summ, wrap=i % 2 == 1), suffix, observer=OBS)
+    batch = b.batch()
+    for d, (summ, suffix) in enumerate(cases):
+        ref = oracle_catchup(summ, suffix)
+        o64 = oracle_catchup(base64_blobs(summ), suffix)
+        rec = OracleDoc(OBS)
+        rec.apply_batch(ctypes.addressof(batch), d)
+        assert rec.status()[0] == o64.status()[0] == ref.status()[0] == 0, d
+        assert o64.snapshot_json() == ref.snapshot_json(), d
+        assert rec.segments_json() == ref.segments_json(), d
+        assert rec.snapshot_json() == ref.snapshot_json(), d
+
+
+def test_blob_encoding_errors():
+    bad_char = json.loads(base64_blobs(fixture("headerOnly")))
+    bad_char["entries"][1]["value"]["entries"][0]["value"]["contents"] = "e30*"
+    other = json.loads(fixture("headerOnly"))
+    other["entries"][1]["value"]["entries"][0]["value"]["encoding"] = "hex"
+    for t in (bad_char, other):
+        with pytest.raises(mte.MteError):
+            mte.Builder().add_doc_from_summary(json.dumps(t), observer=OBS)
+        assert OracleDoc(OBS).load_summary(json.dumps(t)) != 0
+
+
 @pytest.mark.gpu
 def test_gpu_catchup_matches_oracle(engine):
     from tests.gpu_helpers import compare_doc

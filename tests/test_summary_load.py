@@ -222,7 +222,8 @@ def test_gpu_catchup_matches_oracle(engine):
     from tests.gpu_helpers import compare_doc
 
     cases = [(fixture(n), None) for n in FIXTURES]
-    cases += [(fixture(n), None) for n in FIXTURES]  # second copy: LDS- and HBM-resident neighbours
+    # second copy, from base64 blobs: LDS- and HBM-resident neighbours
+    cases += [(base64_blobs(fixture(n)), None) for n in FIXTURES]
     cases += collab_summaries()
     b = mte.Builder()
     for summ, suffix in cases:

@@ -658,9 +658,10 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     e->replayed = e->downloaded = false;
     const uint32_t nd = b->n_docs;
     std::vector<uint64_t> n_ops(nd), pay(nd), pi(nd), an(nd);
-    std::vector<uint8_t> collab(nd), has_nl(nd, 0);
-    bool lean = true, ext = false;
-    for (uint32_t d = 0; d < nd; d++) {
+    std::vector<uint8_t> collab(nd), has_nl(nd, 0), not_lean(nd, 0), doc_ext(nd, 0);
+    // one pass over each document's ops and payload, documents spread over host threads (the scan is
+    // most of mte_load's host time on large batches)
+    auto scan = [&](uint32_t d) {
         for (uint64_t q = b->doc_payload_offsets[d]; q < b->doc_payload_offsets[d + 1]; q++)
             if (b->payload[q] == (uint16_t)'\n') {
                 has_nl[d] = 1;
@@ -670,13 +671,33 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         pay[d] = b->doc_payload_offsets[d + 1] - b->doc_payload_offsets[d];
         bool rel = false;
         count_doc_ops(e->hb, d, pi[d], an[d], &rel);
-        for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1] && !ext; i++)
-            ext = (b->ops[i].flags & (MTE_F_PERM | MTE_F_CATCHUP)) != 0;
+        for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++)
+            if (b->ops[i].flags & (MTE_F_PERM | MTE_F_CATCHUP)) {
+                doc_ext[d] = 1;
+                break;
+            }
         collab[d] = e->hb.client(d, 0).empty() ? 0 : 1;  // empty observer name => local, non-collab
-        lean = lean && !has_nl[d] && !pi[d] && !an[d] && !rel &&
-               e->hb.doc_client_offsets[d + 1] - e->hb.doc_client_offsets[d] <= 32;
+        not_lean[d] = has_nl[d] || pi[d] || an[d] || rel ||
+                      e->hb.doc_client_offsets[d + 1] - e->hb.doc_client_offsets[d] > 32;
         // a document with more than MTE_MAX_CLIENTS clients fails alone (MTE_DOC_UNSUPPORTED at its
         // first op from a client beyond the cap), never the batch
+    };
+    {
+        const unsigned nt = std::max(1u, std::min({16u, std::thread::hardware_concurrency(), (nd + 255) / 256}));
+        std::atomic<uint32_t> next{0};
+        auto work = [&]() {
+            for (uint32_t d0; (d0 = next.fetch_add(256)) < nd;)
+                for (uint32_t d = d0; d < std::min(nd, d0 + 256); d++) scan(d);
+        };
+        std::vector<std::thread> ts;
+        for (unsigned i = 1; i < nt; i++) ts.emplace_back(work);
+        work();
+        for (auto& t : ts) t.join();
+    }
+    bool lean = true, ext = false;
+    for (uint32_t d = 0; d < nd; d++) {
+        lean = lean && !not_lean[d];
+        ext = ext || doc_ext[d];
     }
     auto t0 = std::chrono::steady_clock::now();
     int rc;
@@ -686,7 +707,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     // one per character of its range (every delta segment is visible in the op's view), or at most
     // every segment when a position is relative
     uint64_t cu = 0;
-    for (uint32_t d = 0; d < nd; d++) {
+    for (uint32_t d = 0; d < nd && ext; d++) {  // (no catch-up record in a batch without extensions)
         DocCfg& c = e->cfg[d];
         uint64_t cap = 0;
         for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {

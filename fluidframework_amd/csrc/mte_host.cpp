@@ -84,12 +84,19 @@ struct HostBatch {
         b->msg_text_offsets = msgs ? msg_text_offsets.data() : nullptr;
         b->msg_text = msgs ? msg_text.data() : nullptr;
     }
-    void copy_from(const mte_batch* b) {
+    // with_ops = false: everything but the op records and the payload (mte_load uploads those straight
+    // from the caller's buffers; ensure_host_ops reads them back if a host walker ever needs them)
+    void copy_from(const mte_batch* b, bool with_ops = true) {
         const uint32_t n = b->n_docs;
         doc_op_offsets.assign(b->doc_op_offsets, b->doc_op_offsets + n + 1);
-        ops.assign(b->ops, b->ops + doc_op_offsets[n]);
         doc_payload_offsets.assign(b->doc_payload_offsets, b->doc_payload_offsets + n + 1);
-        payload.assign(b->payload, b->payload + doc_payload_offsets[n]);
+        if (with_ops) {
+            ops.assign(b->ops, b->ops + doc_op_offsets[n]);
+            payload.assign(b->payload, b->payload + doc_payload_offsets[n]);
+        } else {
+            std::vector<mte_op>().swap(ops);
+            std::vector<uint16_t>().swap(payload);
+        }
         propsets.assign(b->propsets, b->propsets + b->n_propsets);
         size_t nkv = 0;
         for (auto& ps : propsets) nkv = std::max<size_t>(nkv, (size_t)ps.first + ps.count);
@@ -369,10 +376,14 @@ static int derive_value_tables(mte_engine* e) {
 }
 
 template <class T>
-static int upload(mte_engine* e, DevBuf<T>& d, const std::vector<T>& h) {
-    HIP_TRY(e, d.alloc(h.size()));
-    if (!h.empty()) HIP_TRY(e, hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, e->stream));
+static int upload(mte_engine* e, DevBuf<T>& d, const T* h, size_t n) {
+    HIP_TRY(e, d.alloc(n));
+    if (n) HIP_TRY(e, hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, e->stream));
     return MTE_OK;
+}
+template <class T>
+static int upload(mte_engine* e, DevBuf<T>& d, const std::vector<T>& h) {
+    return upload(e, d, h.data(), h.size());
 }
 
 static int alloc_slots(mte_engine* e);
@@ -636,10 +647,11 @@ void mte_destroy(mte_engine* e) {
 
 const char* mte_last_error(const mte_engine* e) { return e ? e->err.c_str() : "null engine"; }
 
-static void count_doc_ops(const HostBatch& hb, uint32_t d, uint64_t& pi, uint64_t& an, bool* rel = nullptr) {
+static void count_doc_ops(const mte_op* ops, const uint64_t* off, uint32_t d, uint64_t& pi, uint64_t& an,
+                          bool* rel = nullptr) {
     pi = an = 0;
-    for (uint64_t i = hb.doc_op_offsets[d]; i < hb.doc_op_offsets[d + 1]; i++) {
-        const mte_op& o = hb.ops[i];
+    for (uint64_t i = off[d]; i < off[d + 1]; i++) {
+        const mte_op& o = ops[i];
         if (rel && o.type == MTE_OP_RELPOS) *rel = true;  // FULL kernels only
         if ((o.type == MTE_OP_INSERT || o.type == MTE_OP_INSERT_MARKER || o.type == MTE_OP_LOAD_SEG ||
              o.type == MTE_OP_LOAD_APPEND) && o.props)
@@ -651,10 +663,10 @@ static void count_doc_ops(const HostBatch& hb, uint32_t d, uint64_t& pi, uint64_
 int mte_load(mte_engine* e, const mte_batch* b) {
     if (!e || !b) return MTE_E_ARG;
     HIP_TRY(e, hipSetDevice(e->device));
-    e->hb.copy_from(b);
+    e->hb.copy_from(b, false);
     e->emit_tables = false;
     e->generated = false;
-    e->host_ops_valid = true;
+    e->host_ops_valid = false;
     e->replayed = e->downloaded = false;
     const uint32_t nd = b->n_docs;
     std::vector<uint64_t> n_ops(nd), pay(nd), pi(nd), an(nd);
@@ -670,7 +682,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         n_ops[d] = b->doc_op_offsets[d + 1] - b->doc_op_offsets[d];
         pay[d] = b->doc_payload_offsets[d + 1] - b->doc_payload_offsets[d];
         bool rel = false;
-        count_doc_ops(e->hb, d, pi[d], an[d], &rel);
+        count_doc_ops(b->ops, b->doc_op_offsets, d, pi[d], an[d], &rel);
         for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++)
             if (b->ops[i].flags & (MTE_F_PERM | MTE_F_CATCHUP)) {
                 doc_ext[d] = 1;
@@ -729,8 +741,8 @@ int mte_load(mte_engine* e, const mte_batch* b) {
                                   e->stream));
     }
     e->P.cu_rec = cu ? e->d_cu.p : nullptr;
-    if ((rc = upload(e, e->d_ops, e->hb.ops))) return rc;
-    if ((rc = upload(e, e->d_payload, e->hb.payload))) return rc;
+    if ((rc = upload(e, e->d_ops, b->ops, b->doc_op_offsets[nd]))) return rc;
+    if ((rc = upload(e, e->d_payload, b->payload, b->doc_payload_offsets[nd]))) return rc;
     if ((rc = upload_props(e))) return rc;
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     e->last_h2d_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1644,6 +1656,7 @@ static json::Value insert_seg_json(const mte_engine* e, uint32_t d, const mte_op
 }
 // The catch-up blob of document d: JSON.stringify(messagesSinceMSNChange) at snapshot time.
 static int catch_up_json(mte_engine* e, uint32_t d, std::string& out) {
+    if (int rc = ensure_host_ops(e)) return rc;
     const HostBatch& hb = e->hb;
     const DocRes& r = e->res[d];
     const int32_t minSeq = r.min_seq;

@@ -201,6 +201,8 @@ struct Params {
     u32 gen_nclients;
     u64 gen_seed;
     u32 gen_n_propsets;       // propset ids 1..gen_n_propsets are the generator's annotate sets
+    u32 reg_solo;             // k_solo replays lean documents register-resident first (reg_engine.hpp)
+    u32 reg_lb_limit;         // test knob: leaf blocks the register plan may hold (0 = all it has)
     u32 pad1;
 };
 

@@ -261,6 +261,8 @@ struct mte_engine {
     // options (mte_set_option)
     bool force_hbm = false;           // no LDS-resident waves: every document HBM-resident
     uint32_t pool_limit = 0;
+    uint32_t reg_solo = 1;               // option "reg_solo": k_solo's register-resident engine (lean batches)
+    uint32_t reg_lb_limit = 0;           // option "reg_lb_limit": test knob, leaf blocks the register plan holds
 #ifndef MTE_HBMQ_PER_CU
 #define MTE_HBMQ_PER_CU 8
 #endif
@@ -271,6 +273,9 @@ struct mte_engine {
     // critical-path documents replayed by k_solo (a whole CU's LDS for one wave each)
     bool lean_ok = false;                // batch_is_lean: the replay may run the FULL = false kernels
     bool ext_needed = false;             // catch-up records or permutation runs: the EXT kernels (level 2)
+    bool ext_perm = false;               // the loaded batch has permutation runs (always EXT)
+    bool ext_cu = false;                 // ... MTE_F_CATCHUP ops: EXT only when a legacy summary is emitted
+    bool lean_base = false;              // batch_is_lean, before the catch-up records decide
     bool lean_opt = true;                // option "lean" (0 = always the FULL kernels)
     bool last_lean = false;
     uint32_t solo_max = 16;              // at most this many (0 = off)
@@ -670,7 +675,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     e->replayed = e->downloaded = false;
     const uint32_t nd = b->n_docs;
     std::vector<uint64_t> n_ops(nd), pay(nd), pi(nd), an(nd);
-    std::vector<uint8_t> collab(nd), has_nl(nd, 0), not_lean(nd, 0), doc_ext(nd, 0);
+    std::vector<uint8_t> collab(nd), has_nl(nd, 0), not_lean(nd, 0), doc_ext(nd, 0), doc_cu(nd, 0);
     // one pass over each document's ops and payload, documents spread over host threads (the scan is
     // most of mte_load's host time on large batches)
     auto scan = [&](uint32_t d) {
@@ -683,11 +688,10 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         pay[d] = b->doc_payload_offsets[d + 1] - b->doc_payload_offsets[d];
         bool rel = false;
         count_doc_ops(b->ops, b->doc_op_offsets, d, pi[d], an[d], &rel);
-        for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++)
-            if (b->ops[i].flags & (MTE_F_PERM | MTE_F_CATCHUP)) {
-                doc_ext[d] = 1;
-                break;
-            }
+        for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
+            if (b->ops[i].flags & MTE_F_PERM) doc_ext[d] = 1;
+            if (b->ops[i].flags & MTE_F_CATCHUP) doc_cu[d] = 1;
+        }
         collab[d] = e->hb.client(d, 0).empty() ? 0 : 1;  // empty observer name => local, non-collab
         not_lean[d] = has_nl[d] || pi[d] || an[d] || rel ||
                       e->hb.doc_client_offsets[d + 1] - e->hb.doc_client_offsets[d] > 32;
@@ -706,10 +710,11 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         work();
         for (auto& t : ts) t.join();
     }
-    bool lean = true, ext = false;
+    bool lean = true, ext = false, cu_any = false;
     for (uint32_t d = 0; d < nd; d++) {
         lean = lean && !not_lean[d];
         ext = ext || doc_ext[d];
+        cu_any = cu_any || doc_cu[d];
     }
     auto t0 = std::chrono::steady_clock::now();
     int rc;
@@ -719,7 +724,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     // one per character of its range (every delta segment is visible in the op's view), or at most
     // every segment when a position is relative
     uint64_t cu = 0;
-    for (uint32_t d = 0; d < nd && ext; d++) {  // (no catch-up record in a batch without extensions)
+    for (uint32_t d = 0; d < nd && cu_any; d++) {  // (no catch-up record in a batch without catch-up ops)
         DocCfg& c = e->cfg[d];
         uint64_t cap = 0;
         for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
@@ -748,6 +753,12 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     e->last_h2d_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     e->P.ops = e->d_ops.p;
     e->P.payload = e->d_payload.p;
+    // catch-up delta records are only read by the SnapshotLegacy writer: a batch whose only extension
+    // is MTE_F_CATCHUP runs the lean / FULL kernels (which ignore the flag) unless the replay emits
+    // the legacy format (run_kernel decides, snapshot_format may change after the load)
+    e->lean_base = lean;
+    e->ext_perm = ext;
+    e->ext_cu = cu_any;
     e->lean_ok = lean && !ext;
     e->ext_needed = ext;
     if ((rc = alloc_out_text(e))) return rc;
@@ -884,6 +895,8 @@ static int run_kernel(mte_engine* e, bool gen) {
     HIP_TRY(e, hipSetDevice(e->device));
     const uint32_t nd = e->P.n_docs;
     e->P.pool_limit = e->pool_limit;
+    e->P.reg_solo = e->reg_solo;
+    e->P.reg_lb_limit = e->reg_lb_limit;
     e->P.doc_list = e->d_order.p;
     e->P.n_list = nd;
     int rc;
@@ -891,6 +904,10 @@ static int run_kernel(mte_engine* e, bool gen) {
     uint32_t groups, hbm_waves, lds_active;
     const uint32_t n_solo = e->P.n_solo;
     // engine level (engine.hpp): the generator always runs FULL
+    if (!gen) {
+        e->ext_needed = e->ext_perm || (e->ext_cu && e->legacy);
+        e->lean_ok = e->lean_base && !e->ext_needed;
+    }
     const int full = gen ? 1 : e->ext_needed ? 2 : (e->lean_ok && e->lean_opt) ? 0 : 1;
     e->last_lean = full == 0;
     wave_plan(e, nd, groups, hbm_waves, &lds_active, n_solo);
@@ -1102,8 +1119,8 @@ int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_o
     e->gen_kind = kind;
     e->emit_tables = false;  // names are known after the generator ran
     // kinds 2 and 5 draw no properties and no '\n'; short ids stay below 1 + n_clients
-    e->lean_ok = kind != 3 && n_clients < 32;
-    e->ext_needed = false;
+    e->lean_ok = e->lean_base = kind != 3 && n_clients < 32;
+    e->ext_needed = e->ext_perm = e->ext_cu = false;
     rc = run_kernel(e, true);
     if (rc) return rc;
     // client names: observer + writers in first-appearance (short id) order
@@ -2013,6 +2030,8 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "solo_max") e->solo_max = (uint32_t)std::max<int64_t>(0, value);
     else if (k == "solo_min_ops") e->solo_min_ops = (uint64_t)std::max<int64_t>(1, value);
     else if (k == "lean") e->lean_opt = value != 0;
+    else if (k == "reg_solo") e->reg_solo = value != 0;
+    else if (k == "reg_lb_limit") e->reg_lb_limit = (uint32_t)std::max<int64_t>(0, value);
     else if (k == "emit") e->emit_opt = value != 0;  // SnapshotV1 emission on the device after replay
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
     else return set_err(e, MTE_E_ARG, "unknown option " + k);

@@ -11,6 +11,7 @@
 //               re-run of DOC_SPILL documents.
 #include "wave_hip.hpp"
 #include "engine.hpp"
+#include "reg_handoff.hpp"
 #include "mte_kernels.h"
 
 namespace mte {
@@ -112,13 +113,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_SOLO_WPE
     e.bind_lds(0);
     GenState g;
     bool done;
-    u64 at = 0;
-    e.init();
+    u64 at = p.docs[d].op_begin;
+    bool handed = false;
+    if constexpr (!GEN && LVL == 0) {
+        // lean replay: the whole document state in this wave's registers (reg_engine.hpp); it moves
+        // to the LDS plan below only if it outgrows the registers or reaches an op they do not cover
+        if (p.reg_solo) {
+            RegEngine<> r(p, d);
+            at = r.replay(at, p.docs[d].op_end);
+            if (r.status != REG_HANDOFF) {
+                r.finish();
+                __builtin_amdgcn_s_setprio(0);
+                return;
+            }
+            reg_handoff(r, e);
+            handed = true;
+        }
+    }
+    if (!handed) e.init();
     if (GEN) {
         e.gen_init(g);
         done = e.generate_run(g);
     } else {
-        at = e.replay_run(p.docs[d].op_begin);
+        at = e.replay_run(at);
         done = at >= p.docs[d].op_end;
     }
     if (e.st.status == DOC_SPILL) {

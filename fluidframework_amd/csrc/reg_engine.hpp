@@ -1,0 +1,1154 @@
+// reg_engine.hpp — the row-vectorised replay engine for critical-path documents (k_solo).
+//
+// Same observer replay as engine.hpp (@fluidframework/merge-tree 0.31.0; paths relative to
+// packages/dds/merge-tree/src), same B-tree shape and lazy zamboni schedule, restructured so that one
+// op is a short run of wave-wide instructions with few dependent memory round trips:
+//   * leaf blocks in DOCUMENT ORDER, 8 per "row": block k's slot s is lane 8*(k&7)+s of row k>>3.
+//     A row is 64 slots = 64 lanes, held in LDS exactly where the LDS engine's SoloPlan keeps slots
+//     (vis = len, seq, removedSeq, meta; aux = -, text offset, text capacity / overlap mask,
+//     segment id): one ds_read_b128 per lane fetches a whole row's visibility fields. An empty slot
+//     has len 0 (segments are never empty), so a block's child count is a popcount of one ballot;
+//   * position resolution (insertingWalk + nodeLength, mergeTree.ts:2345-2474,1659-1699): per row
+//     ONE predicate evaluation for 64 slots and ONE DPP prefix scan; the first block whose
+//     cumulative end reaches pos wins (blocks win ties, :2274-2276), then the slot inside it
+//     (breakTie, :2248-2277) from the same registers. No per-block summaries to maintain;
+//   * edits of a block are lane-parallel on its row (DPP shifts inside the 8-lane group); a block
+//     split or pack moves the blocks after it as one LDS memmove;
+//   * interior B-tree levels as child-COUNT vectors in VGPRs (lane = node at that level, document
+//     order): a parent is a prefix-sum lookup, a split 8 -> 4+4 a one-lane shift (mergeTree.ts:
+//     2446-2489, 1876-1887), pack a redistribution of counts (:1368-1420);
+//   * needsScour tri-state (mergeTree.ts:63,1279) in spare meta bits of every slot of its block, so
+//     it moves with the block;
+//   * the LRU heap (collections.ts:213-265) in 2 x 8 VGPRs, positions 1..511;
+//   * op records prefetched 8 per VGPR, decoded with v_readlane.
+// Text stays in HBM (the op payload and the merge arena), as in engine.hpp. Live segments carry
+// removedSeq RSEQ_LIVE and removedClient RCL_LIVE so the visibility predicate needs no removed test.
+// A document whose state outgrows this plan, or that reaches an op this engine does not implement
+// (annotate, summary load records, relative positions, legacy catch-up, permutation runs), hands its
+// state to the LDS engine between two ops (reg_handoff.hpp) and continues there.
+// The same source also builds for the CPU (wave_simd.hpp MTE_CPU): the CPU suite checks it against
+// the oracle (tests/test_reg_engine_cpu.py); the product runs the device build only.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "engine_types.hpp"
+#include "wave_simd.hpp"
+
+namespace mte {
+
+constexpr u32 RG_ROWS = 32;               // slot rows
+constexpr u32 RG_BLOCKS = RG_ROWS * 8;    // leaf blocks
+constexpr u32 RG_LEVELS = 8;              // interior levels (height <= RG_LEVELS + 1)
+constexpr u32 RG_HEAP = 511;              // LRU heap positions 1..511
+constexpr u32 RSEQ_LIVE = 0x7FFFFFFFu;    // removedSeq of a live segment (never <= a refSeq)
+constexpr u32 RCL_LIVE = 0xFFu;           // removedClient byte of a live segment (never a client)
+constexpr i32 REG_HANDOFF = 101;          // internal: continue in the LDS engine from the current op
+// needsScour (mergeTree.ts:63) in meta bits 24..25 of every slot lane of a block
+constexpr u32 NS_SHIFT = 24, NS_MASK = 3u << NS_SHIFT;
+static_assert(RG_BLOCKS <= SOLO_POOL, "the rows live in the SoloPlan's slot arrays");
+
+#ifndef MTE_CPU
+extern __shared__ uint4 g_lds_dyn[];
+#endif
+
+struct RSeg {
+    u32 len;
+    i32 seq;
+    u32 rseq;
+    u32 meta;
+    u32 toff;
+    u32 tz;
+    u32 sid;
+};
+struct RFound {
+    bool ok;
+    u32 k;     // leaf block (document order)
+    u32 cnt;   // its child count
+    i32 slot;  // first qualifying slot, -1 => append at the block end
+    i32 r;     // pos - cumBefore(slot)
+};
+
+template <int NR = (int)RG_ROWS>
+struct RegEngine {
+    typedef simd::V V;
+    typedef simd::B B;
+    static constexpr u32 NBLK = (u32)NR * 8;
+    struct Row {  // one row of slots: vis (len, seq, rseq, meta) + aux (-, toff, tz, sid)
+        V len, seq, rseq, meta, toff, tz, sid;
+    };
+
+    // ---------------------------------------------------------------- state
+    simd::VA<RG_LEVELS> LV;  // LV[i] lane j: child count of node j of level i+1 (0 beyond the last)
+    simd::VA<8> HK, HS;      // heap keys (maxSeq) / segment ids, position q at lane q&63 of reg q>>6
+    u32 n_lb, height, heapSize, segNext, arenaTop, arenaSel;
+    i32 minSeq, curSeq, heapTop, status, failSeq;
+    u32 n_ops, n_msgs, n_gc, max_lb;
+    bool adirty;
+    // per document
+    const Params& p;
+    u32 doc;
+    u16* payload;
+    u16* arena0;
+    u32 seg_cap, arena_cap, payload_len;
+
+    // ---------------------------------------------------------------- slot rows (LDS)
+#ifdef MTE_CPU
+    u32 mem_vis[RG_ROWS * 64][4], mem_aux[RG_ROWS * 64][4];
+    SD Row ldrow(u32 r) const {
+        Row w;
+        for (u32 l = 0; l < 64; l++) {
+            const u32* v = mem_vis[r * 64 + l];
+            const u32* a = mem_aux[r * 64 + l];
+            w.len.x[l] = v[0], w.seq.x[l] = v[1], w.rseq.x[l] = v[2], w.meta.x[l] = v[3];
+            w.toff.x[l] = a[1], w.tz.x[l] = a[2], w.sid.x[l] = a[3];
+        }
+        return w;
+    }
+    SD void strow(u32 r, const Row& w) {
+        for (u32 l = 0; l < 64; l++) {
+            u32* v = mem_vis[r * 64 + l];
+            u32* a = mem_aux[r * 64 + l];
+            v[0] = w.len.x[l], v[1] = w.seq.x[l], v[2] = w.rseq.x[l], v[3] = w.meta.x[l];
+            a[0] = 0, a[1] = w.toff.x[l], a[2] = w.tz.x[l], a[3] = w.sid.x[l];
+        }
+    }
+    SD V ldf(u32 r, u32 aux, u32 c) const {  // one field of a row
+        V x;
+        for (u32 l = 0; l < 64; l++) x.x[l] = aux ? mem_aux[r * 64 + l][c] : mem_vis[r * 64 + l][c];
+        return x;
+    }
+    SD void stf(u32 r, u32 aux, u32 c, V x, B m) {
+        for (u32 l = 0; l < 64; l++)
+            if ((m.m >> l) & 1) (aux ? mem_aux[r * 64 + l] : mem_vis[r * 64 + l])[c] = x.x[l];
+    }
+    // slot-index memmove (blocks move as whole 8-slot groups)
+    SD void mv_slots(u32 dst, u32 src, u32 n) {
+        memmove(mem_vis[dst], mem_vis[src], (size_t)n * 16);
+        memmove(mem_aux[dst], mem_aux[src], (size_t)n * 16);
+    }
+    SD void zero_slots(u32 at, u32 n) {
+        memset(mem_vis[at], 0, (size_t)n * 16);
+        memset(mem_aux[at], 0, (size_t)n * 16);
+    }
+#else
+    SD static uint4* VISP() { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + offsetof(SoloPlan, vis)); }
+    SD static uint4* AUXP() { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + offsetof(SoloPlan, aux)); }
+    SD Row ldrow(u32 r) const {
+        const u32 i = r * 64 + __lane_id();
+        const uint4 v = VISP()[i], a = AUXP()[i];
+        return Row{V{v.x}, V{v.y}, V{v.z}, V{v.w}, V{a.y}, V{a.z}, V{a.w}};
+    }
+    SD void strow(u32 r, const Row& w) {
+        const u32 i = r * 64 + __lane_id();
+        VISP()[i] = make_uint4(w.len.x, w.seq.x, w.rseq.x, w.meta.x);
+        AUXP()[i] = make_uint4(0u, w.toff.x, w.tz.x, w.sid.x);
+        simd::lds_order();
+    }
+    SD V ldf(u32 r, u32 aux, u32 c) const {
+        const u32* b = reinterpret_cast<const u32*>(aux ? AUXP() : VISP());
+        return V{b[(r * 64 + __lane_id()) * 4 + c]};
+    }
+    SD void stf(u32 r, u32 aux, u32 c, V x, B m) {
+        u32* b = reinterpret_cast<u32*>(aux ? AUXP() : VISP());
+        if (m.b) b[(r * 64 + __lane_id()) * 4 + c] = x.x;
+        simd::lds_order();
+    }
+    SD void mv_slots(u32 dst, u32 src, u32 n) {  // overlapping: copy in the safe direction
+        uint4* V4 = VISP();
+        uint4* A4 = AUXP();
+        const u32 L = __lane_id();
+        if (dst > src) {
+            for (i32 b = (i32)n - 64; b > -64; b -= 64) {
+                const i32 i = b + (i32)L;
+                uint4 v = make_uint4(0, 0, 0, 0), a = v;
+                if (i >= 0) {
+                    v = V4[src + (u32)i];
+                    a = A4[src + (u32)i];
+                }
+                simd::lds_order();
+                if (i >= 0) {
+                    V4[dst + (u32)i] = v;
+                    A4[dst + (u32)i] = a;
+                }
+                simd::lds_order();
+            }
+        } else {
+            for (u32 b = 0; b < n; b += 64) {
+                const u32 i = b + L;
+                uint4 v = make_uint4(0, 0, 0, 0), a = v;
+                if (i < n) {
+                    v = V4[src + i];
+                    a = A4[src + i];
+                }
+                simd::lds_order();
+                if (i < n) {
+                    V4[dst + i] = v;
+                    A4[dst + i] = a;
+                }
+                simd::lds_order();
+            }
+        }
+    }
+    SD void zero_slots(u32 at, u32 n) {
+        for (u32 b = __lane_id(); b < n; b += 64) {
+            VISP()[at + b] = make_uint4(0, 0, 0, 0);
+            AUXP()[at + b] = make_uint4(0, 0, 0, 0);
+        }
+        simd::lds_order();
+    }
+#endif
+    SD V ld_len(u32 r) const { return ldf(r, 0, 0); }
+    SD V ld_meta(u32 r) const { return ldf(r, 0, 3); }
+    SD V ld_tz(u32 r) const { return ldf(r, 1, 2); }
+    SD V ld_sid(u32 r) const { return ldf(r, 1, 3); }
+
+    SD RegEngine(const Params& p_, u32 doc_) : p(p_), doc(doc_) {
+        const DocCfg& c = p.docs[doc];
+        payload = p.payload + c.payload_off;
+        arena0 = p.arena + c.arena_off;
+        seg_cap = c.seg_cap;
+        arena_cap = c.arena_cap;
+        payload_len = c.payload_len;
+        init();
+    }
+    SD void init() {
+        zero_slots(0, NBLK * 8);  // every slot empty: rows past the last block stay zero
+        LV.zero();
+        HK.zero();
+        HS.zero();
+        n_lb = 1;
+        height = 1;
+        heapSize = segNext = arenaTop = arenaSel = 0;
+        minSeq = curSeq = heapTop = 0;
+        status = 0;
+        failSeq = -1;
+        n_ops = n_msgs = n_gc = 0;
+        max_lb = 1;
+        adirty = false;
+    }
+
+    SD static V L() { return simd::lanes(); }
+    SD void fail(i32 code, i32 seq) {
+        if (status == 0) {
+            status = code;
+            failSeq = seq;
+        }
+    }
+    SD u32 new_sid() {
+        if (segNext >= seg_cap) {
+            fail(MTE_DOC_CAPACITY, curSeq);
+            return NONE;
+        }
+        return segNext++;
+    }
+
+    // ---------------------------------------------------------------- blocks
+    SD static u32 gbase(u32 k) { return (k & 7u) * 8u; }
+    SD static B in_group(u32 k) { return (L() >> 3) == (k & 7u); }
+    SD static u32 group_bits(u64 m, u32 k) { return (u32)((m >> gbase(k)) & 0xFFull); }
+    SD u32 count(u32 k) const { return (u32)__builtin_popcount(group_bits(simd::ballot(ld_len(k >> 3) != 0u), k)); }
+    SD u32 ns_get(u32 k) const { return (simd::readlane(ld_meta(k >> 3), gbase(k)) >> NS_SHIFT) & 3u; }
+    SD void ns_set(u32 k, u32 sc) {
+        const V m = ld_meta(k >> 3);
+        stf(k >> 3, 0, 3, (m & ~NS_MASK) | (sc << NS_SHIFT), in_group(k));
+    }
+
+    // nodeLength of every slot of a row for (refSeq R, client C) (mergeTree.ts:1659-1699):
+    //   ins = client == C || seq <= R;  rem = removed && (removedClient == C || removedSeq <= R
+    //   || C in removedClientOverlap);  visible = ins && !rem ? len : 0.
+    SD V vis(u32 r, V len, V seq, V rseq, V meta, i32 R, u32 C) const {
+        const B ins = simd::sle(seq, R) | (simd::bfe(meta, 0, 8) == C);
+        B rem = simd::sle(rseq, R) | (simd::bfe(meta, 8, 8) == C);
+        const B ov = (meta & F_OVL) != 0u;  // removedClientOverlap non-empty (clients < 32: in tz)
+        if (simd::ballot(ov)) rem = rem | (((ld_tz(r) & (1u << C)) != 0u) & ov);
+        return simd::sel(simd::andn(ins, rem), len, 0u);
+    }
+
+    // insertingWalk's target for `pos` in the (R, C) view: the first leaf block whose cumulative
+    // visible end is >= pos, then inside it the first slot with pos < its end, or a zero-length slot
+    // at pos that wins breakTie (skip tombstones already seen at R, mergeTree.ts:2257-2261).
+    SD RFound resolve(i32 pos, i32 R, u32 C) const {
+        RFound f;
+        f.ok = false;
+        f.k = 0;
+        f.cnt = 0;
+        f.slot = -1;
+        f.r = 0;
+        const u32 nrows = (n_lb + 7) >> 3;
+        u32 carry = 0;
+        const V lk = L() >> 3;
+        for (u32 r = 0; r < nrows; r++) {
+            const Row w = ldrow(r);
+            const V v = vis(r, w.len, w.seq, w.rseq, w.meta, R, C);
+            const V incl = simd::scan_incl(v) + carry;
+            const B end = ((L() & 7u) == 7u) & ((lk + r * 8u) < n_lb);
+            const u64 hit = simd::ballot(end & simd::sge(incl, pos));
+            if (hit) {
+                const u32 g = (u32)__builtin_ctzll(hit) >> 3;
+                const u32 k = r * 8 + g, gb = g * 8;
+                const V ex = incl - v;
+                const V rr = (u32)pos - ex;
+                const B valid = w.len != 0u;
+                const B seen = simd::sle(w.rseq, R) & (w.rseq != 0u);
+                const B cand = in_group(k) & valid & (simd::slt(rr, v) | ((rr == 0u) & (v == 0u) & ~seen));
+                const u64 cm = simd::ballot(cand);
+                f.ok = true;
+                f.k = k;
+                f.cnt = (u32)__builtin_popcount(group_bits(simd::ballot(valid), k));
+                if (cm) {
+                    const u32 l = (u32)__builtin_ctzll(cm);
+                    f.slot = (i32)(l - gb);
+                    f.r = (i32)simd::readlane(rr, l);
+                }
+                return f;
+            }
+            carry = simd::readlane(incl, 63);
+        }
+        return f;
+    }
+
+    // ---------------------------------------------------------------- interior levels
+    // Parent (node index at level lv+1) of node c at level lv, and its first child.
+    SD u32 parent_of(u32 lv, u32 c, u32& first) const {
+        const V cnt = LV.get(lv);
+        const V incl = simd::scan_incl(cnt);
+        const u64 m = simd::ballot(incl > c);
+        const u32 pi = m ? (u32)__builtin_ctzll(m) : 0u;
+        first = simd::readlane(incl, pi) - simd::readlane(cnt, pi);
+        return pi;
+    }
+    // A new node was placed right after node c at level lv (its parent gains a child): split
+    // parents that reach 8 children 4+4, grow the root (insertingWalk / split / updateRoot,
+    // mergeTree.ts:2446-2489, 1876-1887).
+    SD void insert_after(u32 c, u32 lv) {
+        for (u32 guard = 0; guard <= RG_LEVELS; guard++) {
+            if (lv + 1 >= height) {  // c is the root: a new root [c, new]
+                if (lv >= RG_LEVELS) break;
+                LV.set(lv, simd::sel(L() == 0u, 2u, simd::splat(0)));
+                height++;
+                return;
+            }
+            u32 first;
+            const u32 pi = parent_of(lv, c, first);
+            V P = LV.get(lv);
+            const u32 nc = simd::readlane(P, pi) + 1;
+            if (nc < 8) {
+                LV.set(lv, simd::writelane(P, pi, nc));
+                return;
+            }
+            // split node pi: it keeps 4 children, a new node right after it takes 4
+            P = simd::sel(L() > pi, simd::wave_shr1(P), P);
+            P = simd::sel((L() == pi) | (L() == pi + 1), 4u, P);
+            LV.set(lv, P);
+            c = pi;
+            lv++;
+        }
+        fail(MTE_DOC_CAPACITY, curSeq);
+    }
+
+    // ---------------------------------------------------------------- block edits
+    // Blocks [from, n_lb) move to [from + d, n_lb + d); the 8*d slots this opens (d > 0) are left
+    // for the caller, the ones it frees at the end (d < 0) are zeroed.
+    SD void shift_blocks(u32 from, i32 d) {
+        if (d == 0) return;
+        const u32 n = (n_lb - from) * 8;
+        if (d > 0) {
+            mv_slots((from + (u32)d) * 8, from * 8, n);
+        } else {
+            mv_slots((from - (u32)(-d)) * 8, from * 8, n);
+            zero_slots((n_lb - (u32)(-d)) * 8, (u32)(-d) * 8);
+        }
+    }
+
+    // Insert `rec` at slot j of block k (child count cnt); a block reaching 8 children splits 4+4,
+    // the new block right after it in document order (needsScour undefined). With `upd`, slot j-1
+    // first takes (len ul, tz uz) (the left piece of a split). Returns the block holding rec.
+    SD u32 insert_slot(u32 k, u32 cnt, u32 j, const RSeg& rec, bool upd, u32 ul, u32 uz) {
+        if (cnt >= 8 || j > cnt) {
+            fail(MTE_DOC_CAPACITY, curSeq);
+            return NONE;
+        }
+        const u32 r = k >> 3, gb = gbase(k);
+        Row w = ldrow(r);
+        const V sl = L() & 7u;
+        const B ing = in_group(k);
+        const B mv = ing & (sl > j);
+        const B at = L() == gb + j;
+        const u32 ns = (simd::readlane(w.meta, gb) >> NS_SHIFT) & 3u;
+        if (upd) {
+            const B lf = L() == gb + j - 1;
+            w.len = simd::sel(lf, ul, w.len);
+            w.tz = simd::sel(lf, uz, w.tz);
+        }
+        auto put = [&](V& x, u32 val) MTE_LI {
+            x = simd::sel(mv, simd::row_shr1(x), x);
+            x = simd::sel(at, val, x);
+        };
+        put(w.len, rec.len);
+        put(w.seq, (u32)rec.seq);
+        put(w.rseq, rec.rseq);
+        put(w.meta, (rec.meta & ~NS_MASK) | (ns << NS_SHIFT));
+        put(w.toff, rec.toff);
+        put(w.tz, rec.tz);
+        put(w.sid, rec.sid);
+        strow(r, w);
+        if (cnt + 1 < 8) return k;
+        split_block(k);
+        return j < 4 ? k : k + 1;
+    }
+    // Block k holds 8 children: a new block k+1 takes slots 4..7 (mergeTree.ts:2476-2489).
+    SD void split_block(u32 k) {
+        if (n_lb + 1 > NBLK) {
+            fail(MTE_DOC_CAPACITY, curSeq);
+            return;
+        }
+        shift_blocks(k + 1, 1);
+        const u32 r = k >> 3, r2 = (k + 1) >> 3;
+        const V sl = L() & 7u;
+        const B lo = in_group(k + 1) & (sl < 4u), hi2 = in_group(k + 1) & (sl >= 4u), hi = in_group(k) & (sl >= 4u);
+        const V src = (L() + (r2 == r ? 0u : 64u) - 4u) & 63u;  // new slot s <- old slot 4+s of block k
+        Row w = ldrow(r);
+        const u32 nsk = simd::readlane(w.meta, gbase(k)) & NS_MASK;
+        Row w2 = r2 == r ? w : ldrow(r2);
+        auto mv = [&](V& x, V& y, u32 keepHi) MTE_LI {  // x: row r, y: row r2
+            const V moved = simd::bperm(x, src);
+            if (r2 == r) {
+                x = simd::sel(lo, moved, x);
+                x = simd::sel(hi2, 0u, x);
+                x = simd::sel(hi, keepHi, x);
+            } else {
+                y = simd::sel(lo, moved, simd::sel(hi2, 0u, y));
+                x = simd::sel(hi, keepHi, x);
+            }
+        };
+        mv(w.len, w2.len, 0u);
+        mv(w.seq, w2.seq, 0u);
+        mv(w.rseq, w2.rseq, 0u);
+        mv(w.meta, w2.meta, nsk);  // block k keeps its needsScour in every lane
+        mv(w.toff, w2.toff, 0u);
+        mv(w.tz, w2.tz, 0u);
+        mv(w.sid, w2.sid, 0u);
+        // the new block's needsScour is undefined
+        if (r2 == r) {
+            w.meta = simd::sel(in_group(k + 1), w.meta & ~NS_MASK, w.meta);
+            strow(r, w);
+        } else {
+            w2.meta = simd::sel(in_group(k + 1), w2.meta & ~NS_MASK, w2.meta);
+            strow(r, w);
+            strow(r2, w2);
+        }
+        n_lb++;
+        if (n_lb > max_lb) max_lb = n_lb;
+        insert_after(k, 0);
+    }
+
+    // ---------------------------------------------------------------- LRU heap (collections.ts:213-265)
+    SD u32 hkey(u32 q) const { return simd::readlane(HK.get(q >> 6), q & 63); }
+    SD u32 hsid(u32 q) const { return simd::readlane(HS.get(q >> 6), q & 63); }
+    SD void hset(u32 q, u32 sid, u32 key) {
+        HK.set(q >> 6, simd::writelane(HK.get(q >> 6), q & 63, key));
+        HS.set(q >> 6, simd::writelane(HS.get(q >> 6), q & 63, sid));
+    }
+    // push: keys are op seqs, strictly increasing across messages, so the sift-up never moves an
+    // entry (collections.ts:241-250 moves strictly larger parents only): an append
+    SD void heap_push(u32 sid, i32 key) {
+        if (heapSize + 1 >= RG_HEAP) {
+            fail(MTE_DOC_CAPACITY, curSeq);
+            return;
+        }
+        const u32 n = ++heapSize;
+        if (n == 1) heapTop = key;
+        hset(n, sid, (u32)key);
+    }
+    // pop: sift-down of collections.ts:252-264 (smaller child, left on ties, moves up while
+    // strictly below the moved last entry)
+    SD u32 heap_pop() {
+        const u32 n = heapSize, m = n - 1;
+        const u32 top = hsid(1);
+        const u32 lk = hkey(n), ls = hsid(n);
+        i32 newTop = (i32)lk;
+        u32 k = 1;
+        while ((k << 1) <= m) {
+            u32 j = k << 1;
+            u32 kj = hkey(j);
+            if (j < m) {
+                const u32 kj1 = hkey(j + 1);
+                if ((i32)kj - (i32)kj1 > 0) {
+                    j++;
+                    kj = kj1;
+                }
+            }
+            if ((i32)lk - (i32)kj <= 0) break;
+            if (k == 1) newTop = (i32)kj;
+            hset(k, hsid(j), kj);
+            k = j;
+        }
+        if (m >= 1) hset(k, ls, lk);
+        heapTop = newTop;
+        heapSize = m;
+        return top;
+    }
+    // addToLRUSet (mergeTree.ts:1273-1283) for a segment of block k
+    SD void add_lru(u32 k, u32 sid, i32 seq) {
+        if (ns_get(k) != SC_TRUE && seq > curSeq) {
+            ns_set(k, SC_TRUE);
+            heap_push(sid, seq);
+        }
+    }
+    // the leaf block holding segment sid (segment.parent), NONE when unlinked
+    SD u32 find_seg(u32 sid) const {
+        const u32 nrows = (n_lb + 7) >> 3;
+        for (u32 r = 0; r < nrows; r++) {
+            const u64 m = simd::ballot((ld_sid(r) == sid) & (ld_len(r) != 0u));
+            if (m) return r * 8 + ((u32)__builtin_ctzll(m) >> 3);
+        }
+        return NONE;
+    }
+
+    // ---------------------------------------------------------------- text (HBM)
+    SD u16* arena_cur() const { return arena0 + (u64)arenaSel * arena_cap; }
+    SD void fence_arena() {
+        if (adirty) {
+            simd::wave_fence();
+            adirty = false;
+        }
+    }
+    // copy n units from text offset src (payload or arena) to offset dst of dbase (lanes in parallel)
+    SD void copy_text(u32 dst, u32 src, u32 n, u16* dbase) {
+        const u16* sb = (src & ARENA_BIT) ? arena_cur() : payload;
+        const u32 so = src & ~ARENA_BIT, d0 = dst & ~ARENA_BIT;
+        for (u32 b = 0; b < n; b += 64) {
+            const V i = L() + b;
+            const B m = i < n;
+            const V t = simd::ld(sb, i + so, m);
+            simd::st(dbase, i + d0, t, m);
+        }
+    }
+    // Semispace compaction of the merge arena: every live arena-resident text, document order.
+    SD void arena_gc() {
+        fence_arena();
+        const u32 other = arenaSel ^ 1u;
+        u16* dst = arena0 + (u64)other * arena_cap;
+        u32 top = 0;
+        for (u32 k = 0; k < n_lb; k++) {
+            const u32 r = k >> 3, gb = gbase(k);
+            Row w = ldrow(r);
+            const u32 cnt = (u32)__builtin_popcount(group_bits(simd::ballot(w.len != 0u), k));
+            bool dirty = false;
+            for (u32 s = 0; s < cnt; s++) {
+                const u32 l = gb + s;
+                const u32 meta = simd::readlane(w.meta, l), toff = simd::readlane(w.toff, l);
+                if ((meta & F_MARKER) || !(toff & ARENA_BIT)) continue;
+                const u32 len = simd::readlane(w.len, l), tz = simd::readlane(w.tz, l);
+                const bool rm = simd::readlane(w.rseq, l) != RSEQ_LIVE;  // tz is the overlap mask then
+                const u32 cap = (rm || tz < len) ? len : tz;
+                if ((toff & ~ARENA_BIT) + len > arena_cap || top + cap > arena_cap) {
+                    fail(MTE_DOC_CAPACITY, curSeq);
+                    return;
+                }
+                copy_text(top, toff, len, dst);
+                w.toff = simd::writelane(w.toff, l, top | ARENA_BIT);
+                if (!rm) w.tz = simd::writelane(w.tz, l, cap);
+                dirty = true;
+                top += cap;
+            }
+            if (dirty) strow(r, w);
+        }
+        simd::wave_fence();
+        arenaSel = other;
+        arenaTop = top;
+        n_gc++;
+    }
+
+    // ---------------------------------------------------------------- zamboni (mergeTree.ts:1289-1478)
+    // scourNode on block k (cnt children): tombstones at or below the MSN are dropped and reset the
+    // merge chain, settled live text appends to the chain head under TextSegment.canAppend
+    // (textSegment.ts:63-85; no '\n' in these documents, no properties); kept slots are compacted.
+    // Returns the new child count.
+    SD u32 scour(u32 k, u32 cnt) {
+        if (cnt > 8) cnt = 8;
+        fence_arena();
+        const u32 r = k >> 3, gb = gbase(k);
+        const B ing = in_group(k);
+        Row w = ldrow(r);
+        const B act = ing & (w.len != 0u);
+        const B rem = act & (w.rseq != RSEQ_LIVE);
+        const u32 mREM = group_bits(simd::ballot(rem), k);
+        const u32 mKEPT = group_bits(simd::ballot(rem & simd::sgt(w.rseq, minSeq)), k);
+        const u32 mSET = group_bits(simd::ballot(simd::andn(act, rem) & simd::sle(w.seq, minSeq)), k);
+        if (!(mREM & ~mKEPT) && !(mSET & (mSET << 1))) return cnt;  // nothing dropped, nothing to merge
+        const u32 mTXT = group_bits(simd::ballot(act & ((w.meta & F_MARKER) == 0u)), k);
+        u32 nkeep = 0, jn = 0;
+        V kSrc = simd::splat(0), kLen = kSrc, kOff = kSrc, kCap = kSrc;  // lane i: kept slot i
+        V jdst = kSrc, jsrc = kSrc, jlen = kSrc;                          // lane j: copy job j
+        for (u32 attempt = 0; attempt < 2; attempt++) {
+            nkeep = jn = 0;
+            jdst = jsrc = jlen = simd::splat(0);
+            u32 top = arenaTop, need = 0;
+            i32 prev = -1;
+            u32 pLen = 0, pOff = 0, pCap = 0, pMat = 0;
+            bool pText = false, pFresh = false;
+            auto job = [&](u32 d, u32 s, u32 n) MTE_LI {
+                if (jn < 64) {
+                    jdst = simd::writelane(jdst, jn, d);
+                    jsrc = simd::writelane(jsrc, jn, s);
+                    jlen = simd::writelane(jlen, jn, n);
+                }
+                jn++;
+            };
+            for (u32 s = 0; s < cnt; s++) {
+                const u32 bit = 1u << s;
+                bool keep = true;
+                if (mREM & bit) {
+                    keep = (mKEPT & bit) != 0;
+                    prev = -1;
+                } else if (mSET & bit) {
+                    const u32 ln = simd::readlane(w.len, gb + s), to = simd::readlane(w.toff, gb + s);
+                    const u32 tc = simd::readlane(w.tz, gb + s);
+                    const bool ok = prev >= 0 && pText && (mTXT & bit) && (pLen <= (u32)GRANULARITY || ln <= (u32)GRANULARITY);
+                    if (ok) {  // TextSegment.append
+                        if ((pOff & ARENA_BIT) && pLen + ln <= pCap) {
+                            job(pOff + pLen, to, ln);
+                        } else if (pOff + pLen == to && pMat == pLen) {  // text already contiguous
+                            if (pOff & ARENA_BIT) pCap = to + tc - pOff;
+                            pMat += ln;
+                        } else {
+                            u32 ncap = 2 * (pLen + ln);
+                            if (ncap < 32) ncap = 32;
+                            const u32 dst = top | ARENA_BIT;
+                            top += ncap;
+                            need += ncap;
+                            // pending jobs into the head's chunk follow it to the new one; the
+                            // materialised prefix (none for a chunk built by this batch) is copied
+                            const u32 m0 = pFresh ? 0u : pMat;
+                            const B mvj = (L() < jn) & (jdst >= pOff + m0) & (jdst < pOff + pLen);
+                            jdst = simd::sel(mvj, jdst - pOff + dst, jdst);
+                            if (m0) job(dst, pOff, m0);
+                            job(dst + pLen, to, ln);
+                            pOff = dst;
+                            pCap = ncap;
+                            pFresh = true;
+                        }
+                        pLen += ln;
+                        kLen = simd::writelane(kLen, (u32)prev, pLen);
+                        kOff = simd::writelane(kOff, (u32)prev, pOff);
+                        kCap = simd::writelane(kCap, (u32)prev, pCap);
+                        keep = false;
+                    } else {
+                        prev = (i32)nkeep;
+                        pLen = ln;
+                        pMat = ln;
+                        pOff = to;
+                        pCap = tc;
+                        pText = (mTXT & bit) != 0;
+                        pFresh = false;
+                    }
+                } else {
+                    prev = -1;
+                }
+                if (keep) {
+                    kSrc = simd::writelane(kSrc, nkeep, s);
+                    kLen = simd::writelane(kLen, nkeep, simd::readlane(w.len, gb + s));
+                    kOff = simd::writelane(kOff, nkeep, simd::readlane(w.toff, gb + s));
+                    kCap = simd::writelane(kCap, nkeep, simd::readlane(w.tz, gb + s));
+                    nkeep++;
+                }
+            }
+            if (nkeep == cnt) return cnt;
+            if (arenaTop + need <= arena_cap && jn <= 64) {
+                arenaTop = top;
+                break;
+            }
+            if (attempt == 1) {
+                fail(MTE_DOC_CAPACITY, curSeq);
+                return cnt;
+            }
+            arena_gc();  // moves every arena text: re-read the slots and redo the chain
+            if (status) return cnt;
+            w = ldrow(r);
+        }
+        if (jn) run_jobs(jn, jdst, jsrc, jlen);
+        // compaction: group lane gb+i takes kept slot i
+        const V sl = L() & 7u;
+        const B kp = ing & (sl < nkeep);
+        const V src = simd::bperm(kSrc, sl) + gb;
+        auto cmp = [&](V& x, const V* over, u32 keepEmpty) MTE_LI {  // empty lanes keep only `keepEmpty` bits
+            const V nv = over ? simd::bperm(*over, sl) : simd::bperm(x, src);
+            x = simd::sel(kp, nv, simd::sel(ing, x & keepEmpty, x));
+        };
+        cmp(w.len, &kLen, 0u);
+        cmp(w.toff, &kOff, 0u);
+        cmp(w.tz, &kCap, 0u);
+        cmp(w.seq, nullptr, 0u);
+        cmp(w.rseq, nullptr, 0u);
+        cmp(w.meta, nullptr, NS_MASK);  // the block's needsScour stays in every lane
+        cmp(w.sid, nullptr, 0u);
+        strow(r, w);
+        return nkeep;
+    }
+    // The recorded copies as one flattened gather (sources are never destinations of one scour).
+    SD void run_jobs(u32 jn, V jdst, V jsrc, V jlen) {
+        const V jl = simd::sel(L() < jn, jlen, 0u);
+        const V jinc = simd::scan_incl(jl);
+        const u32 total = simd::readlane(jinc, 63);
+        const V jstart = jinc - jl;
+        u16* ar = arena_cur();
+        for (u32 base = 0; base < total; base += 64) {
+            const V f = L() + base;
+            V j = simd::splat(0);
+            for (u32 q = 1; q < jn; q++) j = simd::sel(f >= simd::readlane(jstart, q), q, j);
+            const V s0 = simd::bperm(jstart, j), d = simd::bperm(jdst, j), sr = simd::bperm(jsrc, j);
+            const B m = f < total;
+            const V o = f - s0;
+            const B fa = (sr & ARENA_BIT) != 0u;
+            const V so = (sr & ~ARENA_BIT) + o;
+            const V t = simd::sel(fa, simd::ld(ar, so, m & fa), simd::ld(payload, so, simd::andn(m, fa)));
+            simd::st(ar, (d & ~ARENA_BIT) + o, t, m);
+        }
+        adirty = true;
+    }
+
+    // pack (mergeTree.ts:1368-1420), leaf level: the m children [k0, k0+m) of level-1 node pi
+    // (already re-scoured; lane i of cn = child i's count) become max(1, min(7, T/4)) fresh blocks.
+    SD void pack_leaves(u32 pi, u32 m, u32 k0, V cn) {
+        const u32 T = simd::readlane(simd::scan_incl(simd::sel(L() < m, cn, 0u)), 63);
+        u32 kk = T / 4;
+        if (kk > 7) kk = 7;
+        if (kk < 1) kk = 1;
+        const u32 base = T / kk, extra = T % kk;
+        if (n_lb + kk > NBLK + m) {
+            fail(MTE_DOC_CAPACITY, curSeq);
+            return;
+        }
+        // item t (lane t < T) of the concatenated children: block k0 + sib, slot q
+        V sib = simd::splat(0), q = L();
+        for (u32 i = 0; i < m; i++) {
+            const u32 n = simd::readlane(cn, i);
+            const B adv = (q >= n) & (sib == i);
+            q = simd::sel(adv, q - n, q);
+            sib = simd::sel(adv, i + 1, sib);
+        }
+        const V sg = (sib + k0) * 8u + q;  // source slot (global)
+        const u32 r0 = k0 >> 3, r1 = r0 + 1 < (u32)NR ? r0 + 1 : r0;
+        const B inr0 = (sg >> 6) == r0;
+        Row a = ldrow(r0), b = ldrow(r1);
+        auto gather = [&](const V& x0, const V& x1) MTE_LI {
+            return simd::sel(inr0, simd::bperm(x0, sg & 63u), simd::bperm(x1, sg & 63u));
+        };
+        Row t;
+        t.len = gather(a.len, b.len);
+        t.seq = gather(a.seq, b.seq);
+        t.rseq = gather(a.rseq, b.rseq);
+        t.meta = gather(a.meta, b.meta) & ~NS_MASK;  // packed blocks: needsScour undefined
+        t.toff = gather(a.toff, b.toff);
+        t.tz = gather(a.tz, b.tz);
+        t.sid = gather(a.sid, b.sid);
+        const i32 d = (i32)kk - (i32)m;
+        shift_blocks(k0 + m, d);
+        // destination: block k0 + dj slot dq <- item dj*base + min(dj, extra) + dq
+        const u32 rA = k0 >> 3, rB = (k0 + kk - 1) >> 3;
+        for (u32 rr = rA; rr <= rB; rr++) {
+            const V G = L() + rr * 64;
+            const V blk = G >> 3;
+            const B inb = (blk >= k0) & (blk < k0 + kk);
+            const V dj = blk - k0, dq = G & 7u;
+            const V big = simd::sel(dj < extra, dj, simd::splat(extra));
+            const V nB = simd::sel(dj < extra, base + 1, simd::splat(base));
+            const B have = inb & (dq < nB);
+            const V ti = (dj * base + big + dq) & 63u;
+            Row w = ldrow(rr);
+            auto put = [&](V& x, const V& tv) MTE_LI { x = simd::sel(have, simd::bperm(tv, ti), simd::sel(inb, 0u, x)); };
+            put(w.len, t.len);
+            put(w.seq, t.seq);
+            put(w.rseq, t.rseq);
+            put(w.meta, t.meta);
+            put(w.toff, t.toff);
+            put(w.tz, t.tz);
+            put(w.sid, t.sid);
+            strow(rr, w);
+        }
+        n_lb = (u32)((i32)n_lb + d);
+        if (n_lb > max_lb) max_lb = n_lb;
+        LV.set(0, simd::writelane(LV.get(0), pi, kk));
+        if (kk < 4 && height > 2) pack_internal(pi, 1);
+    }
+    // pack on an interior level: node pi of level lv underflowed; the children of its parent are
+    // redistributed into max(1, min(7, T/4)) nodes, T their total child count.
+    SD void pack_internal(u32 pi, u32 lv) {
+        for (u32 guard = 0; guard < RG_LEVELS + 2; guard++) {
+            u32 i0;
+            const u32 qi = parent_of(lv, pi, i0);  // parent at level lv+1
+            const V Q = LV.get(lv);
+            const u32 m = simd::readlane(Q, qi);
+            V C = LV.get(lv - 1);  // child counts of the level-lv nodes
+            const u32 T = simd::readlane(simd::scan_incl(simd::sel((L() >= i0) & (L() < i0 + m), C, 0u)), 63);
+            u32 kk = T / 4;
+            if (kk > 7) kk = 7;
+            if (kk < 1) kk = 1;
+            const u32 base = T / kk, extra = T % kk;
+            const i32 d = (i32)kk - (i32)m;
+            // lanes after the old range move by d
+            const V src = L() - (u32)d;
+            const V moved = simd::bperm(C, src & 63u);
+            C = simd::sel(L() >= i0 + kk, simd::sel(src < 64u, moved, 0u), C);
+            const V dj = L() - i0;
+            C = simd::sel((L() >= i0) & (L() < i0 + kk), simd::sel(dj < extra, base + 1, simd::splat(base)), C);
+            LV.set(lv - 1, C);
+            LV.set(lv, simd::writelane(Q, qi, kk));
+            if (kk < 4 && lv + 2 < height) {
+                pi = qi;
+                lv++;
+                continue;
+            }
+            return;
+        }
+        fail(MTE_DOC_CAPACITY, curSeq);
+    }
+
+    // zamboniSegments (mergeTree.ts:1422-1478): up to 2 heap entries with maxSeq <= minSeq.
+    SD void zamboni() {
+        for (int i = 0; i < 2 && !status; i++) {
+            if (heapSize == 0 || heapTop > minSeq) break;
+            const u32 sid = heap_pop();
+            const u32 k = find_seg(sid);
+            if (k == NONE) continue;  // no longer linked
+            if (ns_get(k) == SC_FALSE) continue;
+            const u32 cnt = count(k);
+            const u32 nc = scour(k, cnt);
+            if (status) return;
+            ns_set(k, SC_FALSE);
+            if (!(nc < cnt && nc < 4 && height > 1)) continue;
+            u32 k0;
+            const u32 pi = parent_of(0, k, k0);
+            const u32 m = simd::readlane(LV.get(0), pi);
+            if (m == 0 || m > 8 || k0 + m > n_lb) {
+                fail(MTE_DOC_CAPACITY, curSeq);
+                return;
+            }
+            V cn = simd::splat(0);
+            for (u32 idx = 0; idx < m; idx++) {
+                const u32 c = scour(k0 + idx, count(k0 + idx));
+                if (status) return;
+                cn = simd::writelane(cn, idx, c);
+            }
+            pack_leaves(pi, m, k0, cn);
+        }
+    }
+
+    // ---------------------------------------------------------------- ops
+    // ensureIntervalBoundary at the resolved slot (BaseSegment.splitAt, mergeTree.ts:524-568): the
+    // right piece copies everything and follows the left one. Returns the insert_slot result.
+    SD u32 split_at(const RFound& f) {
+        const u32 r = f.k >> 3, l = gbase(f.k) + (u32)f.slot;
+        const Row w = ldrow(r);
+        RSeg t;
+        t.len = simd::readlane(w.len, l);
+        t.seq = (i32)simd::readlane(w.seq, l);
+        t.rseq = simd::readlane(w.rseq, l);
+        t.meta = simd::readlane(w.meta, l);
+        t.toff = simd::readlane(w.toff, l);
+        t.tz = simd::readlane(w.tz, l);
+        const u32 sid = new_sid();
+        if (sid == NONE) return NONE;
+        const u32 rr = (u32)f.r;
+        const bool rm = t.rseq != RSEQ_LIVE;  // tz is the overlap mask then
+        const bool ar = (t.toff & ARENA_BIT) != 0;
+        const u32 lz = rm ? t.tz : (ar ? rr : 0u);
+        RSeg right = t;
+        right.len = t.len - rr;
+        right.toff = t.toff + rr;
+        right.tz = rm ? t.tz : (ar ? t.tz - rr : 0u);
+        right.sid = sid;
+        return insert_slot(f.k, f.cnt, (u32)f.slot + 1, right, true, rr, lz);
+    }
+
+    // insertSegments (mergeTree.ts:1968-1998): split at pos, then place the new segment.
+    SD bool op_insert(i32 pos, i32 R, u32 C, i32 seq, RSeg rec) {
+        RFound f = resolve(pos, R, C);
+        if (!f.ok) {
+            fail(MTE_DOC_INSERT_FAILED, seq);
+            return false;
+        }
+        u32 k = f.k, j;
+        if (f.slot >= 0 && f.r > 0) {
+            if (split_at(f) == NONE || status) return false;
+            // the insertion point follows from the split: before the right piece, except when the
+            // block split 4+4 right between the two pieces (blocks win ties: append to the left)
+            const u32 s = (u32)f.slot;
+            if (f.cnt + 1 < 8 || s + 1 < 4) {
+                j = s + 1;
+                f.cnt = f.cnt + 1 < 8 ? f.cnt + 1 : 4;
+            } else if (s == 3) {
+                j = 4;
+                f.cnt = 4;
+            } else {
+                k = f.k + 1;
+                j = s - 3;
+                f.cnt = 4;
+            }
+        } else {
+            j = f.slot >= 0 ? (u32)f.slot : f.cnt;
+        }
+        if (rec.len == 0) return false;  // blockInsert skips empty segments (:2196)
+        rec.sid = new_sid();
+        if (rec.sid == NONE) return false;
+        const u32 b = insert_slot(k, f.cnt, j, rec, false, 0, 0);
+        if (status) return false;
+        if (seq > minSeq) add_lru(b, rec.sid, seq);
+        return status == 0;
+    }
+
+    // markRangeRemoved (mergeTree.ts:2607-2719): split at p1 and p2, then mark [p1, p2) of the
+    // (R, C) view before the op: first remover wins, later ones join removedClientOverlap.
+    SD bool op_remove(i32 p1, i32 p2, i32 R, u32 C, i32 seq) {
+        for (u32 ph = 0; ph < 2; ph++) {
+            const RFound f = resolve(ph ? p2 : p1, R, C);
+            if (!f.ok || !(f.slot >= 0 && f.r > 0)) continue;
+            if (split_at(f) == NONE || status) return false;
+        }
+        const u32 nrows = (n_lb + 7) >> 3;
+        u32 carry = 0;
+        const u32 cbit = 1u << C;
+        for (u32 r = 0; r < nrows && (i32)carry < p2; r++) {
+            Row w = ldrow(r);
+            const V v = vis(r, w.len, w.seq, w.rseq, w.meta, R, C);
+            const V incl = simd::scan_incl(v) + carry;
+            const V ex = incl - v;
+            const B mark = (v != 0u) & simd::slt(ex, p2) & simd::sgt(incl, p1);
+            carry = simd::readlane(incl, 63);
+            const u64 mm = simd::ballot(mark);
+            if (!mm) continue;
+            const B was = mark & (w.rseq != RSEQ_LIVE);  // already removed: addOverlappingClient
+            const B fresh = simd::andn(mark, was);
+            // the overlap mask starts empty at the first removal (tz is dead then), so it is written
+            // only when a client joins it
+            if (simd::ballot(was)) w.tz = simd::sel(was, simd::sel((w.meta & F_OVL) != 0u, w.tz | cbit, simd::splat(cbit)), w.tz);
+            w.meta = simd::sel(was, w.meta | F_OVL, simd::sel(fresh, (w.meta & ~0xFF00u) | (C << 8) | F_REMOVED, w.meta));
+            w.rseq = simd::sel(fresh, (u32)seq, w.rseq);
+            strow(r, w);
+            // addToLRUSet per block, document order: the first marked slot of each block
+            for (u64 gm = mm; gm;) {
+                const u32 l = (u32)__builtin_ctzll(gm);
+                const u32 g = l >> 3;
+                gm &= ~(0xFFull << (g * 8));
+                add_lru(r * 8 + g, simd::readlane(w.sid, l), seq);
+                if (status) return false;
+            }
+        }
+        return status == 0;
+    }
+
+    // Room for one more op (margins for the splits, packs and heap pushes an op can cause);
+    // false => hand the document to the LDS engine before this op.
+    SD bool room() const {
+        const u32 lim = p.reg_lb_limit && p.reg_lb_limit < NBLK ? p.reg_lb_limit : NBLK;
+        return n_lb + 16 <= lim && heapSize + n_lb + 8 < RG_HEAP && height + 2 <= RG_LEVELS &&
+               simd::readlane(LV.get(0), 56) == 0u;
+    }
+
+    // Client.applyMsg for one op record (client.ts:805-836); false => not applied, hand off.
+    SD bool apply(const mte_op& op) {
+        const u32 type = op.type;
+        const bool ins = type == MTE_OP_INSERT || type == MTE_OP_INSERT_MARKER;
+        if (!(ins || type == MTE_OP_REMOVE || type == MTE_OP_NOOP)) return false;
+        // (MTE_F_CATCHUP only asks for delta records, which only a legacy-format replay reads: that one
+        // runs the EXT kernels, so here the flag is ignored like the lean LDS kernels do)
+        if ((op.flags & (MTE_F_REL | MTE_F_PERM)) || op.props) return false;
+        if (type != MTE_OP_NOOP && (op.client == 0 || op.client >= 32)) return false;
+        if (!room()) return false;
+        const u32 C = op.client;
+        const i32 seq = op.seq, R = op.ref_seq;
+        if (type != MTE_OP_NOOP && !(curSeq < seq)) {
+            fail(MTE_DOC_SEQ_ORDER, seq);
+            return true;
+        }
+        bool edited = false;
+        if (ins) {
+            RSeg rec;
+            const bool mk = type == MTE_OP_INSERT_MARKER;
+            rec.len = mk ? 1u : op.b;
+            rec.seq = seq;
+            rec.rseq = RSEQ_LIVE;
+            rec.meta = (C & 0xFFu) | (RCL_LIVE << 8) | (mk ? F_MARKER : 0u);
+            rec.toff = mk ? op.b : (u32)op.a;
+            rec.tz = 0;
+            rec.sid = 0;
+            edited = op_insert(op.pos1, R, C, seq, rec);
+            n_ops++;
+        } else if (type == MTE_OP_REMOVE) {
+            edited = op_remove(op.pos1, op.a, R, C, seq);
+            n_ops++;
+        }
+        if (status) return true;
+        if (edited) zamboni();
+        if (status) return true;
+        if (op.flags & MTE_F_END_OF_MSG) {
+            n_msgs++;
+            if (op.seq < curSeq || op.msn > op.seq || op.msn < minSeq) {
+                fail(MTE_DOC_SEQ_ORDER, op.seq);
+                return true;
+            }
+            curSeq = op.seq;
+            if (op.msn > minSeq) {
+                minSeq = op.msn;
+                zamboni();
+            }
+        }
+        return true;
+    }
+
+    // Replay ops [i, e): returns the first op not applied (e when done or failed; earlier when the
+    // document hands over to the LDS engine). Records are prefetched 8 per VGPR (lane 8*r + w holds
+    // word w of record r), four chunks ahead.
+    SD u64 replay(u64 i, u64 e) {
+        if (!p.docs[doc].collab) {  // local, non-collaborative edits: the LDS engine's path
+            status = REG_HANDOFF;
+            return i;
+        }
+        const u32* src = (const u32*)p.ops;
+        simd::VA<4> Q;
+        const u64 b = i;
+        auto load_chunk = [&](u64 c0) MTE_LI {  // records [c0, c0+8)
+            const u64 left = e > c0 ? e - c0 : 0;
+            const u32 nw = left >= 8 ? 64u : (u32)left * 8u;
+            return simd::ld(src + c0 * 8, L(), L() < nw);
+        };
+        for (u32 c = 0; c < 4; c++) Q.set(c, load_chunk(b + (u64)c * 8));
+        for (; i < e && !status; i++) {
+            const u32 r = (u32)((i - b) & 7);
+            if (r == 0 && i != b) {
+                Q.set(0, Q.get(1));
+                Q.set(1, Q.get(2));
+                Q.set(2, Q.get(3));
+                Q.set(3, load_chunk(i + 24));
+            }
+            const V q = Q.get(0);
+            u32 w[8];
+            for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(q, r * 8 + x);
+            mte_op op;
+            __builtin_memcpy(&op, w, sizeof op);
+            if (!apply(op)) {
+                status = REG_HANDOFF;
+                return i;
+            }
+        }
+        return i;
+    }
+
+    // ---------------------------------------------------------------- results
+    // The final segments in document order (walkAllSegments, mergeTree.ts:2969-2983) in the LDS
+    // engine's row format (removedSeq 0 and removedClient 0 for live segments), text gathered into
+    // the document's run of the output text pool, and the per-document result record.
+    SD u32 atomic_reserve(u32* ctr, u32 n) const {
+#ifdef MTE_CPU
+        const u32 o = *ctr;
+        *ctr += n;
+        return o;
+#else
+        u32 o = 0;
+        if (simd::lane0()) o = atomicAdd(ctr, n);
+        return __builtin_amdgcn_readfirstlane(o);
+#endif
+    }
+    SD u64 atomic_reserve64(u64* ctr, u64 n) const {
+#ifdef MTE_CPU
+        const u64 o = *ctr;
+        *ctr += n;
+        return o;
+#else
+        u64 o = 0;
+        if (simd::lane0()) o = atomicAdd((unsigned long long*)ctr, (unsigned long long)n);
+        const u32 lo = __builtin_amdgcn_readfirstlane((u32)o), hi = __builtin_amdgcn_readfirstlane((u32)(o >> 32));
+        return ((u64)hi << 32) | lo;
+#endif
+    }
+    SD void finish() {
+        fence_arena();
+        const u32 nrows = (n_lb + 7) >> 3;
+        u32 nseg = 0, ntext = 0;
+        for (u32 r = 0; r < nrows; r++) {
+            const V len = ld_len(r);
+            const B txt = (len != 0u) & ((ld_meta(r) & F_MARKER) == 0u);
+            nseg += (u32)__builtin_popcountll(simd::ballot(len != 0u));
+            ntext += simd::readlane(simd::scan_incl(simd::sel(txt, len, 0u)), 63);
+        }
+        u32 off = 0, toff = 0;
+        if (status == 0) {
+            off = atomic_reserve(&p.counters[1], nseg);
+            toff = (u32)atomic_reserve64((u64*)&p.counters[6], ntext);
+            if ((u64)off + nseg > p.out_cap || (u64)toff + ntext > p.out_text_cap) {
+                fail(MTE_DOC_CAPACITY, curSeq);
+                nseg = 0;
+            }
+        } else {
+            nseg = 0;
+        }
+        if (nseg) {
+            u32 run = off, trun = 0;
+            u16* tdst = p.out_text + toff;
+            u32* ov = (u32*)p.out_vis;
+            u32* oa = (u32*)p.out_aux;
+            u32* oo = (u32*)p.out_ovl;
+            for (u32 r = 0; r < nrows; r++) {
+                const Row w = ldrow(r);
+                const B have = w.len != 0u;
+                const B txt = have & ((w.meta & F_MARKER) == 0u);
+                const V one = simd::sel(have, 1u, simd::splat(0));
+                const V at = simd::scan_incl(one) - one + run;
+                const V tl = simd::sel(txt, w.len, 0u);
+                const V tat = simd::scan_incl(tl) - tl + trun;
+                const B live = w.rseq == RSEQ_LIVE;
+                const B hasov = (w.meta & F_OVL) != 0u;
+                const V m2 = simd::sel(live, w.meta & ~0xFF00u, w.meta) & ~NS_MASK;
+                const V ovl = simd::sel(hasov, w.tz, 0u);
+                const V z2 = simd::sel(simd::andn(~live, hasov), 0u, w.tz);  // removed, no overlap: empty mask
+                const V t4 = at * 4u;
+                simd::st(ov, t4, w.len, have);
+                simd::st(ov, t4 + 1u, w.seq, have);
+                simd::st(ov, t4 + 2u, simd::sel(live, 0u, w.rseq), have);
+                simd::st(ov, t4 + 3u, m2, have);
+                simd::st(oa, t4, simd::splat(0), have);
+                simd::st(oa, t4 + 1u, simd::sel(txt, tat, w.toff), have);
+                simd::st(oa, t4 + 2u, z2, have);
+                simd::st(oa, t4 + 3u, w.sid, have);
+                simd::st(oo, at * 2u, ovl, have);
+                simd::st(oo, at * 2u + 1u, simd::splat(0), have);
+                // text, one segment at a time, 64 units per step
+                for (u64 tm = simd::ballot(txt); tm; tm &= tm - 1) {
+                    const u32 l = (u32)__builtin_ctzll(tm);
+                    copy_text(simd::readlane(tat, l), simd::readlane(w.toff, l), simd::readlane(w.len, l), tdst);
+                }
+                run += (u32)__builtin_popcountll(simd::ballot(have));
+                trun += simd::readlane(simd::scan_incl(tl), 63);
+            }
+        }
+        DocRes& o = p.res[doc];
+        if (simd::lane0()) {
+            o.status = status;
+            o.failing_seq = status ? failSeq : -1;
+            o.ops = n_ops;
+            o.msgs = n_msgs;
+            o.min_seq = minSeq;
+            o.cur_seq = curSeq;
+            o.height = height;
+            o.n_lb = n_lb;
+            o.arena_sel = arenaSel;
+            o.arena_top = arenaTop;
+            o.map_next = 1;
+            o.seg_next = segNext;
+            o.heap_size = heapSize;
+            o.n_gc = n_gc;
+            o.out_off = off;
+            o.n_segs = nseg;
+            o.text_off = toff;
+            o.max_lb = max_lb;
+            o.cu_n = 0;
+            o.mode = 4;  // solo, row-vectorised engine
+            o.spill_why = 0;
+        }
+    }
+};
+
+}  // namespace mte

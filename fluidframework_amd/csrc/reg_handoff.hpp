@@ -1,0 +1,131 @@
+// reg_handoff.hpp — hand a document from the register-resident engine (reg_engine.hpp) to the
+// LDS-resident solo engine (engine.hpp, Engine<true, true, LVL>) between two ops.
+//
+// The register engine keeps leaf blocks in document order and the interior levels as child-count
+// vectors; the LDS engine keeps blocks and interior nodes by id with parent pointers and a doc-order
+// block list. The handoff assigns ids in document order (leaf block k -> id k; interior nodes level by
+// level), writes every slot, block summary, interior node and heap entry, and copies the replay state
+// and per-document counters. Taken only when a document outgrows the register plan or reaches an op
+// the register engine does not implement (reg_engine.hpp apply()), so it is built for clarity, not speed.
+#pragma once
+#include "engine.hpp"
+#include "reg_engine.hpp"
+
+namespace mte {
+
+template <class E, class R>
+MTE_DEV void reg_handoff(R& r, E& e) {
+    using simd::V;
+    const u32 L = lane_id();
+    const u32 nrows = (r.n_lb + 7) >> 3;
+    // interior node ids: level i (1..height-1) nodes get ids base[i] .. base[i] + n[i] - 1
+    const u32 H = r.height;
+    u32 base[RG_LEVELS + 2], nn[RG_LEVELS + 2];
+    u32 tot = 0;
+    for (u32 i = 1; i < H; i++) {
+        nn[i] = i == H - 1 ? 1u : simd::readlane(simd::scan_incl(r.LV.get(i)), 63);
+        base[i] = tot;
+        tot += nn[i];
+    }
+    // leaf block summaries and metadata (parent | needsScour << 30)
+    u32 node = 0, left = H > 1 ? simd::readlane(r.LV.get(0), 0) : 0u;
+    for (u32 k = 0; k < r.n_lb; k++) {
+        if (H > 1) {
+            while (left == 0 && node + 1 < 64) left = simd::readlane(r.LV.get(0), ++node);
+            left--;
+        }
+        const u32 rr = k >> 3, gb = (k & 7) * 8;
+        const auto w = r.ldrow(rr);
+        u32 olen = 0, cnt = 0;
+        i32 mx = 0;
+        for (u32 s = 0; s < 8; s++) {
+            const u32 len = simd::readlane(w.len, gb + s);
+            if (!len) continue;
+            const i32 seq = (i32)simd::readlane(w.seq, gb + s);
+            const u32 rseq = simd::readlane(w.rseq, gb + s);
+            const bool live = rseq == RSEQ_LIVE;
+            cnt++;
+            olen += live ? len : 0u;
+            const i32 hi = !live && (i32)rseq > seq ? (i32)rseq : seq;
+            if (cnt == 1 || hi > mx) mx = hi;
+        }
+        const u32 par = H > 1 ? base[1] + node : BM_NOPAR;
+        if (L == 0) {
+            e.ORD()[k] = make_uint4(k, olen, (u32)mx, cnt);
+            e.BMETA()[k] = (par & BM_PAR) | (((simd::readlane(w.meta, gb) >> NS_SHIFT) & 3u) << 30);
+        }
+    }
+    // interior nodes: children, counts, parents
+    for (u32 i = 1; i < H; i++) {
+        const simd::V cntv = r.LV.get(i - 1);
+        u32 first = 0, pnode = 0, pleft = i + 1 < H ? simd::readlane(r.LV.get(i), 0) : 0u;
+        for (u32 j = 0; j < nn[i]; j++) {
+            const u32 c = simd::readlane(cntv, j);
+            const u32 id = base[i] + j;
+            u32 par = NONE;
+            if (i + 1 < H) {
+                while (pleft == 0 && pnode + 1 < 64) pleft = simd::readlane(r.LV.get(i), ++pnode);
+                pleft--;
+                par = base[i + 1] + pnode;
+            }
+            if (L < c && L < 8) e.INCH()[id * 8 + L] = i == 1 ? first + L : base[i - 1] + first + L;
+            if (L == 0) {
+                e.INCNT()[id] = c;
+                e.INPAR()[id] = par;
+            }
+            first += c;
+        }
+    }
+    // LRU heap (positions 1..heapSize)
+    for (u32 q0 = 0; q0 <= r.heapSize; q0 += 64) {
+        const u32 q = q0 + L;
+        const u32 hk = r.HK.get(q0 >> 6).x, hs = r.HS.get(q0 >> 6).x;
+        if (q >= 1 && q <= r.heapSize) e.HEAP()[q] = make_uint2(hs, hk);
+    }
+    // slots: row rr lane l is block 8*rr + l/8, slot l%8 = the LDS engine's slot index 64*rr + l,
+    // already in place; only the encoding of live segments and needsScour differ
+    lds_order();
+    for (u32 rr = 0; rr < nrows; rr++) {
+        const uint4 v = e.VIS()[64 * rr + L], a = e.AUX()[64 * rr + L];
+        const bool live = v.z == RSEQ_LIVE, ov = (v.w & F_OVL) != 0;
+        const u32 m2 = (live ? (v.w & ~0xFF00u) : v.w) & ~NS_MASK;
+        e.VIS()[64 * rr + L] = make_uint4(v.x, v.y, live ? 0u : v.z, m2);
+        e.AUX()[64 * rr + L] = make_uint4(0u, a.y, !live && !ov ? 0u : a.z, a.w);
+    }
+    // replay state and per-document counters
+    St& st = e.st;
+    st.root = H > 1 ? base[H - 1] : 0u;
+    st.height = H;
+    st.n_lb = r.n_lb;
+    st.minSeq = r.minSeq;
+    st.curSeq = r.curSeq;
+    st.heapSize = r.heapSize;
+    st.heapTop = r.heapTop;
+    st.segNext = r.segNext;
+    st.arenaTop = r.arenaTop;
+    st.arenaSel = r.arenaSel;
+    st.mapNext = 1;
+    st.lbFree = NONE;
+    st.lbBump = r.n_lb;
+    st.inFree = NONE;
+    st.inBump = tot;
+    st.inUsed = tot;
+    st.credit = 0;
+    st.status = 0;
+    st.adirty = 1;  // merge-arena text written by other lanes: fence before the next read
+    st.gdirty = 0;
+    if (L == 0) {
+        u32* S = e.STATS();
+        S[ST_OPS] = r.n_ops;
+        S[ST_MSGS] = r.n_msgs;
+        S[ST_GC] = r.n_gc;
+        S[ST_MAXLB] = r.max_lb;
+        S[ST_FAILSEQ] = NONE;
+        S[ST_APPEND] = 0;
+        S[ST_CU] = 0;
+        S[E::ST_CUOP] = 0;
+    }
+    wave_sync();  // LDS state and the arena text the register engine wrote, before the LDS engine reads
+}
+
+}  // namespace mte

@@ -1,0 +1,65 @@
+// TEST INFRASTRUCTURE ONLY: the register-resident replay engine (fluidframework_amd/csrc/reg_engine.hpp)
+// built for the CPU with the emulated wave backend (wave_simd.hpp MTE_CPU), so the CPU suite can check
+// the engine's logic against the oracle without a GPU (tests/test_reg_engine_cpu.py). The product
+// runs the device build only (k_solo); nothing in fluidframework_amd/ loads this library.
+#define MTE_CPU 1
+#include <string.h>
+
+#include <vector>
+
+#include "../../fluidframework_amd/csrc/reg_engine.hpp"
+
+using namespace mte;
+
+extern "C" {
+
+// Replays one document's op records. Outputs are the engine's own final rows (LDS-engine format:
+// vis = len, seq, removedSeq, meta; aux = props, text offset, text capacity / overlap, segment id),
+// the gathered text, and the DocRes record. Returns the op index the replay stopped at (n_ops when
+// done or failed; earlier when the document would hand over to the LDS engine).
+uint64_t regcpu_replay(const mte_op* ops, uint64_t n_ops, const uint16_t* payload, uint32_t payload_len,
+                       uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
+                       uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
+                       DocRes* res) {
+    std::vector<uint16_t> pay(payload, payload + payload_len + 1);
+    std::vector<uint16_t> arena((size_t)arena_cap * 2 + 1, 0);
+    DocCfg cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.op_begin = 0;
+    cfg.op_end = n_ops;
+    cfg.payload_len = payload_len;
+    cfg.arena_cap = arena_cap;
+    cfg.seg_cap = seg_cap;
+    cfg.collab = 1;
+    uint32_t counters[16] = {0};
+    Params p;
+    memset(&p, 0, sizeof p);
+    p.ops = (mte_op*)ops;
+    p.payload = pay.data();
+    p.docs = &cfg;
+    p.n_docs = 1;
+    p.res = res;
+    p.arena = arena.data();
+    p.out_vis = (uint4*)out_vis;
+    p.out_aux = (uint4*)out_aux;
+    p.out_ovl = out_ovl;
+    p.out_cap = out_cap;
+    p.out_text = out_text;
+    p.out_text_cap = out_text_cap;
+    p.counters = counters;
+    RegEngine<> e(p, 0);
+    const uint64_t at = e.replay(0, n_ops);
+    if (e.status == REG_HANDOFF) {
+        memset(res, 0, sizeof *res);
+        res->status = REG_HANDOFF;
+        res->n_lb = e.n_lb;
+        res->heap_size = e.heapSize;
+        res->height = e.height;
+        return at;
+    }
+    e.finish();
+    return at;
+}
+
+uint32_t regcpu_docres_size(void) { return (uint32_t)sizeof(DocRes); }
+}

@@ -33,7 +33,7 @@ def test_scaled_c4_zipf_batch_matches_oracle(engine):
     info = engine.run_info()
     assert info["solo"] >= 1 and info["lean"] == 1, info
     head = engine.doc_result(0)
-    assert head["ops"] == 250_000 and head["mode"] == 3, head  # solo, stayed LDS-resident
+    assert head["ops"] == 250_000 and head["mode"] == 4, head  # solo, row engine start to end
     bad, _, _ = compare_batch_checksums(engine, batch)
     if bad:
         compare_doc(engine, batch, bad[0])
@@ -48,7 +48,7 @@ def test_lone_long_document_solo_matches_oracle(engine):
     batch = engine.export_batch()
     engine.replay()
     r = engine.doc_result(0)
-    assert r["mode"] == 3 and r["status"] == 0, r
+    assert r["mode"] == 4 and r["status"] == 0, r  # solo, row engine
     bad, _, _ = compare_batch_checksums(engine, batch, threads=1)
     if bad:
         compare_doc(engine, batch, bad[0])

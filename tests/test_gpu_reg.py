@@ -1,0 +1,119 @@
+"""GPU: the row-vectorised solo engine (fluidframework_amd/csrc/reg_engine.hpp) that replays lean
+critical-path documents on k_solo, and its handoff to the LDS engine (reg_handoff.hpp). Every case is
+bit-exact against the oracle: checksums (text + SnapshotV1 blobs) and, for a document that differs,
+the full segment table."""
+import ctypes
+
+import pytest
+
+from fluidframework_amd import mte
+from tests.gpu_helpers import compare_batch_checksums, compare_doc
+
+pytestmark = pytest.mark.gpu
+
+MODE_ROWS = 4  # DocRes.mode: solo, replayed start to end by the row engine
+MODE_SOLO_LDS = 3  # solo, LDS engine (from the start, or after a handoff)
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = mte.Engine(0)
+    e.set_option("solo_min_ops", 1)  # one-document batches take the solo route
+    yield e
+    e.set_option("reg_lb_limit", 0)
+    e.close()
+
+
+def _check(engine, batch, n_docs=1):
+    bad, _, _ = compare_batch_checksums(engine, batch, threads=min(16, n_docs))
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad
+
+
+@pytest.mark.parametrize("kind,n_ops,clients", [(2, 1, 2), (2, 60, 3), (2, 3000, 8), (5, 3000, 8),
+                                                (2, 40_000, 8), (5, 40_000, 16), (2, 8000, 31)])
+def test_row_engine_lone_documents(engine, kind, n_ops, clients):
+    engine.set_option("reg_lb_limit", 0)
+    engine.generate(kind, 1, n_ops, n_clients=clients, seed=17)
+    batch = engine.export_batch()
+    st = engine.replay()
+    assert engine.run_info()["solo"] == 1 and engine.run_info()["lean"] == 1
+    r = engine.doc_result(0)
+    assert r["status"] == 0 and st["ops"] == n_ops, r
+    # a 31-writer document outgrows the row plan (more than 240 leaf blocks) and finishes on the LDS
+    # engine; every other one stays on the rows
+    assert r["mode"] == (MODE_SOLO_LDS if clients == 31 else MODE_ROWS), r
+    _check(engine, batch)
+
+
+@pytest.mark.parametrize("limit", [1, 20, 40])
+def test_row_engine_hands_off_mid_document(engine, limit):
+    """reg_lb_limit shrinks the row plan: the document moves to the LDS engine at op 0 (limit 1) or
+    part-way (its leaf blocks pass limit - 16) and the result is unchanged."""
+    engine.set_option("reg_lb_limit", limit)
+    try:
+        engine.generate(2, 1, 6000, n_clients=8, seed=23)
+        batch = engine.export_batch()
+        engine.replay()
+        r = engine.doc_result(0)
+        assert r["status"] == 0 and r["mode"] == MODE_SOLO_LDS, r
+        _check(engine, batch)
+    finally:
+        engine.set_option("reg_lb_limit", 0)
+
+
+def test_row_engine_off_equals_on(engine):
+    """The same documents with the row engine disabled (LDS solo engine) give the same checksums."""
+    engine.generate(5, 1, 20_000, n_clients=8, seed=29)
+    engine.replay()
+    assert engine.doc_result(0)["mode"] == MODE_ROWS
+    a = engine.summaries()["checksum"].copy()
+    engine.set_option("reg_solo", 0)
+    try:
+        engine.replay()
+        assert engine.doc_result(0)["mode"] == MODE_SOLO_LDS
+        b = engine.summaries()["checksum"].copy()
+    finally:
+        engine.set_option("reg_solo", 1)
+    assert a.tolist() == b.tolist()
+
+
+def test_row_engine_markers_and_builder_logs(engine):
+    """Marker inserts (no properties: still a lean batch) through the JSON builder, concurrent
+    writers; the row engine replays them and the segment tables equal the oracle's."""
+    import random
+
+    from tests.oplog import dumps, ins, msg, rem
+    from oracle import OracleDoc
+
+    rng = random.Random(5)
+    d = OracleDoc()
+    msgs, refs, seq = [], {c: 0 for c in "abcd"}, 0
+    order = []
+    for _ in range(3000):
+        c = rng.choice("abcd")
+        refs[c] = rng.randint(refs[c], seq)
+        if c not in order:
+            order.append(c)
+        short = order.index(c) + 1
+        L = d.length_at(refs[c], short)
+        if L == 0 or rng.random() < 0.55:
+            seg = {"marker": {"refType": rng.choice([0, 1, 2])}} if rng.random() < 0.15 else \
+                "".join(rng.choice("xyz") for _ in range(rng.randint(1, 6)))
+            contents = ins(rng.randint(0, L), seg)
+        else:
+            a = rng.randint(0, L - 1)
+            contents = rem(a, min(L, a + rng.randint(1, 9)))
+        seq += 1
+        m = msg(c, seq, refs[c], contents, min(refs.values()))
+        msgs.append(m)
+        d.apply_json(dumps([m]))
+    b = mte.Builder()
+    b.add_doc(dumps(msgs))
+    batch = b.batch()
+    engine.load(batch)
+    engine.replay()
+    assert engine.run_info()["lean"] == 1
+    assert engine.doc_result(0)["mode"] == MODE_ROWS
+    compare_doc(engine, batch, 0)

@@ -1,0 +1,93 @@
+"""CPU: the row-vectorised solo engine (fluidframework_amd/csrc/reg_engine.hpp) built with the emulated
+wave backend (tests/native/reg_cpu.cpp) against the oracle on the same op records: segment table
+(text, boundaries, seq / client / removal info, overlap sets) and observer text, bit-exact. The device
+build of the same source runs on k_solo (tests/test_gpu_reg.py)."""
+import ctypes
+import json
+import random
+
+import numpy as np
+import pytest
+
+from fluidframework_amd import mte
+from tests import regcpu
+from tests.oplog import dumps, ins, msg, rem
+
+
+@pytest.mark.parametrize("kind", [2, 5])
+@pytest.mark.parametrize("clients", [2, 3, 8, 16])
+def test_generated_documents(kind, clients):
+    for gid in range(4):
+        n = [1, 40, 900, 6000][gid]
+        ops, pay = regcpu.generated(kind, 1000 + gid, n, n_clients=clients, seed=clients)
+        regcpu.compare(ops, pay)
+
+
+def test_critical_path_document_prefix():
+    """The first 200k ops of C4's longest document (global id 111877, SURVEY §8d's Zipf head)."""
+    ops, pay = regcpu.generated(2, 111877, 200_000, n_clients=8, seed=1000)
+    r = regcpu.compare(ops, pay)
+    assert int(r["max_lb"]) <= 200 and int(r["height"]) >= 3
+
+
+@pytest.mark.parametrize("arena_cap", [1200, 3000])
+def test_arena_compaction(arena_cap):
+    """A small merge arena forces the semispace compaction (arena_gc) many times."""
+    ops, pay = regcpu.generated(2, 77, 15_000, n_clients=8, seed=3)
+    r = regcpu.compare(ops, pay, arena_cap=arena_cap)
+    assert int(r["n_gc"]) > 10
+
+
+def test_outgrows_the_rows_and_hands_off():
+    """31 concurrent writers keep hundreds of tombstones and heap entries in the collaboration window:
+    the document outgrows the row plan's margins (leaf blocks, level-1 nodes or heap) and would hand
+    off to the LDS engine between two ops (GPU only: tests/test_gpu_reg.py)."""
+    ops, pay = regcpu.generated(2, 4, 3000, n_clients=31, seed=4)
+    at, res, _, _ = regcpu.replay(ops, pay)
+    assert int(res["status"]) == regcpu.REG_HANDOFF and 0 < at < len(ops)
+    assert int(res["n_lb"]) > 100
+
+
+def _builder_ops(msgs):
+    b = mte.Builder()
+    b.add_doc(dumps(msgs))
+    batch = b.batch()
+    ops = mte.batch_ops(batch).copy()
+    n_pay = batch.doc_payload_offsets[1]
+    pay = np.ctypeslib.as_array(batch.payload, shape=(max(n_pay, 1),))[:n_pay].copy()
+    cno = batch.client_name_offsets
+    names = [ctypes.string_at(batch.client_names + cno[i], cno[i + 1] - cno[i]).decode()
+             for i in range(batch.doc_client_offsets[1])]
+    return ops, pay, names
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_markers_and_concurrent_writers_from_json(seed):
+    """Marker inserts (no properties), overlapping removes and ties from concurrent writers, through
+    the JSON builder: the engine's records path against the oracle's."""
+    from oracle import OracleDoc
+
+    rng = random.Random(seed)
+    d = OracleDoc()
+    msgs, refs, seq, order = [], {c: 0 for c in "abcde"}, 0, []
+    for _ in range(1500):
+        c = rng.choice("abcde")
+        refs[c] = rng.randint(max(refs[c], seq - 12), seq)
+        if c not in order:
+            order.append(c)
+        L = d.length_at(refs[c], order.index(c) + 1)
+        if L == 0 or rng.random() < 0.5:
+            seg = {"marker": {"refType": rng.choice([0, 1, 2])}} if rng.random() < 0.15 else \
+                "".join(rng.choice("pq") for _ in range(rng.randint(1, 5)))
+            contents = ins(rng.randint(0, L), seg)
+        else:
+            a = rng.randint(0, L - 1)
+            contents = rem(a, min(L, a + rng.randint(1, 7)))
+        seq += 1
+        m = msg(c, seq, refs[c], contents, min(refs.values()))
+        msgs.append(m)
+        d.apply_json(dumps([m]))
+    ops, pay, names = _builder_ops(msgs)
+    assert (ops["type"] == mte.MTE_OP_INSERT_MARKER).sum() > 50
+    res = regcpu.compare(ops, pay, names=names)
+    assert int(res["n_segs"]) == len(json.loads(d.segments_json()))

@@ -256,11 +256,6 @@ struct Engine {
         maps = p.maps + c.map_off * MAP_WORDS;
         collab = c.collab != 0;
         has_nl = c.has_nl != 0;
-#ifdef MTE_VCONST
-        // per-document constants held in VGPRs: the replay state needs every SGPR it can get
-        asm volatile("" : "+v"(seg_cap), "+v"(arena_cap), "+v"(payload_len), "+v"(map_cap));
-        asm volatile("" : "+v"(payload), "+v"(arena0), "+v"(ovl), "+v"(maps));
-#endif
         st.root = NONE;
         st.height = 1;
         st.n_lb = 0;
@@ -495,42 +490,6 @@ struct Engine {
     // The dirty blocks (max seq > R) are evaluated slot by slot, lane = slot: up to 8 blocks per
     // pass, lanes 8g..8g+7 holding the slots of the g-th dirty block of the batch; each block's sum
     // goes back to the lane that holds it (mbcnt rank -> bpermute from its group's last lane).
-#ifdef MTE_NEW_BLEN
-    MTE_DEV u32 blen_all(uint4 o, bool valid, i32 R, u32 C) const {
-        u32 v = valid ? o.y : 0u;
-        if (C == 0) return v;  // the observer sees every block settled
-        u64 dirty = wave_ballot(valid && (i32)o.z > R);
-        if (!dirty) return v;
-        const u32 g = L >> 3, s = L & 7;
-        const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(dirty >> 32), __builtin_amdgcn_mbcnt_lo((u32)dirty, 0u));
-        for (u32 pass = 0; dirty; pass++) {
-            // group g takes the g-th remaining dirty block
-            u32 b = NONE, cnt = 0;
-            u64 m = dirty;
-            for (u32 i = 0; i < 8 && m; i++) {
-                const u32 j = (u32)__builtin_ctzll(m);
-                m &= m - 1;
-                const u32 bj = wave_read(o.x, j), cj = wave_read(o.w, j);
-                b = g == i ? bj : b;
-                cnt = g == i ? cj : cnt;
-            }
-            const bool act = s < cnt && b < blk_cap();
-            const u32 idx = (act ? b : 0u) * 8 + s;
-            const uint4 q = VIS()[idx];
-            const u32 z = AUX()[idx].z;
-            const u32 sv = act ? vis_len(q, z, idx, R, C, 0u) : 0u;
-            const u32 tot = group8_scan(sv);
-            // the lanes whose block was taken in this pass read their group's total
-            const u32 r = below - pass * 8;
-            const bool mine = ((dirty >> L) & 1ull) && r < 8;
-            const u32 t = wave_shfl(tot, (mine ? r : 0u) * 8 + 7);
-            v = mine ? t : v;
-            dirty = m;
-        }
-        return v;
-    }
-
-#else
     MTE_DEV u32 blen_all(uint4 o, bool valid, i32 R, u32 C) const {
         const u32 cz = C == 0 ? 1u : 0u;
         const bool fast = !valid | (cz != 0) | ((i32)o.z <= R);
@@ -538,7 +497,6 @@ struct Engine {
         const u64 dm = wave_ballot(!fast);
         if (dm) {
             MTE_PROF(PF_BLEN_DIRTY);
-#ifndef MTE_OLD_BLEN
             if (!(dm & (dm - 1))) {
                 // one dirty block (the common case): lane = slot, one conflict-free LDS read per lane
                 // instead of every lane reading 8 slots of its own block (the 128-B block stride
@@ -554,23 +512,10 @@ struct Engine {
                 const u32 tot = wave_read(group8_scan(sv1), 7);
                 return L == j ? tot : v;
             }
-#endif
             const u32 b = o.x < blk_cap() ? o.x : 0u;
             uint4 q[8];
-#ifdef MTE_MASK_BLEN
-            // only the dirty lanes read: the same slot of 64 different blocks (128-B stride) would
-            // hit two bank groups with every lane of the wave
-            if (!fast) {
-#pragma unroll
-                for (u32 s = 0; s < 8; s++) q[s] = VIS()[b * 8 + s];
-            } else {
-#pragma unroll
-                for (u32 s = 0; s < 8; s++) q[s] = make_uint4(0, 0, 0, 0);
-            }
-#else
 #pragma unroll
             for (u32 s = 0; s < 8; s++) q[s] = VIS()[b * 8 + s];
-#endif
             u32 sv = 0;
             if (FULL && C >= 32) {  // clients 32..63: the general predicate (HBM half of the overlap mask)
 #pragma unroll
@@ -596,7 +541,6 @@ struct Engine {
         return v;
     }
 
-#endif
     // Recompute (visible length, max seq) of ORD()[k0 .. k0+n), n <= 8, from the slots.
     MTE_DEV void refresh(u32 k0, u32 n) {
         const u32 g = L >> 3, s = L & 7;
@@ -1226,25 +1170,14 @@ struct Engine {
         sync();
     }
     // Pop: sift-down of collections.ts:252-264 (the smaller child, left on ties, moves up while
-    // strictly below the moved last entry). LDS modes: one round of reads gives every lane l the
-    // smaller child of node l and of node 64 + l; the root-to-leaf path is then followed with
-    // readlanes (deeper nodes, heaps over 255 entries, read their child pair directly). Only the
-    // moved entries are written. HBM mode: lane 0 walks the pairs in memory.
-#ifdef MTE_NEW_HEAP
-    static constexpr bool NEW_HEAP = true;
-#else
-    static constexpr bool NEW_HEAP = false;
-#endif
+    // strictly below the moved last entry). k_lds: the whole heap (<= HEAP_CAP) read once as a
+    // register image, the root-to-leaf path followed with readlanes; k_solo and HBM mode: lane 0
+    // walks the child pairs in memory. Only the moved entries are written.
     // heap entry at a uniform position held in registers (position i: lane i % 64 of set i / 64)
     MTE_DEV static uint2 hent(uint2 h0, uint2 h1, uint2 h2, u32 i) {
         if (i < 64) return make_uint2(wave_read(h0.x, i), wave_read(h0.y, i));
         if (i < 128) return make_uint2(wave_read(h1.x, i - 64), wave_read(h1.y, i - 64));
         return make_uint2(wave_read(h2.x, i - 128), wave_read(h2.y, i - 128));
-    }
-    MTE_DEV static void min_child(uint4 pr, u32 i, u32 m, u32& j, uint2& e) {
-        const bool right = (2 * i + 1 <= m) && ((i32)pr.y - (i32)pr.w > 0);
-        j = 2 * i + (right ? 1u : 0u);
-        e = right ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
     }
     MTE_DEV uint2 heap_pop() {
         MTE_PROF(PF_HEAP);
@@ -1253,7 +1186,6 @@ struct Engine {
         const u32 n = st.heapSize;
         const u32 m = n - 1;
         uint2 x;
-#ifndef MTE_NEW_HEAP
         if constexpr (SHARED) {  // the whole heap (<= HEAP_CAP) as a register image, scalar walk
             static_assert(HEAP_CAP < 192, "heap register image holds 192 positions");
             uint2 h0 = make_uint2(0, 0), h1 = h0, h2 = h0;
@@ -1273,42 +1205,6 @@ struct Engine {
                         j++;
                         hj = hj1;
                     }
-                }
-                if ((i32)last.y - (i32)hj.y <= 0) break;
-                if (k == 1) newTop = (i32)hj.y;
-                if (L == 0) H[k] = hj;
-                k = j;
-            }
-            if (m >= 1 && L == 0) H[k] = last;
-            st.heapTop = newTop;
-        } else
-#endif
-        if constexpr (LDSM && NEW_HEAP) {
-            const u32 i1 = 64 + L;
-            uint4 p0 = make_uint4(0, 0, 0, 0), p1 = p0;
-            if (L >= 1 && 2 * L <= m) p0 = *(const uint4*)(H + 2 * L);
-            if (2 * i1 <= m) p1 = *(const uint4*)(H + 2 * i1);
-            const uint2 top = H[1], lst = H[n];
-            x = make_uint2(U(top.x), U(top.y));
-            const uint2 last = make_uint2(U(lst.x), U(lst.y));
-            u32 j0, j1;
-            uint2 e0, e1;
-            min_child(p0, L, m, j0, e0);
-            min_child(p1, i1, m, j1, e1);
-            u32 k = 1;
-            i32 newTop = (i32)last.y;
-            while (2 * k <= m) {
-                u32 j;
-                uint2 hj;
-                if (k < 64) {
-                    j = wave_read(j0, k);
-                    hj = make_uint2(wave_read(e0.x, k), wave_read(e0.y, k));
-                } else if (k < 128) {
-                    j = wave_read(j1, k - 64);
-                    hj = make_uint2(wave_read(e1.x, k - 64), wave_read(e1.y, k - 64));
-                } else {
-                    const uint4 pr = U(*(const uint4*)(H + 2 * k));
-                    min_child(pr, k, m, j, hj);
                 }
                 if ((i32)last.y - (i32)hj.y <= 0) break;
                 if (k == 1) newTop = (i32)hj.y;
@@ -1537,9 +1433,6 @@ struct Engine {
     // jobs (sources are never destinations of the same batch, see scour()).
     MTE_DEV void run_jobs(const Jobs& jb) {
         MTE_PROF(PF_TEXT);
-#ifdef MTE_NO_TEXT  // timing experiment only (wrong text): the cost of the scour's text copies
-        return;
-#endif
         const u32 jl = L < jb.n ? jb.len : 0u;
         const u32 jinc = wave_scan_incl(jl);
         const u32 total = wave_read(jinc, 63);
@@ -1921,11 +1814,7 @@ struct Engine {
         // layout it saw holds (a boundary split that splits its block 8 -> 4+4 changes n_lb: the later
         // phases scan again); blocks keep their visible lengths across a boundary split
         u32 pv = 0, pincl = 0, pn = NONE;
-#ifdef MTE_NO_FUSE
-        if (false) {
-#else
         if (!ins && st.n_lb <= 64) {
-#endif
             fence_ovl();
             const bool valid = L < st.n_lb;
             const uint4 po = valid ? ORD()[L] : make_uint4(0, 0, 0, 0);

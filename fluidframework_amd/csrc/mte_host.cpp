@@ -665,6 +665,22 @@ static void count_doc_ops(const mte_op* ops, const uint64_t* off, uint32_t d, ui
     }
 }
 
+// Runs `work` on up to n threads, the caller being one of them. `work` pulls from a shared queue, so a
+// thread that cannot be created (std::system_error under RLIMIT_NPROC or a cgroup pids limit) only
+// leaves its share to the others: the caller alone still finishes, and no exception crosses the C ABI.
+extern "C++" {
+template <class F>
+static void run_pool(unsigned n, F&& work) {
+    std::vector<std::thread> ts;
+    try {
+        for (unsigned i = 1; i < n; i++) ts.emplace_back(work);
+    } catch (...) {
+    }
+    work();
+    for (auto& t : ts) t.join();
+}
+}
+
 int mte_load(mte_engine* e, const mte_batch* b) {
     if (!e || !b) return MTE_E_ARG;
     HIP_TRY(e, hipSetDevice(e->device));
@@ -705,10 +721,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
             for (uint32_t d0; (d0 = next.fetch_add(256)) < nd;)
                 for (uint32_t d = d0; d < std::min(nd, d0 + 256); d++) scan(d);
         };
-        std::vector<std::thread> ts;
-        for (unsigned i = 1; i < nt; i++) ts.emplace_back(work);
-        work();
-        for (auto& t : ts) t.join();
+        run_pool(nt, work);
     }
     bool lean = true, ext = false, cu_any = false;
     for (uint32_t d = 0; d < nd; d++) {
@@ -1850,10 +1863,7 @@ int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap) {
             s.doc_id = e->cfg[d].gid;
         }
     };
-    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::thread> ts;
-    for (unsigned i = 0; i < nt; i++) ts.emplace_back(work);
-    for (auto& t : ts) t.join();
+    run_pool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())), work);
     return MTE_OK;
 }
 
@@ -2504,6 +2514,61 @@ static int legacy_to_v1(const std::u16string& path, json::Value& c) {
     return MTE_OK;
 }
 
+// Buffer.toString("utf8") of the decoded base64 bytes (fromBase64ToUtf8, common-utils
+// base64Encoding.ts): the WHATWG UTF-8 decoder, each maximal invalid subpart becomes U+FFFD.
+// Re-encoded as UTF-8 for the JSON parser.
+static std::string utf8_replace_invalid(const std::string& in) {
+    std::string out;
+    out.reserve(in.size());
+    auto put = [&](u32 cp) {
+        if (cp < 0x80) {
+            out.push_back((char)cp);
+        } else if (cp < 0x800) {
+            out.push_back((char)(0xC0 | (cp >> 6)));
+            out.push_back((char)(0x80 | (cp & 0x3F)));
+        } else if (cp < 0x10000) {
+            out.push_back((char)(0xE0 | (cp >> 12)));
+            out.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+            out.push_back((char)(0x80 | (cp & 0x3F)));
+        } else {
+            out.push_back((char)(0xF0 | (cp >> 18)));
+            out.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+            out.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+            out.push_back((char)(0x80 | (cp & 0x3F)));
+        }
+    };
+    u32 need = 0, seen = 0, cp = 0, lo = 0x80, hi = 0xBF;
+    for (size_t i = 0; i < in.size();) {
+        const u32 b = (unsigned char)in[i];
+        if (need == 0) {
+            i++;
+            if (b < 0x80) put(b);
+            else if (b >= 0xC2 && b <= 0xDF) { need = 1; cp = b & 0x1F; }
+            else if (b >= 0xE0 && b <= 0xEF) { if (b == 0xE0) lo = 0xA0; if (b == 0xED) hi = 0x9F; need = 2; cp = b & 0xF; }
+            else if (b >= 0xF0 && b <= 0xF4) { if (b == 0xF0) lo = 0x90; if (b == 0xF4) hi = 0x8F; need = 3; cp = b & 0x7; }
+            else put(0xFFFD);
+            continue;
+        }
+        if (b < lo || b > hi) {  // the byte starts over (not consumed)
+            need = seen = cp = 0;
+            lo = 0x80;
+            hi = 0xBF;
+            put(0xFFFD);
+            continue;
+        }
+        i++;
+        lo = 0x80;
+        hi = 0xBF;
+        cp = (cp << 6) | (b & 0x3F);
+        if (++seen == need) {
+            put(cp);
+            need = seen = cp = 0;
+        }
+    }
+    if (need) put(0xFFFD);
+    return out;
+}
+
 // An ITree blob's text (IBlob { contents, encoding: "utf-8" | "base64" }): what storage.read(path) +
 // fromBase64ToUtf8 give the loader (snapshotV1.ts:255,267; snapshotLoader.ts:225). Base64 as Node's
 // Buffer.from(s, "base64") reads it: standard or url-safe alphabet, whitespace skipped, '=' ends the
@@ -2536,6 +2601,7 @@ static int blob_utf8(const json::Value* v, std::string& out) {
             out.push_back((char)((acc >> nb) & 0xff));
         }
     }
+    out = utf8_replace_invalid(out);
     return 0;
 }
 static int blob_text(DocBuild& db, const json::Value* v, std::string& out, const char* missing) {

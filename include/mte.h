@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MTE_ABI_VERSION 1
+#define MTE_ABI_VERSION 2  /* 2: mte_batch gained the catch-up message fields, mte_config.snapshot_format */
 
 /* ---- status codes ------------------------------------------------------------------------ */
 enum {

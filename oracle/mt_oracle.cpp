@@ -792,6 +792,61 @@ static void segment_json(std::string& o, const Segment* s) {
 }
 
 // FNV-1a-64
+// Buffer.toString("utf8") of the decoded base64 bytes (fromBase64ToUtf8,
+// common/lib/common-utils/src/base64Encoding.ts): the WHATWG UTF-8 decoder, each maximal invalid subpart becomes U+FFFD.
+// Re-encoded as UTF-8 for the JSON parser.
+static std::string utf8ReplaceInvalid(const std::string& in) {
+    std::string out;
+    out.reserve(in.size());
+    auto put = [&](uint32_t cp) {
+        if (cp < 0x80) {
+            out.push_back((char)cp);
+        } else if (cp < 0x800) {
+            out.push_back((char)(0xC0 | (cp >> 6)));
+            out.push_back((char)(0x80 | (cp & 0x3F)));
+        } else if (cp < 0x10000) {
+            out.push_back((char)(0xE0 | (cp >> 12)));
+            out.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+            out.push_back((char)(0x80 | (cp & 0x3F)));
+        } else {
+            out.push_back((char)(0xF0 | (cp >> 18)));
+            out.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+            out.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+            out.push_back((char)(0x80 | (cp & 0x3F)));
+        }
+    };
+    uint32_t need = 0, seen = 0, cp = 0, lo = 0x80, hi = 0xBF;
+    for (size_t i = 0; i < in.size();) {
+        const uint32_t b = (unsigned char)in[i];
+        if (need == 0) {
+            i++;
+            if (b < 0x80) put(b);
+            else if (b >= 0xC2 && b <= 0xDF) { need = 1; cp = b & 0x1F; }
+            else if (b >= 0xE0 && b <= 0xEF) { if (b == 0xE0) lo = 0xA0; if (b == 0xED) hi = 0x9F; need = 2; cp = b & 0xF; }
+            else if (b >= 0xF0 && b <= 0xF4) { if (b == 0xF0) lo = 0x90; if (b == 0xF4) hi = 0x8F; need = 3; cp = b & 0x7; }
+            else put(0xFFFD);
+            continue;
+        }
+        if (b < lo || b > hi) {  // the byte starts over (not consumed)
+            need = seen = cp = 0;
+            lo = 0x80;
+            hi = 0xBF;
+            put(0xFFFD);
+            continue;
+        }
+        i++;
+        lo = 0x80;
+        hi = 0xBF;
+        cp = (cp << 6) | (b & 0x3F);
+        if (++seen == need) {
+            put(cp);
+            need = seen = cp = 0;
+        }
+    }
+    if (need) put(0xFFFD);
+    return out;
+}
+
 static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
     const uint8_t* b = (const uint8_t*)p;
     for (size_t i = 0; i < n; i++) { h ^= b[i]; h *= 0x100000001b3ull; }
@@ -1192,7 +1247,7 @@ class Doc {
                 out.push_back((char)((acc >> nb) & 0xff));
             }
         }
-        return out;
+        return utf8ReplaceInvalid(out);
     }
     // storage.read(path) + SnapshotV1.processChunk (snapshotV1.ts:249-270)
     static JVP chunkAt(const JV& tree, const u16s& path) {  // (legacy chunks converted to v1)

@@ -16,14 +16,16 @@ class BatchedMergeEngine {
     constructor(options = {}) {
         this.device = options.device || 0;
         this.chunkSize = options.chunkSize || 10000;  // SnapshotV1.chunkSize (snapshotV1.ts:40)
-        // newMergeTreeSnapshotFormat (client.ts:930-941): true (default here) SnapshotV1, false SnapshotLegacy
-        this.legacyFormat = options.newMergeTreeSnapshotFormat === false;
+        // newMergeTreeSnapshotFormat (client.ts:930-941): SnapshotV1 only when it is true, else the
+        // reference's default, SnapshotLegacy
+        this.legacyFormat = options.newMergeTreeSnapshotFormat !== true;
         this._engine = addon.createEngine(this.device, this.chunkSize, this.legacyFormat ? 1 : 0);
         this._docs = 0;
     }
     /** Stage per-document logs: docs = [{ observer, messages: ISequencedDocumentMessage[], summary? }]
      *  summary (optional): a SnapshotV1 ITree to resume from (SnapshotLoader); messages are the suffix. */
     load(docs) {
+        this._idle();
         const b = addon.createBuilder();
         for (const d of docs) {
             const obs = d.observer === undefined ? "__observer__" : d.observer;
@@ -40,6 +42,7 @@ class BatchedMergeEngine {
         this._docs = addon.builderDocCount(b);
     }
     generate(kind, nDocs, nOps, nClients = 8, seed = 0) {
+        this._idle();
         addon.generate(this._engine, kind, nDocs, nOps, nClients, seed);
         this._docs = nDocs;
     }
@@ -60,15 +63,17 @@ class BatchedMergeEngine {
     docStatus(doc) { this._idle(); return addon.docStatus(this._engine, doc); }
     getText(doc) { this._idle(); return addon.getText(this._engine, doc); }
     /** The ITree SnapshotV1.emit(serializer) returns: { entries: [...], id: null } */
-    snapshotV1(doc) { return JSON.parse(addon.snapshotV1(this._engine, doc)); }
+    snapshotV1(doc) { this._idle(); return JSON.parse(addon.snapshotV1(this._engine, doc)); }
     /** SharedMatrix summary of a { matrix } document pair (its rows and cols PermutationVectors) */
-    snapshotMatrix(rowsDoc, colsDoc) { return JSON.parse(addon.snapshotMatrix(this._engine, rowsDoc, colsDoc)); }
+    snapshotMatrix(rowsDoc, colsDoc) { this._idle(); return JSON.parse(addon.snapshotMatrix(this._engine, rowsDoc, colsDoc)); }
     /** SnapshotLegacy ITree (snapshotlegacy.ts:103-182): header, body, catch-up messages */
     snapshotLegacy(doc, catchUpBlobName = "catchupOps") {
+        this._idle();
         return JSON.parse(addon.snapshotLegacy(this._engine, doc, catchUpBlobName));
     }
     /** 32-byte records {checksum u64, ops, length, segments, snapshotBytes, status, docId} */
     summaries() {
+        this._idle();
         const buf = addon.summaries(this._engine, this._docs);
         const out = [];
         for (let i = 0; i < this._docs; i++) {
@@ -99,38 +104,49 @@ class MergeTreeClient {
         this.messages = [];
         this.summary = undefined;
         this._engine = undefined;
-        this._dirty = true;
+        this._version = 0;        // bumped by every staged change
+        this._replayed = -1;      // the version the engine's results belong to
+        this._flushing = null;    // pending flush() promise
     }
+    get _dirty() { return this._version !== this._replayed; }
     /** Client.load / SnapshotLoader (client.ts:944-952): resume from a summary ITree before applyMsg. */
-    load(summary) { this.summary = summary; this.messages = []; this._dirty = true; }
-    applyMsg(msg) { this.messages.push(msg); this._dirty = true; }
+    load(summary) { this.summary = summary; this.messages = []; this._version++; }
+    applyMsg(msg) { this.messages.push(msg); this._version++; }
     /** Stage a batch of sequenced messages at once (one replay serves them all). */
-    applyMsgs(msgs) { for (const m of msgs) this.messages.push(m); this._dirty = true; }
-    _check() {
+    applyMsgs(msgs) { for (const m of msgs) this.messages.push(m); this._version++; }
+    _check(version) {
         const [code, seq] = this._engine.docStatus(0);
         if (code === DocStatus.InsertFailed) throw new Error(`MergeTree insert failed at seq ${seq}`);
         if (code !== DocStatus.Ok) throw new Error(`replay failed (status ${code}) at seq ${seq}`);
-        this._dirty = false;
+        this._replayed = version;  // messages staged during an async flush keep the client dirty
     }
     _stage() {
         if (!this._engine) this._engine = new BatchedMergeEngine(this.options);
-        this._engine.load([{ observer: this.observer, messages: this.messages, summary: this.summary }]);
+        this._engine.load([{ observer: this.observer, messages: this.messages.slice(), summary: this.summary }]);
+        return this._version;
     }
     _run() {
+        if (this._flushing) throw new Error("MergeTreeClient: a flush() is still running; await it first");
         if (this._dirty) {
-            this._stage();
+            const v = this._stage();
             this._engine.replay();
-            this._check();
+            this._check(v);
         }
         return this._engine;
     }
-    /** Replay the staged messages off the event loop; resolves when outputs can be read. */
+    /** Replay the staged messages off the event loop; resolves when outputs can be read. Reads while
+     *  it is pending throw (the engine is not re-entrant); a second flush() waits for the first. */
     async flush() {
-        if (this._dirty) {
-            this._stage();
-            await this._engine.replayAsync();
-            this._check();
+        while (this._flushing) await this._flushing.catch(() => {});
+        if (!this._dirty) return;
+        const v = this._stage();
+        this._flushing = this._engine.replayAsync();
+        try {
+            await this._flushing;
+        } finally {
+            this._flushing = null;
         }
+        this._check(v);
     }
     getText() { return this._run().getText(0); }
     /** Client.getLength (client.ts:1057): markers count 1, unlike getText().length. */

@@ -2,7 +2,7 @@
 "use strict";
 const assert = require("assert");
 const m = require("..");
-assert.strictEqual(m.abiVersion(), 1);
+assert.strictEqual(m.abiVersion(), 2);
 assert.ok(/gfx950/.test(m.buildInfo()));
 for (const f of ["BatchedMergeEngine", "MergeTreeClient", "createBuilder", "builderAddDoc", "builderDocCount"]) {
     assert.strictEqual(typeof m[f], "function", f);

@@ -16,7 +16,7 @@ const tree = c1.snapshot();
 assert.strictEqual(tree.entries[0].path, "header");
 // Client.load (SnapshotLoader) from a reference v1 fixture: re-emits the same tree, then catches up
 const fixture = JSON.parse(require("fs").readFileSync(__dirname + "/../../../tests/golden/v1/withAnnotations.json", "utf8"));
-const c2 = new MergeTreeClient("catchup");
+const c2 = new MergeTreeClient("catchup", { newMergeTreeSnapshotFormat: true });
 c2.load(fixture);
 assert.deepStrictEqual(c2.snapshot(), fixture.entries[1].value);
 const len0 = c2.getLength();
@@ -40,7 +40,10 @@ for (let i = 0; i < 1250; i++) lc.applyMsg(msg("", i + 1, i, { pos1: 0, seg: `te
 const lt = lc.snapshot();
 assert.deepStrictEqual(lt.entries.map((x) => [x.path, x.value.contents]),
     legacyFix.entries[1].value.entries.map((x) => [x.path, x.value.contents]));
-const e = new BatchedMergeEngine();
+// the reference's default summary format is SnapshotLegacy (client.ts:930-941)
+assert.strictEqual(new MergeTreeClient()._engine, undefined);
+assert.strictEqual(c1._engine.legacyFormat, true);
+const e = new BatchedMergeEngine({ newMergeTreeSnapshotFormat: true });
 e.generate(2, 8, 500, 8, 3);
 const st = e.replay();
 assert.strictEqual(st.failedDocs, 0);
@@ -54,13 +57,19 @@ const sums = e.summaries();
     const timer = setInterval(() => { ticks++; }, 0);
     const pending = big.replayAsync();
     assert.throws(() => big.getText(0), /still running/);
+    assert.throws(() => big.load([]), /still running/);
+    assert.throws(() => big.snapshotV1(0), /still running/);
+    assert.throws(() => big.summaries(), /still running/);
     const st2 = await pending;
     clearInterval(timer);
     assert.strictEqual(st2.failedDocs, 0);
     assert.deepStrictEqual(big.summaries().map((s) => s.checksum.toString()), syncSums);
     const c4 = new MergeTreeClient();
     c4.applyMsgs(hello);
-    await c4.flush();
-    assert.strictEqual(c4.getText(), "hello world");
+    const fl = c4.flush();
+    assert.throws(() => c4.getText(), /flush\(\) is still running/);
+    c4.applyMsg(msg("late", 12, 11, { pos1: 11, seg: "!", type: 0 }));  // staged during the flush
+    await fl;
+    assert.strictEqual(c4.getText(), "hello world!");  // the late message makes the client dirty again
     console.log(JSON.stringify({ ops: st.ops, checksums: sums.map((s) => s.checksum.toString()), async_ticks: ticks }));
 })().catch((err) => { console.error(err); process.exit(1); });

@@ -33,7 +33,7 @@ def test_library_exports_diag_symbols():
 
 def test_abi_version_and_info():
     L = mte.lib()
-    assert L.mte_abi_version() == 1
+    assert L.mte_abi_version() == 2
     assert b"gfx950" in L.mte_build_info()
 
 

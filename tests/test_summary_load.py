@@ -206,6 +206,34 @@ def test_base64_blobs_load_like_utf8():
         assert rec.snapshot_json() == ref.snapshot_json(), d
 
 
+def test_base64_blob_with_invalid_utf8():
+    """fromBase64ToUtf8 is Buffer.from(s, "base64").toString("utf8") (common-utils
+    base64Encoding.ts:8): invalid UTF-8 inside a base64 blob decodes to U+FFFD per maximal invalid
+    subpart (the WHATWG decoder Node uses; Python's errors="replace" follows the same rule and is the
+    expectation here), in the oracle and in the builder's records alike."""
+    import base64
+
+    tree = json.loads(fixture("headerOnly"))
+    blob = tree["entries"][1]["value"]["entries"][0]["value"]
+    raw = blob["contents"].encode("utf-8")
+    first = raw.index(b'"segments":["') + len(b'"segments":["')
+    bad = raw[:first] + b"\xff A\xe2\x82 B\xf0\x80\x80 C\xed\xa0\x80 D" + raw[first:]
+    blob["contents"] = base64.b64encode(bad).decode("ascii")
+    blob["encoding"] = "base64"
+    summ = json.dumps(tree)
+    expected = json.loads(bad.decode("utf-8", errors="replace"))["segments"][0]
+    expected = expected if isinstance(expected, str) else expected["text"]
+    assert expected.count("\ufffd") == 1 + 1 + 3 + 3
+    o = oracle_catchup(summ, None)
+    assert o.text().startswith(expected)
+    b = mte.Builder()
+    b.add_doc_from_summary(summ, observer=OBS)
+    rec = OracleDoc(OBS)
+    rec.apply_batch(ctypes.addressof(b.batch()), 0)
+    assert rec.segments_json() == o.segments_json()
+    assert rec.text().startswith(expected)
+
+
 def test_blob_encoding_errors():
     bad_char = json.loads(base64_blobs(fixture("headerOnly")))
     bad_char["entries"][1]["value"]["entries"][0]["value"]["contents"] = "e30*"

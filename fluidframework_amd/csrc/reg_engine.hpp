@@ -125,10 +125,12 @@ struct RegEngine {
     }
     // slot-index memmove (blocks move as whole 8-slot groups)
     SD void mv_slots(u32 dst, u32 src, u32 n) {
+        cr = NONE;
         memmove(mem_vis[dst], mem_vis[src], (size_t)n * 16);
         memmove(mem_aux[dst], mem_aux[src], (size_t)n * 16);
     }
     SD void zero_slots(u32 at, u32 n) {
+        cr = NONE;
         memset(mem_vis[at], 0, (size_t)n * 16);
         memset(mem_aux[at], 0, (size_t)n * 16);
     }
@@ -156,6 +158,7 @@ struct RegEngine {
         simd::lds_order();
     }
     SD void mv_slots(u32 dst, u32 src, u32 n) {  // overlapping: copy in the safe direction
+        cr = NONE;
         uint4* V4 = VISP();
         uint4* A4 = AUXP();
         const u32 L = __lane_id();
@@ -192,6 +195,7 @@ struct RegEngine {
         }
     }
     SD void zero_slots(u32 at, u32 n) {
+        cr = NONE;
         for (u32 b = __lane_id(); b < n; b += 64) {
             VISP()[at + b] = make_uint4(0, 0, 0, 0);
             AUXP()[at + b] = make_uint4(0, 0, 0, 0);
@@ -201,8 +205,24 @@ struct RegEngine {
 #endif
     SD V ld_len(u32 r) const { return ldf(r, 0, 0); }
     SD V ld_meta(u32 r) const { return ldf(r, 0, 3); }
-    SD V ld_tz(u32 r) const { return ldf(r, 1, 2); }
     SD V ld_sid(u32 r) const { return ldf(r, 1, 3); }
+    // The row an op is working on stays in registers between its steps (resolve -> split -> insert ->
+    // LRU; heap pop -> scour -> needsScour): row(r) reads LDS only when r is not the cached row,
+    // putrow writes through. Anything that moves blocks (mv_slots / zero_slots) drops the cache.
+    Row cw;
+    u32 cr = NONE;
+    SD Row row(u32 r) {
+        if (r != cr) {
+            cw = ldrow(r);
+            cr = r;
+        }
+        return cw;
+    }
+    SD void putrow(u32 r, const Row& w) {
+        strow(r, w);
+        cw = w;
+        cr = r;
+    }
 
     SD RegEngine(const Params& p_, u32 doc_) : p(p_), doc(doc_) {
         const DocCfg& c = p.docs[doc];
@@ -248,28 +268,32 @@ struct RegEngine {
     SD static u32 gbase(u32 k) { return (k & 7u) * 8u; }
     SD static B in_group(u32 k) { return (L() >> 3) == (k & 7u); }
     SD static u32 group_bits(u64 m, u32 k) { return (u32)((m >> gbase(k)) & 0xFFull); }
-    SD u32 count(u32 k) const { return (u32)__builtin_popcount(group_bits(simd::ballot(ld_len(k >> 3) != 0u), k)); }
-    SD u32 ns_get(u32 k) const { return (simd::readlane(ld_meta(k >> 3), gbase(k)) >> NS_SHIFT) & 3u; }
+    SD static u32 count_in(const Row& w, u32 k) { return (u32)__builtin_popcount(group_bits(simd::ballot(w.len != 0u), k)); }
+    SD static u32 ns_in(const Row& w, u32 k) { return (simd::readlane(w.meta, gbase(k)) >> NS_SHIFT) & 3u; }
+    SD static void ns_put(Row& w, u32 k, u32 sc) { w.meta = simd::sel(in_group(k), (w.meta & ~NS_MASK) | (sc << NS_SHIFT), w.meta); }
+    SD u32 count(u32 k) { return count_in(row(k >> 3), k); }
+    SD u32 ns_get(u32 k) { return ns_in(row(k >> 3), k); }
     SD void ns_set(u32 k, u32 sc) {
-        const V m = ld_meta(k >> 3);
-        stf(k >> 3, 0, 3, (m & ~NS_MASK) | (sc << NS_SHIFT), in_group(k));
+        Row w = row(k >> 3);
+        ns_put(w, k, sc);
+        putrow(k >> 3, w);
     }
 
     // nodeLength of every slot of a row for (refSeq R, client C) (mergeTree.ts:1659-1699):
     //   ins = client == C || seq <= R;  rem = removed && (removedClient == C || removedSeq <= R
     //   || C in removedClientOverlap);  visible = ins && !rem ? len : 0.
-    SD V vis(u32 r, V len, V seq, V rseq, V meta, i32 R, u32 C) const {
-        const B ins = simd::sle(seq, R) | (simd::bfe(meta, 0, 8) == C);
-        B rem = simd::sle(rseq, R) | (simd::bfe(meta, 8, 8) == C);
-        const B ov = (meta & F_OVL) != 0u;  // removedClientOverlap non-empty (clients < 32: in tz)
-        if (simd::ballot(ov)) rem = rem | (((ld_tz(r) & (1u << C)) != 0u) & ov);
-        return simd::sel(simd::andn(ins, rem), len, 0u);
+    SD static V vis(const Row& w, i32 R, u32 C) {
+        const B ins = simd::sle(w.seq, R) | (simd::bfe(w.meta, 0, 8) == C);
+        B rem = simd::sle(w.rseq, R) | (simd::bfe(w.meta, 8, 8) == C);
+        const B ov = (w.meta & F_OVL) != 0u;  // removedClientOverlap non-empty (clients < 32: in tz)
+        if (simd::ballot(ov)) rem = rem | (((w.tz & (1u << C)) != 0u) & ov);
+        return simd::sel(simd::andn(ins, rem), w.len, 0u);
     }
 
     // insertingWalk's target for `pos` in the (R, C) view: the first leaf block whose cumulative
     // visible end is >= pos, then inside it the first slot with pos < its end, or a zero-length slot
     // at pos that wins breakTie (skip tombstones already seen at R, mergeTree.ts:2257-2261).
-    SD RFound resolve(i32 pos, i32 R, u32 C) const {
+    SD RFound resolve(i32 pos, i32 R, u32 C) {
         RFound f;
         f.ok = false;
         f.k = 0;
@@ -279,9 +303,11 @@ struct RegEngine {
         const u32 nrows = (n_lb + 7) >> 3;
         u32 carry = 0;
         const V lk = L() >> 3;
+        Row nxt = row(0);
         for (u32 r = 0; r < nrows; r++) {
-            const Row w = ldrow(r);
-            const V v = vis(r, w.len, w.seq, w.rseq, w.meta, R, C);
+            const Row w = nxt;
+            if (r + 1 < nrows) nxt = ldrow(r + 1);  // the next row's read overlaps this row's scan
+            const V v = vis(w, R, C);
             const V incl = simd::scan_incl(v) + carry;
             const B end = ((L() & 7u) == 7u) & ((lk + r * 8u) < n_lb);
             const u64 hit = simd::ballot(end & simd::sge(incl, pos));
@@ -297,6 +323,8 @@ struct RegEngine {
                 f.ok = true;
                 f.k = k;
                 f.cnt = (u32)__builtin_popcount(group_bits(simd::ballot(valid), k));
+                cw = w;
+                cr = r;
                 if (cm) {
                     const u32 l = (u32)__builtin_ctzll(cm);
                     f.slot = (i32)(l - gb);
@@ -371,7 +399,7 @@ struct RegEngine {
             return NONE;
         }
         const u32 r = k >> 3, gb = gbase(k);
-        Row w = ldrow(r);
+        Row w = row(r);
         const V sl = L() & 7u;
         const B ing = in_group(k);
         const B mv = ing & (sl > j);
@@ -393,7 +421,7 @@ struct RegEngine {
         put(w.toff, rec.toff);
         put(w.tz, rec.tz);
         put(w.sid, rec.sid);
-        strow(r, w);
+        putrow(r, w);
         if (cnt + 1 < 8) return k;
         split_block(k);
         return j < 4 ? k : k + 1;
@@ -409,7 +437,7 @@ struct RegEngine {
         const V sl = L() & 7u;
         const B lo = in_group(k + 1) & (sl < 4u), hi2 = in_group(k + 1) & (sl >= 4u), hi = in_group(k) & (sl >= 4u);
         const V src = (L() + (r2 == r ? 0u : 64u) - 4u) & 63u;  // new slot s <- old slot 4+s of block k
-        Row w = ldrow(r);
+        Row w = row(r);
         const u32 nsk = simd::readlane(w.meta, gbase(k)) & NS_MASK;
         Row w2 = r2 == r ? w : ldrow(r2);
         auto mv = [&](V& x, V& y, u32 keepHi) MTE_LI {  // x: row r, y: row r2
@@ -433,11 +461,11 @@ struct RegEngine {
         // the new block's needsScour is undefined
         if (r2 == r) {
             w.meta = simd::sel(in_group(k + 1), w.meta & ~NS_MASK, w.meta);
-            strow(r, w);
+            putrow(r, w);
         } else {
             w2.meta = simd::sel(in_group(k + 1), w2.meta & ~NS_MASK, w2.meta);
-            strow(r, w);
             strow(r2, w2);
+            putrow(r, w);
         }
         n_lb++;
         if (n_lb > max_lb) max_lb = n_lb;
@@ -498,11 +526,19 @@ struct RegEngine {
         }
     }
     // the leaf block holding segment sid (segment.parent), NONE when unlinked
-    SD u32 find_seg(u32 sid) const {
+    SD u32 find_seg(u32 sid) {
         const u32 nrows = (n_lb + 7) >> 3;
-        for (u32 r = 0; r < nrows; r++) {
-            const u64 m = simd::ballot((ld_sid(r) == sid) & (ld_len(r) != 0u));
-            if (m) return r * 8 + ((u32)__builtin_ctzll(m) >> 3);
+        for (u32 r0 = 0; r0 < nrows; r0 += 4) {  // four rows' reads in flight per round
+            V s4[4], l4[4];
+            for (u32 i = 0; i < 4; i++) {
+                const u32 r = r0 + i < nrows ? r0 + i : r0;
+                s4[i] = ld_sid(r);
+                l4[i] = ld_len(r);
+            }
+            for (u32 i = 0; i < 4 && r0 + i < nrows; i++) {
+                const u64 m = simd::ballot((s4[i] == sid) & (l4[i] != 0u));
+                if (m) return (r0 + i) * 8 + ((u32)__builtin_ctzll(m) >> 3);
+            }
         }
         return NONE;
     }
@@ -554,7 +590,7 @@ struct RegEngine {
                 dirty = true;
                 top += cap;
             }
-            if (dirty) strow(r, w);
+            if (dirty) putrow(r, w);
         }
         simd::wave_fence();
         arenaSel = other;
@@ -572,7 +608,7 @@ struct RegEngine {
         fence_arena();
         const u32 r = k >> 3, gb = gbase(k);
         const B ing = in_group(k);
-        Row w = ldrow(r);
+        Row w = row(r);
         const B act = ing & (w.len != 0u);
         const B rem = act & (w.rseq != RSEQ_LIVE);
         const u32 mREM = group_bits(simd::ballot(rem), k);
@@ -667,7 +703,7 @@ struct RegEngine {
             }
             arena_gc();  // moves every arena text: re-read the slots and redo the chain
             if (status) return cnt;
-            w = ldrow(r);
+            w = row(r);
         }
         if (jn) run_jobs(jn, jdst, jsrc, jlen);
         // compaction: group lane gb+i takes kept slot i
@@ -685,7 +721,7 @@ struct RegEngine {
         cmp(w.rseq, nullptr, 0u);
         cmp(w.meta, nullptr, NS_MASK);  // the block's needsScour stays in every lane
         cmp(w.sid, nullptr, 0u);
-        strow(r, w);
+        putrow(r, w);
         return nkeep;
     }
     // The recorded copies as one flattened gather (sources are never destinations of one scour).
@@ -769,6 +805,7 @@ struct RegEngine {
             put(w.sid, t.sid);
             strow(rr, w);
         }
+        cr = NONE;
         n_lb = (u32)((i32)n_lb + d);
         if (n_lb > max_lb) max_lb = n_lb;
         LV.set(0, simd::writelane(LV.get(0), pi, kk));
@@ -842,7 +879,7 @@ struct RegEngine {
     // right piece copies everything and follows the left one. Returns the insert_slot result.
     SD u32 split_at(const RFound& f) {
         const u32 r = f.k >> 3, l = gbase(f.k) + (u32)f.slot;
-        const Row w = ldrow(r);
+        const Row w = row(r);
         RSeg t;
         t.len = simd::readlane(w.len, l);
         t.seq = (i32)simd::readlane(w.seq, l);
@@ -912,8 +949,8 @@ struct RegEngine {
         u32 carry = 0;
         const u32 cbit = 1u << C;
         for (u32 r = 0; r < nrows && (i32)carry < p2; r++) {
-            Row w = ldrow(r);
-            const V v = vis(r, w.len, w.seq, w.rseq, w.meta, R, C);
+            Row w = row(r);
+            const V v = vis(w, R, C);
             const V incl = simd::scan_incl(v) + carry;
             const V ex = incl - v;
             const B mark = (v != 0u) & simd::slt(ex, p2) & simd::sgt(incl, p1);
@@ -927,7 +964,7 @@ struct RegEngine {
             if (simd::ballot(was)) w.tz = simd::sel(was, simd::sel((w.meta & F_OVL) != 0u, w.tz | cbit, simd::splat(cbit)), w.tz);
             w.meta = simd::sel(was, w.meta | F_OVL, simd::sel(fresh, (w.meta & ~0xFF00u) | (C << 8) | F_REMOVED, w.meta));
             w.rseq = simd::sel(fresh, (u32)seq, w.rseq);
-            strow(r, w);
+            putrow(r, w);
             // addToLRUSet per block, document order: the first marked slot of each block
             for (u64 gm = mm; gm;) {
                 const u32 l = (u32)__builtin_ctzll(gm);

@@ -49,6 +49,32 @@ constexpr i32 REG_HANDOFF = 101;          // internal: continue in the LDS engin
 constexpr u32 NS_SHIFT = 24, NS_MASK = 3u << NS_SHIFT;
 static_assert(RG_BLOCKS <= SOLO_POOL, "the rows live in the SoloPlan's slot arrays");
 
+// Phase profile of the row engine (MTE_PROFILE device builds, `make prof`): inclusive s_memtime
+// cycles and event counts accumulated in registers and written once per document by finish(), in
+// the LDS engine's slot numbering (engine.hpp ProfSlot, mte.PROF_NAMES).
+enum RgProf : u32 {
+    RP_TOTAL, RP_FETCH, RP_APPLY, RP_RESOLVE, RP_INSERT_SLOT, RP_SPLIT, RP_RANGE, RP_ZAMBONI, RP_SCOUR,
+    RP_HEAP, RP_FIND_SEG, RP_PACK, RP_LRU, RP_OPS, RP_N_RESOLVE, RP_N_SCOUR, RP_N_SCOUR_CHANGED,
+    RP_N_PACK, RP_N_POP, RP_N_SPLIT_BLK, RP_N_MOVE, RP_N
+};
+#if defined(MTE_PROFILE) && !defined(MTE_CPU)
+struct RgScope {
+    u64& acc;
+    u64 t0;
+    __device__ __forceinline__ RgScope(u64& a) : acc(a), t0(__builtin_amdgcn_s_memtime()) {}
+    __device__ __forceinline__ ~RgScope() { acc += __builtin_amdgcn_s_memtime() - t0; }
+};
+#define RG_PROF(slot) RgScope _rg_scope_##slot(pf[slot])
+#define RG_COUNT(slot, n) (pf[slot] += (u64)(n))
+#else
+#define RG_PROF(slot) \
+    do {              \
+    } while (0)
+#define RG_COUNT(slot, n) \
+    do {                  \
+    } while (0)
+#endif
+
 #ifndef MTE_CPU
 extern __shared__ uint4 g_lds_dyn[];
 #endif
@@ -86,6 +112,9 @@ struct RegEngine {
     i32 minSeq, curSeq, heapTop, status, failSeq;
     u32 n_ops, n_msgs, n_gc, max_lb;
     bool adirty;
+#if defined(MTE_PROFILE) && !defined(MTE_CPU)
+    u64 pf[RP_N];
+#endif
     // per document
     const Params& p;
     u32 doc;
@@ -247,6 +276,9 @@ struct RegEngine {
         n_ops = n_msgs = n_gc = 0;
         max_lb = 1;
         adirty = false;
+#if defined(MTE_PROFILE) && !defined(MTE_CPU)
+        for (u32 i = 0; i < RP_N; i++) pf[i] = 0;
+#endif
     }
 
     SD static V L() { return simd::lanes(); }
@@ -294,6 +326,7 @@ struct RegEngine {
     // visible end is >= pos, then inside it the first slot with pos < its end, or a zero-length slot
     // at pos that wins breakTie (skip tombstones already seen at R, mergeTree.ts:2257-2261).
     SD RFound resolve(i32 pos, i32 R, u32 C) {
+        RG_PROF(RP_RESOLVE);
         RFound f;
         f.ok = false;
         f.k = 0;
@@ -306,6 +339,7 @@ struct RegEngine {
         Row nxt = row(0);
         for (u32 r = 0; r < nrows; r++) {
             const Row w = nxt;
+            RG_COUNT(RP_N_RESOLVE, 1);
             if (r + 1 < nrows) nxt = ldrow(r + 1);  // the next row's read overlaps this row's scan
             const V v = vis(w, R, C);
             const V incl = simd::scan_incl(v) + carry;
@@ -381,6 +415,7 @@ struct RegEngine {
     // for the caller, the ones it frees at the end (d < 0) are zeroed.
     SD void shift_blocks(u32 from, i32 d) {
         if (d == 0) return;
+        RG_COUNT(RP_N_MOVE, n_lb - from);
         const u32 n = (n_lb - from) * 8;
         if (d > 0) {
             mv_slots((from + (u32)d) * 8, from * 8, n);
@@ -394,6 +429,7 @@ struct RegEngine {
     // the new block right after it in document order (needsScour undefined). With `upd`, slot j-1
     // first takes (len ul, tz uz) (the left piece of a split). Returns the block holding rec.
     SD u32 insert_slot(u32 k, u32 cnt, u32 j, const RSeg& rec, bool upd, u32 ul, u32 uz) {
+        RG_PROF(RP_INSERT_SLOT);
         if (cnt >= 8 || j > cnt) {
             fail(MTE_DOC_CAPACITY, curSeq);
             return NONE;
@@ -428,6 +464,8 @@ struct RegEngine {
     }
     // Block k holds 8 children: a new block k+1 takes slots 4..7 (mergeTree.ts:2476-2489).
     SD void split_block(u32 k) {
+        RG_PROF(RP_SPLIT);
+        RG_COUNT(RP_N_SPLIT_BLK, 1);
         if (n_lb + 1 > NBLK) {
             fail(MTE_DOC_CAPACITY, curSeq);
             return;
@@ -493,6 +531,8 @@ struct RegEngine {
     // pop: sift-down of collections.ts:252-264 (smaller child, left on ties, moves up while
     // strictly below the moved last entry)
     SD u32 heap_pop() {
+        RG_PROF(RP_HEAP);
+        RG_COUNT(RP_N_POP, 1);
         const u32 n = heapSize, m = n - 1;
         const u32 top = hsid(1);
         const u32 lk = hkey(n), ls = hsid(n);
@@ -520,6 +560,7 @@ struct RegEngine {
     }
     // addToLRUSet (mergeTree.ts:1273-1283) for a segment of block k
     SD void add_lru(u32 k, u32 sid, i32 seq) {
+        RG_PROF(RP_LRU);
         if (ns_get(k) != SC_TRUE && seq > curSeq) {
             ns_set(k, SC_TRUE);
             heap_push(sid, seq);
@@ -527,6 +568,7 @@ struct RegEngine {
     }
     // the leaf block holding segment sid (segment.parent), NONE when unlinked
     SD u32 find_seg(u32 sid) {
+        RG_PROF(RP_FIND_SEG);
         const u32 nrows = (n_lb + 7) >> 3;
         for (u32 r0 = 0; r0 < nrows; r0 += 4) {  // four rows' reads in flight per round
             V s4[4], l4[4];
@@ -604,6 +646,8 @@ struct RegEngine {
     // (textSegment.ts:63-85; no '\n' in these documents, no properties); kept slots are compacted.
     // Returns the new child count.
     SD u32 scour(u32 k, u32 cnt) {
+        RG_PROF(RP_SCOUR);
+        RG_COUNT(RP_N_SCOUR, 1);
         if (cnt > 8) cnt = 8;
         fence_arena();
         const u32 r = k >> 3, gb = gbase(k);
@@ -615,6 +659,7 @@ struct RegEngine {
         const u32 mKEPT = group_bits(simd::ballot(rem & simd::sgt(w.rseq, minSeq)), k);
         const u32 mSET = group_bits(simd::ballot(simd::andn(act, rem) & simd::sle(w.seq, minSeq)), k);
         if (!(mREM & ~mKEPT) && !(mSET & (mSET << 1))) return cnt;  // nothing dropped, nothing to merge
+        RG_COUNT(RP_N_SCOUR_CHANGED, 1);
         const u32 mTXT = group_bits(simd::ballot(act & ((w.meta & F_MARKER) == 0u)), k);
         u32 nkeep = 0, jn = 0;
         V kSrc = simd::splat(0), kLen = kSrc, kOff = kSrc, kCap = kSrc;  // lane i: kept slot i
@@ -749,6 +794,8 @@ struct RegEngine {
     // pack (mergeTree.ts:1368-1420), leaf level: the m children [k0, k0+m) of level-1 node pi
     // (already re-scoured; lane i of cn = child i's count) become max(1, min(7, T/4)) fresh blocks.
     SD void pack_leaves(u32 pi, u32 m, u32 k0, V cn) {
+        RG_PROF(RP_PACK);
+        RG_COUNT(RP_N_PACK, 1);
         const u32 T = simd::readlane(simd::scan_incl(simd::sel(L() < m, cn, 0u)), 63);
         u32 kk = T / 4;
         if (kk > 7) kk = 7;
@@ -846,6 +893,7 @@ struct RegEngine {
 
     // zamboniSegments (mergeTree.ts:1422-1478): up to 2 heap entries with maxSeq <= minSeq.
     SD void zamboni() {
+        RG_PROF(RP_ZAMBONI);
         for (int i = 0; i < 2 && !status; i++) {
             if (heapSize == 0 || heapTop > minSeq) break;
             const u32 sid = heap_pop();
@@ -945,6 +993,7 @@ struct RegEngine {
             if (!f.ok || !(f.slot >= 0 && f.r > 0)) continue;
             if (split_at(f) == NONE || status) return false;
         }
+        RG_PROF(RP_RANGE);
         const u32 nrows = (n_lb + 7) >> 3;
         u32 carry = 0;
         const u32 cbit = 1u << C;
@@ -987,6 +1036,7 @@ struct RegEngine {
 
     // Client.applyMsg for one op record (client.ts:805-836); false => not applied, hand off.
     SD bool apply(const mte_op& op) {
+        RG_PROF(RP_APPLY);
         const u32 type = op.type;
         const bool ins = type == MTE_OP_INSERT || type == MTE_OP_INSERT_MARKER;
         if (!(ins || type == MTE_OP_REMOVE || type == MTE_OP_NOOP)) return false;
@@ -1044,6 +1094,7 @@ struct RegEngine {
             status = REG_HANDOFF;
             return i;
         }
+        RG_PROF(RP_TOTAL);
         const u32* src = (const u32*)p.ops;
         simd::VA<4> Q;
         const u64 b = i;
@@ -1061,11 +1112,15 @@ struct RegEngine {
                 Q.set(2, Q.get(3));
                 Q.set(3, load_chunk(i + 24));
             }
-            const V q = Q.get(0);
-            u32 w[8];
-            for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(q, r * 8 + x);
             mte_op op;
-            __builtin_memcpy(&op, w, sizeof op);
+            {
+                RG_PROF(RP_FETCH);
+                const V q = Q.get(0);
+                u32 w[8];
+                for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(q, r * 8 + x);
+                __builtin_memcpy(&op, w, sizeof op);
+            }
+            RG_COUNT(RP_OPS, 1);
             if (!apply(op)) {
                 status = REG_HANDOFF;
                 return i;
@@ -1185,6 +1240,16 @@ struct RegEngine {
             o.mode = 4;  // solo, row-vectorised engine
             o.spill_why = 0;
         }
+#if defined(MTE_PROFILE) && !defined(MTE_CPU)
+        if (simd::lane0()) {
+            static constexpr u32 map[RP_N] = {PF_TOTAL, PF_FETCH, PF_APPLY, PF_RESOLVE, PF_INSERT_SLOT, PF_SPLIT,
+                                              PF_RANGE, PF_ZAMBONI, PF_SCOUR, PF_HEAP, PF_FIND_SEG, PF_PACK,
+                                              PF_LRU, PF_OPS, PN_RESOLVE, PN_SCOUR, PN_SCOUR_CHANGED, PN_PACK,
+                                              PN_POP, PN_SPLIT_BLK, PN_DIRTY};
+            u64* o2 = p.prof + (u64)doc * PROF_SLOTS;
+            for (u32 i = 0; i < RP_N; i++) o2[map[i]] += pf[i];
+        }
+#endif
     }
 };
 

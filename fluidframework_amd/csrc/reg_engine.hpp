@@ -66,6 +66,17 @@ struct RgScope {
 };
 #define RG_PROF(slot) RgScope _rg_scope_##slot(pf[slot])
 #define RG_COUNT(slot, n) (pf[slot] += (u64)(n))
+#elif defined(MTE_MARKERS) && !defined(MTE_CPU)
+// static code inspection: row-engine scopes as assembly comments "MTE_BEGIN 100+slot"
+template <u32 S>
+struct RgMark {
+    __device__ __forceinline__ RgMark() { asm volatile("; MTE_BEGIN %0" ::"i"(S + 100)); }
+    __device__ __forceinline__ ~RgMark() { asm volatile("; MTE_END %0" ::"i"(S + 100)); }
+};
+#define RG_PROF(slot) RgMark<slot> _rg_mark_##slot
+#define RG_COUNT(slot, n) \
+    do {                  \
+    } while (0)
 #else
 #define RG_PROF(slot) \
     do {              \
@@ -85,7 +96,8 @@ struct RSeg {
     u32 rseq;
     u32 meta;
     u32 toff;
-    u32 tz;
+    u32 cap;  // owned merge-arena capacity from toff (0 for payload text)
+    u32 rm;   // removers: bit c for removedClient c and every client in removedClientOverlap
     u32 sid;
 };
 struct RFound {
@@ -101,8 +113,10 @@ struct RegEngine {
     typedef simd::V V;
     typedef simd::B B;
     static constexpr u32 NBLK = (u32)NR * 8;
-    struct Row {  // one row of slots: vis (len, seq, rseq, meta) + aux (-, toff, tz, sid)
-        V len, seq, rseq, meta, toff, tz, sid;
+    // One row of slots: vis = (len, seq, rseq, meta), aux = (cap, toff, rm, sid). A live segment has
+    // rm 0, so nodeLength's removal test is one bit test of rm (no separate overlap-set lookup).
+    struct Row {
+        V len, seq, rseq, meta, cap, toff, rm, sid;
     };
 
     // ---------------------------------------------------------------- state
@@ -131,7 +145,7 @@ struct RegEngine {
             const u32* v = mem_vis[r * 64 + l];
             const u32* a = mem_aux[r * 64 + l];
             w.len.x[l] = v[0], w.seq.x[l] = v[1], w.rseq.x[l] = v[2], w.meta.x[l] = v[3];
-            w.toff.x[l] = a[1], w.tz.x[l] = a[2], w.sid.x[l] = a[3];
+            w.cap.x[l] = a[0], w.toff.x[l] = a[1], w.rm.x[l] = a[2], w.sid.x[l] = a[3];
         }
         return w;
     }
@@ -140,7 +154,7 @@ struct RegEngine {
             u32* v = mem_vis[r * 64 + l];
             u32* a = mem_aux[r * 64 + l];
             v[0] = w.len.x[l], v[1] = w.seq.x[l], v[2] = w.rseq.x[l], v[3] = w.meta.x[l];
-            a[0] = 0, a[1] = w.toff.x[l], a[2] = w.tz.x[l], a[3] = w.sid.x[l];
+            a[0] = w.cap.x[l], a[1] = w.toff.x[l], a[2] = w.rm.x[l], a[3] = w.sid.x[l];
         }
     }
     SD V ldf(u32 r, u32 aux, u32 c) const {  // one field of a row
@@ -169,12 +183,12 @@ struct RegEngine {
     SD Row ldrow(u32 r) const {
         const u32 i = r * 64 + __lane_id();
         const uint4 v = VISP()[i], a = AUXP()[i];
-        return Row{V{v.x}, V{v.y}, V{v.z}, V{v.w}, V{a.y}, V{a.z}, V{a.w}};
+        return Row{V{v.x}, V{v.y}, V{v.z}, V{v.w}, V{a.x}, V{a.y}, V{a.z}, V{a.w}};
     }
     SD void strow(u32 r, const Row& w) {
         const u32 i = r * 64 + __lane_id();
         VISP()[i] = make_uint4(w.len.x, w.seq.x, w.rseq.x, w.meta.x);
-        AUXP()[i] = make_uint4(0u, w.toff.x, w.tz.x, w.sid.x);
+        AUXP()[i] = make_uint4(w.cap.x, w.toff.x, w.rm.x, w.sid.x);
         simd::lds_order();
     }
     SD V ldf(u32 r, u32 aux, u32 c) const {
@@ -314,11 +328,10 @@ struct RegEngine {
     // nodeLength of every slot of a row for (refSeq R, client C) (mergeTree.ts:1659-1699):
     //   ins = client == C || seq <= R;  rem = removed && (removedClient == C || removedSeq <= R
     //   || C in removedClientOverlap);  visible = ins && !rem ? len : 0.
+    // (live: rseq RSEQ_LIVE and rm 0; removed: bit C of rm covers removedClient and the overlap set)
     SD static V vis(const Row& w, i32 R, u32 C) {
         const B ins = simd::sle(w.seq, R) | (simd::bfe(w.meta, 0, 8) == C);
-        B rem = simd::sle(w.rseq, R) | (simd::bfe(w.meta, 8, 8) == C);
-        const B ov = (w.meta & F_OVL) != 0u;  // removedClientOverlap non-empty (clients < 32: in tz)
-        if (simd::ballot(ov)) rem = rem | (((w.tz & (1u << C)) != 0u) & ov);
+        const B rem = simd::sle(w.rseq, R) | (((w.rm >> C) & 1u) != 0u);
         return simd::sel(simd::andn(ins, rem), w.len, 0u);
     }
 
@@ -336,37 +349,45 @@ struct RegEngine {
         const u32 nrows = (n_lb + 7) >> 3;
         u32 carry = 0;
         const V lk = L() >> 3;
-        Row nxt = row(0);
-        for (u32 r = 0; r < nrows; r++) {
-            const Row w = nxt;
+        // one row: its visible lengths, their prefix sum, and the first block end reaching pos
+        auto step = [&](const Row& w, u32 r) MTE_LI {
             RG_COUNT(RP_N_RESOLVE, 1);
-            if (r + 1 < nrows) nxt = ldrow(r + 1);  // the next row's read overlaps this row's scan
             const V v = vis(w, R, C);
             const V incl = simd::scan_incl(v) + carry;
             const B end = ((L() & 7u) == 7u) & ((lk + r * 8u) < n_lb);
             const u64 hit = simd::ballot(end & simd::sge(incl, pos));
-            if (hit) {
-                const u32 g = (u32)__builtin_ctzll(hit) >> 3;
-                const u32 k = r * 8 + g, gb = g * 8;
-                const V ex = incl - v;
-                const V rr = (u32)pos - ex;
-                const B valid = w.len != 0u;
-                const B seen = simd::sle(w.rseq, R) & (w.rseq != 0u);
-                const B cand = in_group(k) & valid & (simd::slt(rr, v) | ((rr == 0u) & (v == 0u) & ~seen));
-                const u64 cm = simd::ballot(cand);
-                f.ok = true;
-                f.k = k;
-                f.cnt = (u32)__builtin_popcount(group_bits(simd::ballot(valid), k));
-                cw = w;
-                cr = r;
-                if (cm) {
-                    const u32 l = (u32)__builtin_ctzll(cm);
-                    f.slot = (i32)(l - gb);
-                    f.r = (i32)simd::readlane(rr, l);
-                }
-                return f;
+            if (!hit) {
+                carry = simd::readlane(incl, 63);
+                return false;
             }
-            carry = simd::readlane(incl, 63);
+            const u32 g = (u32)__builtin_ctzll(hit) >> 3;
+            const u32 k = r * 8 + g, gb = g * 8;
+            const V ex = incl - v;
+            const V rr = (u32)pos - ex;
+            const B valid = w.len != 0u;
+            const B seen = simd::sle(w.rseq, R) & (w.rseq != 0u);
+            const B cand = in_group(k) & valid & (simd::slt(rr, v) | ((rr == 0u) & (v == 0u) & ~seen));
+            const u64 cm = simd::ballot(cand);
+            f.ok = true;
+            f.k = k;
+            f.cnt = (u32)__builtin_popcount(group_bits(simd::ballot(valid), k));
+            cw = w;
+            cr = r;
+            if (cm) {
+                const u32 l = (u32)__builtin_ctzll(cm);
+                f.slot = (i32)(l - gb);
+                f.r = (i32)simd::readlane(rr, l);
+            }
+            return true;
+        };
+        // two row buffers, each refilled while the other is scanned (no register copies per row)
+        Row a = row(0), b;
+        for (u32 r = 0; r < nrows; r += 2) {
+            if (r + 1 < nrows) b = ldrow(r + 1);
+            if (step(a, r)) return f;
+            if (r + 1 >= nrows) break;
+            if (r + 2 < nrows) a = ldrow(r + 2);
+            if (step(b, r + 1)) return f;
         }
         return f;
     }
@@ -427,8 +448,8 @@ struct RegEngine {
 
     // Insert `rec` at slot j of block k (child count cnt); a block reaching 8 children splits 4+4,
     // the new block right after it in document order (needsScour undefined). With `upd`, slot j-1
-    // first takes (len ul, tz uz) (the left piece of a split). Returns the block holding rec.
-    SD u32 insert_slot(u32 k, u32 cnt, u32 j, const RSeg& rec, bool upd, u32 ul, u32 uz) {
+    // first takes (len ul, cap uc) (the left piece of a split). Returns the block holding rec.
+    SD u32 insert_slot(u32 k, u32 cnt, u32 j, const RSeg& rec, bool upd, u32 ul, u32 uc) {
         RG_PROF(RP_INSERT_SLOT);
         if (cnt >= 8 || j > cnt) {
             fail(MTE_DOC_CAPACITY, curSeq);
@@ -444,7 +465,7 @@ struct RegEngine {
         if (upd) {
             const B lf = L() == gb + j - 1;
             w.len = simd::sel(lf, ul, w.len);
-            w.tz = simd::sel(lf, uz, w.tz);
+            w.cap = simd::sel(lf, uc, w.cap);
         }
         auto put = [&](V& x, u32 val) MTE_LI {
             x = simd::sel(mv, simd::row_shr1(x), x);
@@ -455,7 +476,8 @@ struct RegEngine {
         put(w.rseq, rec.rseq);
         put(w.meta, (rec.meta & ~NS_MASK) | (ns << NS_SHIFT));
         put(w.toff, rec.toff);
-        put(w.tz, rec.tz);
+        put(w.cap, rec.cap);
+        put(w.rm, rec.rm);
         put(w.sid, rec.sid);
         putrow(r, w);
         if (cnt + 1 < 8) return k;
@@ -494,7 +516,8 @@ struct RegEngine {
         mv(w.rseq, w2.rseq, 0u);
         mv(w.meta, w2.meta, nsk);  // block k keeps its needsScour in every lane
         mv(w.toff, w2.toff, 0u);
-        mv(w.tz, w2.tz, 0u);
+        mv(w.cap, w2.cap, 0u);
+        mv(w.rm, w2.rm, 0u);
         mv(w.sid, w2.sid, 0u);
         // the new block's needsScour is undefined
         if (r2 == r) {
@@ -511,11 +534,69 @@ struct RegEngine {
     }
 
     // ---------------------------------------------------------------- LRU heap (collections.ts:213-265)
-    SD u32 hkey(u32 q) const { return simd::readlane(HK.get(q >> 6), q & 63); }
-    SD u32 hsid(u32 q) const { return simd::readlane(HS.get(q >> 6), q & 63); }
+    // Position q lives in register q >> 6, lane q & 63. A walk unrolled by heap level names its
+    // registers statically (level d <= 5: register 0; 6: 1; 7: 2..3; 8: 4..7): a VA indexed by a
+    // run-time register number compiles to a v_cndmask chain over all eight registers per access.
+    template <int D>
+    SD static u32 hrd(const simd::VA<8>& A, u32 q) {
+        const u32 l = q & 63u;
+        if constexpr (D <= 5) {
+            return simd::readlane(A.get(0), l);
+        } else if constexpr (D == 6) {
+            return simd::readlane(A.get(1), l);
+        } else if constexpr (D == 7) {
+            const u32 a = simd::readlane(A.get(2), l), b = simd::readlane(A.get(3), l);
+            return (q >> 6) & 1u ? b : a;
+        } else {
+            const u32 a = simd::readlane(A.get(4), l), b = simd::readlane(A.get(5), l);
+            const u32 c = simd::readlane(A.get(6), l), d = simd::readlane(A.get(7), l);
+            const u32 r = (q >> 6) & 3u;
+            return r == 0 ? a : r == 1 ? b : r == 2 ? c : d;
+        }
+    }
+    template <int D>
+    SD static void hwr(simd::VA<8>& A, u32 q, u32 v) {
+        const u32 l = q & 63u;
+        if constexpr (D <= 5) {
+            A.set(0, simd::writelane(A.get(0), l, v));
+        } else if constexpr (D == 6) {
+            A.set(1, simd::writelane(A.get(1), l, v));
+        } else if constexpr (D == 7) {
+            if ((q >> 6) & 1u) A.set(3, simd::writelane(A.get(3), l, v));
+            else A.set(2, simd::writelane(A.get(2), l, v));
+        } else {
+            switch ((q >> 6) & 3u) {
+                case 0: A.set(4, simd::writelane(A.get(4), l, v)); break;
+                case 1: A.set(5, simd::writelane(A.get(5), l, v)); break;
+                case 2: A.set(6, simd::writelane(A.get(6), l, v)); break;
+                default: A.set(7, simd::writelane(A.get(7), l, v)); break;
+            }
+        }
+    }
+    SD static u32 hlevel(u32 q) { return 31u - (u32)__builtin_clz(q); }
+    SD u32 hkey(u32 q) const {  // any position (run-time level)
+        const u32 d = hlevel(q);
+        return d <= 5 ? hrd<0>(HK, q) : d == 6 ? hrd<6>(HK, q) : d == 7 ? hrd<7>(HK, q) : hrd<8>(HK, q);
+    }
+    SD u32 hsid(u32 q) const {
+        const u32 d = hlevel(q);
+        return d <= 5 ? hrd<0>(HS, q) : d == 6 ? hrd<6>(HS, q) : d == 7 ? hrd<7>(HS, q) : hrd<8>(HS, q);
+    }
     SD void hset(u32 q, u32 sid, u32 key) {
-        HK.set(q >> 6, simd::writelane(HK.get(q >> 6), q & 63, key));
-        HS.set(q >> 6, simd::writelane(HS.get(q >> 6), q & 63, sid));
+        const u32 d = hlevel(q);
+        if (d <= 5) {
+            hwr<0>(HK, q, key);
+            hwr<0>(HS, q, sid);
+        } else if (d == 6) {
+            hwr<6>(HK, q, key);
+            hwr<6>(HS, q, sid);
+        } else if (d == 7) {
+            hwr<7>(HK, q, key);
+            hwr<7>(HS, q, sid);
+        } else {
+            hwr<8>(HK, q, key);
+            hwr<8>(HS, q, sid);
+        }
     }
     // push: keys are op seqs, strictly increasing across messages, so the sift-up never moves an
     // entry (collections.ts:241-250 moves strictly larger parents only): an append
@@ -529,31 +610,40 @@ struct RegEngine {
         hset(n, sid, (u32)key);
     }
     // pop: sift-down of collections.ts:252-264 (smaller child, left on ties, moves up while
-    // strictly below the moved last entry)
+    // strictly below the moved last entry (lk, ls)); node k sits at level D, m entries remain
+    template <int D>
+    SD void sift(u32 k, u32 m, u32 lk, u32 ls, i32& newTop) {
+        if constexpr (D < 8) {
+            u32 j = k << 1;
+            if (j <= m) {
+                u32 kj = hrd<D + 1>(HK, j);
+                if (j < m) {
+                    const u32 kj1 = hrd<D + 1>(HK, j + 1);
+                    if ((i32)kj - (i32)kj1 > 0) {
+                        j++;
+                        kj = kj1;
+                    }
+                }
+                if ((i32)lk - (i32)kj > 0) {
+                    if (D == 0) newTop = (i32)kj;
+                    hwr<D>(HK, k, kj);
+                    hwr<D>(HS, k, hrd<D + 1>(HS, j));
+                    sift<D + 1>(j, m, lk, ls, newTop);
+                    return;
+                }
+            }
+        }
+        hwr<D>(HK, k, lk);
+        hwr<D>(HS, k, ls);
+    }
     SD u32 heap_pop() {
         RG_PROF(RP_HEAP);
         RG_COUNT(RP_N_POP, 1);
         const u32 n = heapSize, m = n - 1;
-        const u32 top = hsid(1);
+        const u32 top = hrd<0>(HS, 1);
         const u32 lk = hkey(n), ls = hsid(n);
         i32 newTop = (i32)lk;
-        u32 k = 1;
-        while ((k << 1) <= m) {
-            u32 j = k << 1;
-            u32 kj = hkey(j);
-            if (j < m) {
-                const u32 kj1 = hkey(j + 1);
-                if ((i32)kj - (i32)kj1 > 0) {
-                    j++;
-                    kj = kj1;
-                }
-            }
-            if ((i32)lk - (i32)kj <= 0) break;
-            if (k == 1) newTop = (i32)kj;
-            hset(k, hsid(j), kj);
-            k = j;
-        }
-        if (m >= 1) hset(k, ls, lk);
+        if (m >= 1) sift<0>(1, m, lk, ls, newTop);
         heapTop = newTop;
         heapSize = m;
         return top;
@@ -619,16 +709,16 @@ struct RegEngine {
                 const u32 l = gb + s;
                 const u32 meta = simd::readlane(w.meta, l), toff = simd::readlane(w.toff, l);
                 if ((meta & F_MARKER) || !(toff & ARENA_BIT)) continue;
-                const u32 len = simd::readlane(w.len, l), tz = simd::readlane(w.tz, l);
-                const bool rm = simd::readlane(w.rseq, l) != RSEQ_LIVE;  // tz is the overlap mask then
-                const u32 cap = (rm || tz < len) ? len : tz;
+                const u32 len = simd::readlane(w.len, l), oc = simd::readlane(w.cap, l);
+                const bool rm = simd::readlane(w.rseq, l) != RSEQ_LIVE;
+                const u32 cap = (rm || oc < len) ? len : oc;
                 if ((toff & ~ARENA_BIT) + len > arena_cap || top + cap > arena_cap) {
                     fail(MTE_DOC_CAPACITY, curSeq);
                     return;
                 }
                 copy_text(top, toff, len, dst);
                 w.toff = simd::writelane(w.toff, l, top | ARENA_BIT);
-                if (!rm) w.tz = simd::writelane(w.tz, l, cap);
+                w.cap = simd::writelane(w.cap, l, cap);
                 dirty = true;
                 top += cap;
             }
@@ -645,10 +735,143 @@ struct RegEngine {
     // merge chain, settled live text appends to the chain head under TextSegment.canAppend
     // (textSegment.ts:63-85; no '\n' in these documents, no properties); kept slots are compacted.
     // Returns the new child count.
+    //
+    // Lane-parallel form: in the lean documents this engine replays (no properties, no '\n'), a
+    // settled slot joins the run of the settled slot before it exactly when both are text (a removed
+    // or unsettled slot resets the chain; a marker head or marker slot starts a new one), unless
+    // TextSegment.canAppend's granularity test fails, which needs the run's accumulated length: a
+    // block where a joining slot is longer than GRANULARITY takes the serial walk (scour_serial).
+    // Each run becomes its head with the run's text: already contiguous (no copy), appended into the
+    // head's arena chunk when it has the capacity, or else copied into a fresh chunk of
+    // max(32, 2 * total) units; all copies of the block run as one flattened gather.
     SD u32 scour(u32 k, u32 cnt) {
         RG_PROF(RP_SCOUR);
         RG_COUNT(RP_N_SCOUR, 1);
         if (cnt > 8) cnt = 8;
+        const u32 r = k >> 3, gb = gbase(k);
+        const B ing = in_group(k);
+        Row w = row(r);
+        const B act = ing & (w.len != 0u);
+        const B rem = act & (w.rseq != RSEQ_LIVE);
+        const u32 mDROP = group_bits(simd::ballot(rem & simd::sle(w.rseq, minSeq)), k);
+        const u32 mSET = group_bits(simd::ballot(simd::andn(act, rem) & simd::sle(w.seq, minSeq)), k);
+        const u32 mTXT = group_bits(simd::ballot(act & ((w.meta & F_MARKER) == 0u)), k);
+        const u32 mST = mSET & mTXT;
+        const u32 mJOIN = mST & (mST << 1) & 0xFFu;  // slot s joins the run of slot s-1
+        if (!mDROP && !mJOIN) return cnt;            // nothing dropped, nothing merged
+        if (mJOIN & group_bits(simd::ballot(w.len > (u32)GRANULARITY), k)) return scour_serial(k, cnt);
+        RG_COUNT(RP_N_SCOUR_CHANGED, 1);
+        fence_arena();
+        const V sl = L() & 7u;
+        V jdst = simd::splat(0), jlen = jdst, jsrc = jdst;  // per slot lane: jlen units from jsrc to jdst
+        for (u32 attempt = 0; attempt < 2; attempt++) {
+            // offsets inside a run: exclusive prefix sum of the block's lengths
+            const V gl = simd::sel(ing, w.len, 0u);
+            const V ex = simd::scan_incl(gl) - gl;
+            const B cont = w.toff == simd::row_shr1(w.toff + w.len);  // text starts where slot s-1's ends
+            const u32 mCONT = group_bits(simd::ballot(cont), k);
+            jdst = jlen = simd::splat(0);
+            u32 top = arenaTop, need = 0;
+            Row nw = w;
+            for (u32 heads = mST & ~mJOIN & (mJOIN >> 1); heads; heads &= heads - 1) {
+                const u32 h = (u32)__builtin_ctz(heads);
+                const u32 run = (u32)__builtin_ctz(~(mJOIN >> (h + 1)));  // joining slots after h
+                const u32 e = h + run, rb = ((2u << e) - 1u) & ~((2u << h) - 1u);  // bits h+1..e
+                const u32 lh = gb + h, le = gb + e;
+                const u32 off = simd::readlane(w.toff, lh), cap = simd::readlane(w.cap, lh);
+                const u32 exh = simd::readlane(ex, lh);
+                const u32 total = simd::readlane(ex, le) + simd::readlane(w.len, le) - exh;
+                u32 noff = off, ncap = cap, cbits = 0;
+                if ((mCONT & rb) == rb) {  // the run's text is one contiguous range already
+                    if (off & ARENA_BIT) ncap = simd::readlane(w.toff, le) + simd::readlane(w.cap, le) - off;
+                } else if ((off & ARENA_BIT) && total <= cap) {  // append into the head's chunk
+                    cbits = rb;
+                } else {  // a fresh chunk
+                    ncap = 2 * total < 32 ? 32u : 2 * total;
+                    noff = top | ARENA_BIT;
+                    top += ncap;
+                    need += ncap;
+                    cbits = rb | (1u << h);
+                }
+                if (cbits) {
+                    const B cp = ing & (((simd::splat(cbits) >> sl) & 1u) != 0u);
+                    jdst = simd::sel(cp, ex + (noff - exh), jdst);
+                    jlen = simd::sel(cp, w.len, jlen);
+                }
+                nw.len = simd::writelane(nw.len, lh, total);
+                nw.toff = simd::writelane(nw.toff, lh, noff);
+                nw.cap = simd::writelane(nw.cap, lh, ncap);
+            }
+            if (arenaTop + need <= arena_cap) {
+                arenaTop = top;
+                jsrc = w.toff;  // the slots' text before the runs' heads move
+                w = nw;
+                break;
+            }
+            if (attempt == 1) {
+                fail(MTE_DOC_CAPACITY, curSeq);
+                return cnt;
+            }
+            arena_gc();  // moves every arena text: re-read the slots and redo the runs
+            if (status) return cnt;
+            w = row(r);
+            fence_arena();
+        }
+        copy_runs(jdst, jsrc, jlen);
+        // compaction: kept slots (not dropped, not joined) in order at the front of the group, the
+        // rest behind them; a push permutation (ds_permute) inside the group
+        const u32 mKEEP = group_bits(simd::ballot(act), k) & ~mDROP & ~mJOIN;
+        const u32 nkeep = (u32)__builtin_popcount(mKEEP);
+        const V below = (simd::shl(simd::splat(1), sl) - 1u);
+        const B kp = ((simd::splat(mKEEP) >> sl) & 1u) != 0u;
+        const V dst = simd::sel(ing, simd::sel(kp, simd::bcnt(simd::splat(mKEEP) & below),
+                                               simd::bcnt(simd::splat(~mKEEP & 0xFFu) & below) + nkeep) + gb,
+                                L());
+        const B tail = ing & (sl >= nkeep);
+        auto cmp = [&](V& x, u32 keepEmpty) MTE_LI {
+            const V nv = simd::push(x, dst);
+            x = simd::sel(tail, nv & keepEmpty, nv);
+        };
+        cmp(w.len, 0u);
+        cmp(w.seq, 0u);
+        cmp(w.rseq, 0u);
+        cmp(w.meta, NS_MASK);  // the block's needsScour stays in every lane
+        cmp(w.cap, 0u);
+        cmp(w.toff, 0u);
+        cmp(w.rm, 0u);
+        cmp(w.sid, 0u);
+        putrow(r, w);
+        return nkeep;
+    }
+    // The runs' text copies of one block as one flattened gather: slot lane l copies jlen units from
+    // its text src to jdst (sources are never destinations of the same scour).
+    SD void copy_runs(V jdst, V jsrc, V jlen) {
+        const V jinc = simd::scan_incl(jlen);
+        const u32 total = simd::readlane(jinc, 63);
+        if (!total) return;
+        const V jstart = jinc - jlen;
+        u64 jm = simd::ballot(jlen != 0u);
+        u16* ar = arena_cur();
+        for (u32 base = 0; base < total; base += 64) {
+            const V f = L() + base;
+            V j = simd::splat(0);
+            for (u64 m = jm; m; m &= m - 1) {
+                const u32 q = (u32)__builtin_ctzll(m);
+                j = simd::sel(f >= simd::readlane(jstart, q), q, j);
+            }
+            const V s0 = simd::bperm(jstart, j), d = simd::bperm(jdst, j), sr = simd::bperm(jsrc, j);
+            const B m = f < total;
+            const V o = f - s0;
+            const B fa = (sr & ARENA_BIT) != 0u;
+            const V so = (sr & ~ARENA_BIT) + o;
+            const V t = simd::sel(fa, simd::ld(ar, so, m & fa), simd::ld(payload, so, simd::andn(m, fa)));
+            simd::st(ar, (d & ~ARENA_BIT) + o, t, m);
+        }
+        adirty = true;
+    }
+    // The serial walk of scourNode (any lengths): the granularity test needs the run's accumulated
+    // length.
+    SD u32 scour_serial(u32 k, u32 cnt) {
         fence_arena();
         const u32 r = k >> 3, gb = gbase(k);
         const B ing = in_group(k);
@@ -659,7 +882,6 @@ struct RegEngine {
         const u32 mKEPT = group_bits(simd::ballot(rem & simd::sgt(w.rseq, minSeq)), k);
         const u32 mSET = group_bits(simd::ballot(simd::andn(act, rem) & simd::sle(w.seq, minSeq)), k);
         if (!(mREM & ~mKEPT) && !(mSET & (mSET << 1))) return cnt;  // nothing dropped, nothing to merge
-        RG_COUNT(RP_N_SCOUR_CHANGED, 1);
         const u32 mTXT = group_bits(simd::ballot(act & ((w.meta & F_MARKER) == 0u)), k);
         u32 nkeep = 0, jn = 0;
         V kSrc = simd::splat(0), kLen = kSrc, kOff = kSrc, kCap = kSrc;  // lane i: kept slot i
@@ -687,7 +909,7 @@ struct RegEngine {
                     prev = -1;
                 } else if (mSET & bit) {
                     const u32 ln = simd::readlane(w.len, gb + s), to = simd::readlane(w.toff, gb + s);
-                    const u32 tc = simd::readlane(w.tz, gb + s);
+                    const u32 tc = simd::readlane(w.cap, gb + s);
                     const bool ok = prev >= 0 && pText && (mTXT & bit) && (pLen <= (u32)GRANULARITY || ln <= (u32)GRANULARITY);
                     if (ok) {  // TextSegment.append
                         if ((pOff & ARENA_BIT) && pLen + ln <= pCap) {
@@ -733,7 +955,7 @@ struct RegEngine {
                     kSrc = simd::writelane(kSrc, nkeep, s);
                     kLen = simd::writelane(kLen, nkeep, simd::readlane(w.len, gb + s));
                     kOff = simd::writelane(kOff, nkeep, simd::readlane(w.toff, gb + s));
-                    kCap = simd::writelane(kCap, nkeep, simd::readlane(w.tz, gb + s));
+                    kCap = simd::writelane(kCap, nkeep, simd::readlane(w.cap, gb + s));
                     nkeep++;
                 }
             }
@@ -761,7 +983,8 @@ struct RegEngine {
         };
         cmp(w.len, &kLen, 0u);
         cmp(w.toff, &kOff, 0u);
-        cmp(w.tz, &kCap, 0u);
+        cmp(w.cap, &kCap, 0u);
+        cmp(w.rm, nullptr, 0u);
         cmp(w.seq, nullptr, 0u);
         cmp(w.rseq, nullptr, 0u);
         cmp(w.meta, nullptr, NS_MASK);  // the block's needsScour stays in every lane
@@ -826,7 +1049,8 @@ struct RegEngine {
         t.rseq = gather(a.rseq, b.rseq);
         t.meta = gather(a.meta, b.meta) & ~NS_MASK;  // packed blocks: needsScour undefined
         t.toff = gather(a.toff, b.toff);
-        t.tz = gather(a.tz, b.tz);
+        t.cap = gather(a.cap, b.cap);
+        t.rm = gather(a.rm, b.rm);
         t.sid = gather(a.sid, b.sid);
         const i32 d = (i32)kk - (i32)m;
         shift_blocks(k0 + m, d);
@@ -848,7 +1072,8 @@ struct RegEngine {
             put(w.rseq, t.rseq);
             put(w.meta, t.meta);
             put(w.toff, t.toff);
-            put(w.tz, t.tz);
+            put(w.cap, t.cap);
+            put(w.rm, t.rm);
             put(w.sid, t.sid);
             strow(rr, w);
         }
@@ -934,19 +1159,19 @@ struct RegEngine {
         t.rseq = simd::readlane(w.rseq, l);
         t.meta = simd::readlane(w.meta, l);
         t.toff = simd::readlane(w.toff, l);
-        t.tz = simd::readlane(w.tz, l);
+        t.cap = simd::readlane(w.cap, l);
+        t.rm = simd::readlane(w.rm, l);
         const u32 sid = new_sid();
         if (sid == NONE) return NONE;
         const u32 rr = (u32)f.r;
-        const bool rm = t.rseq != RSEQ_LIVE;  // tz is the overlap mask then
-        const bool ar = (t.toff & ARENA_BIT) != 0;
-        const u32 lz = rm ? t.tz : (ar ? rr : 0u);
+        const bool ar = (t.toff & ARENA_BIT) != 0;  // arena text: cap >= len, split between the pieces
+        const u32 lc = ar ? rr : 0u;
         RSeg right = t;
         right.len = t.len - rr;
         right.toff = t.toff + rr;
-        right.tz = rm ? t.tz : (ar ? t.tz - rr : 0u);
+        right.cap = ar ? t.cap - rr : 0u;
         right.sid = sid;
-        return insert_slot(f.k, f.cnt, (u32)f.slot + 1, right, true, rr, lz);
+        return insert_slot(f.k, f.cnt, (u32)f.slot + 1, right, true, rr, lc);
     }
 
     // insertSegments (mergeTree.ts:1968-1998): split at pos, then place the new segment.
@@ -1008,9 +1233,7 @@ struct RegEngine {
             if (!mm) continue;
             const B was = mark & (w.rseq != RSEQ_LIVE);  // already removed: addOverlappingClient
             const B fresh = simd::andn(mark, was);
-            // the overlap mask starts empty at the first removal (tz is dead then), so it is written
-            // only when a client joins it
-            if (simd::ballot(was)) w.tz = simd::sel(was, simd::sel((w.meta & F_OVL) != 0u, w.tz | cbit, simd::splat(cbit)), w.tz);
+            w.rm = simd::sel(mark, w.rm | cbit, w.rm);
             w.meta = simd::sel(was, w.meta | F_OVL, simd::sel(fresh, (w.meta & ~0xFF00u) | (C << 8) | F_REMOVED, w.meta));
             w.rseq = simd::sel(fresh, (u32)seq, w.rseq);
             putrow(r, w);
@@ -1060,7 +1283,8 @@ struct RegEngine {
             rec.rseq = RSEQ_LIVE;
             rec.meta = (C & 0xFFu) | (RCL_LIVE << 8) | (mk ? F_MARKER : 0u);
             rec.toff = mk ? op.b : (u32)op.a;
-            rec.tz = 0;
+            rec.cap = 0;
+            rec.rm = 0;
             rec.sid = 0;
             edited = op_insert(op.pos1, R, C, seq, rec);
             n_ops++;
@@ -1194,8 +1418,10 @@ struct RegEngine {
                 const B live = w.rseq == RSEQ_LIVE;
                 const B hasov = (w.meta & F_OVL) != 0u;
                 const V m2 = simd::sel(live, w.meta & ~0xFF00u, w.meta) & ~NS_MASK;
-                const V ovl = simd::sel(hasov, w.tz, 0u);
-                const V z2 = simd::sel(simd::andn(~live, hasov), 0u, w.tz);  // removed, no overlap: empty mask
+                // removedClientOverlap = the removers but removedClient (the LDS engine's format)
+                const V ovm = w.rm & (simd::shl(simd::splat(1), simd::bfe(w.meta, 8, 8)) ^ 0xFFFFFFFFu);
+                const V ovl = simd::sel(hasov, ovm, 0u);
+                const V z2 = simd::sel(live, w.cap, ovl);
                 const V t4 = at * 4u;
                 simd::st(ov, t4, w.len, have);
                 simd::st(ov, t4 + 1u, w.seq, have);

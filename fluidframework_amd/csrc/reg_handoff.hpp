@@ -89,8 +89,11 @@ MTE_DEV void reg_handoff(R& r, E& e) {
         const uint4 v = e.VIS()[64 * rr + L], a = e.AUX()[64 * rr + L];
         const bool live = v.z == RSEQ_LIVE, ov = (v.w & F_OVL) != 0;
         const u32 m2 = (live ? (v.w & ~0xFF00u) : v.w) & ~NS_MASK;
+        // aux.z: a live segment's text capacity, a removed one's removedClientOverlap (rm without
+        // removedClient) or 0
+        const u32 ovm = a.z & ~(1u << ((v.w >> 8) & 31u));
         e.VIS()[64 * rr + L] = make_uint4(v.x, v.y, live ? 0u : v.z, m2);
-        e.AUX()[64 * rr + L] = make_uint4(0u, a.y, !live && !ov ? 0u : a.z, a.w);
+        e.AUX()[64 * rr + L] = make_uint4(0u, a.y, live ? a.x : (ov ? ovm : 0u), a.w);
     }
     // replay state and per-document counters
     St& st = e.st;

@@ -55,6 +55,7 @@ SD V operator*(V a, u32 b) { return {a.x * b}; }
 SD V operator<<(V a, u32 s) { return {a.x << s}; }
 SD V operator>>(V a, u32 s) { return {a.x >> s}; }
 SD V operator>>(V a, V s) { return {a.x >> s.x}; }
+SD V shl(V a, V s) { return {a.x << (s.x & 31u)}; }  // per-lane shift count (low 5 bits, as v_lshlrev)
 SD V bfe(V a, u32 off, u32 w) { return {__builtin_amdgcn_ubfe(a.x, off, w)}; }
 
 // unsigned compares
@@ -89,6 +90,9 @@ extern "C" __device__ int mte_llvm_writelane(int, int, int) __asm("llvm.amdgcn.w
 SD V writelane(V v, u32 l, u32 s) { return {(u32)mte_llvm_writelane((int)s, (int)l, (int)v.x)}; }
 // v from lane src[l] for every lane l (ds_bpermute: LDS crossbar, no LDS memory)
 SD V bperm(V v, V src) { return {(u32)__builtin_amdgcn_ds_bpermute((int)(src.x << 2), (int)v.x)}; }
+// lane l's v to lane dst[l] (ds_permute; dst must be a permutation of the lanes)
+SD V push(V v, V dst) { return {(u32)__builtin_amdgcn_ds_permute((int)(dst.x << 2), (int)v.x)}; }
+SD V bcnt(V v) { return {(u32)__builtin_popcount(v.x)}; }
 
 // Inclusive prefix sum over the 64 lanes (DPP row_shr 1/2/4/8, row_bcast 15/31).
 SD V scan_incl(V v) {
@@ -212,6 +216,11 @@ SD V operator>>(V a, V s) {
     MTE_L r.x[l] = a.x[l] >> (s.x[l] & 31);
     return r;
 }
+SD V shl(V a, V s) {
+    V r;
+    MTE_L r.x[l] = a.x[l] << (s.x[l] & 31);
+    return r;
+}
 SD V bfe(V a, u32 off, u32 w) {
     V r;
     MTE_L r.x[l] = (a.x[l] >> off) & (w >= 32 ? 0xFFFFFFFFu : ((1u << w) - 1u));
@@ -259,6 +268,22 @@ SD V writelane(V v, u32 l, u32 s) {
 SD V bperm(V v, V src) {
     V r;
     MTE_L r.x[l] = v.x[src.x[l] & 63];
+    return r;
+}
+SD V push(V v, V dst) {
+    V r;
+    bool hit[64] = {false};
+    MTE_L {
+        const u32 d = dst.x[l] & 63;
+        if (hit[d]) __builtin_trap();  // not a permutation
+        hit[d] = true;
+        r.x[d] = v.x[l];
+    }
+    return r;
+}
+SD V bcnt(V v) {
+    V r;
+    MTE_L r.x[l] = (u32)__builtin_popcount(v.x[l]);
     return r;
 }
 SD V scan_incl(V v) {

@@ -91,3 +91,34 @@ def test_markers_and_concurrent_writers_from_json(seed):
     assert (ops["type"] == mte.MTE_OP_INSERT_MARKER).sum() > 50
     res = regcpu.compare(ops, pay, names=names)
     assert int(res["n_segs"]) == len(json.loads(d.segments_json()))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_long_segments_granularity(seed):
+    """Inserts of 1..600 characters: zamboni's merge runs meet TextSegment.canAppend's granularity
+    test (textSegment.ts:63-85, either side <= 256 by the run's accumulated length), which the
+    lane-parallel scour hands to the serial walk; short runs merge lane-parallel, contiguous or not."""
+    from oracle import OracleDoc
+
+    rng = random.Random(100 + seed)
+    d = OracleDoc()
+    msgs, refs, seq, order = [], {c: 0 for c in "abc"}, 0, []
+    for _ in range(1200):
+        c = rng.choice("abc")
+        refs[c] = rng.randint(max(refs[c], seq - 6), seq)
+        if c not in order:
+            order.append(c)
+        L = d.length_at(refs[c], order.index(c) + 1)
+        if L == 0 or rng.random() < 0.6:
+            n = rng.choice([1, 2, 5, 40, 120, 250, 257, 300, 600])
+            contents = ins(rng.randint(0, L), "".join(rng.choice("xyz") for _ in range(n)))
+        else:
+            a = rng.randint(0, L - 1)
+            contents = rem(a, min(L, a + rng.randint(1, 30)))
+        seq += 1
+        m = msg(c, seq, refs[c], contents, min(refs.values()))
+        msgs.append(m)
+        d.apply_json(dumps([m]))
+    ops, pay, names = _builder_ops(msgs)
+    res = regcpu.compare(ops, pay, names=names)
+    assert int(res["n_segs"]) == len(json.loads(d.segments_json()))

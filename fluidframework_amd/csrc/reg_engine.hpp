@@ -106,6 +106,8 @@ struct RFound {
     u32 cnt;   // its child count
     i32 slot;  // first qualifying slot, -1 => append at the block end
     i32 r;     // pos - cumBefore(slot)
+    u32 row;   // the row of block k
+    u32 carry; // visible length before that row
 };
 
 template <int NR = (int)RG_ROWS>
@@ -302,12 +304,14 @@ struct RegEngine {
             failSeq = seq;
         }
     }
+    // Segment ids are 1-based in the rows (an empty slot holds 0), the LDS engine's id + 1: the
+    // heap's segment lookup compares ids alone. finish() and the handoff write id - 1.
     SD u32 new_sid() {
         if (segNext >= seg_cap) {
             fail(MTE_DOC_CAPACITY, curSeq);
             return NONE;
         }
-        return segNext++;
+        return ++segNext;
     }
 
     // ---------------------------------------------------------------- blocks
@@ -331,14 +335,16 @@ struct RegEngine {
     // (live: rseq RSEQ_LIVE and rm 0; removed: bit C of rm covers removedClient and the overlap set)
     SD static V vis(const Row& w, i32 R, u32 C) {
         const B ins = simd::sle(w.seq, R) | (simd::bfe(w.meta, 0, 8) == C);
-        const B rem = simd::sle(w.rseq, R) | (((w.rm >> C) & 1u) != 0u);
+        const B rem = simd::sle(w.rseq, R) | ((w.rm & (1u << C)) != 0u);
         return simd::sel(simd::andn(ins, rem), w.len, 0u);
     }
 
     // insertingWalk's target for `pos` in the (R, C) view: the first leaf block whose cumulative
     // visible end is >= pos, then inside it the first slot with pos < its end, or a zero-length slot
     // at pos that wins breakTie (skip tombstones already seen at R, mergeTree.ts:2257-2261).
-    SD RFound resolve(i32 pos, i32 R, u32 C) {
+    // The scan starts at row r0 with the visible length before it, carry0 (a previous resolve of
+    // the same op found its block in r0: rows before it are unchanged by the splits since).
+    SD RFound resolve(i32 pos, i32 R, u32 C, u32 r0 = 0, u32 carry0 = 0) {
         RG_PROF(RP_RESOLVE);
         RFound f;
         f.ok = false;
@@ -346,24 +352,18 @@ struct RegEngine {
         f.cnt = 0;
         f.slot = -1;
         f.r = 0;
+        f.row = 0;
+        f.carry = 0;
         const u32 nrows = (n_lb + 7) >> 3;
-        u32 carry = 0;
-        const V lk = L() >> 3;
-        // one row: its visible lengths, their prefix sum, and the first block end reaching pos
-        auto step = [&](const Row& w, u32 r) MTE_LI {
-            RG_COUNT(RP_N_RESOLVE, 1);
-            const V v = vis(w, R, C);
-            const V incl = simd::scan_incl(v) + carry;
-            const B end = ((L() & 7u) == 7u) & ((lk + r * 8u) < n_lb);
-            const u64 hit = simd::ballot(end & simd::sge(incl, pos));
-            if (!hit) {
-                carry = simd::readlane(incl, 63);
-                return false;
-            }
+        u32 carry = carry0;
+        // Block ends are the lanes 8g+7; blocks past n_lb are empty (rows past the last block stay
+        // zero), so their ends never reach pos before a real block's end does.
+        const B end = (L() & 7u) == 7u;
+        // the hit row: the block and slot from the registers of the scan
+        auto hit_row = [&](const Row& w, u32 r, u64 hit, const V& v, const V& incl) MTE_LI {
             const u32 g = (u32)__builtin_ctzll(hit) >> 3;
             const u32 k = r * 8 + g, gb = g * 8;
-            const V ex = incl - v;
-            const V rr = (u32)pos - ex;
+            const V rr = (u32)pos - (incl - v);
             const B valid = w.len != 0u;
             const B seen = simd::sle(w.rseq, R) & (w.rseq != 0u);
             const B cand = in_group(k) & valid & (simd::slt(rr, v) | ((rr == 0u) & (v == 0u) & ~seen));
@@ -371,6 +371,8 @@ struct RegEngine {
             f.ok = true;
             f.k = k;
             f.cnt = (u32)__builtin_popcount(group_bits(simd::ballot(valid), k));
+            f.row = r;
+            f.carry = carry;
             cw = w;
             cr = r;
             if (cm) {
@@ -378,17 +380,40 @@ struct RegEngine {
                 f.slot = (i32)(l - gb);
                 f.r = (i32)simd::readlane(rr, l);
             }
-            return true;
         };
-        // two row buffers, each refilled while the other is scanned (no register copies per row)
-        Row a = row(0), b;
-        for (u32 r = 0; r < nrows; r += 2) {
-            if (r + 1 < nrows) b = ldrow(r + 1);
-            if (step(a, r)) return f;
-            if (r + 1 >= nrows) break;
-            if (r + 2 < nrows) a = ldrow(r + 2);
-            if (step(b, r + 1)) return f;
+        // two row buffers, each refilled (unconditionally: the last row again at the end, so the
+        // LDS counter wait stays exact) while the other one is scanned; the loop only finds the hit
+        // row (no state written in it, so no per-row register copies)
+        const u32 last = nrows - 1;
+        Row a = row(r0), b;
+        V v, incl;
+        u64 hit = 0;
+        bool inb = false;
+        u32 r = r0;
+        for (;;) {
+            b = ldrow(r + 1 < last ? r + 1 : last);
+            RG_COUNT(RP_N_RESOLVE, 1);
+            v = vis(a, R, C);
+            incl = simd::scan_incl(v) + carry;
+            hit = simd::ballot(end & simd::sge(incl, pos));
+            if (hit) break;
+            carry = simd::readlane(incl, 63);
+            if (++r >= nrows) break;
+            a = ldrow(r + 1 < last ? r + 1 : last);
+            RG_COUNT(RP_N_RESOLVE, 1);
+            v = vis(b, R, C);
+            incl = simd::scan_incl(v) + carry;
+            hit = simd::ballot(end & simd::sge(incl, pos));
+            if (hit) {
+                inb = true;
+                break;
+            }
+            carry = simd::readlane(incl, 63);
+            if (++r >= nrows) break;
         }
+        if (!hit) return f;
+        if (inb) a = b;
+        hit_row(a, r, hit, v, incl);
         return f;
     }
 
@@ -660,15 +685,11 @@ struct RegEngine {
     SD u32 find_seg(u32 sid) {
         RG_PROF(RP_FIND_SEG);
         const u32 nrows = (n_lb + 7) >> 3;
-        for (u32 r0 = 0; r0 < nrows; r0 += 4) {  // four rows' reads in flight per round
-            V s4[4], l4[4];
-            for (u32 i = 0; i < 4; i++) {
-                const u32 r = r0 + i < nrows ? r0 + i : r0;
-                s4[i] = ld_sid(r);
-                l4[i] = ld_len(r);
-            }
-            for (u32 i = 0; i < 4 && r0 + i < nrows; i++) {
-                const u64 m = simd::ballot((s4[i] == sid) & (l4[i] != 0u));
+        for (u32 r0 = 0; r0 < nrows; r0 += 8) {  // eight rows' reads in flight per round
+            V s8[8];
+            for (u32 i = 0; i < 8; i++) s8[i] = ld_sid(r0 + i < nrows ? r0 + i : r0);
+            for (u32 i = 0; i < 8 && r0 + i < nrows; i++) {
+                const u64 m = simd::ballot(s8[i] == sid);
                 if (m) return (r0 + i) * 8 + ((u32)__builtin_ctzll(m) >> 3);
             }
         }
@@ -1213,16 +1234,23 @@ struct RegEngine {
     // markRangeRemoved (mergeTree.ts:2607-2719): split at p1 and p2, then mark [p1, p2) of the
     // (R, C) view before the op: first remover wins, later ones join removedClientOverlap.
     SD bool op_remove(i32 p1, i32 p2, i32 R, u32 C, i32 seq) {
+        // the p2 resolve and the marking start at p1's row: nothing before it moves or changes
+        // visible length (a split keeps the lengths, a block split shifts only later blocks)
+        u32 r1 = 0, c1 = 0;
         for (u32 ph = 0; ph < 2; ph++) {
-            const RFound f = resolve(ph ? p2 : p1, R, C);
+            const RFound f = resolve(ph ? p2 : p1, R, C, r1, c1);
+            if (ph == 0 && f.ok) {
+                r1 = f.row;
+                c1 = f.carry;
+            }
             if (!f.ok || !(f.slot >= 0 && f.r > 0)) continue;
             if (split_at(f) == NONE || status) return false;
         }
         RG_PROF(RP_RANGE);
         const u32 nrows = (n_lb + 7) >> 3;
-        u32 carry = 0;
+        u32 carry = c1;
         const u32 cbit = 1u << C;
-        for (u32 r = 0; r < nrows && (i32)carry < p2; r++) {
+        for (u32 r = r1; r < nrows && (i32)carry < p2; r++) {
             Row w = row(r);
             const V v = vis(w, R, C);
             const V incl = simd::scan_incl(v) + carry;
@@ -1430,7 +1458,7 @@ struct RegEngine {
                 simd::st(oa, t4, simd::splat(0), have);
                 simd::st(oa, t4 + 1u, simd::sel(txt, tat, w.toff), have);
                 simd::st(oa, t4 + 2u, z2, have);
-                simd::st(oa, t4 + 3u, w.sid, have);
+                simd::st(oa, t4 + 3u, w.sid - 1u, have);
                 simd::st(oo, at * 2u, ovl, have);
                 simd::st(oo, at * 2u + 1u, simd::splat(0), have);
                 // text, one segment at a time, 64 units per step

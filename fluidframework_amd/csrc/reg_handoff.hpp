@@ -80,7 +80,7 @@ MTE_DEV void reg_handoff(R& r, E& e) {
     for (u32 q0 = 0; q0 <= r.heapSize; q0 += 64) {
         const u32 q = q0 + L;
         const u32 hk = r.HK.get(q0 >> 6).x, hs = r.HS.get(q0 >> 6).x;
-        if (q >= 1 && q <= r.heapSize) e.HEAP()[q] = make_uint2(hs, hk);
+        if (q >= 1 && q <= r.heapSize) e.HEAP()[q] = make_uint2(hs - 1u, hk);  // ids 1-based in the rows
     }
     // slots: row rr lane l is block 8*rr + l/8, slot l%8 = the LDS engine's slot index 64*rr + l,
     // already in place; only the encoding of live segments and needsScour differ
@@ -93,7 +93,7 @@ MTE_DEV void reg_handoff(R& r, E& e) {
         // removedClient) or 0
         const u32 ovm = a.z & ~(1u << ((v.w >> 8) & 31u));
         e.VIS()[64 * rr + L] = make_uint4(v.x, v.y, live ? 0u : v.z, m2);
-        e.AUX()[64 * rr + L] = make_uint4(0u, a.y, live ? a.x : (ov ? ovm : 0u), a.w);
+        e.AUX()[64 * rr + L] = make_uint4(0u, a.y, live ? a.x : (ov ? ovm : 0u), v.x ? a.w - 1u : 0u);
     }
     // replay state and per-document counters
     St& st = e.st;

@@ -661,6 +661,42 @@ struct RegEngine {
         hwr<D>(HK, k, lk);
         hwr<D>(HS, k, ls);
     }
+    // The same sift-down, lane-parallel while the heap fits positions 1..127 (registers 0 and 1):
+    // every node k of register 0 (lane k) picks its child c(k) and whether the moved entry goes
+    // below it (lk > K[c(k)]) at once; the path from the root is then a chain of readlanes of
+    // next(k), and every node on it above the stop node takes its child's entry in one select.
+    SD void pop_fast(u32 m, u32 lk, u32 ls, i32& newTop) {
+        const V K0 = HK.get(0), K1 = HK.get(1), S0 = HS.get(0), S1 = HS.get(1);
+        const V cl = L() * 2u, cr = cl + 1u;
+        const V kL = simd::sel(cl < 64u, simd::bperm(K0, cl & 63u), simd::bperm(K1, cl & 63u));
+        const V kR = simd::sel(cr < 64u, simd::bperm(K0, cr & 63u), simd::bperm(K1, cr & 63u));
+        const B right = (cr < m + 1u) & simd::slt(kR, kL);  // smaller child, the left one on ties
+        const V c = simd::sel(right, cr, cl);
+        const V kc = simd::sel(right, kR, kL);
+        const B go = (cl < m + 1u) & simd::slt(kc, (i32)lk);  // the moved entry goes below k
+        const V nxt = simd::sel(go, c, 0u);
+        u32 k = 1;
+        u64 path = 0;  // nodes of register 0 that take their child's entry
+        while (k < 64u) {
+            const u32 nk = simd::readlane(nxt, k);
+            if (!nk) break;
+            path |= 1ull << k;
+            k = nk;
+        }
+        const B mv = simd::ballot_mask(path);
+        const V sc = simd::sel(c < 64u, simd::bperm(S0, c & 63u), simd::bperm(S1, c & 63u));
+        V N0 = simd::sel(mv, kc, K0), T0 = simd::sel(mv, sc, S0);
+        if (path & 2u) newTop = (i32)simd::readlane(kc, 1);
+        if (k < 64u) {
+            N0 = simd::writelane(N0, k, lk);
+            T0 = simd::writelane(T0, k, ls);
+        } else {
+            HK.set(1, simd::writelane(K1, k & 63u, lk));
+            HS.set(1, simd::writelane(S1, k & 63u, ls));
+        }
+        HK.set(0, N0);
+        HS.set(0, T0);
+    }
     SD u32 heap_pop() {
         RG_PROF(RP_HEAP);
         RG_COUNT(RP_N_POP, 1);
@@ -668,7 +704,10 @@ struct RegEngine {
         const u32 top = hrd<0>(HS, 1);
         const u32 lk = hkey(n), ls = hsid(n);
         i32 newTop = (i32)lk;
-        if (m >= 1) sift<0>(1, m, lk, ls, newTop);
+        if (m >= 1) {
+            if (m < 128u) pop_fast(m, lk, ls, newTop);
+            else sift<0>(1, m, lk, ls, newTop);
+        }
         heapTop = newTop;
         heapSize = m;
         return top;

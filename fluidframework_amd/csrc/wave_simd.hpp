@@ -73,6 +73,7 @@ SD B sle(V a, i32 b) { return {(u32)((i32)a.x <= b)}; }
 SD B sgt(V a, i32 b) { return {(u32)((i32)a.x > b)}; }
 SD B sge(V a, i32 b) { return {(u32)((i32)a.x >= b)}; }
 SD B slt(V a, i32 b) { return {(u32)((i32)a.x < b)}; }
+SD B slt(i32 a, V b) { return {(u32)(a < (i32)b.x)}; }
 
 SD B operator&(B a, B b) { return {a.b & b.b}; }
 SD B operator|(B a, B b) { return {a.b | b.b}; }
@@ -84,6 +85,8 @@ SD V sel(B c, u32 a, V b) { return {c.b ? a : b.x}; }
 SD V sel(B c, V a, u32 b) { return {c.b ? a.x : b}; }
 
 SD u64 ballot(B c) { return __ballot(c.b != 0); }
+// the per-lane predicate of a uniform 64-bit mask (lane l: bit l)
+SD B ballot_mask(u64 m) { return {(u32)((m >> __lane_id()) & 1ull)}; }
 SD u32 readlane(V v, u32 l) { return __builtin_amdgcn_readlane(v.x, l); }
 // v_writelane_b32 through the LLVM intrinsic (this clang has no __builtin for it)
 extern "C" __device__ int mte_llvm_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
@@ -245,6 +248,7 @@ MTE_CMP(sle(V a, i32 b), (i32)a.x[l] <= b)
 MTE_CMP(sgt(V a, i32 b), (i32)a.x[l] > b)
 MTE_CMP(sge(V a, i32 b), (i32)a.x[l] >= b)
 MTE_CMP(slt(V a, i32 b), (i32)a.x[l] < b)
+MTE_CMP(slt(i32 a, V b), a < (i32)b.x[l])
 #undef MTE_CMP
 SD B operator&(B a, B b) { return {a.m & b.m}; }
 SD B operator|(B a, B b) { return {a.m | b.m}; }
@@ -260,6 +264,7 @@ SD V sel(B c, u32 a, V b) { return sel(c, splat(a), b); }
 SD V sel(B c, V a, u32 b) { return sel(c, a, splat(b)); }
 
 SD u64 ballot(B c) { return c.m; }
+SD B ballot_mask(u64 m) { return {m}; }
 SD u32 readlane(V v, u32 l) { return v.x[l & 63]; }
 SD V writelane(V v, u32 l, u32 s) {
     v.x[l & 63] = s;

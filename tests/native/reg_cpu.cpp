@@ -62,4 +62,32 @@ uint64_t regcpu_replay(const mte_op* ops, uint64_t n_ops, const uint16_t* payloa
 }
 
 uint32_t regcpu_docres_size(void) { return (uint32_t)sizeof(DocRes); }
+
+// The engine's LRU heap alone: ops[i] > 0 pushes (segment id i + 1, key ops[i]), ops[i] == 0 pops.
+// Writes the popped segment ids in order; returns how many (the heap's own sift rules, both the
+// lane-parallel and the serial pop, against tests/test_reg_engine_cpu.py's restatement).
+uint32_t regcpu_heap(const int32_t* ops, uint32_t n, uint32_t* popped) {
+    DocCfg cfg;
+    memset(&cfg, 0, sizeof cfg);
+    cfg.seg_cap = 1;
+    cfg.arena_cap = 1;
+    Params p;
+    memset(&p, 0, sizeof p);
+    p.docs = &cfg;
+    p.n_docs = 1;
+    uint16_t pay[2] = {0, 0};
+    p.payload = pay;
+    p.arena = pay;
+    RegEngine<>* e = new RegEngine<>(p, 0);
+    uint32_t np = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (ops[i] > 0) {
+            e->heap_push(i + 1, ops[i]);
+        } else if (e->heapSize) {
+            popped[np++] = e->heap_pop();
+        }
+    }
+    delete e;
+    return np;
+}
 }

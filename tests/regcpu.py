@@ -35,6 +35,8 @@ def lib():
         L.regcpu_replay.restype = u64
         L.regcpu_replay.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u32, vp, u64, vp]
         L.regcpu_docres_size.restype = u32
+        L.regcpu_heap.restype = u32
+        L.regcpu_heap.argtypes = [vp, u32, vp]
         assert L.regcpu_docres_size() == DOCRES.itemsize
         _lib = L
     return _lib

@@ -122,3 +122,55 @@ def test_long_segments_granularity(seed):
     ops, pay, names = _builder_ops(msgs)
     res = regcpu.compare(ops, pay, names=names)
     assert int(res["n_segs"]) == len(json.loads(d.segments_json()))
+
+
+def _heap_pops(ops):
+    """collections.ts:213-265 restated: push appends then sifts up while the parent is strictly
+    larger; pop moves the last entry to the root and sifts down to the smaller child (left on
+    ties) while that child is strictly smaller."""
+    h, out = [None], []
+    for i, k in enumerate(ops):
+        if k > 0:
+            h.append((k, i + 1))
+            j = len(h) - 1
+            while j > 1 and h[j // 2][0] > h[j][0]:
+                h[j // 2], h[j] = h[j], h[j // 2]
+                j //= 2
+        elif len(h) > 1:
+            out.append(h[1][1])
+            last = h.pop()
+            if len(h) > 1:
+                h[1] = last
+                k2, m = 1, len(h) - 1
+                while 2 * k2 <= m:
+                    j = 2 * k2
+                    if j < m and h[j][0] > h[j + 1][0]:
+                        j += 1
+                    if last[0] <= h[j][0]:
+                        break
+                    h[k2] = h[j]
+                    k2 = j
+                h[k2] = last
+    return out
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_lru_heap_pop_order(seed):
+    """The engine's heap (lane-parallel pop up to 127 entries, serial beyond) pops in exactly the
+    reference heap's order, ties included (keys are op seqs: non-decreasing pushes, runs of equal
+    keys from one op)."""
+    rng = random.Random(seed)
+    ops, key, size = [], 1, 0
+    target = [20, 100, 126, 127, 128, 300][seed]
+    for _ in range(6000):
+        if size < target and (size == 0 or rng.random() < 0.55):
+            key += rng.choice([0, 0, 1, 1, 2])
+            ops.append(key)
+            size += 1
+        else:
+            ops.append(0)
+            size -= 1
+    arr = np.array(ops, dtype=np.int32)
+    out = np.zeros(len(ops), dtype=np.uint32)
+    n = regcpu.lib().regcpu_heap(arr.ctypes.data, len(ops), out.ctypes.data)
+    assert list(out[:n]) == _heap_pops(ops)

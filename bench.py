@@ -275,6 +275,8 @@ def run(args):
             "extra": {"ops_per_step_rank0": ops_applied, "longest_doc_ops": int(counts.max()),
                       "solo_docs": info["solo"], "solo_modes": [r["mode"] for r in solo],
                       "solo_ms_last_step": info.get("solo_us", 0) / 1000.0,  # critical-path workgroups' pass
+                      "solo_lead_ms": info.get("solo_lead_us", 0) / 1000.0,  # pass start -> solo start
+                      "solo_tail_ms": info.get("solo_tail_us", 0) / 1000.0,  # solo end -> pass end
                       "us_per_op_critical_path": (info.get("solo_us", 0) / max(int(counts.max()), 1)) if info["solo"] else None,
                       "docs_rerun_hbm": info["spilled"], "docs_continued_hbm": info["continued"],
                       "docs_hbm_waves": info["hbm_docs"], "lds_groups": info["lds_groups"],

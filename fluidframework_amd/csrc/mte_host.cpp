@@ -289,6 +289,7 @@ struct mte_engine {
     uint32_t last_spilled = 0, last_continued = 0, last_hbm_docs = 0, last_hbm_waves = 0, last_lds_groups = 0;
     uint32_t last_solo = 0;
     double last_solo_ms = 0;
+    double last_solo_lead_ms = 0, last_solo_tail_ms = 0;  // pass start -> solo start, solo end -> pass end
     uint32_t n_groups = 256;
     // SnapshotV1 emission on the device (emit.hip): property / name tables, scratch, and two output
     // pools -- round 0 (every document but the solo ones) runs while the critical path is still
@@ -994,6 +995,8 @@ static int run_kernel(mte_engine* e, bool gen) {
     if (n_solo) {
         float sm = 0;
         if (hipEventElapsedTime(&sm, e->ev_s0, e->ev_s1) == hipSuccess) e->last_solo_ms = sm;
+        if (hipEventElapsedTime(&sm, e->ev0, e->ev_s0) == hipSuccess) e->last_solo_lead_ms = sm;
+        if (hipEventElapsedTime(&sm, e->ev_s1, e->ev1) == hipSuccess) e->last_solo_tail_ms = sm;
     }
     e->last_spilled = (uint32_t)spill.size();
     if (!spill.empty()) {
@@ -2061,6 +2064,8 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "slots") *value = e->n_slots;
     else if (k == "solo") *value = e->last_solo;
     else if (k == "solo_us") *value = (int64_t)(e->last_solo_ms * 1000.0);  // the solo workgroups' pass (critical path)
+    else if (k == "solo_lead_us") *value = (int64_t)(e->last_solo_lead_ms * 1000.0);
+    else if (k == "solo_tail_us") *value = (int64_t)(e->last_solo_tail_ms * 1000.0);
     else if (k == "lean") *value = e->last_lean;
     else if (k == "emit_us") *value = (int64_t)(e->last_emit_ms * 1000.0);  // emission after the replay pass
     else if (k == "out_text") {  // UTF-16 units Engine::finish gathered (counters[6..7])

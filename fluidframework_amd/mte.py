@@ -395,7 +395,8 @@ class Engine:
                                        ctypes.byref(rows), ctypes.byref(co)), "mte_run_info")
         out = {"spilled": sp.value, "continued": co.value, "lds_ms": a.value, "hbm_ms": b.value,
                "out_rows": rows.value}
-        for k in ("lds_groups", "hbm_waves", "hbm_docs", "slot_bytes", "slots", "solo", "solo_us", "lean", "out_text"):
+        for k in ("lds_groups", "hbm_waves", "hbm_docs", "slot_bytes", "slots", "solo", "solo_us", "solo_lead_us",
+                  "solo_tail_us", "lean", "out_text"):
             out[k] = self.get_info(k)
         return out
 

@@ -162,9 +162,11 @@ def run(args):
     t_start = time.perf_counter()
     kms = []
     st = None
+    solo_steps = []
     for _ in range(args.steps):
         st = eng.replay()
         kms.append(st["kernel_ms"])
+        solo_steps.append(eng.get_info("solo_us") / 1000.0)  # host-side read of the last pass's events
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -275,6 +277,8 @@ def run(args):
             "extra": {"ops_per_step_rank0": ops_applied, "longest_doc_ops": int(counts.max()),
                       "solo_docs": info["solo"], "solo_modes": [r["mode"] for r in solo],
                       "solo_ms_last_step": info.get("solo_us", 0) / 1000.0,  # critical-path workgroups' pass
+                      "kernel_ms_steps": [round(x, 1) for x in kms],
+                      "solo_ms_steps": [round(x, 1) for x in solo_steps],
                       "solo_lead_ms": info.get("solo_lead_us", 0) / 1000.0,  # pass start -> solo start
                       "solo_tail_ms": info.get("solo_tail_us", 0) / 1000.0,  # solo end -> pass end
                       "us_per_op_critical_path": (info.get("solo_us", 0) / max(int(counts.max()), 1)) if info["solo"] else None,

@@ -55,16 +55,26 @@ static_assert(RG_BLOCKS <= SOLO_POOL, "the rows live in the SoloPlan's slot arra
 enum RgProf : u32 {
     RP_TOTAL, RP_FETCH, RP_APPLY, RP_RESOLVE, RP_INSERT_SLOT, RP_SPLIT, RP_RANGE, RP_ZAMBONI, RP_SCOUR,
     RP_HEAP, RP_FIND_SEG, RP_PACK, RP_LRU, RP_OPS, RP_N_RESOLVE, RP_N_SCOUR, RP_N_SCOUR_CHANGED,
-    RP_N_PACK, RP_N_POP, RP_N_SPLIT_BLK, RP_N_MOVE, RP_N
+    RP_N_PACK, RP_N_POP, RP_N_SPLIT_BLK, RP_N_MOVE, RP_SPLIT_AT, RP_INS, RP_REM, RP_MSN, RP_ZAM_EDIT, RP_N
 };
 #if defined(MTE_PROFILE) && !defined(MTE_CPU)
+// RG_PROF_ONLY=<slot>: time that one scope only (each s_memtime pair costs a lone wave ~100 cycles,
+// which a full profile charges to the enclosing scopes); RP_TOTAL and the event counts stay on
+#ifdef RG_PROF_ONLY
+#define RG_ON(slot) ((slot) == RG_PROF_ONLY || (slot) == RP_TOTAL)
+#else
+#define RG_ON(slot) true
+#endif
+template <bool ON>
 struct RgScope {
     u64& acc;
     u64 t0;
-    __device__ __forceinline__ RgScope(u64& a) : acc(a), t0(__builtin_amdgcn_s_memtime()) {}
-    __device__ __forceinline__ ~RgScope() { acc += __builtin_amdgcn_s_memtime() - t0; }
+    __device__ __forceinline__ RgScope(u64& a) : acc(a), t0(ON ? __builtin_amdgcn_s_memtime() : 0) {}
+    __device__ __forceinline__ ~RgScope() {
+        if (ON) acc += __builtin_amdgcn_s_memtime() - t0;
+    }
 };
-#define RG_PROF(slot) RgScope _rg_scope_##slot(pf[slot])
+#define RG_PROF(slot) RgScope<RG_ON(slot)> _rg_scope_##slot(pf[slot])
 #define RG_COUNT(slot, n) (pf[slot] += (u64)(n))
 #elif defined(MTE_MARKERS) && !defined(MTE_CPU)
 // static code inspection: row-engine scopes as assembly comments "MTE_BEGIN 100+slot"
@@ -1211,6 +1221,7 @@ struct RegEngine {
     // ensureIntervalBoundary at the resolved slot (BaseSegment.splitAt, mergeTree.ts:524-568): the
     // right piece copies everything and follows the left one. Returns the insert_slot result.
     SD u32 split_at(const RFound& f) {
+        RG_PROF(RP_SPLIT_AT);
         const u32 r = f.k >> 3, l = gbase(f.k) + (u32)f.slot;
         const Row w = row(r);
         RSeg t;
@@ -1236,6 +1247,7 @@ struct RegEngine {
 
     // insertSegments (mergeTree.ts:1968-1998): split at pos, then place the new segment.
     SD bool op_insert(i32 pos, i32 R, u32 C, i32 seq, RSeg rec) {
+        RG_PROF(RP_INS);
         RFound f = resolve(pos, R, C);
         if (!f.ok) {
             fail(MTE_DOC_INSERT_FAILED, seq);
@@ -1273,6 +1285,7 @@ struct RegEngine {
     // markRangeRemoved (mergeTree.ts:2607-2719): split at p1 and p2, then mark [p1, p2) of the
     // (R, C) view before the op: first remover wins, later ones join removedClientOverlap.
     SD bool op_remove(i32 p1, i32 p2, i32 R, u32 C, i32 seq) {
+        RG_PROF(RP_REM);
         // the p2 resolve and the marking start at p1's row: nothing before it moves or changes
         // visible length (a split keeps the lengths, a block split shifts only later blocks)
         u32 r1 = 0, c1 = 0;
@@ -1360,7 +1373,10 @@ struct RegEngine {
             n_ops++;
         }
         if (status) return true;
-        if (edited) zamboni();
+        if (edited) {
+            RG_PROF(RP_ZAM_EDIT);
+            zamboni();
+        }
         if (status) return true;
         if (op.flags & MTE_F_END_OF_MSG) {
             n_msgs++;
@@ -1370,6 +1386,7 @@ struct RegEngine {
             }
             curSeq = op.seq;
             if (op.msn > minSeq) {
+                RG_PROF(RP_MSN);
                 minSeq = op.msn;
                 zamboni();
             }
@@ -1538,7 +1555,8 @@ struct RegEngine {
             static constexpr u32 map[RP_N] = {PF_TOTAL, PF_FETCH, PF_APPLY, PF_RESOLVE, PF_INSERT_SLOT, PF_SPLIT,
                                               PF_RANGE, PF_ZAMBONI, PF_SCOUR, PF_HEAP, PF_FIND_SEG, PF_PACK,
                                               PF_LRU, PF_OPS, PN_RESOLVE, PN_SCOUR, PN_SCOUR_CHANGED, PN_PACK,
-                                              PN_POP, PN_SPLIT_BLK, PN_DIRTY};
+                                              PN_POP, PN_SPLIT_BLK, PN_DIRTY, PF_ALLOC, PF_OP_INS, PF_OP_REM,
+                                              PF_ZAM_MSN, PF_ZAM_EDIT};
             u64* o2 = p.prof + (u64)doc * PROF_SLOTS;
             for (u32 i = 0; i < RP_N; i++) o2[map[i]] += pf[i];
         }

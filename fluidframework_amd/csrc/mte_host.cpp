@@ -31,6 +31,7 @@
 #include "../../include/mte_diag.h"
 #include "emit.h"
 #include "engine_types.hpp"
+#include "gather_plan.hpp"
 #include "jsonlite.hpp"
 #include "mte_kernels.h"
 
@@ -1972,29 +1973,23 @@ int mte_gather_summaries(mte_engine* e, int rank, int world, void* comm, mte_doc
     std::vector<uint64_t> counts((size_t)world);
     HIP_TRY(e, hipMemcpyAsync(counts.data(), all_cnt.p, 8 * (size_t)world, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
-    uint64_t mx = 0, total = 0;
-    for (uint64_t x : counts) {
-        mx = std::max(mx, x);
-        total += x;
-    }
-    if (n) *n = total;
+    const GatherPlan g = gather_plan(counts.data(), world);
+    if (n) *n = g.total;
     if (!out) return MTE_OK;
-    if (cap < total) return MTE_E_RANGE;
+    if (cap < g.total) return MTE_E_RANGE;
     const size_t words = sizeof(mte_doc_summary) / 8;  // 32-B records as 4 u64 words
+    std::vector<mte_doc_summary> blk(g.stride), flat(g.stride * (size_t)world);
+    gather_pack(mine.data(), nd, g, blk.data());
     DevBuf<uint64_t> send, recv;
-    HIP_TRY(e, send.alloc(std::max<uint64_t>(mx, 1) * words));
-    HIP_TRY(e, recv.alloc(std::max<uint64_t>(mx, 1) * words * (size_t)world));
-    HIP_TRY(e, hipMemsetAsync(send.p, 0, std::max<uint64_t>(mx, 1) * words * 8, e->stream));
-    if (nd) HIP_TRY(e, hipMemcpyAsync(send.p, mine.data(), nd * sizeof(mte_doc_summary), hipMemcpyHostToDevice, e->stream));
-    r = rccl().allGather(send.p, recv.p, std::max<uint64_t>(mx, 1) * words, ncclUint64, c, e->stream);
+    HIP_TRY(e, send.alloc(g.stride * words));
+    HIP_TRY(e, recv.alloc(g.stride * words * (size_t)world));
+    HIP_TRY(e, hipMemcpyAsync(send.p, blk.data(), g.stride * sizeof(mte_doc_summary), hipMemcpyHostToDevice, e->stream));
+    r = rccl().allGather(send.p, recv.p, g.stride * words, ncclUint64, c, e->stream);
     if (r != ncclSuccess) return set_err(e, MTE_E_HIP, std::string("ncclAllGather: ") + rccl().errStr(r));
-    std::vector<mte_doc_summary> flat(std::max<uint64_t>(mx, 1) * (size_t)world);
     HIP_TRY(e, hipMemcpyAsync(flat.data(), recv.p, flat.size() * sizeof(mte_doc_summary), hipMemcpyDeviceToHost,
                               e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
-    size_t k = 0;
-    for (int q = 0; q < world; q++)
-        for (uint64_t i = 0; i < counts[(size_t)q]; i++) out[k++] = flat[(size_t)q * std::max<uint64_t>(mx, 1) + i];
+    gather_concat(flat.data(), counts.data(), world, g, out);
     return MTE_OK;
 }
 

@@ -30,7 +30,18 @@ export declare class BatchedMergeEngine {
     /** After a replay with newMergeTreeSnapshotFormat: false. */
     snapshotLegacy(doc: number, catchUpBlobName?: string): ITree;
     summaries(): DocSummary[];
+    /** Multi-GPU collective: every rank's summaries in rank order, all-gathered over RCCL (mte_gather_summaries).
+     *  comm: this engine's communicator (rcclCommCreate), or null when world is 1. */
+    gatherSummaries(rank: number, world: number, comm?: RcclComm | null): DocSummary[];
+    /** This rank's RCCL communicator on the engine's device, from rank 0's rcclUniqueId(). */
+    rcclCommCreate(id: Buffer, rank: number, world: number): RcclComm;
 }
+
+/** An RCCL communicator handle (released by rcclCommDestroy or when collected). */
+export type RcclComm = { readonly __rcclComm: unique symbol };
+/** Rank 0 makes the id (MTE_RCCL_ID_BYTES = 128 bytes) and sends it to every rank. */
+export declare function rcclUniqueId(): Buffer;
+export declare function rcclCommDestroy(comm: RcclComm): void;
 
 /** Client-shaped facade (merge-tree client.ts:42) for one document. Batch semantics: messages are
  *  staged and replayed on the GPU when an output is next read (see index.js). */

@@ -74,18 +74,31 @@ class BatchedMergeEngine {
     /** 32-byte records {checksum u64, ops, length, segments, snapshotBytes, status, docId} */
     summaries() {
         this._idle();
-        const buf = addon.summaries(this._engine, this._docs);
-        const out = [];
-        for (let i = 0; i < this._docs; i++) {
-            const o = i * 32;
-            out.push({
-                checksum: buf.readBigUInt64LE ? buf.readBigUInt64LE(o) : buf.toString("hex", o, o + 8),
-                ops: buf.readUInt32LE(o + 8), length: buf.readUInt32LE(o + 12), segments: buf.readUInt32LE(o + 16),
-                snapshotBytes: buf.readUInt32LE(o + 20), status: buf.readInt32LE(o + 24), docId: buf.readUInt32LE(o + 28),
-            });
-        }
-        return out;
+        return parseSummaries(addon.summaries(this._engine, this._docs));
     }
+    /**
+     * Multi-GPU (one process per GPU, documents sharded by id): every rank's summaries in rank order,
+     * all-gathered over RCCL (mte_gather_summaries). A collective: every rank calls it after its replay.
+     * comm: rcclCommCreate(...) of this engine; null when world is 1.
+     */
+    gatherSummaries(rank, world, comm = null) {
+        this._idle();
+        return parseSummaries(addon.gatherSummaries(this._engine, rank, world, comm));
+    }
+    /** This rank's RCCL communicator on the engine's device, from the id rank 0 made (rcclUniqueId()). */
+    rcclCommCreate(id, rank, world) { this._idle(); return addon.rcclCommCreate(this._engine, id, rank, world); }
+}
+
+function parseSummaries(buf) {
+    const out = [];
+    for (let o = 0; o + 32 <= buf.length; o += 32) {
+        out.push({
+            checksum: buf.readBigUInt64LE ? buf.readBigUInt64LE(o) : buf.toString("hex", o, o + 8),
+            ops: buf.readUInt32LE(o + 8), length: buf.readUInt32LE(o + 12), segments: buf.readUInt32LE(o + 16),
+            snapshotBytes: buf.readUInt32LE(o + 20), status: buf.readInt32LE(o + 24), docId: buf.readUInt32LE(o + 28),
+        });
+    }
+    return out;
 }
 
 /**
@@ -165,4 +178,8 @@ module.exports = {
     createBuilder: addon.createBuilder, builderAddDoc: addon.builderAddDoc, builderDocCount: addon.builderDocCount,
     builderAddDocFromSummary: addon.builderAddDocFromSummary, builderAddContainerLog: addon.builderAddContainerLog,
     builderAddMatrixLog: addon.builderAddMatrixLog,
+    /** rank 0: the RCCL id (Buffer) to send to every rank; rcclCommDestroy(comm) releases a communicator */
+    rcclUniqueId: addon.rcclUniqueId, rcclCommDestroy: addon.rcclCommDestroy,
+    /** low level: (engine handle, rank, world, comm) -> Buffer of 32-byte records */
+    gatherSummariesRaw: addon.gatherSummaries, rcclCommCreateRaw: addon.rcclCommCreate,
 };

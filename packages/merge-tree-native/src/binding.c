@@ -463,6 +463,103 @@ static napi_value js_summaries(napi_env env, napi_callback_info info) {
     return buf;
 }
 
+/* Multi-GPU (mte.h mte_rccl_* / mte_gather_summaries): rank 0 makes the id, the host sends its bytes to
+ * every rank (worker_threads message, IPC, ...), each rank creates its communicator on its engine's
+ * device and every rank calls gatherSummaries (a collective). */
+typedef struct comm_box {  /* the handle's payload: destroyed once, by rcclCommDestroy or the GC */
+    void* comm;
+} comm_box;
+static void finalize_comm(napi_env env, void* data, void* hint) {
+    (void)env;
+    (void)hint;
+    comm_box* c = (comm_box*)data;
+    if (c && c->comm) mte_rccl_comm_destroy(c->comm);
+    free(c);
+}
+static void* get_comm(napi_env env, napi_value v) {
+    comm_box* c = (comm_box*)get_external(env, v);
+    return c ? c->comm : NULL;
+}
+
+/* rcclUniqueId(): Buffer of MTE_RCCL_ID_BYTES */
+static napi_value js_rccl_unique_id(napi_env env, napi_callback_info info) {
+    (void)info;
+    void* data = NULL;
+    napi_value buf;
+    CHECK(env, napi_create_buffer(env, MTE_RCCL_ID_BYTES, &data, &buf));
+    int rc = mte_rccl_unique_id((uint8_t*)data);
+    if (rc) return throw_mte(env, "mte_rccl_unique_id", rc, NULL);
+    return buf;
+}
+
+/* rcclCommCreate(engine, idBuffer, rank, world): communicator handle (destroyed by rcclCommDestroy or
+ * by the garbage collector) */
+static napi_value js_rccl_comm_create(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return throw_mte(env, "rcclCommCreate", -1, "expects (engine, id, rank, world)");
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    void* id = NULL;
+    size_t idlen = 0;
+    bool isbuf = false;
+    napi_is_buffer(env, argv[1], &isbuf);
+    if (!e || !isbuf || napi_get_buffer_info(env, argv[1], &id, &idlen) != napi_ok || idlen != MTE_RCCL_ID_BYTES)
+        return throw_mte(env, "rcclCommCreate", -1, "expects an engine and a Buffer from rcclUniqueId()");
+    int32_t rank = 0, world = 0;
+    napi_get_value_int32(env, argv[2], &rank);
+    napi_get_value_int32(env, argv[3], &world);
+    void* comm = NULL;
+    int rc = mte_rccl_comm_create(e, (const uint8_t*)id, rank, world, &comm);
+    if (rc) return throw_mte(env, "mte_rccl_comm_create", rc, mte_last_error(e));
+    comm_box* box = (comm_box*)malloc(sizeof *box);
+    if (!box) {
+        mte_rccl_comm_destroy(comm);
+        return throw_mte(env, "rcclCommCreate", -1, "out of memory");
+    }
+    box->comm = comm;
+    napi_value out;
+    if (napi_create_external(env, box, finalize_comm, NULL, &out) != napi_ok) {
+        finalize_comm(env, box, NULL);
+        return throw_mte(env, "rcclCommCreate", -1, "napi_create_external");
+    }
+    return out;
+}
+
+/* rcclCommDestroy(comm): releases the communicator now (the handle must not be used again) */
+static napi_value js_rccl_comm_destroy(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return NULL;
+    comm_box* c = (comm_box*)get_external(env, argv[0]);
+    if (c && c->comm) {
+        mte_rccl_comm_destroy(c->comm);
+        c->comm = NULL;
+    }
+    return NULL;
+}
+
+/* gatherSummaries(engine, rank, world, comm|null): Buffer of every rank's 32-byte records, rank order */
+static napi_value js_gather_summaries(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) return throw_mte(env, "gatherSummaries", -1, "expects (engine, rank, world, comm)");
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    int32_t rank = 0, world = 0;
+    napi_get_value_int32(env, argv[1], &rank);
+    napi_get_value_int32(env, argv[2], &world);
+    napi_valuetype t = napi_undefined;
+    napi_typeof(env, argv[3], &t);
+    void* comm = t == napi_external ? get_comm(env, argv[3]) : NULL;
+    if (!e || world < 1 || rank < 0 || rank >= world || (world > 1 && !comm))
+        return throw_mte(env, "gatherSummaries", -1, "expects an engine, 0 <= rank < world and a live communicator when world > 1");
+    size_t n = 0;
+    int rc = mte_gather_summaries(e, rank, world, comm, NULL, 0, &n);
+    if (rc) return throw_mte(env, "mte_gather_summaries", rc, mte_last_error(e));
+    void* data = NULL;
+    napi_value buf;
+    CHECK(env, napi_create_buffer(env, n * sizeof(mte_doc_summary), &data, &buf));
+    rc = mte_gather_summaries(e, rank, world, comm, (mte_doc_summary*)data, n, &n);
+    if (rc) return throw_mte(env, "mte_gather_summaries", rc, mte_last_error(e));
+    return buf;
+}
+
 static napi_value init(napi_env env, napi_value exports) {
     napi_property_descriptor props[] = {
         {"abiVersion", 0, js_abi_version, 0, 0, 0, napi_default, 0},
@@ -485,6 +582,10 @@ static napi_value init(napi_env env, napi_value exports) {
         {"snapshotV1", 0, js_snapshot, 0, 0, 0, napi_default, 0},
         {"snapshotLegacy", 0, js_snapshot_legacy, 0, 0, 0, napi_default, 0},
         {"summaries", 0, js_summaries, 0, 0, 0, napi_default, 0},
+        {"rcclUniqueId", 0, js_rccl_unique_id, 0, 0, 0, napi_default, 0},
+        {"rcclCommCreate", 0, js_rccl_comm_create, 0, 0, 0, napi_default, 0},
+        {"rcclCommDestroy", 0, js_rccl_comm_destroy, 0, 0, 0, napi_default, 0},
+        {"gatherSummaries", 0, js_gather_summaries, 0, 0, 0, napi_default, 0},
     };
     napi_define_properties(env, exports, sizeof props / sizeof props[0], props);
     return exports;

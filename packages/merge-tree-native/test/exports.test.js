@@ -28,4 +28,13 @@ m.builderAddMatrixLog(b, "readonly", JSON.stringify([msg("a", 1, 0, splice("rows
 assert.strictEqual(m.builderDocCount(b), 6);
 assert.throws(() => m.builderAddMatrixLog(b, "readonly", JSON.stringify([msg("a", 1, 0, { type: 2, row: 0, col: 0, value: 1 })])),
     /mte_builder_add_matrix_log/);
+// multi-GPU entry points (the collective itself needs GPUs: parity.gpu.js runs world 1)
+for (const f of ["rcclUniqueId", "rcclCommDestroy", "gatherSummariesRaw", "rcclCommCreateRaw"]) {
+    assert.strictEqual(typeof m[f], "function", f);
+}
+assert.strictEqual(typeof m.BatchedMergeEngine.prototype.gatherSummaries, "function");
+assert.strictEqual(typeof m.BatchedMergeEngine.prototype.rcclCommCreate, "function");
+assert.throws(() => m.gatherSummariesRaw(null, 0, 1, null), /gatherSummaries/);
+assert.throws(() => m.rcclCommCreateRaw(null, Buffer.alloc(128), 0, 2), /rcclCommCreate/);
+assert.throws(() => m.rcclCommCreateRaw(null, Buffer.alloc(3), 0, 2), /rcclCommCreate/);
 console.log("exports ok");

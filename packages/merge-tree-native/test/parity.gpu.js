@@ -48,6 +48,10 @@ e.generate(2, 8, 500, 8, 3);
 const st = e.replay();
 assert.strictEqual(st.failedDocs, 0);
 const sums = e.summaries();
+// the multi-GPU gather at world 1 (no communicator) is this engine's own records, rank order
+assert.deepStrictEqual(e.gatherSummaries(0, 1, null).map((x) => [x.checksum.toString(), x.docId]),
+    sums.map((x) => [x.checksum.toString(), x.docId]));
+assert.throws(() => e.gatherSummaries(0, 2, null), /communicator/);
 (async () => {
     // replayAsync: the same replay on a worker thread while the event loop keeps turning
     const big = new BatchedMergeEngine();

@@ -29,6 +29,10 @@ namespace mte {
 #ifndef MTE_SOLO_WPE
 #define MTE_SOLO_WPE 1
 #endif
+// waves of a solo workgroup: one per SIMD, so the critical-path CU holds no other kernel's waves
+#ifndef SOLO_WAVES
+#define SOLO_WAVES 4
+#endif
 
 template <bool GEN, int LVL>
 __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(MTE_LDS_WPE))) void k_lds(Params p) {
@@ -104,7 +108,7 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
 // latency of the longest document bounds a Zipf batch, so it gets the plan with the
 // most room and no LDS-pool sharing; it continues HBM-resident only if it outgrows even that.
 template <bool GEN, int LVL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_SOLO_WPE, MTE_SOLO_WPE))) void k_solo(Params p) {
+MTE_DEV void solo_doc(const Params& p) {
     const u32 i = blockIdx.x;
     if (i >= p.n_solo) return;
     const u32 d = p.doc_list[i];
@@ -156,6 +160,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_SOLO_WPE
         e.finish();
     }
     __builtin_amdgcn_s_setprio(0);
+}
+
+// The solo workgroup is SOLO_WAVES waves that each claim a whole SIMD's register file (512 VGPRs +
+// AGPRs: the clobbers below make the kernel's allocation the maximum), and all of the CU's LDS: no
+// other wave of the pass can be resident on a critical-path CU. Wave 0 replays the document; the
+// others wait at the barrier (issuing nothing) until it is done.
+template <bool GEN, int LVL>
+__global__ __launch_bounds__(64 * SOLO_WAVES) __attribute__((amdgpu_waves_per_eu(MTE_SOLO_WPE, MTE_SOLO_WPE))) void k_solo(Params p) {
+    asm volatile("" ::: "v255", "a255");
+    if (wave_first(threadIdx.x >> 6) == 0) solo_doc<GEN, LVL>(p);
+    __syncthreads();
 }
 
 // HBM slot of a k_hbmq wave: a free bit of the slot bitmap (cleared by the host before each run).
@@ -294,7 +309,7 @@ hipError_t launch_solo(const Params& p, bool gen, int full, u32 n_solo, hipStrea
     }();
     if (attr != hipSuccess) return attr;
     void* args[] = {(void*)&p};
-    return hipLaunchKernel(MTE_PICK(k_solo, gen, full), dim3(n_solo), dim3(64), args, sizeof(SoloPlan), s);
+    return hipLaunchKernel(MTE_PICK(k_solo, gen, full), dim3(n_solo), dim3(64 * SOLO_WAVES), args, sizeof(SoloPlan), s);
 }
 hipError_t launch_hbm(const Params& p, bool gen, int full, u32 n_docs, hipStream_t s) {
     void* args[] = {(void*)&p};

@@ -916,6 +916,9 @@ struct RegEngine {
     // The runs' text copies of one block as one flattened gather: slot lane l copies jlen units from
     // its text src to jdst (sources are never destinations of the same scour).
     SD void copy_runs(V jdst, V jsrc, V jlen) {
+#ifdef RG_NO_TEXT_COPY  // A/B timing only: wrong text
+        return;
+#endif
         const V jinc = simd::scan_incl(jlen);
         const u32 total = simd::readlane(jinc, 63);
         if (!total) return;

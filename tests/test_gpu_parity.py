@@ -384,3 +384,28 @@ def test_reference_spec_pins_on_gpu(engine):
                     assert s["text"] == "el" and json.loads(s["props"]) == expected
                     break
                 at += s["len"]
+
+
+def test_hbm_slot_exhaustion_completes(engine):
+    """Far fewer HBM slots than resident k_hbmq waves (force_hbm: one wave per document, all launched
+    at once; a slot budget of ~3 slots): waves without a slot spin in acquire_hslot until a holder --
+    a resident wave of the same kernel, which always progresses -- releases one. The pass completes
+    and every document matches the oracle (no spin-wait depends on another stream's
+    kernel being co-resident)."""
+    engine.generate(2, 384, 1500, n_clients=8, seed=29)
+    batch = engine.export_batch()
+    engine.set_option("force_hbm", 1)
+    try:
+        engine.replay()
+        slot = engine.run_info()["slot_bytes"]
+        engine.set_option("slot_budget_mb", max(1, (3 * slot) >> 20))
+        engine.replay()
+        info = engine.run_info()
+    finally:
+        engine.set_option("force_hbm", 0)
+        engine.set_option("slot_budget_mb", 48 << 10)
+    assert 1 <= info["hbm_waves"] <= 8 and info["lds_groups"] == 0, info  # hbm_waves = the slot count
+    bad, _, _ = compare_batch_checksums(engine, batch)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad

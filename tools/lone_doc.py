@@ -41,7 +41,7 @@ def main():
     res["us_per_op"] = res[f"kernel_ms_{a.reps - 1}"] * 1e3 / a.ops
     res["run_info"] = e.run_info()
     res["doc0"] = e.doc_result(0)
-    if os.environ.get("MTE_LIB", "").startswith(("prof", "po_")):
+    if os.environ.get("MTE_LIB", "").startswith(("prof", "po_", "rp_")):
         prof = e.profile().astype(np.float64)
         ops = prof[:, mte.PROF_NAMES.index("ops")].sum()
         res["cycles_per_op"] = {n: round(float(prof[:, i].sum() / max(ops, 1)), 2)

@@ -203,6 +203,7 @@ struct Params {
     u32 gen_n_propsets;       // propset ids 1..gen_n_propsets are the generator's annotate sets
     u32 reg_solo;             // k_solo replays lean documents register-resident first (reg_engine.hpp)
     u32 reg_lb_limit;         // test knob: leaf blocks the register plan may hold (0 = all it has)
+    u32 reg_lt_limit;         // test knob: LDS text units per semispace of the register plan (0 = all)
     u32 pad1;
 };
 

@@ -228,6 +228,10 @@ struct mte_engine {
     hipStream_t stream3 = nullptr;                    // stream3: the solo workgroups (k_solo)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
     hipEvent_t ev_s0 = nullptr, ev_s1 = nullptr;  // timing of the solo workgroups (critical path)
+    // pinned staging for uploads from the caller's (pageable) buffers: two chunks, each refilled by
+    // host threads while the DMA engine copies the other one (upload_staged)
+    void* stage[2] = {nullptr, nullptr};
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};
     std::string err;
     HostBatch hb;
     bool generated = false;    // ops/payload live on the device; host copy filled on demand
@@ -264,6 +268,7 @@ struct mte_engine {
     uint32_t pool_limit = 0;
     uint32_t reg_solo = 1;               // option "reg_solo": k_solo's register-resident engine (lean batches)
     uint32_t reg_lb_limit = 0;           // option "reg_lb_limit": test knob, leaf blocks the register plan holds
+    uint32_t reg_lt_limit = 0;           // option "reg_lt_limit": test knob, LDS text units of the register plan
 #ifndef MTE_HBMQ_PER_CU
 #define MTE_HBMQ_PER_CU 8
 #endif
@@ -382,10 +387,48 @@ static int derive_value_tables(mte_engine* e) {
     return MTE_OK;
 }
 
+template <class F>
+static void run_pool(unsigned n, F&& work);
+
+// Host -> device copy of a large caller buffer through two pinned chunks: host threads copy chunk i+1
+// out of the (pageable) source while the DMA engine moves chunk i. A pageable hipMemcpyAsync stages
+// through the runtime's own buffers and ran at 3.6 GB/s on the first C4-sized load
+// (profiles/pcie_r02l_c4.json); this path does not depend on what the runtime has pinned before.
+static constexpr size_t STAGE_BYTES = 64ull << 20;
+static int upload_staged(mte_engine* e, void* dst, const void* src, size_t bytes) {
+    if (bytes < (4ull << 20)) {  // small: the runtime's path is fine
+        HIP_TRY(e, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->stream));
+        return MTE_OK;
+    }
+    for (int i = 0; i < 2; i++) {
+        if (!e->stage[i]) HIP_TRY(e, hipHostMalloc(&e->stage[i], STAGE_BYTES, hipHostMallocDefault));
+        if (!e->ev_stage[i]) HIP_TRY(e, hipEventCreateWithFlags(&e->ev_stage[i], hipEventDisableTiming));
+    }
+    const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    int k = 0;
+    for (size_t off = 0; off < bytes; off += STAGE_BYTES, k ^= 1) {
+        const size_t n = std::min(STAGE_BYTES, bytes - off);
+        HIP_TRY(e, hipEventSynchronize(e->ev_stage[k]));  // the DMA out of this chunk is done
+        char* stg = (char*)e->stage[k];
+        const char* from = (const char*)src + off;
+        const size_t piece = (n + nt - 1) / nt;
+        std::atomic<unsigned> next{0};
+        run_pool(nt, [&]() {
+            for (unsigned t; (t = next.fetch_add(1)) < nt;) {
+                const size_t a = (size_t)t * piece;
+                if (a < n) memcpy(stg + a, from + a, std::min(piece, n - a));
+            }
+        });
+        HIP_TRY(e, hipMemcpyAsync((char*)dst + off, stg, n, hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(e, hipEventRecord(e->ev_stage[k], e->stream));
+    }
+    return MTE_OK;
+}
+
 template <class T>
 static int upload(mte_engine* e, DevBuf<T>& d, const T* h, size_t n) {
     HIP_TRY(e, d.alloc(n));
-    if (n) HIP_TRY(e, hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, e->stream));
+    if (n) return upload_staged(e, d.p, h, n * sizeof(T));
     return MTE_OK;
 }
 template <class T>
@@ -640,6 +683,10 @@ void mte_destroy(mte_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (int i = 0; i < 2; i++) {
+        if (e->stage[i]) (void)hipHostFree(e->stage[i]);
+        if (e->ev_stage[i]) (void)hipEventDestroy(e->ev_stage[i]);
+    }
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->ev2) (void)hipEventDestroy(e->ev2);
@@ -912,6 +959,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     e->P.pool_limit = e->pool_limit;
     e->P.reg_solo = e->reg_solo;
     e->P.reg_lb_limit = e->reg_lb_limit;
+    e->P.reg_lt_limit = e->reg_lt_limit;
     e->P.doc_list = e->d_order.p;
     e->P.n_list = nd;
     int rc;
@@ -2040,6 +2088,7 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "lean") e->lean_opt = value != 0;
     else if (k == "reg_solo") e->reg_solo = value != 0;
     else if (k == "reg_lb_limit") e->reg_lb_limit = (uint32_t)std::max<int64_t>(0, value);
+    else if (k == "reg_lt_limit") e->reg_lt_limit = (uint32_t)std::max<int64_t>(0, value);
     else if (k == "emit") e->emit_opt = value != 0;  // SnapshotV1 emission on the device after replay
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
     else return set_err(e, MTE_E_ARG, "unknown option " + k);

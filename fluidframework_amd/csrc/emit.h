@@ -15,7 +15,8 @@ struct EmitParams {
     const DocCfg* cfg;
     const uint4* vis;          // rows: (len, seq, removedSeq, client | removedClient << 8 | flags)
     const uint4* aux;          // rows: (map, text offset in the doc's run | marker refType, ...)
-    const u32* maps;           // the property map of every row with props (MAP_WORDS per row), or null
+    const u32* maps;           // the property map of every row with props (map_words per row), or null
+    u32 map_words;
     const u16* text;           // gathered text of every row
     // property text tables (interned JSON texts of keys and values)
     const char* key_text;

@@ -138,7 +138,7 @@ struct Doc {
         r = p.res[d];
         row0 = r.out_off;
     }
-    MTE_DEV const u32* map(u64 row) const { return p.maps + row * MAP_WORDS; }
+    MTE_DEV const u32* map(u64 row) const { return p.maps + row * p.map_words; }
     // matchProperties (properties.ts:62-93) on two rows' maps (host DocView::match_props)
     MTE_DEV bool val_match(u32 a, u32 b) const {
         if (a == b) return true;

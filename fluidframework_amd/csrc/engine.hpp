@@ -170,7 +170,7 @@ struct Engine {
     const Params& p;
     u32 doc;
     // hot per-document limits (DocCfg, engine_types.hpp)
-    u32 seg_cap, arena_cap, payload_len, map_cap;
+    u32 seg_cap, arena_cap, payload_len, map_cap, mw;  // mw: words per property-map record
     u32 L;  // lane
     St st;
     bool collab, has_nl;
@@ -253,7 +253,8 @@ struct Engine {
         payload = p.payload + c.payload_off;
         arena0 = p.arena + c.arena_off;
         ovl = p.ovl + c.ovl_off;
-        maps = p.maps + c.map_off * MAP_WORDS;
+        mw = p.map_words;
+        maps = p.maps + c.map_off * mw;
         collab = c.collab != 0;
         has_nl = c.has_nl != 0;
         st.root = NONE;
@@ -1278,8 +1279,9 @@ struct Engine {
         if constexpr (!FULL) return false;  // a batch without properties: every map id is 0
         if (a == 0 || b == 0) return false;
         if (a >= map_cap || b >= map_cap) return false;
-        const u32* ma = maps + (u64)a * MAP_WORDS;
-        const u32* mb = maps + (u64)b * MAP_WORDS;
+        const_cast<Engine*>(this)->fence_ovl();  // map records are written lane-parallel (build_map)
+        const u32* ma = maps + (u64)a * mw;
+        const u32* mb = maps + (u64)b * mw;
         const u32 na = U(ma[0]), nb = U(mb[0]);
         if (na != nb) return false;
         for (u32 i = 0; i < na; i++) {
@@ -1297,73 +1299,82 @@ struct Engine {
         return true;
     }
     // SegmentPropertiesManager.addProperties (segmentPropertiesManager.ts:35-111) on an immutable map:
-    // returns a fresh map id. Executed by lane 0; result broadcast.
+    // returns a fresh map id. Lane-parallel: lane i holds the map's pair i (key, value ids) in JS
+    // insertion order, up to (mw - 1) / 2 pairs (<= MTE_MAX_PROPS); more fails the document alone.
     MTE_DEV u32 build_map(u32 old, u32 propset, bool rewrite) {
         if constexpr (!FULL) return 0;
         MTE_PROF(PF_MAP);
-        u32 id = NONE;
-        i32 err = 0;
-        if (st.mapNext >= map_cap) err = MTE_DOC_CAPACITY;
-        if (L == 0 && !err) {
-            u32 kv[2 * MTE_MAX_PROPS];
-            u32 n = 0;
-            if (old && old < map_cap) {
-                const u32* mo = maps + (u64)old * MAP_WORDS;
-                n = mo[0] > MTE_MAX_PROPS ? MTE_MAX_PROPS : mo[0];
-                for (u32 i = 0; i < 2 * n; i++) kv[i] = mo[1 + i];
-            }
-            const mte_propset ps = p.propsets[propset];
-            if (rewrite) {  // delete keys whose new value is falsy / absent (:65-78)
-                u32 w = 0;
-                for (u32 i = 0; i < n; i++) {
-                    u32 k = kv[2 * i];
-                    bool keep = false;
-                    for (u32 q = 0; q < ps.count; q++)
-                        if (p.prop_keys[ps.first + q] == k) keep = !(p.val_flags[p.prop_vals[ps.first + q]] & 1u);
-                    if (keep) {
-                        kv[2 * w] = k;
-                        kv[2 * w + 1] = kv[2 * i + 1];
-                        w++;
-                    }
-                }
-                n = w;
-            }
-            for (u32 q = 0; q < ps.count && !err; q++) {
-                u32 k = p.prop_keys[ps.first + q], v = p.prop_vals[ps.first + q];
-                u32 at = NONE;
-                for (u32 i = 0; i < n; i++)
-                    if (kv[2 * i] == k) at = i;
-                if (v == 0) {  // null deletes (:98-100)
-                    if (at != NONE) {
-                        for (u32 i = at; i + 1 < n; i++) {
-                            kv[2 * i] = kv[2 * i + 2];
-                            kv[2 * i + 1] = kv[2 * i + 3];
-                        }
-                        n--;
-                    }
-                } else if (at != NONE) {
-                    kv[2 * at + 1] = v;
-                } else if (n < MTE_MAX_PROPS) {
-                    kv[2 * n] = k;
-                    kv[2 * n + 1] = v;
-                    n++;
-                } else {
-                    err = MTE_DOC_UNSUPPORTED;
-                }
-            }
-            if (!err) {
-                id = st.mapNext;
-                u32* m = maps + (u64)id * MAP_WORDS;
-                m[0] = n;
-                for (u32 i = 0; i < 2 * n; i++) m[1 + i] = kv[i];
+        if (st.mapNext >= map_cap) {
+            fail(MTE_DOC_CAPACITY, st.curSeq);
+            return 0;
+        }
+        const u32 maxp = (mw - 1) / 2 < MTE_MAX_PROPS ? (mw - 1) / 2 : MTE_MAX_PROPS;
+        u32 n = 0, K = 0, V = 0;
+        if (old && old < map_cap) {
+            const u32* mo = maps + (u64)old * mw;
+            n = U(mo[0]);
+            if (n > maxp) n = maxp;
+            if (L < n) {
+                K = mo[1 + 2 * L];
+                V = mo[2 + 2 * L];
             }
         }
-        err = wave_read(err, 0);
-        id = wave_read(id, 0);
+        const mte_propset ps = p.propsets[propset];
+        const u32 pc = U(ps.count), pf = U(ps.first);
+        if (rewrite) {  // delete keys whose new value is falsy / absent (:65-78); order kept
+            bool keep = false;
+            for (u32 q = 0; q < pc; q++) {
+                const u32 k = U(p.prop_keys[pf + q]);
+                const bool falsy = (U(p.val_flags[U(p.prop_vals[pf + q])]) & 1u) != 0;
+                if (L < n && K == k) keep = !falsy;
+            }
+            keep = keep && L < n;
+            const u64 km = wave_ballot(keep);
+            const u32 nk = (u32)__builtin_popcountll(km);
+            const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(km >> 32), __builtin_amdgcn_mbcnt_lo((u32)km, 0u));
+            const u32 dst = keep ? below : nk + (L - below);  // a permutation of the lanes
+            K = (u32)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)K);
+            V = (u32)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)V);
+            n = nk;
+        }
+        i32 err = 0;
+        for (u32 q = 0; q < pc && !err; q++) {
+            const u32 k = U(p.prop_keys[pf + q]), v = U(p.prop_vals[pf + q]);
+            const u64 hm = wave_ballot(L < n && K == k);
+            if (v == 0) {  // null deletes (:98-100): the pairs after it move down one lane
+                if (hm) {
+                    const u32 at = (u32)__builtin_ctzll(hm);
+                    const u32 K1 = wave_shfl(K, (L + 1) & 63), V1 = wave_shfl(V, (L + 1) & 63);
+                    if (L >= at) {
+                        K = K1;
+                        V = V1;
+                    }
+                    n--;
+                }
+            } else if (hm) {
+                if (L == (u32)__builtin_ctzll(hm)) V = v;
+            } else if (n < maxp) {
+                if (L == n) {
+                    K = k;
+                    V = v;
+                }
+                n++;
+            } else {
+                err = MTE_DOC_UNSUPPORTED;
+            }
+        }
         if (err) {
             fail(err, st.curSeq);
             return 0;
         }
+        const u32 id = st.mapNext;
+        u32* m = maps + (u64)id * mw;
+        if (L < n) {
+            m[1 + 2 * L] = K;
+            m[2 + 2 * L] = V;
+        }
+        if (L == 0) m[0] = n;
+        st.gdirty = 1;  // other lanes read these pairs later: fence_ovl first
         st.mapNext++;
         return id;
     }
@@ -2351,6 +2362,7 @@ struct Engine {
         return t;
     }
     MTE_DEV void finish() {
+        fence_ovl();
         u32 nseg = 0, ntext = 0;
         for (u32 base = 0; base < st.n_lb; base += 64) {
             u32 k = base + L;
@@ -2404,13 +2416,14 @@ struct Engine {
                         tat += v.x;
                     }
                     if (a.x && p.out_maps) {  // the row's property map, indexed by row
-                        const uint4* ms = (const uint4*)(maps + (u64)a.x * MAP_WORDS);
-                        uint4* md = (uint4*)(p.out_maps + (u64)(at + s) * MAP_WORDS);
+                        const uint4* ms = (const uint4*)(maps + (u64)a.x * mw);
+                        uint4* md = (uint4*)(p.out_maps + (u64)(at + s) * mw);
                         const uint4 m0 = ms[0], m1 = ms[1], m2 = ms[2], m3 = ms[3];
                         md[0] = m0;
                         md[1] = m1;
                         md[2] = m2;
                         md[3] = m3;
+                        for (u32 q = 4; q < mw / 4; q++) md[q] = ms[q];  // wider records
                     }
                     p.out_vis[at + s] = v;
                     p.out_aux[at + s] = a;

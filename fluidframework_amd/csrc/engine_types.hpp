@@ -21,7 +21,9 @@ constexpr u32 F_REMOVED = 1u << 16, F_MARKER = 1u << 17;  // slot meta flags
 constexpr u32 F_OVL = 1u << 18;    // removedClientOverlap non-empty: clients 0..31 in aux.z (dead tcap)
 constexpr u32 F_OVLHI = 1u << 19;  // ... and clients 32..63 in the HBM mask by segment id
 constexpr u32 F_PERM = 1u << 20;   // PermutationSegment run (SharedMatrix row / col vector): no text
-constexpr u32 MAP_WORDS = 16;                            // [0]=count, then 7 (key,val) pairs
+constexpr u32 MAP_WORDS = 16;  // the narrowest map record: [0] = count, then 7 (key, val) pairs; a batch
+                               // whose documents carry more distinct keys gets wider records
+                               // (Params::map_words = 1 + 2 * keys, rounded up to 4, <= 128)
 constexpr i32 GRANULARITY = 256;                         // TextSegmentGranularity (mergeTree.ts:1059)
 
 // Leaf-block metadata word: parent interior node (bits 0..29) | needsScour (bits 30..31).
@@ -204,6 +206,7 @@ struct Params {
     u32 reg_solo;             // k_solo replays lean documents register-resident first (reg_engine.hpp)
     u32 reg_lb_limit;         // test knob: leaf blocks the register plan may hold (0 = all it has)
     u32 reg_lt_limit;         // test knob: LDS text units per semispace of the register plan (0 = all)
+    u32 map_words;            // words per property-map record (a multiple of 4, >= MAP_WORDS)
     u32 pad1;
 };
 

@@ -269,6 +269,7 @@ struct mte_engine {
     uint32_t reg_solo = 1;               // option "reg_solo": k_solo's register-resident engine (lean batches)
     uint32_t reg_lb_limit = 0;           // option "reg_lb_limit": test knob, leaf blocks the register plan holds
     uint32_t reg_lt_limit = 0;           // option "reg_lt_limit": test knob, LDS text units of the register plan
+    uint32_t map_words = MAP_WORDS;      // property-map record width of the loaded batch (Params::map_words)
 #ifndef MTE_HBMQ_PER_CU
 #define MTE_HBMQ_PER_CU 8
 #endif
@@ -487,11 +488,11 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     }
     HIP_TRY(e, e->d_arena.alloc(ar));
     HIP_TRY(e, e->d_ovl.alloc(seg));
-    HIP_TRY(e, e->d_maps.alloc(mp * MAP_WORDS));
+    HIP_TRY(e, e->d_maps.alloc(mp * e->map_words));
     HIP_TRY(e, e->d_out_vis.alloc(out));
     HIP_TRY(e, e->d_out_aux.alloc(out));
     HIP_TRY(e, e->d_out_ovl.alloc(out));
-    if (any_props) HIP_TRY(e, e->d_out_maps.alloc(out * MAP_WORDS));  // some document can carry props
+    if (any_props) HIP_TRY(e, e->d_out_maps.alloc(out * e->map_words));  // some document can carry props
     HIP_TRY(e, e->d_counters.alloc(8));
     HIP_TRY(e, e->d_res.alloc(nd));
     HIP_TRY(e, e->d_prof.alloc((size_t)nd * PROF_SLOTS));
@@ -513,6 +514,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     P.arena = e->d_arena.p;
     P.ovl = e->d_ovl.p;
     P.maps = e->d_maps.p;
+    P.map_words = e->map_words;
     P.out_vis = e->d_out_vis.p;
     P.out_aux = e->d_out_aux.p;
     P.out_ovl = e->d_out_ovl.p;
@@ -741,6 +743,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     const uint32_t nd = b->n_docs;
     std::vector<uint64_t> n_ops(nd), pay(nd), pi(nd), an(nd);
     std::vector<uint8_t> collab(nd), has_nl(nd, 0), not_lean(nd, 0), doc_ext(nd, 0), doc_cu(nd, 0);
+    std::vector<uint32_t> doc_keys(nd, 0);  // distinct property keys of each document's ops
     // one pass over each document's ops and payload, documents spread over host threads (the scan is
     // most of mte_load's host time on large batches)
     auto scan = [&](uint32_t d) {
@@ -753,9 +756,17 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         pay[d] = b->doc_payload_offsets[d + 1] - b->doc_payload_offsets[d];
         bool rel = false;
         count_doc_ops(b->ops, b->doc_op_offsets, d, pi[d], an[d], &rel);
+        std::vector<uint32_t> keys;
         for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
             if (b->ops[i].flags & MTE_F_PERM) doc_ext[d] = 1;
             if (b->ops[i].flags & MTE_F_CATCHUP) doc_cu[d] = 1;
+            const uint32_t ps = b->ops[i].props;
+            if (ps && ps < b->n_propsets)
+                for (uint32_t q = 0; q < b->propsets[ps].count; q++) keys.push_back(b->prop_keys[b->propsets[ps].first + q]);
+        }
+        if (keys.size() > 7) {  // only a document that could exceed the narrow record pays the sort
+            std::sort(keys.begin(), keys.end());
+            doc_keys[d] = (uint32_t)(std::unique(keys.begin(), keys.end()) - keys.begin());
         }
         collab[d] = e->hb.client(d, 0).empty() ? 0 : 1;  // empty observer name => local, non-collab
         not_lean[d] = has_nl[d] || pi[d] || an[d] || rel ||
@@ -773,6 +784,9 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         run_pool(nt, work);
     }
     bool lean = true, ext = false, cu_any = false;
+    uint32_t max_keys = 7;
+    for (uint32_t d = 0; d < nd; d++) max_keys = std::max(max_keys, std::min<uint32_t>(doc_keys[d], MTE_MAX_PROPS));
+    e->map_words = ((1 + 2 * max_keys) + 3) & ~3u;  // 16 for up to 7 keys, 128 for MTE_MAX_PROPS
     for (uint32_t d = 0; d < nd; d++) {
         lean = lean && !not_lean[d];
         ext = ext || doc_ext[d];
@@ -895,6 +909,7 @@ static EmitParams emit_params(mte_engine* e) {
     P.vis = e->d_out_vis.p;
     P.aux = e->d_out_aux.p;
     P.maps = e->P.out_maps;
+    P.map_words = e->map_words;
     P.text = e->d_out_text.p;
     P.key_text = e->d_key_text.p;
     P.key_off = e->d_key_off.p;
@@ -1146,6 +1161,7 @@ int mte_generate(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, 
 int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, const uint32_t* ops_per_doc,
                      const uint32_t* doc_ids, uint32_t n_clients, uint64_t seed_base) {
     if (!e || n_docs == 0 || n_clients == 0 || n_clients >= MTE_MAX_CLIENTS) return MTE_E_ARG;
+    e->map_words = MAP_WORDS;  // the generator's property sets hold at most four keys
     if (kind != 2 && kind != 3 && kind != 5) return set_err(e, MTE_E_ARG, "generator kind must be 2, 3 or 5");
     HIP_TRY(e, hipSetDevice(e->device));
     e->hb = HostBatch();
@@ -1243,7 +1259,7 @@ static int ensure_download(mte_engine* e) {
         if (n) HIP_TRY(e, hipMemcpy(h.data(), d.p, n * sizeof(h[0]), hipMemcpyDeviceToHost));
         return MTE_OK;
     };
-    if (e->P.out_maps && (rc = dl(e->h_maps, e->d_out_maps, rows * MAP_WORDS))) return rc;
+    if (e->P.out_maps && (rc = dl(e->h_maps, e->d_out_maps, rows * e->map_words))) return rc;
     if ((rc = dl(e->h_out_vis, e->d_out_vis, rows))) return rc;
     if ((rc = dl(e->h_out_aux, e->d_out_aux, rows))) return rc;
     if ((rc = dl(e->h_out_ovl, e->d_out_ovl, rows))) return rc;
@@ -1302,7 +1318,7 @@ struct DocView {
         return e->hb.client(d, (uint32_t)shortId);
     }
     // SegView::props: 1 + the row's index in the output pool (its map was copied there), 0 = none
-    const uint32_t* map(uint32_t id) const { return e->h_maps.data() + (uint64_t)(id - 1) * MAP_WORDS; }
+    const uint32_t* map(uint32_t id) const { return e->h_maps.data() + (uint64_t)(id - 1) * e->map_words; }
     // JSON of a property map in JS key order (integer-like keys ascending first, then insertion order)
     void props_json(std::string& o, uint32_t id) const {
         const uint32_t* m = map(id);
@@ -1647,14 +1663,15 @@ static json::Value jnumv(double x) {
     v.num = x;
     return v;
 }
-// one property map of document d from the device (MAP_WORDS words: count, then (key, value) ids)
+// one property map of document d from the device (map_words words: count, then (key, value) ids)
 static int read_map(mte_engine* e, uint32_t d, uint32_t id, std::vector<std::pair<uint32_t, uint32_t>>& kv) {
     kv.clear();
     if (id == 0) return MTE_OK;
     if (id >= e->cfg[d].map_cap) return set_err(e, MTE_E_STATE, "catch-up: property map id out of range");
-    uint32_t w[MAP_WORDS];
-    HIP_TRY(e, hipMemcpy(w, e->d_maps.p + (e->cfg[d].map_off + id) * MAP_WORDS, sizeof w, hipMemcpyDeviceToHost));
-    for (uint32_t i = 0; i < std::min<uint32_t>(w[0], MTE_MAX_PROPS); i++) kv.emplace_back(w[1 + 2 * i], w[2 + 2 * i]);
+    std::vector<uint32_t> w(e->map_words);
+    HIP_TRY(e, hipMemcpy(w.data(), e->d_maps.p + (e->cfg[d].map_off + id) * e->map_words, w.size() * 4,
+                         hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < std::min<uint32_t>(w[0], (e->map_words - 1) / 2); i++) kv.emplace_back(w[1 + 2 * i], w[2 + 2 * i]);
     return MTE_OK;
 }
 static json::Value parse_text(const std::string& t) { return json::parse(t.data(), t.size()); }

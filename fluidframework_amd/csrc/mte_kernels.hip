@@ -175,9 +175,13 @@ MTE_DEV void solo_doc(const Params& p) {
 // others wait at the barrier (issuing nothing) until it is done.
 template <bool GEN, int LVL>
 __global__ __launch_bounds__(64 * SOLO_WAVES) __attribute__((amdgpu_waves_per_eu(MTE_SOLO_WPE, MTE_SOLO_WPE))) void k_solo(Params p) {
+#if SOLO_WAVES > 1
     asm volatile("" ::: "v255", "a255");
     if (wave_first(threadIdx.x >> 6) == 0) solo_doc<GEN, LVL>(p);
     __syncthreads();
+#else
+    solo_doc<GEN, LVL>(p);
+#endif
 }
 
 // HBM slot of a k_hbmq wave: a free bit of the slot bitmap (cleared by the host before each run).

@@ -159,6 +159,8 @@ struct RegEngine {
     u32 mem_vis[RG_ROWS * 64][4], mem_aux[RG_ROWS * 64][4];
     u16 mem_lt[2][RG_LT_UNITS];
     SD u16* lt_base(u32 sel) const { return const_cast<u16*>(mem_lt[sel & 1]); }
+    u32 mem_ring[4 * 64];
+    SD u32* ring() { return mem_ring; }
     SD Row ldrow(u32 r) const {
         Row w;
         for (u32 l = 0; l < 64; l++) {
@@ -201,6 +203,8 @@ struct RegEngine {
     SD static uint4* VISP() { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + offsetof(SoloPlan, vis)); }
     SD static uint4* AUXP() { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + offsetof(SoloPlan, aux)); }
     SD static u16* lt_base(u32 sel) { return reinterpret_cast<u16*>((sel & 1 ? AUXP() : VISP()) + RG_BLOCKS * 8); }
+    // op-record ring: 4 chunks of 8 records in the SoloPlan's region (unused by this engine)
+    SD static u32* ring() { return reinterpret_cast<u32*>(g_lds_dyn); }
     SD Row ldrow(u32 r) const {
         const u32 i = r * 64 + __lane_id();
         const uint4 v = VISP()[i], a = AUXP()[i];
@@ -1477,36 +1481,44 @@ struct RegEngine {
         }
         RG_PROF(RP_TOTAL);
         const u32* src = (const u32*)p.ops;
-        simd::VA<4> Q;
         const u64 b = i;
-        auto load_chunk = [&](u64 c0) MTE_LI {  // records [c0, c0+8)
+        auto load_chunk = [&](u64 c0) MTE_LI {  // records [c0, c0+8): lane 8r + w = word w of record r
             const u64 left = e > c0 ? e - c0 : 0;
             const u32 nw = left >= 8 ? 64u : (u32)left * 8u;
             return simd::ld(src + c0 * 8, L(), L() < nw);
         };
-        for (u32 c = 0; c < 4; c++) Q.set(c, load_chunk(b + (u64)c * 8));
-        // Inserted text, eight ops ahead: the payload units of chunk Q[1]'s inserts (up to 64 units)
-        // load into TQ while Q[0] replays; when Q[1] becomes current they are written to the LDS
-        // text arena in one store, so an insert's text is in LDS before the op runs.
-        V TQ = simd::splat(0), TS = TQ, CS = TQ;  // units; record starts (lane r) next / current
+        u32* RG = ring();
+        auto ring_put = [&](u32 slot, const V& x) MTE_LI {
+            simd::st(RG + slot * 64, L(), x, simd::splat(1u) == 1u);
+            simd::lds_order();
+        };
+        auto ring_get = [&](u32 slot) MTE_LI { return simd::ld(RG + slot * 64, L(), simd::splat(1u) == 1u); };
+        // Op records stream through a 4-chunk LDS ring, 32 ops ahead; inserted text 8 ops ahead (the
+        // payload units of the next chunk's inserts, up to 64, go to the LDS text arena when that
+        // chunk becomes current). Each in-flight global load lands in one register (QL, TQ) that is
+        // consumed at the next chunk boundary before it is reloaded: no register move of a load in
+        // flight, so no wait on it (a shifted register queue waited for its newest load every 8 ops).
+        for (u32 c = 0; c < 4; c++) ring_put(c, load_chunk(b + (u64)c * 8));
+        V QL = load_chunk(b + 32);                // chunk 4
+        V q = ring_get(0);                         // the current chunk
+        V TQ = simd::splat(0), TS = TQ, CS = TQ;  // text units; record starts (lane r) next / current
         u32 TM = 0, TN = 0, CM = 0, CB = 0;         // records with prefetched text, units; current
-        prefetch_text(Q.get(0), TQ, TS, TM, TN);
+        prefetch_text(q, TQ, TS, TM, TN);
         activate_text(TQ, TS, TM, TN, CS, CM, CB);
-        prefetch_text(Q.get(1), TQ, TS, TM, TN);
+        prefetch_text(ring_get(1), TQ, TS, TM, TN);
         for (; i < e && !status; i++) {
             const u32 r = (u32)((i - b) & 7);
             if (r == 0 && i != b) {
-                Q.set(0, Q.get(1));
-                Q.set(1, Q.get(2));
-                Q.set(2, Q.get(3));
-                Q.set(3, load_chunk(i + 24));
-                activate_text(TQ, TS, TM, TN, CS, CM, CB);
-                prefetch_text(Q.get(1), TQ, TS, TM, TN);
+                const u32 k = (u32)((i - b) >> 3);  // chunk k becomes current
+                ring_put((k + 3) & 3u, QL);          // chunk k+3 (loaded at the last boundary)
+                activate_text(TQ, TS, TM, TN, CS, CM, CB);  // chunk k's text (loaded at the last boundary)
+                QL = load_chunk(i + 32);              // chunk k+4
+                q = ring_get(k & 3u);
+                prefetch_text(ring_get((k + 1) & 3u), TQ, TS, TM, TN);  // chunk k+1's text
             }
             mte_op op;
             {
                 RG_PROF(RP_FETCH);
-                const V q = Q.get(0);
                 u32 w[8];
                 for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(q, r * 8 + x);
                 __builtin_memcpy(&op, w, sizeof op);

@@ -52,7 +52,8 @@ enum {
 };
 
 #define MTE_MAX_CLIENTS 64       /* short ids 0..63 (observer = 0), overlap kept as a u64 mask */
-#define MTE_MAX_PROPS 7          /* keys per segment property map on the device */
+#define MTE_MAX_PROPS 63         /* keys per segment property map on the device; the map records of a
+                                    batch are as wide as its widest document needs (its distinct keys) */
 
 /* ---- op records (one per merge-tree delta op; 32 bytes) ---------------------------------- */
 /* Types follow ops.ts:29-34 (MergeTreeDeltaType) plus two engine-level kinds. */

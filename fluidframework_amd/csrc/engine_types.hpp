@@ -205,7 +205,6 @@ struct Params {
     u32 gen_n_propsets;       // propset ids 1..gen_n_propsets are the generator's annotate sets
     u32 reg_solo;             // k_solo replays lean documents register-resident first (reg_engine.hpp)
     u32 reg_lb_limit;         // test knob: leaf blocks the register plan may hold (0 = all it has)
-    u32 reg_lt_limit;         // test knob: LDS text units per semispace of the register plan (0 = all)
     u32 map_words;            // words per property-map record (a multiple of 4, >= MAP_WORDS)
     u32 pad1;
 };

@@ -268,7 +268,6 @@ struct mte_engine {
     uint32_t pool_limit = 0;
     uint32_t reg_solo = 1;               // option "reg_solo": k_solo's register-resident engine (lean batches)
     uint32_t reg_lb_limit = 0;           // option "reg_lb_limit": test knob, leaf blocks the register plan holds
-    uint32_t reg_lt_limit = 0;           // option "reg_lt_limit": test knob, LDS text units of the register plan
     uint32_t map_words = MAP_WORDS;      // property-map record width of the loaded batch (Params::map_words)
 #ifndef MTE_HBMQ_PER_CU
 #define MTE_HBMQ_PER_CU 8
@@ -974,7 +973,6 @@ static int run_kernel(mte_engine* e, bool gen) {
     e->P.pool_limit = e->pool_limit;
     e->P.reg_solo = e->reg_solo;
     e->P.reg_lb_limit = e->reg_lb_limit;
-    e->P.reg_lt_limit = e->reg_lt_limit;
     e->P.doc_list = e->d_order.p;
     e->P.n_list = nd;
     int rc;
@@ -2105,7 +2103,6 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "lean") e->lean_opt = value != 0;
     else if (k == "reg_solo") e->reg_solo = value != 0;
     else if (k == "reg_lb_limit") e->reg_lb_limit = (uint32_t)std::max<int64_t>(0, value);
-    else if (k == "reg_lt_limit") e->reg_lt_limit = (uint32_t)std::max<int64_t>(0, value);
     else if (k == "emit") e->emit_opt = value != 0;  // SnapshotV1 emission on the device after replay
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
     else return set_err(e, MTE_E_ARG, "unknown option " + k);

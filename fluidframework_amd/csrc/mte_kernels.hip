@@ -125,13 +125,6 @@ MTE_DEV void solo_doc(const Params& p) {
         if (p.reg_solo) {
             RegEngine<> r(p, d);
             at = r.replay(at, p.docs[d].op_end);
-            if (r.status == REG_HANDOFF) {
-                // between two ops: its LDS text moves to the HBM arena (the LDS engine takes over the
-                // slot arrays the text lives in)
-                r.status = 0;
-                r.evict_text();
-                if (r.status == 0) r.status = REG_HANDOFF;
-            }
             if (r.status != REG_HANDOFF) {
                 r.finish();
                 __builtin_amdgcn_s_setprio(0);

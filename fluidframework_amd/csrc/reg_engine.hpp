@@ -48,12 +48,6 @@ constexpr i32 REG_HANDOFF = 101;          // internal: continue in the LDS engin
 // needsScour (mergeTree.ts:63) in meta bits 24..25 of every slot lane of a block
 constexpr u32 NS_SHIFT = 24, NS_MASK = 3u << NS_SHIFT;
 static_assert(RG_BLOCKS <= SOLO_POOL, "the rows live in the SoloPlan's slot arrays");
-// Text in LDS: the slot arrays' tails past the rows (vis and aux: two semispaces) hold the critical
-// document's live text, so merges copy LDS to LDS and no global-memory round trip sits on the op path.
-constexpr u32 LT_BIT = 0x40000000u;                                 // toff: LDS text (current semispace)
-constexpr u32 TOFF_MASK = ~(ARENA_BIT | LT_BIT);                    // the offset inside its space
-constexpr u32 RG_LT_UNITS = (SOLO_POOL - RG_BLOCKS) * 8 * 16 / 2;   // UTF-16 units per semispace
-constexpr u32 RG_PF_UNITS = 64;                                     // payload units prefetched per 8 ops
 
 // Phase profile of the row engine (MTE_PROFILE device builds, `make prof`): inclusive s_memtime
 // cycles and event counts accumulated in registers and written once per document by finish(), in
@@ -140,7 +134,7 @@ struct RegEngine {
     // ---------------------------------------------------------------- state
     simd::VA<RG_LEVELS> LV;  // LV[i] lane j: child count of node j of level i+1 (0 beyond the last)
     simd::VA<8> HK, HS;      // heap keys (maxSeq) / segment ids, position q at lane q&63 of reg q>>6
-    u32 n_lb, height, heapSize, segNext, arenaTop, arenaSel, ltTop, ltSel, ltCap;
+    u32 n_lb, height, heapSize, segNext, arenaTop, arenaSel;
     i32 minSeq, curSeq, heapTop, status, failSeq;
     u32 n_ops, n_msgs, n_gc, max_lb;
     bool adirty;
@@ -157,10 +151,6 @@ struct RegEngine {
     // ---------------------------------------------------------------- slot rows (LDS)
 #ifdef MTE_CPU
     u32 mem_vis[RG_ROWS * 64][4], mem_aux[RG_ROWS * 64][4];
-    u16 mem_lt[2][RG_LT_UNITS];
-    SD u16* lt_base(u32 sel) const { return const_cast<u16*>(mem_lt[sel & 1]); }
-    u32 mem_ring[4 * 64];
-    SD u32* ring() { return mem_ring; }
     SD Row ldrow(u32 r) const {
         Row w;
         for (u32 l = 0; l < 64; l++) {
@@ -202,9 +192,6 @@ struct RegEngine {
 #else
     SD static uint4* VISP() { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + offsetof(SoloPlan, vis)); }
     SD static uint4* AUXP() { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + offsetof(SoloPlan, aux)); }
-    SD static u16* lt_base(u32 sel) { return reinterpret_cast<u16*>((sel & 1 ? AUXP() : VISP()) + RG_BLOCKS * 8); }
-    // op-record ring: 4 chunks of 8 records in the SoloPlan's region (unused by this engine)
-    SD static u32* ring() { return reinterpret_cast<u32*>(g_lds_dyn); }
     SD Row ldrow(u32 r) const {
         const u32 i = r * 64 + __lane_id();
         const uint4 v = VISP()[i], a = AUXP()[i];
@@ -308,8 +295,7 @@ struct RegEngine {
         HS.zero();
         n_lb = 1;
         height = 1;
-        heapSize = segNext = arenaTop = arenaSel = ltTop = ltSel = 0;
-        ltCap = p.reg_lt_limit && p.reg_lt_limit < RG_LT_UNITS ? p.reg_lt_limit : RG_LT_UNITS;
+        heapSize = segNext = arenaTop = arenaSel = 0;
         minSeq = curSeq = heapTop = 0;
         status = 0;
         failSeq = -1;
@@ -759,37 +745,27 @@ struct RegEngine {
         return NONE;
     }
 
-    // ---------------------------------------------------------------- text
-    // A text offset names its space: payload (HBM, the op log's text), ARENA_BIT (the HBM merge arena,
-    // two semispaces) or LT_BIT (LDS, two semispaces). Inserted text is prefetched from the payload
-    // into LDS eight ops ahead (replay); merge runs copy into LDS while it has room.
+    // ---------------------------------------------------------------- text (HBM)
     SD u16* arena_cur() const { return arena0 + (u64)arenaSel * arena_cap; }
-    SD u16* lt_cur() const { return lt_base(ltSel); }
     SD void fence_arena() {
         if (adirty) {
             simd::wave_fence();
             adirty = false;
         }
     }
-    // n units of the text at offset src, per lane i (lanes < n of this 64-unit step)
-    SD V ld_text(u32 src, V i, B m) const {
-        const u32 so = src & TOFF_MASK;
-        if (src & LT_BIT) return simd::ld(lt_cur(), i + so, m);
-        return simd::ld((src & ARENA_BIT) ? arena_cur() : payload, i + so, m);
-    }
-    // copy n units from text offset src (any space) to offset dst of the global buffer dbase
+    // copy n units from text offset src (payload or arena) to offset dst of dbase (lanes in parallel)
     SD void copy_text(u32 dst, u32 src, u32 n, u16* dbase) {
-        const u32 d0 = dst & TOFF_MASK;
+        const u16* sb = (src & ARENA_BIT) ? arena_cur() : payload;
+        const u32 so = src & ~ARENA_BIT, d0 = dst & ~ARENA_BIT;
         for (u32 b = 0; b < n; b += 64) {
             const V i = L() + b;
             const B m = i < n;
-            simd::st(dbase, i + d0, ld_text(src, i, m), m);
+            const V t = simd::ld(sb, i + so, m);
+            simd::st(dbase, i + d0, t, m);
         }
     }
-    // Semispace compaction of the HBM merge arena: every live arena text, document order; with
-    // `evict` the LDS texts move into it too (before the LDS engine takes over the slot arrays).
-    // False when the live text does not fit (the caller fails the document).
-    SD bool arena_gc(bool evict = false) {
+    // Semispace compaction of the merge arena: every live arena-resident text, document order.
+    SD void arena_gc() {
         fence_arena();
         const u32 other = arenaSel ^ 1u;
         u16* dst = arena0 + (u64)other * arena_cap;
@@ -802,13 +778,13 @@ struct RegEngine {
             for (u32 s = 0; s < cnt; s++) {
                 const u32 l = gb + s;
                 const u32 meta = simd::readlane(w.meta, l), toff = simd::readlane(w.toff, l);
-                if ((meta & F_MARKER) || !((toff & ARENA_BIT) || (evict && (toff & LT_BIT)))) continue;
+                if ((meta & F_MARKER) || !(toff & ARENA_BIT)) continue;
                 const u32 len = simd::readlane(w.len, l), oc = simd::readlane(w.cap, l);
                 const bool rm = simd::readlane(w.rseq, l) != RSEQ_LIVE;
                 const u32 cap = (rm || oc < len) ? len : oc;
-                if (top + cap > arena_cap) {
+                if ((toff & ~ARENA_BIT) + len > arena_cap || top + cap > arena_cap) {
                     fail(MTE_DOC_CAPACITY, curSeq);
-                    return false;
+                    return;
                 }
                 copy_text(top, toff, len, dst);
                 w.toff = simd::writelane(w.toff, l, top | ARENA_BIT);
@@ -816,64 +792,12 @@ struct RegEngine {
                 dirty = true;
                 top += cap;
             }
-            if (dirty) strow(r, w);
+            if (dirty) putrow(r, w);
         }
-        cr = NONE;
         simd::wave_fence();
         arenaSel = other;
         arenaTop = top;
         n_gc++;
-        return true;
-    }
-    SD bool evict_text() { return arena_gc(true); }
-    // Semispace compaction of the LDS text: every live LDS text, row by row (its capacity trimmed to
-    // its length when removed). False when it does not fit (new text then stays in the payload).
-    SD bool lds_gc() {
-        const u32 nrows = (n_lb + 7) >> 3;
-        u16* src = lt_cur();
-        u16* dst = lt_base(ltSel ^ 1u);
-        u32 top = 0;
-        for (u32 r = 0; r < nrows; r++) {
-            Row w = ldrow(r);
-            const B lt = (w.len != 0u) & ((w.meta & F_MARKER) == 0u) & ((w.toff & LT_BIT) != 0u);
-            const u64 jm = simd::ballot(lt);
-            if (!jm) continue;
-            const V cap = simd::sel(lt, simd::sel((w.rseq != RSEQ_LIVE) | simd::slt(w.cap, w.len), w.len, w.cap), 0u);
-            const V inc = simd::scan_incl(cap);
-            const u32 total = simd::readlane(inc, 63);
-            if (top + total > ltCap) {  // unreachable: live LDS texts own disjoint ranges of one
-                fail(MTE_DOC_CAPACITY, curSeq);  // semispace, and compaction only trims them
-                return false;
-            }
-            const V at = inc - cap + top;
-            // flattened copy of the row's texts (job = slot lane, len units)
-            const V jl = simd::sel(lt, w.len, 0u);
-            const V jinc = simd::scan_incl(jl);
-            const u32 units = simd::readlane(jinc, 63);
-            const V jst = jinc - jl;
-            for (u32 base = 0; base < units; base += 64) {
-                const V f = L() + base;
-                V j = simd::splat(0);
-                for (u64 m = jm; m; m &= m - 1) {
-                    const u32 q = (u32)__builtin_ctzll(m);
-                    j = simd::sel(f >= simd::readlane(jst, q), q, j);
-                }
-                const B m = f < units;
-                const V o = f - simd::bperm(jst, j);
-                const V t = simd::ld(src, (simd::bperm(w.toff, j) & TOFF_MASK) + o, m);
-                simd::st(dst, simd::bperm(at, j) + o, t, m);
-            }
-            simd::lds_order();
-            w.toff = simd::sel(lt, at | LT_BIT, w.toff);
-            w.cap = simd::sel(lt, cap, w.cap);
-            strow(r, w);
-            top += total;
-        }
-        cr = NONE;
-        ltSel ^= 1u;
-        ltTop = top;
-        n_gc++;  // (DocRes n_gc: compactions of either text arena)
-        return true;
     }
 
     // ---------------------------------------------------------------- zamboni (mergeTree.ts:1289-1478)
@@ -917,7 +841,7 @@ struct RegEngine {
             const B cont = w.toff == simd::row_shr1(w.toff + w.len);  // text starts where slot s-1's ends
             const u32 mCONT = group_bits(simd::ballot(cont), k);
             jdst = jlen = simd::splat(0);
-            u32 top = arenaTop, need = 0, ltop = ltTop;
+            u32 top = arenaTop, need = 0;
             Row nw = w;
             for (u32 heads = mST & ~mJOIN & (mJOIN >> 1); heads; heads &= heads - 1) {
                 const u32 h = (u32)__builtin_ctz(heads);
@@ -929,19 +853,14 @@ struct RegEngine {
                 const u32 total = simd::readlane(ex, le) + simd::readlane(w.len, le) - exh;
                 u32 noff = off, ncap = cap, cbits = 0;
                 if ((mCONT & rb) == rb) {  // the run's text is one contiguous range already
-                    if (off & (ARENA_BIT | LT_BIT)) ncap = simd::readlane(w.toff, le) + simd::readlane(w.cap, le) - off;
-                } else if ((off & (ARENA_BIT | LT_BIT)) && total <= cap) {  // append into the head's chunk
+                    if (off & ARENA_BIT) ncap = simd::readlane(w.toff, le) + simd::readlane(w.cap, le) - off;
+                } else if ((off & ARENA_BIT) && total <= cap) {  // append into the head's chunk
                     cbits = rb;
-                } else {  // a fresh chunk: in LDS while it has room, else in the HBM arena
+                } else {  // a fresh chunk
                     ncap = 2 * total < 32 ? 32u : 2 * total;
-                    if (ltop + ncap <= ltCap) {
-                        noff = ltop | LT_BIT;
-                        ltop += ncap;
-                    } else {
-                        noff = top | ARENA_BIT;
-                        top += ncap;
-                        need += ncap;
-                    }
+                    noff = top | ARENA_BIT;
+                    top += ncap;
+                    need += ncap;
                     cbits = rb | (1u << h);
                 }
                 if (cbits) {
@@ -955,7 +874,6 @@ struct RegEngine {
             }
             if (arenaTop + need <= arena_cap) {
                 arenaTop = top;
-                ltTop = ltop;
                 jsrc = w.toff;  // the slots' text before the runs' heads move
                 w = nw;
                 break;
@@ -964,7 +882,8 @@ struct RegEngine {
                 fail(MTE_DOC_CAPACITY, curSeq);
                 return cnt;
             }
-            if (!arena_gc()) return cnt;  // moves every arena text: re-read the slots and redo the runs
+            arena_gc();  // moves every arena text: re-read the slots and redo the runs
+            if (status) return cnt;
             w = row(r);
             fence_arena();
         }
@@ -995,20 +914,14 @@ struct RegEngine {
         return nkeep;
     }
     // The runs' text copies of one block as one flattened gather: slot lane l copies jlen units from
-    // its text src (any space) to jdst (LDS or the HBM arena; sources are never destinations of the
-    // same scour). Global loads and stores are issued only for the units that need them.
+    // its text src to jdst (sources are never destinations of the same scour).
     SD void copy_runs(V jdst, V jsrc, V jlen) {
-#ifdef RG_NO_TEXT_COPY  // A/B timing only: wrong text
-        return;
-#endif
         const V jinc = simd::scan_incl(jlen);
         const u32 total = simd::readlane(jinc, 63);
         if (!total) return;
         const V jstart = jinc - jlen;
         u64 jm = simd::ballot(jlen != 0u);
         u16* ar = arena_cur();
-        u16* lt = lt_cur();
-        bool hbm = false;
         for (u32 base = 0; base < total; base += 64) {
             const V f = L() + base;
             V j = simd::splat(0);
@@ -1019,22 +932,12 @@ struct RegEngine {
             const V s0 = simd::bperm(jstart, j), d = simd::bperm(jdst, j), sr = simd::bperm(jsrc, j);
             const B m = f < total;
             const V o = f - s0;
-            const B fl = (sr & LT_BIT) != 0u, fa = (sr & ARENA_BIT) != 0u;
-            const V so = (sr & TOFF_MASK) + o;
-            V t = simd::ld(lt, so, m & fl);
-            if (simd::ballot(simd::andn(m, fl))) {
-                t = simd::sel(fl, t, simd::sel(fa, simd::ld(ar, so, m & fa), simd::ld(payload, so, simd::andn(simd::andn(m, fa), fl))));
-            }
-            const B dl = (d & LT_BIT) != 0u;
-            const V dd = (d & TOFF_MASK) + o;
-            simd::st(lt, dd, t, m & dl);
-            if (simd::ballot(simd::andn(m, dl))) {
-                simd::st(ar, dd, t, simd::andn(m, dl));
-                hbm = true;
-            }
+            const B fa = (sr & ARENA_BIT) != 0u;
+            const V so = (sr & ~ARENA_BIT) + o;
+            const V t = simd::sel(fa, simd::ld(ar, so, m & fa), simd::ld(payload, so, simd::andn(m, fa)));
+            simd::st(ar, (d & ~ARENA_BIT) + o, t, m);
         }
-        simd::lds_order();
-        if (hbm) adirty = true;
+        adirty = true;
     }
     // The serial walk of scourNode (any lengths): the granularity test needs the run's accumulated
     // length.
@@ -1079,10 +982,10 @@ struct RegEngine {
                     const u32 tc = simd::readlane(w.cap, gb + s);
                     const bool ok = prev >= 0 && pText && (mTXT & bit) && (pLen <= (u32)GRANULARITY || ln <= (u32)GRANULARITY);
                     if (ok) {  // TextSegment.append
-                        if ((pOff & (ARENA_BIT | LT_BIT)) && pLen + ln <= pCap) {
+                        if ((pOff & ARENA_BIT) && pLen + ln <= pCap) {
                             job(pOff + pLen, to, ln);
                         } else if (pOff + pLen == to && pMat == pLen) {  // text already contiguous
-                            if (pOff & (ARENA_BIT | LT_BIT)) pCap = to + tc - pOff;
+                            if (pOff & ARENA_BIT) pCap = to + tc - pOff;
                             pMat += ln;
                         } else {
                             u32 ncap = 2 * (pLen + ln);
@@ -1139,7 +1042,7 @@ struct RegEngine {
             if (status) return cnt;
             w = row(r);
         }
-        if (jn) copy_runs(jdst, jsrc, simd::sel(L() < jn, jlen, 0u));
+        if (jn) run_jobs(jn, jdst, jsrc, jlen);
         // compaction: group lane gb+i takes kept slot i
         const V sl = L() & 7u;
         const B kp = ing & (sl < nkeep);
@@ -1158,6 +1061,27 @@ struct RegEngine {
         cmp(w.sid, nullptr, 0u);
         putrow(r, w);
         return nkeep;
+    }
+    // The recorded copies as one flattened gather (sources are never destinations of one scour).
+    SD void run_jobs(u32 jn, V jdst, V jsrc, V jlen) {
+        const V jl = simd::sel(L() < jn, jlen, 0u);
+        const V jinc = simd::scan_incl(jl);
+        const u32 total = simd::readlane(jinc, 63);
+        const V jstart = jinc - jl;
+        u16* ar = arena_cur();
+        for (u32 base = 0; base < total; base += 64) {
+            const V f = L() + base;
+            V j = simd::splat(0);
+            for (u32 q = 1; q < jn; q++) j = simd::sel(f >= simd::readlane(jstart, q), q, j);
+            const V s0 = simd::bperm(jstart, j), d = simd::bperm(jdst, j), sr = simd::bperm(jsrc, j);
+            const B m = f < total;
+            const V o = f - s0;
+            const B fa = (sr & ARENA_BIT) != 0u;
+            const V so = (sr & ~ARENA_BIT) + o;
+            const V t = simd::sel(fa, simd::ld(ar, so, m & fa), simd::ld(payload, so, simd::andn(m, fa)));
+            simd::st(ar, (d & ~ARENA_BIT) + o, t, m);
+        }
+        adirty = true;
     }
 
     // pack (mergeTree.ts:1368-1420), leaf level: the m children [k0, k0+m) of level-1 node pi
@@ -1311,7 +1235,7 @@ struct RegEngine {
         const u32 sid = new_sid();
         if (sid == NONE) return NONE;
         const u32 rr = (u32)f.r;
-        const bool ar = (t.toff & (ARENA_BIT | LT_BIT)) != 0;  // owned text: cap >= len, split between the pieces
+        const bool ar = (t.toff & ARENA_BIT) != 0;  // arena text: cap >= len, split between the pieces
         const u32 lc = ar ? rr : 0u;
         RSeg right = t;
         right.len = t.len - rr;
@@ -1414,8 +1338,7 @@ struct RegEngine {
     }
 
     // Client.applyMsg for one op record (client.ts:805-836); false => not applied, hand off.
-    // lt: the op's inserted text in LDS (LT_BIT | offset), NONE when it stays in the payload
-    SD bool apply(const mte_op& op, u32 lt) {
+    SD bool apply(const mte_op& op) {
         RG_PROF(RP_APPLY);
         const u32 type = op.type;
         const bool ins = type == MTE_OP_INSERT || type == MTE_OP_INSERT_MARKER;
@@ -1439,8 +1362,8 @@ struct RegEngine {
             rec.seq = seq;
             rec.rseq = RSEQ_LIVE;
             rec.meta = (C & 0xFFu) | (RCL_LIVE << 8) | (mk ? F_MARKER : 0u);
-            rec.toff = mk ? op.b : (lt != NONE ? lt : (u32)op.a);
-            rec.cap = !mk && lt != NONE ? op.b : 0u;  // LDS text is owned (its chunk of the prefetch)
+            rec.toff = mk ? op.b : (u32)op.a;
+            rec.cap = 0;
             rec.rm = 0;
             rec.sid = 0;
             edited = op_insert(op.pos1, R, C, seq, rec);
@@ -1481,93 +1404,37 @@ struct RegEngine {
         }
         RG_PROF(RP_TOTAL);
         const u32* src = (const u32*)p.ops;
+        simd::VA<4> Q;
         const u64 b = i;
-        auto load_chunk = [&](u64 c0) MTE_LI {  // records [c0, c0+8): lane 8r + w = word w of record r
+        auto load_chunk = [&](u64 c0) MTE_LI {  // records [c0, c0+8)
             const u64 left = e > c0 ? e - c0 : 0;
             const u32 nw = left >= 8 ? 64u : (u32)left * 8u;
             return simd::ld(src + c0 * 8, L(), L() < nw);
         };
-        u32* RG = ring();
-        auto ring_put = [&](u32 slot, const V& x) MTE_LI {
-            simd::st(RG + slot * 64, L(), x, simd::splat(1u) == 1u);
-            simd::lds_order();
-        };
-        auto ring_get = [&](u32 slot) MTE_LI { return simd::ld(RG + slot * 64, L(), simd::splat(1u) == 1u); };
-        // Op records stream through a 4-chunk LDS ring, 32 ops ahead; inserted text 8 ops ahead (the
-        // payload units of the next chunk's inserts, up to 64, go to the LDS text arena when that
-        // chunk becomes current). Each in-flight global load lands in one register (QL, TQ) that is
-        // consumed at the next chunk boundary before it is reloaded: no register move of a load in
-        // flight, so no wait on it (a shifted register queue waited for its newest load every 8 ops).
-        for (u32 c = 0; c < 4; c++) ring_put(c, load_chunk(b + (u64)c * 8));
-        V QL = load_chunk(b + 32);                // chunk 4
-        V q = ring_get(0);                         // the current chunk
-        V TQ = simd::splat(0), TS = TQ, CS = TQ;  // text units; record starts (lane r) next / current
-        u32 TM = 0, TN = 0, CM = 0, CB = 0;         // records with prefetched text, units; current
-        prefetch_text(q, TQ, TS, TM, TN);
-        activate_text(TQ, TS, TM, TN, CS, CM, CB);
-        prefetch_text(ring_get(1), TQ, TS, TM, TN);
+        for (u32 c = 0; c < 4; c++) Q.set(c, load_chunk(b + (u64)c * 8));
         for (; i < e && !status; i++) {
             const u32 r = (u32)((i - b) & 7);
             if (r == 0 && i != b) {
-                const u32 k = (u32)((i - b) >> 3);  // chunk k becomes current
-                ring_put((k + 3) & 3u, QL);          // chunk k+3 (loaded at the last boundary)
-                activate_text(TQ, TS, TM, TN, CS, CM, CB);  // chunk k's text (loaded at the last boundary)
-                QL = load_chunk(i + 32);              // chunk k+4
-                q = ring_get(k & 3u);
-                prefetch_text(ring_get((k + 1) & 3u), TQ, TS, TM, TN);  // chunk k+1's text
+                Q.set(0, Q.get(1));
+                Q.set(1, Q.get(2));
+                Q.set(2, Q.get(3));
+                Q.set(3, load_chunk(i + 24));
             }
             mte_op op;
             {
                 RG_PROF(RP_FETCH);
+                const V q = Q.get(0);
                 u32 w[8];
                 for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(q, r * 8 + x);
                 __builtin_memcpy(&op, w, sizeof op);
             }
             RG_COUNT(RP_OPS, 1);
-            const u32 lt = (CM >> r) & 1u ? LT_BIT | (CB + simd::readlane(CS, r)) : NONE;
-            if (!apply(op, lt)) {
+            if (!apply(op)) {
                 status = REG_HANDOFF;
                 return i;
             }
         }
         return i;
-    }
-    // The payload text of chunk q's inserts (records r < 8: lane 8r + w holds word w): record r's text
-    // goes to units [TS[r], TS[r] + len) of TQ when it is a plain insert and the chunk's texts up to it
-    // fit RG_PF_UNITS; the loads are left in flight.
-    SD void prefetch_text(const V& q, V& TQ, V& TS, u32& TM, u32& TN) const {
-        const V l8 = L() * 8u;
-        const V w7 = simd::bperm(q, l8 + 7u), a = simd::bperm(q, l8 + 4u), n = simd::bperm(q, l8 + 5u);
-        const B ins = (L() < 8u) & ((w7 & 0xFFu) == (u32)MTE_OP_INSERT) & (((w7 >> 16) & MTE_F_PERM) == 0u) &
-                      (n != 0u) & (n < RG_PF_UNITS + 1u);
-        const V len = simd::sel(ins, n, 0u);
-        const V inc = simd::scan_incl(len);
-        const B fit = ins & (inc < RG_PF_UNITS + 1u);  // a prefix of the records (inc is monotone)
-        TM = (u32)simd::ballot(fit) & 0xFFu;
-        TS = inc - len;
-        TN = TM ? simd::readlane(inc, 31u - (u32)__builtin_clz(TM)) : 0u;
-        if (!TN) return;
-        V rec = simd::splat(0);  // the record of unit lane u
-        for (u32 m = TM; m; m &= m - 1) {
-            const u32 x = (u32)__builtin_ctz(m);
-            rec = simd::sel(L() >= simd::readlane(TS, x), x, rec);
-        }
-        const V off = simd::bperm(a, rec) + (L() - simd::bperm(TS, rec));
-        TQ = simd::ld(payload, off, L() < TN);
-    }
-    // The prefetched units become the current chunk's texts in the LDS arena (compacted first when
-    // full; with no room the chunk's inserts keep their payload text).
-    SD void activate_text(const V& TQ, const V& TS, u32 TM, u32 TN, V& CS, u32& CM, u32& CB) {
-        CM = 0;
-        if (!TN) return;
-        if (ltTop + TN + 256u > ltCap && !lds_gc()) return;  // (slack for the merges' chunks)
-        if (ltTop + TN > ltCap) return;
-        simd::st(lt_cur(), L() + ltTop, TQ, L() < TN);
-        simd::lds_order();
-        CS = TS;
-        CM = TM;
-        CB = ltTop;
-        ltTop += TN;
     }
 
     // ---------------------------------------------------------------- results

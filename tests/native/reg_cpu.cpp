@@ -20,7 +20,7 @@ extern "C" {
 uint64_t regcpu_replay(const mte_op* ops, uint64_t n_ops, const uint16_t* payload, uint32_t payload_len,
                        uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
                        uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
-                       DocRes* res, uint32_t lt_limit) {
+                       DocRes* res) {
     std::vector<uint16_t> pay(payload, payload + payload_len + 1);
     std::vector<uint16_t> arena((size_t)arena_cap * 2 + 1, 0);
     DocCfg cfg;
@@ -47,9 +47,7 @@ uint64_t regcpu_replay(const mte_op* ops, uint64_t n_ops, const uint16_t* payloa
     p.out_text = out_text;
     p.out_text_cap = out_text_cap;
     p.counters = counters;
-    p.reg_lt_limit = lt_limit;
-    RegEngine<>* ep = new RegEngine<>(p, 0);  // (its LDS text arrays are too large for the stack)
-    RegEngine<>& e = *ep;
+    RegEngine<> e(p, 0);
     const uint64_t at = e.replay(0, n_ops);
     if (e.status == REG_HANDOFF) {
         memset(res, 0, sizeof *res);
@@ -57,11 +55,9 @@ uint64_t regcpu_replay(const mte_op* ops, uint64_t n_ops, const uint16_t* payloa
         res->n_lb = e.n_lb;
         res->heap_size = e.heapSize;
         res->height = e.height;
-        delete ep;
         return at;
     }
     e.finish();
-    delete ep;
     return at;
 }
 

@@ -1304,8 +1304,8 @@ struct Engine {
     MTE_DEV u32 build_map(u32 old, u32 propset, bool rewrite) {
         if constexpr (!FULL) return 0;
         MTE_PROF(PF_MAP);
-        if (st.mapNext >= map_cap) {
-            fail(MTE_DOC_CAPACITY, st.curSeq);
+        if (st.mapNext >= map_cap) {  // the load-time estimate was short: re-run with the worst case
+            fail(p.map_rerun ? MTE_DOC_CAPACITY : DOC_SPILL, st.curSeq);
             return 0;
         }
         const u32 maxp = (mw - 1) / 2 < MTE_MAX_PROPS ? (mw - 1) / 2 : MTE_MAX_PROPS;

@@ -206,6 +206,7 @@ struct Params {
     u32 reg_solo;             // k_solo replays lean documents register-resident first (reg_engine.hpp)
     u32 reg_lb_limit;         // test knob: leaf blocks the register plan may hold (0 = all it has)
     u32 map_words;            // words per property-map record (a multiple of 4, >= MAP_WORDS)
+    u32 map_rerun;            // 1 in the host's re-run pass: a full map table is a capacity failure
     u32 pad1;
 };
 

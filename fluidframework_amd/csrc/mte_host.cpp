@@ -257,6 +257,10 @@ struct mte_engine {
     DevBuf<uint32_t> d_out_maps, d_prop_keys, d_prop_vals, d_val_flags, d_val_objidx, d_order, d_list, d_maps, d_counters,
         d_first_seen;
     DevBuf<uint64_t> d_val_objmatch, d_ovl, d_out_ovl, d_prof;
+    // property maps of the documents the host re-ran (their worst-case table), by document
+    DevBuf<uint32_t> d_maps_rr;
+    std::vector<uint64_t> map_rr_off;  // UINT64_MAX = the document's maps are in d_maps
+    std::vector<uint32_t> map_rr_cap;
     DevBuf<DocCfg> d_cfg;
     DevBuf<DocRes> d_res;
     DevBuf<uint4> d_out_vis, d_out_aux;
@@ -1003,6 +1007,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, e->d_prof.n * sizeof(uint64_t), s_main));  // profiling build
     HIP_TRY(e, hipEventRecord(e->ev0, s_main));
     std::vector<uint32_t> spill;
+    e->map_rr_off.clear();  // (set again below for this pass's re-run documents)
     float lds_ms = 0, hbm_ms = 0;
     // pass 1: the solo workgroups first (third stream: each takes a CU), then the LDS workgroups
     // (one per remaining CU, all of its LDS), then the HBM-resident waves on the second stream so
@@ -1071,17 +1076,58 @@ static int run_kernel(mte_engine* e, bool gen) {
             total += (bytes + 255) & ~255ull;
         }
         HIP_TRY(e, e->d_hbm.alloc(total));
+        // property maps: the load-time estimate (prop inserts + 4 per annotate) may be short for a
+        // re-run document; it gets the worst case, a new map per annotated character, in a table of
+        // its own (e->map_rr_off; the first pass's layout stays as it was)
+        std::vector<std::pair<uint64_t, uint32_t>> keep_maps;
+        uint64_t mtot = 0;
+        e->map_rr_off.assign(nd, UINT64_MAX);
+        e->map_rr_cap.assign(nd, 0);
+        for (uint32_t d : spill) {
+            DocCfg& c = e->cfg[d];
+            uint64_t cap = 16;
+            if (gen) {
+                cap += e->n_ops_doc[d] * 17;  // generated annotates span at most 16 characters
+            } else {
+                std::vector<mte_op> ops(c.op_end - c.op_begin);
+                if (!ops.empty())
+                    HIP_TRY(e, hipMemcpy(ops.data(), e->d_ops.p + c.op_begin, ops.size() * sizeof(mte_op), hipMemcpyDeviceToHost));
+                for (const mte_op& o : ops) {
+                    if (o.type == MTE_OP_ANNOTATE)
+                        cap += (o.flags & MTE_F_REL) ? (uint64_t)c.payload_len + 2 : (uint64_t)std::max<int64_t>(0, (int64_t)o.a - o.pos1) + 2;
+                    else if (o.props)
+                        cap += 1;
+                }
+            }
+            keep_maps.emplace_back(c.map_off, c.map_cap);
+            c.map_cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFF0ull);
+            c.map_off = mtot;
+            e->map_rr_off[d] = mtot;
+            e->map_rr_cap[d] = c.map_cap;
+            mtot += c.map_cap;
+        }
+        HIP_TRY(e, e->d_maps_rr.alloc(std::max<uint64_t>(mtot, 1) * e->map_words));
         if ((rc = upload(e, e->d_cfg, e->cfg))) return rc;
         if ((rc = upload(e, e->d_list, spill))) return rc;
         e->P.docs = e->d_cfg.p;
         e->P.hbm = e->d_hbm.p;
         e->P.doc_list = e->d_list.p;
         e->P.n_list = (uint32_t)spill.size();
+        e->P.maps = e->d_maps_rr.p;
+        e->P.map_rerun = 1;
         HIP_TRY(e, hipEventRecord(e->ev0, e->stream));
         HIP_TRY(e, launch_hbm(e->P, gen, full, (uint32_t)spill.size(), e->stream));
         HIP_TRY(e, hipEventRecord(e->ev1, e->stream));
         HIP_TRY(e, hipStreamSynchronize(e->stream));
         HIP_TRY(e, hipEventElapsedTime(&hbm_ms, e->ev0, e->ev1));
+        e->P.maps = e->d_maps.p;
+        e->P.map_rerun = 0;
+        for (size_t q = 0; q < spill.size(); q++) {  // the next pass starts from the load-time layout
+            e->cfg[spill[q]].map_off = keep_maps[q].first;
+            e->cfg[spill[q]].map_cap = keep_maps[q].second;
+        }
+        if ((rc = upload(e, e->d_cfg, e->cfg))) return rc;
+        e->P.docs = e->d_cfg.p;
         e->P.doc_list = e->d_order.p;
         e->P.n_list = nd;
     }
@@ -1665,10 +1711,13 @@ static json::Value jnumv(double x) {
 static int read_map(mte_engine* e, uint32_t d, uint32_t id, std::vector<std::pair<uint32_t, uint32_t>>& kv) {
     kv.clear();
     if (id == 0) return MTE_OK;
-    if (id >= e->cfg[d].map_cap) return set_err(e, MTE_E_STATE, "catch-up: property map id out of range");
+    const bool rr0 = d < e->map_rr_off.size() && e->map_rr_off[d] != UINT64_MAX;
+    if (id >= (rr0 ? e->map_rr_cap[d] : e->cfg[d].map_cap))
+        return set_err(e, MTE_E_STATE, "catch-up: property map id out of range");
     std::vector<uint32_t> w(e->map_words);
-    HIP_TRY(e, hipMemcpy(w.data(), e->d_maps.p + (e->cfg[d].map_off + id) * e->map_words, w.size() * 4,
-                         hipMemcpyDeviceToHost));
+    const bool rr = d < e->map_rr_off.size() && e->map_rr_off[d] != UINT64_MAX;
+    const uint32_t* base = rr ? e->d_maps_rr.p + e->map_rr_off[d] * e->map_words : e->d_maps.p + e->cfg[d].map_off * e->map_words;
+    HIP_TRY(e, hipMemcpy(w.data(), base + (uint64_t)id * e->map_words, w.size() * 4, hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < std::min<uint32_t>(w[0], (e->map_words - 1) / 2); i++) kv.emplace_back(w[1 + 2 * i], w[2 + 2 * i]);
     return MTE_OK;
 }

@@ -62,6 +62,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=None, help="default: one per host core available")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify-docs", type=int, default=32, help="docs checked against the oracle after timing")
+    ap.add_argument("--opt", action="append", default=[], help="engine option key=value (A/B runs; repeatable)")
     a = ap.parse_args(argv)
     c = CONFIGS[a.config]
     a.docs = c["docs"] if a.docs is None else a.docs
@@ -140,6 +141,9 @@ def run(args):
 
     cfg = CONFIGS[args.config]
     eng = mte.Engine(local)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
     t0 = time.time()
     ids, counts = plan_shard(args.config, world, rank, args.docs, args.ops)
     n_local = len(ids)

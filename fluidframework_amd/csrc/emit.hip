@@ -165,33 +165,42 @@ struct Doc {
         }
         return true;
     }
-    // {"k":v,...} in JS key order
+    // {"k":v,...} in JS key order: array-index keys ascending (repeated minimum; the keys of a map are
+    // distinct), then the others in insertion order. Up to (map_words - 1) / 2 pairs.
     MTE_DEV void put_props(Out& o, u64 row) const {
         const u32* m = map(row);
-        const u32 n = m[0] < 7 ? m[0] : 7u;
-        u32 ord[7];
-        u32 k = 0;
-        // array-index keys ascending first (insertion sort of at most 7), then insertion order
-        for (u32 i = 0; i < n; i++) {
-            const u32 key = m[1 + 2 * i];
-            if (!p.key_is_index[key]) continue;
-            u32 j = k++;
-            while (j > 0 && p.key_index[m[1 + 2 * ord[j - 1]]] > p.key_index[key]) {
-                ord[j] = ord[j - 1];
-                j--;
-            }
-            ord[j] = i;
-        }
-        for (u32 i = 0; i < n; i++)
-            if (!p.key_is_index[m[1 + 2 * i]]) ord[k++] = i;
-        put(o, "{");
-        for (u32 q = 0; q < n; q++) {
-            if (q) put(o, ",");
-            const u32 key = m[1 + 2 * ord[q]], val = m[2 + 2 * ord[q]];
+        const u32 cap = (p.map_words - 1) / 2;
+        const u32 n = m[0] < cap ? m[0] : cap;
+        bool first = true;
+        auto pair = [&](u32 i) {
+            if (!first) put(o, ",");
+            first = false;
+            const u32 key = m[1 + 2 * i], val = m[2 + 2 * i];
             put_bytes(o, p.key_text + p.key_off[key], p.key_off[key + 1] - p.key_off[key]);
             put(o, ":");
             put_bytes(o, p.val_text + p.val_off[val], p.val_off[val + 1] - p.val_off[val]);
+        };
+        put(o, "{");
+        bool have = false;
+        u32 last = 0;
+        for (;;) {
+            u32 best = NONE, bidx = 0;
+            for (u32 i = 0; i < n; i++) {
+                const u32 key = m[1 + 2 * i];
+                if (!p.key_is_index[key]) continue;
+                const u32 idx = p.key_index[key];
+                if ((!have || idx > last) && (best == NONE || idx < bidx)) {
+                    best = i;
+                    bidx = idx;
+                }
+            }
+            if (best == NONE) break;
+            pair(best);
+            last = bidx;
+            have = true;
         }
+        for (u32 i = 0; i < n; i++)
+            if (!p.key_is_index[m[1 + 2 * i]]) pair(i);
         put(o, "}");
     }
     MTE_DEV void put_name(Out& o, u32 slot) const {  // getLongClientId, JSON-quoted

@@ -299,6 +299,7 @@ struct mte_engine {
     uint32_t last_spilled = 0, last_continued = 0, last_hbm_docs = 0, last_hbm_waves = 0, last_lds_groups = 0;
     uint32_t last_solo = 0;
     double last_solo_ms = 0;
+    double last_alloc_ms = 0;  // mte_load: device layout and allocation (inside h2d_ms)
     double last_solo_lead_ms = 0, last_solo_tail_ms = 0;  // pass start -> solo start, solo end -> pass end
     uint32_t n_groups = 256;
     // SnapshotV1 emission on the device (emit.hip): property / name tables, scratch, and two output
@@ -799,6 +800,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     int rc;
     if ((rc = layout_and_alloc(e, n_ops, pay, pi, an, collab, has_nl, 0, b->doc_op_offsets, b->doc_payload_offsets)))
         return rc;
+    e->last_alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     // catch-up delta records (legacy summaries): an insert has one range, a remove / annotate at most
     // one per character of its range (every delta segment is visible in the op's view), or at most
     // every segment when a position is relative
@@ -2172,6 +2174,7 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "solo") *value = e->last_solo;
     else if (k == "solo_us") *value = (int64_t)(e->last_solo_ms * 1000.0);  // the solo workgroups' pass (critical path)
     else if (k == "solo_lead_us") *value = (int64_t)(e->last_solo_lead_ms * 1000.0);
+    else if (k == "load_alloc_us") *value = (int64_t)(e->last_alloc_ms * 1000.0);
     else if (k == "solo_tail_us") *value = (int64_t)(e->last_solo_tail_ms * 1000.0);
     else if (k == "lean") *value = e->last_lean;
     else if (k == "emit_us") *value = (int64_t)(e->last_emit_ms * 1000.0);  // emission after the replay pass

@@ -219,13 +219,14 @@ struct Doc {
 
     // 1. entries: ent[row0 + k] = (first row, last row, length, kind) with kind 0 a settled text
     // run, 1 a settled marker, 2 a merge-info segment, 3 a settled PermutationSegment run (its
-    // canAppend: two unallocated runs always append, permutationvector.ts:88-94); returns the count
+    // canAppend, permutationvector.ts:88-94: two unallocated runs, or a handle run continuing the
+    // previous one; aux.y = start handle, 0 = unallocated); returns the count
     MTE_DEV u32 build_entries() const {
         const u32 L = lane_id(), n = r.n_segs;
         const i32 minSeq = r.min_seq;
         u32 ne = 0;
         bool open = false, runText = false, runProps = false, runPerm = false;
-        u32 runFirst = 0, runLast = 0, runLen = 0, runLast16 = 0;
+        u32 runFirst = 0, runLast = 0, runLen = 0, runLast16 = 0, runStart = 0;
         auto close = [&]() {
             if (open && L == 0) p.ent[row0 + ne] = make_uint4(runFirst, runLast, runLen, runPerm ? 3u : runText ? 0u : 1u);
             ne += open ? 1u : 0u;
@@ -243,13 +244,13 @@ struct Doc {
             const u32 cnt = n - base < 64 ? n - base : 64u;
             for (u32 j = 0; j < cnt; j++) {
                 const u32 len = wave_read(v.x, j), seq = wave_read(v.y, j), rseq = wave_read(v.z, j);
-                const u32 meta = wave_read(v.w, j), hasP = wave_read(a.x, j) != 0;
+                const u32 meta = wave_read(v.w, j), hasP = wave_read(a.x, j) != 0, start = wave_read(a.y, j);
                 const bool removed = (meta & F_REMOVED) != 0, marker = (meta & F_MARKER) != 0, perm = (meta & F_PERM) != 0;
                 const u32 row = base + j;
                 if (removed && (i32)rseq <= minSeq) continue;  // elided (:184-186)
                 if (p.legacy && (i32)seq > minSeq) continue;   // not in the view at minSeq (legacy :195-196)
                 if ((i32)seq <= minSeq && (!removed || p.legacy)) {
-                    if (open && (runPerm ? perm
+                    if (open && (runPerm ? perm && start == (runStart ? runStart + runLen : 0u)
                                          : runText && !marker && !perm && !(runLen && runLast16 == u'\n') &&
                                                (runLen <= 256 || len <= 256)) &&
                         match(row0 + runFirst, runProps, row0 + row, hasP)) {
@@ -262,6 +263,7 @@ struct Doc {
                     open = true;
                     runText = !marker && !perm;
                     runPerm = perm;
+                    runStart = start;
                     runProps = hasP;
                     runFirst = runLast = row;
                     runLen = len;
@@ -313,7 +315,9 @@ struct Doc {
         if (v.w & F_PERM) {  // PermutationSegment.toJSONObject (permutationvector.ts:75-77): [length, start]
             put(o, "[");
             put_int(o, (i64)n);
-            put(o, ",-2147483648]");  // Handle.unallocated: an observer never allocates handles
+            put(o, ",");
+            put_int(o, a.y ? (i64)a.y : (i64)-2147483648LL);  // the start handle, or Handle.unallocated
+            put(o, "]");
             return;
         }
         if (v.w & F_MARKER) {

@@ -192,6 +192,7 @@ struct Engine {
     u32* m_hint;   // HBM mode: HBM_HINTS entries
     u32 m_blk_cap, m_ord_cap, m_in_cap, m_heap_cap;
     u32 wave;
+    i32 zseq = 0;            // EXT: seq of the op being applied (UNLINK time of freed handles)
     bool continued = false;  // HBM-resident after starting in LDS
     bool capped = false;     // HBM slot smaller than this document's worst case
 
@@ -743,6 +744,163 @@ struct Engine {
             op.a = (rr.flags & MTE_F_REL_BEFORE2) ? q - (i32)rr.props : q + 1 + (i32)rr.props;
         }
         return true;
+    }
+
+    // ---------------------------------------------------------------- SharedMatrix cell ops
+    // getContainingSegment (mergeTree.ts:1623-1634 -> searchBlock :1797-1829): the first segment whose
+    // visible length in the (R, C) view exceeds the remaining position. f.slot / f.r: the segment and
+    // the offset in it; !f.ok when pos is beyond the view's length.
+    MTE_DEV Found contain(i32 pos, i32 R, u32 C) {
+        Found f;
+        f.ok = false;
+        f.k = 0;
+        f.blk = NONE;
+        f.cnt = 0;
+        f.slot = -1;
+        f.r = 0;
+        f.cum = 0;
+        if (pos < 0) return f;
+        fence_ovl();
+        i32 cum = 0;
+        for (u32 base = 0; base < st.n_lb; base += 64) {
+            const u32 k = base + L;
+            const bool valid = k < st.n_lb;
+            const uint4 o = valid ? ORD()[k] : make_uint4(0, 0, 0, 0);
+            const u32 v = blen_all(o, valid, R, C);
+            const u32 incl = wave_scan_incl(v);
+            const u64 hit = wave_ballot(valid && cum + (i32)incl > pos);
+            if (hit) {
+                const u32 j = (u32)__builtin_ctzll(hit);
+                f.k = base + j;
+                f.blk = wave_read(o.x, j);
+                f.cnt = wave_read(o.w, j);
+                f.cum = cum + (i32)wave_read(incl - v, j);
+                const u32 idx = sidx(f.blk, L);
+                const bool in = L < f.cnt && L < 8;
+                const u32 sv = in ? vis_len(VIS()[idx], AUX()[idx].z, idx, R, C, C == 0 ? 1u : 0u) : 0u;
+                const u32 si = group8_scan(sv);
+                const i32 r = pos - (f.cum + (i32)(si - sv));
+                const u64 m = wave_ballot(in && r >= 0 && r < (i32)sv);
+                if (m) {
+                    f.ok = true;
+                    f.slot = (i32)__builtin_ctzll(m);
+                    f.r = wave_read(r, (u32)f.slot);
+                }
+                return f;
+            }
+            cum += (i32)wave_read(incl, 63);
+        }
+        return f;
+    }
+    // PermutationVector.adjustPosition (permutationvector.ts:198-209): the containing segment in the
+    // op's view; undefined (-1) when there is none or it is removed (removedSeq set, whatever its
+    // seq), else its position in the local view (getPosition at currentSeq, mergeTree.ts:1586-1603)
+    // plus the offset.
+    MTE_DEV i32 cell_adjust(i32 pos, i32 R, u32 C) {
+        const Found f = contain(pos, R, C);
+        if (!f.ok) return -1;
+        const u32 meta = wave_first(VIS()[sidx(f.blk, (u32)f.slot)].w);
+        if (meta & F_REMOVED) return -1;
+        return obs_prefix(f.k, f.blk, (u32)f.slot) + f.r;
+    }
+    // HandleTable (handletable.ts:19-86) of this vector in HBM: ht[0] = the handles array's length,
+    // ht[1 + i] = handles[i] (handles[0] = the free-list head), ht[1 + cap + i] = the seq of the op
+    // whose zamboni last freed handle i (0 = never). Lane 0 owns it; results are broadcast.
+    MTE_DEV u32* ht_base() const { return p.htab + p.docs[doc].ht_off; }
+    MTE_DEV void ht_reset() {
+        const u32 cap = p.docs[doc].ht_cap;
+        if (!cap || !p.htab) return;
+        u32* ht = ht_base();
+        for (u32 i = L; i < cap; i += 64) ht[1 + cap + i] = 0;
+        if (L == 0) {
+            ht[0] = 1;  // new HandleTable(): [1]
+            ht[1] = 1;
+        }
+        wave_sync();
+    }
+    MTE_DEV u32 ht_alloc() {  // HandleTable.allocate (handletable.ts:35-40)
+        const u32 cap = p.docs[doc].ht_cap;
+        u32 h = NONE;
+        if (L == 0 && cap && p.htab) {
+            u32* ht = ht_base();
+            const u32 len = ht[0], fr = ht[1];
+            if (fr >= 1 && fr < cap && fr <= len) {
+                ht[1] = fr < len ? ht[1 + fr] : fr + 1;  // handles[free] ?? free + 1
+                ht[1 + fr] = 0;
+                if (fr == len) ht[0] = len + 1;
+                h = fr;
+            }
+        }
+        h = wave_read(h, 0);
+        if (h == NONE) fail(MTE_DOC_CAPACITY, st.curSeq);
+        return h;
+    }
+    MTE_DEV void ht_free(u32 h0, u32 n) {  // HandleTable.free (:56-59) of h0 .. h0 + n - 1
+        const u32 cap = p.docs[doc].ht_cap;
+        bool bad = false;
+        if (L == 0) {
+            u32* ht = ht_base();
+            for (u32 i = 0; i < n; i++) {
+                const u32 h = h0 + i;
+                if (h >= cap) {
+                    bad = true;
+                    break;
+                }
+                ht[1 + h] = ht[1];
+                ht[1] = h;
+                ht[1 + cap + h] = (u32)zseq;
+            }
+        }
+        if (wave_ballot(bad)) fail(MTE_DOC_CAPACITY, st.curSeq);
+        wave_sync();
+    }
+    // getAllocatedHandle (permutationvector.ts:176-196) at local position pos: the segment's handle
+    // when allocated, else walkSegments(pos, pos + 1, splitRange) -- ensureIntervalBoundary at pos
+    // and pos + 1 in the local view (mergeTree.ts:2797-2807, 2241-2245) -- and the new length-1
+    // segment takes the next handle.
+    MTE_DEV u32 cell_handle(i32 pos, i32 seq) {
+        const i32 R = st.curSeq;
+        Found f = contain(pos, R, 0);
+        if (!f.ok) {
+            fail(MTE_DOC_CAPACITY, seq);
+            return 0;
+        }
+        const u32 toff = wave_first(AUX()[sidx(f.blk, (u32)f.slot)].y);
+        if (toff) return toff + (u32)f.r;
+        Seg none;
+        none.len = 0;
+        edit(MTE_OP_CELL, pos, pos + 1, R, 0, seq, none, 0, false, false);
+        if (st.status) return 0;
+        f = contain(pos, R, 0);
+        if (!f.ok || f.r != 0) {
+            fail(MTE_DOC_CAPACITY, seq);
+            return 0;
+        }
+        const u32 h = ht_alloc();
+        if (st.status) return 0;
+        sync();
+        if (L == 0) AUX()[sidx(f.blk, (u32)f.slot)].y = h;
+        sync();
+        return h;
+    }
+    // SharedMatrix.processCore's remote set (matrix.ts:575-601) as this vector sees it: pass 1 records
+    // adjustPosition; pass 2 allocates when both vectors' positions were defined (the row's gates the
+    // column's, and both gate the handles).
+    MTE_DEV void cell_op(const mte_op& op, i32 R, u32 C) {
+        const u32 g = op.b, w = (op.flags & MTE_F_CELL_COL) ? 1u : 0u;
+        if (!p.cell_pos || !p.cell_h) {
+            fail(MTE_DOC_UNSUPPORTED, op.seq);
+            return;
+        }
+        if (p.cell_mode == 1) {
+            const i32 a = cell_adjust(op.pos1, R, C);
+            if (L == 0) p.cell_pos[2 * (u64)g + w] = a < 0 ? NONE : (u32)a;
+            return;
+        }
+        const u32 pr = wave_first(p.cell_pos[2 * (u64)g]), pc = wave_first(p.cell_pos[2 * (u64)g + 1]);
+        u32 h = 0;
+        if (pr != NONE && pc != NONE) h = cell_handle((i32)(w ? pc : pr), op.seq);
+        if (L == 0) p.cell_h[2 * (u64)g + w] = h;
     }
 
     // ---------------------------------------------------------------- legacy catch-up delta ranges
@@ -1486,8 +1644,9 @@ struct Engine {
         if (!(mREM & ~mKEPT) && !(mSET & (mSET << 1))) return cnt;  // nothing dropped, nothing to merge
         MTE_COUNT(PN_SCOUR_CHANGED, 1);
         const u64 mTXT = wave_ballot(act && !(me.meta & (F_MARKER | F_PERM)));
-        // PermutationSegment runs (FULL batches only): canAppend holds between two unallocated runs
-        // (permutationvector.ts:88-94; an observer never allocates handles), no granularity, no text
+        // PermutationSegment runs (EXT batches only): canAppend holds between two unallocated runs or
+        // two handle runs where the second starts at the first's end (permutationvector.ts:88-94; toff
+        // holds the start handle, 0 = unallocated), no granularity, no text
         const u64 mPERM = EXT ? wave_ballot(act && (me.meta & F_PERM)) : 0ull;
         const u64 mNL = (FULL && has_nl) ? wave_ballot(act && !(me.meta & F_MARKER) && ends_nl(me.toff, me.len)) : 0ull;
         u32 nkeep = 0;
@@ -1516,7 +1675,7 @@ struct Engine {
                     const u32 len = wave_read(me.len, s), props = wave_read(me.props, s);
                     const u32 toff = wave_read(me.toff, s), tcap = wave_read(me.tcap, s);
                     const bool ok = prev >= 0 && match_props(pProps, props) &&
-                                    (pPerm ? (mPERM & bit) != 0
+                                    (pPerm ? (mPERM & bit) != 0 && toff == (pOff ? pOff + pLen : 0u)
                                            : pText && !pNL && (mTXT & bit) &&
                                                  (pLen <= (u32)GRANULARITY || len <= (u32)GRANULARITY));
                     if (ok) {  // TextSegment.append (textSegment.ts:74-85) / PermutationSegment.append
@@ -1587,6 +1746,16 @@ struct Engine {
             arena_gc();  // moves every arena text: re-read the slots and redo the chain
             if (st.status) return cnt;
             if (act) me = load(blk, L);
+        }
+        if constexpr (EXT) {
+            // MergeTreeMaintenanceType.UNLINK of each dropped permutation run, in slot order
+            // (PermutationVector.onMaintenance, permutationvector.ts:357-382): its handles go back to
+            // the free list in ascending order
+            for (u64 fm = mREM & ~mKEPT & mPERM; fm && p.docs[doc].ht_cap; fm &= fm - 1) {
+                const u32 s = (u32)__builtin_ctzll(fm);
+                const u32 h0 = wave_read(me.toff, s), n = wave_read(me.len, s);
+                if (h0) ht_free(h0, n);
+            }
         }
 #ifdef MTE_PROFILE
         if (MTE_PON(PF_SCOUR_CHAIN) && L == 0) atomicAdd(prof + PF_SCOUR_CHAIN, __builtin_amdgcn_s_memtime() - _tc0);
@@ -1839,6 +2008,7 @@ struct Engine {
         }
         for (u32 ph = 0; ph < nphase; ph++) {
             if (!ins && ph == 2) {
+                if (EXT && type == MTE_OP_CELL) return st.status == 0;  // walkSegments' splitRange only
                 range_op(type == MTE_OP_REMOVE, p1, p2, R, C, seq, propset, rewrite, pn == st.n_lb, pv, pincl, cu);
                 return st.status == 0;
             }
@@ -1870,7 +2040,9 @@ struct Engine {
                 task = left;
                 const u32 r = (u32)f.r;
                 task.len = left.len - r;
-                task.toff = left.toff + r;
+                // PermutationSegment.createSplitSegmentAt (permutationvector.ts:105-117): the handle
+                // run continues (toff = start handle, 0 = Handle.unallocated)
+                task.toff = (EXT && (left.meta & F_PERM) && left.toff == 0u) ? 0u : left.toff + r;
                 const bool rm = (left.meta & F_REMOVED) != 0;  // tcap holds the overlap mask then
                 task.tcap = rm ? left.tcap : ((left.toff & ARENA_BIT) ? left.tcap - r : 0u);
                 task.sid = sid;
@@ -2241,9 +2413,16 @@ struct Engine {
         const u32 C = collab ? (u32)op.client : 0u;
         const i32 seq = collab ? op.seq : 0;
         const i32 R = collab && !ld ? op.ref_seq : 0;
+        if constexpr (EXT) zseq = op.seq;  // the time of this op's UNLINKs (ht_free)
         if (collab && op.type != MTE_OP_NOOP && !ld && !(st.curSeq < op.seq)) {
             fail(MTE_DOC_SEQ_ORDER, op.seq);
             return;
+        }
+        if constexpr (EXT) {
+            if (op.type == MTE_OP_CELL) {  // no merge-tree op, no seq / msn movement (include/mte.h)
+                cell_op(op, R, C);
+                return;
+            }
         }
         if constexpr (FULL) {  // relative positions need marker ids, i.e. properties
             if (op.flags & MTE_F_REL) {
@@ -2313,6 +2492,7 @@ struct Engine {
 
     // ---------------------------------------------------------------- driver
     MTE_DEV void init() {
+        if constexpr (EXT) ht_reset();
         u32 r = alloc_lb();
         st.root = r;
         st.height = 1;

@@ -110,7 +110,8 @@ struct DocCfg {
     u64 hb_off;        // byte offset of this doc's HBM-resident state (HBM mode only)
     u64 cu_off;        // first catch-up delta record (Params::cu_rec, 2 x uint4 each) of this doc
     u32 cu_cap;        // catch-up delta records it may write (MTE_F_CATCHUP ops)
-    u32 cu_pad;
+    u32 ht_cap;        // SharedMatrix vector with cell ops: HandleTable slots (cell records + 2), else 0
+    u64 ht_off;        // its HandleTable in Params::htab: [length, handles[ht_cap], last free seq[ht_cap]]
     u32 payload_len;
     u32 arena_cap;
     u32 seg_cap;       // segment ids available
@@ -207,7 +208,13 @@ struct Params {
     u32 reg_lb_limit;         // test knob: leaf blocks the register plan may hold (0 = all it has)
     u32 map_words;            // words per property-map record (a multiple of 4, >= MAP_WORDS)
     u32 map_rerun;            // 1 in the host's re-run pass: a full map table is a capacity failure
-    u32 pad1;
+    // SharedMatrix cell ops (MTE_OP_CELL): pass 1 (cell_mode 1) writes each record's adjustPosition
+    // (NONE = undefined) to cell_pos[2 * cell + col]; pass 2 (cell_mode 2) allocates the handles of the
+    // cells both vectors defined and writes them to cell_h (0 = none)
+    u32 cell_mode;
+    u32* cell_pos;
+    u32* cell_h;
+    u32* htab;
 };
 
 // MTE_PROFILE builds: s_memtime cycles per engine phase, per document (engine.hpp PROF_*).

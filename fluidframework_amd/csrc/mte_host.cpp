@@ -218,6 +218,7 @@ struct mte_builder {
     std::unique_ptr<Interner> in;
     std::string err;
     std::vector<std::string> paths;  // per document: channel full path (container logs), else ""
+    uint32_t n_cells = 0;            // SharedMatrix cell ops so far (MTE_OP_CELL's cell index)
     mte_builder() { in.reset(new Interner(&hb)); }
 };
 
@@ -284,6 +285,16 @@ struct mte_engine {
     bool lean_ok = false;                // batch_is_lean: the replay may run the FULL = false kernels
     bool ext_needed = false;             // catch-up records or permutation runs: the EXT kernels (level 2)
     bool ext_perm = false;               // the loaded batch has permutation runs (always EXT)
+    // SharedMatrix cell ops (MTE_OP_CELL): two passes (engine_types.hpp Params::cell_mode); per doc
+    // with cell records, the records' (cell index, seq, value id) for the cells blob
+    struct CellRec {
+        uint32_t cell;
+        int32_t seq;
+        uint32_t val;
+    };
+    std::unordered_map<uint32_t, std::vector<CellRec>> cell_recs;
+    uint64_t n_cells = 0;                // cell indices 0 .. n_cells - 1
+    DevBuf<uint32_t> d_cell_pos, d_cell_h, d_htab;
     bool ext_cu = false;                 // ... MTE_F_CATCHUP ops: EXT only when a legacy summary is emitted
     bool lean_base = false;              // batch_is_lean, before the catch-up records decide
     bool lean_opt = true;                // option "lean" (0 = always the FULL kernels)
@@ -300,6 +311,7 @@ struct mte_engine {
     uint32_t last_solo = 0;
     double last_solo_ms = 0;
     double last_alloc_ms = 0;  // mte_load: device layout and allocation (inside h2d_ms)
+    double stage_copy_ms = 0, stage_wait_ms = 0;  // mte_load: host memcpy into / DMA waits on the stage
     double last_solo_lead_ms = 0, last_solo_tail_ms = 0;  // pass start -> solo start, solo end -> pass end
     uint32_t n_groups = 256;
     // SnapshotV1 emission on the device (emit.hip): property / name tables, scratch, and two output
@@ -413,7 +425,9 @@ static int upload_staged(mte_engine* e, void* dst, const void* src, size_t bytes
     int k = 0;
     for (size_t off = 0; off < bytes; off += STAGE_BYTES, k ^= 1) {
         const size_t n = std::min(STAGE_BYTES, bytes - off);
+        auto t0 = std::chrono::steady_clock::now();
         HIP_TRY(e, hipEventSynchronize(e->ev_stage[k]));  // the DMA out of this chunk is done
+        auto t1 = std::chrono::steady_clock::now();
         char* stg = (char*)e->stage[k];
         const char* from = (const char*)src + off;
         const size_t piece = (n + nt - 1) / nt;
@@ -424,6 +438,9 @@ static int upload_staged(mte_engine* e, void* dst, const void* src, size_t bytes
                 if (a < n) memcpy(stg + a, from + a, std::min(piece, n - a));
             }
         });
+        auto t2 = std::chrono::steady_clock::now();
+        e->stage_wait_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        e->stage_copy_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
         HIP_TRY(e, hipMemcpyAsync((char*)dst + off, stg, n, hipMemcpyHostToDevice, e->stream));
         HIP_TRY(e, hipEventRecord(e->ev_stage[k], e->stream));
     }
@@ -592,6 +609,7 @@ static uint32_t solo_count(const mte_engine* e) {
     while (k < nd && k < cap) {
         const uint64_t n = e->n_ops_doc[e->order[k]];
         if (n < e->solo_min_ops || n * e->solo_div < nmax || (nd > 1 && (double)n < 8.0 * mean)) break;
+        if (e->cell_recs.count(e->order[k])) break;  // cell ops run in the LDS / HBM engines only
         k++;
     }
     return k;
@@ -736,6 +754,44 @@ static void run_pool(unsigned n, F&& work) {
 }
 }
 
+// SharedMatrix cell records (include/mte.h MTE_OP_CELL): each vector document with some gets a
+// HandleTable region (1 + 2 * (records + 2) words) and the batch two words per cell index for each
+// pass's results; the records' cell / seq / value are kept for the cells blob (mte_snapshot_matrix).
+static int load_cells(mte_engine* e, const mte_batch* b, const std::vector<uint32_t>& n_cell) {
+    e->cell_recs.clear();
+    e->n_cells = 0;
+    uint64_t words = 0;
+    for (uint32_t d = 0; d < b->n_docs; d++) {
+        DocCfg& c = e->cfg[d];
+        c.ht_cap = 0;
+        c.ht_off = 0;
+        if (!n_cell[d]) continue;
+        std::vector<mte_engine::CellRec>& v = e->cell_recs[d];
+        for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
+            const mte_op& o = b->ops[i];
+            if (o.type != MTE_OP_CELL) continue;
+            if (o.b >= (1u << 28)) return set_err(e, MTE_E_RANGE, "cell index beyond 2^28");
+            v.push_back({o.b, o.seq, o.props < b->n_vals ? o.props : 0u});
+            e->n_cells = std::max<uint64_t>(e->n_cells, (uint64_t)o.b + 1);
+        }
+        c.ht_cap = n_cell[d] + 2;
+        c.ht_off = words;
+        words += 1 + 2 * (uint64_t)c.ht_cap;
+    }
+    e->P.cell_pos = e->P.cell_h = e->P.htab = nullptr;
+    if (!e->n_cells) return MTE_OK;
+    if (e->d_cell_pos.n < 2 * e->n_cells) HIP_TRY(e, e->d_cell_pos.alloc(2 * e->n_cells));
+    if (e->d_cell_h.n < 2 * e->n_cells) HIP_TRY(e, e->d_cell_h.alloc(2 * e->n_cells));
+    if (e->d_htab.n < words) HIP_TRY(e, e->d_htab.alloc(words));
+    // a cell index no document carries keeps both positions undefined
+    HIP_TRY(e, hipMemsetAsync(e->d_cell_pos.p, 0xFF, 2 * e->n_cells * sizeof(uint32_t), e->stream));
+    HIP_TRY(e, hipMemsetAsync(e->d_cell_h.p, 0, 2 * e->n_cells * sizeof(uint32_t), e->stream));
+    e->P.cell_pos = e->d_cell_pos.p;
+    e->P.cell_h = e->d_cell_h.p;
+    e->P.htab = e->d_htab.p;
+    return MTE_OK;
+}
+
 int mte_load(mte_engine* e, const mte_batch* b) {
     if (!e || !b) return MTE_E_ARG;
     HIP_TRY(e, hipSetDevice(e->device));
@@ -744,10 +800,12 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     e->generated = false;
     e->host_ops_valid = false;
     e->replayed = e->downloaded = false;
+    e->stage_copy_ms = e->stage_wait_ms = 0;
     const uint32_t nd = b->n_docs;
     std::vector<uint64_t> n_ops(nd), pay(nd), pi(nd), an(nd);
     std::vector<uint8_t> collab(nd), has_nl(nd, 0), not_lean(nd, 0), doc_ext(nd, 0), doc_cu(nd, 0);
     std::vector<uint32_t> doc_keys(nd, 0);  // distinct property keys of each document's ops
+    std::vector<uint32_t> n_cell(nd, 0);    // SharedMatrix cell records (MTE_OP_CELL)
     // one pass over each document's ops and payload, documents spread over host threads (the scan is
     // most of mte_load's host time on large batches)
     auto scan = [&](uint32_t d) {
@@ -762,7 +820,8 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         count_doc_ops(b->ops, b->doc_op_offsets, d, pi[d], an[d], &rel);
         std::vector<uint32_t> keys;
         for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
-            if (b->ops[i].flags & MTE_F_PERM) doc_ext[d] = 1;
+            if ((b->ops[i].flags & MTE_F_PERM) || b->ops[i].type == MTE_OP_CELL) doc_ext[d] = 1;
+            if (b->ops[i].type == MTE_OP_CELL) n_cell[d]++;
             if (b->ops[i].flags & MTE_F_CATCHUP) doc_cu[d] = 1;
             const uint32_t ps = b->ops[i].props;
             if (ps && ps < b->n_propsets)
@@ -819,14 +878,14 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         c.cu_cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFF0ull);
         cu += c.cu_cap;
     }
-    if (cu) {
-        HIP_TRY(e, e->d_cu.alloc(2 * cu));
-        // same size: copy into the buffer the kernels' Params::docs already points at (upload would
-        // reallocate it and leave that pointer dangling)
+    // (the catch-up offsets reach the device with the cell tables' below: the same size, copied into
+    // the buffer the kernels' Params::docs already points at -- upload would reallocate it)
+    if (cu) HIP_TRY(e, e->d_cu.alloc(2 * cu));
+    e->P.cu_rec = cu ? e->d_cu.p : nullptr;
+    if ((rc = load_cells(e, b, n_cell))) return rc;
+    if (cu || e->n_cells)  // ht_off / ht_cap: the same re-upload as the catch-up offsets above
         HIP_TRY(e, hipMemcpyAsync(e->d_cfg.p, e->cfg.data(), e->cfg.size() * sizeof(DocCfg), hipMemcpyHostToDevice,
                                   e->stream));
-    }
-    e->P.cu_rec = cu ? e->d_cu.p : nullptr;
     if ((rc = upload(e, e->d_ops, b->ops, b->doc_op_offsets[nd]))) return rc;
     if ((rc = upload(e, e->d_payload, b->payload, b->doc_payload_offsets[nd]))) return rc;
     if ((rc = upload_props(e))) return rc;
@@ -1158,7 +1217,20 @@ static int run_kernel(mte_engine* e, bool gen) {
 int mte_replay(mte_engine* e, mte_stats* out) {
     if (!e) return MTE_E_ARG;
     if (!e->P.ops) return set_err(e, MTE_E_STATE, "mte_replay before mte_load/mte_generate");
-    int rc = run_kernel(e, false);
+    int rc;
+    if (e->n_cells && !e->generated) {
+        // cell ops: pass 1 evaluates adjustPosition in both vectors of every cell op, pass 2 replays
+        // with the handle allocations both gate (a vector's positions do not depend on its handles)
+        e->P.cell_mode = 1;
+        rc = run_kernel(e, false);
+        const double ms1 = e->last_kernel_ms;
+        e->P.cell_mode = 2;
+        if (!rc) rc = run_kernel(e, false);
+        e->last_kernel_ms += ms1;
+    } else {
+        e->P.cell_mode = 0;
+        rc = run_kernel(e, false);
+    }
     if (rc) return rc;
     if (out) {
         memset(out, 0, sizeof *out);
@@ -1353,7 +1425,8 @@ struct DocView {
                 sv.rclient = c.collab ? (int32_t)((v.w >> 8) & 0xff) : -1;
                 sv.ovl = e->h_out_ovl[i];
                 sv.props = a.x ? (uint32_t)(i + 1) : 0u;
-                sv.reftype = sv.kind == 1 ? (t.x & 0xFFFFu) : 0;  // bits 16..31: the marker's tag
+                // bits 16..31 of a marker's word: its tag; a permutation run's word: its start handle
+                sv.reftype = sv.kind == 1 ? (t.x & 0xFFFFu) : sv.kind == 2 ? t.x : 0;
                 sv.text = sv.kind ? nullptr : txt + t.x;
                 segs.push_back(sv);
             }
@@ -1530,7 +1603,7 @@ int mte_segments_json(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t
         o += "{\"kind\":";
         o += s.kind == 1 ? "\"M\"" : s.kind == 2 ? "\"P\"" : "\"T\"";
         if (s.kind == 1) o += ",\"refType\":" + std::to_string(s.reftype);
-        else if (s.kind == 2) o += ",\"start\":" + std::to_string(INT32_MIN);
+        else if (s.kind == 2) o += ",\"start\":" + std::to_string(s.reftype ? (int64_t)s.reftype : (int64_t)INT32_MIN);
         else {
             o += ",\"text\":";
             json::quote(o, (const char16_t*)s.text, s.len);
@@ -1661,26 +1734,127 @@ int mte_snapshot_v1(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t* 
     return MTE_OK;
 }
 
+// SparseArray2D's Morton keys (sparsearray2d.ts:10-41): the bits of a 16-bit row / col interleaved,
+// row bits odd, col bits even.
+static uint32_t interlace16(uint32_t x) {
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+static uint32_t morton2x16(uint32_t row, uint32_t col) { return (interlace16(row) << 1) | interlace16(col); }
+
+// One SparseArray2D tile (256 entries): sub-tiles above the last level, values (val ids) in it.
+struct CellTile {
+    std::map<uint32_t, std::unique_ptr<CellTile>> sub;
+    std::map<uint32_t, uint32_t> val;  // NONE: cleared (undefined)
+    CellTile* at(uint32_t k) {
+        std::unique_ptr<CellTile>& t = sub[k];
+        if (!t) t.reset(new CellTile());
+        return t.get();
+    }
+};
+static void cell_tile_json(std::string& o, const CellTile& t, int depth, const HostBatch& hb) {
+    o += '[';
+    for (uint32_t i = 0; i < 256; i++) {
+        if (i) o += ',';
+        if (depth < 3) {
+            auto it = t.sub.find(i);
+            if (it == t.sub.end()) o += "null";
+            else cell_tile_json(o, *it->second, depth + 1, hb);
+        } else {
+            auto it = t.val.find(i);
+            if (it == t.val.end() || it->second == NONE) o += "null";
+            else o.append(hb.val_text, hb.val_offsets[it->second], hb.val_offsets[it->second + 1] - hb.val_offsets[it->second]);
+        }
+    }
+    o += ']';
+}
+
+// A vector's HandleTable as the device left it: the handles array (HandleTable.snapshot,
+// handletable.ts:80-82) and the seq of each handle's last free.
+static int read_handle_table(mte_engine* e, uint32_t doc, std::vector<uint32_t>& handles, std::vector<uint32_t>& freed) {
+    handles.assign(1, 1u);  // new HandleTable(): [1]
+    freed.clear();
+    const DocCfg& c = e->cfg[doc];
+    if (!c.ht_cap || !e->d_htab.p) return MTE_OK;
+    std::vector<uint32_t> w(1 + 2 * (size_t)c.ht_cap);
+    HIP_TRY(e, hipMemcpy(w.data(), e->d_htab.p + c.ht_off, w.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    const uint32_t len = w[0];
+    if (len < 1 || len > c.ht_cap) return set_err(e, MTE_E_STATE, "handle table out of range");
+    handles.assign(w.begin() + 1, w.begin() + 1 + len);
+    freed.assign(w.begin() + 1 + c.ht_cap, w.end());
+    return MTE_OK;
+}
+
 // SharedMatrix.snapshotCore (matrix.ts:405-430) over PermutationVector.snapshot (permutationvector.ts:260-273).
+// The segments trees are the vectors' SnapshotV1 (the emission kernels); the handle tables and the
+// cells come from the replay's device results: a gated set wrote cell (row handle, col handle) at its
+// seq, and a zamboni UNLINK of the row (col) handle after that seq cleared it (onRowHandlesRecycled /
+// onColHandlesRecycled, matrix.ts:626-640: clearRows / clearCols leave the tiles in place).
 int mte_snapshot_matrix(mte_engine* e, uint32_t rows_doc, uint32_t cols_doc, char* buf, size_t cap, size_t* len) {
     if (!e) return MTE_E_ARG;
+    if (rows_doc >= e->P.n_docs || cols_doc >= e->P.n_docs) return MTE_E_RANGE;
     std::string o = "{\"entries\":[";
     const uint32_t docs[2] = {rows_doc, cols_doc};
+    std::vector<uint32_t> handles[2], freed[2];
     for (int i = 0; i < 2; i++) {
         size_t n = 0;
         int rc = mte_snapshot_v1(e, docs[i], nullptr, 0, &n, nullptr);
         if (rc) return rc;
         std::string seg(n, '\0');
         if ((rc = mte_snapshot_v1(e, docs[i], &seg[0], n, &n, nullptr))) return rc;
+        if ((rc = read_handle_table(e, docs[i], handles[i], freed[i]))) return rc;
+        std::string ht = "[";
+        for (size_t q = 0; q < handles[i].size(); q++) {
+            if (q) ht += ',';
+            ht += std::to_string(handles[i][q]);
+        }
+        ht += ']';
         o += std::string("{\"mode\":\"040000\",\"path\":\"") + (i ? "cols" : "rows") + "\",\"type\":\"Tree\",\"value\":";
-        // the handle table: [1] (its free-list head) until a cell op allocates a handle
         o += "{\"entries\":[{\"mode\":\"040000\",\"path\":\"segments\",\"type\":\"Tree\",\"value\":" + seg +
-             "},{\"mode\":\"100644\",\"path\":\"handleTable\",\"type\":\"Blob\",\"value\":"
-             "{\"contents\":\"[1]\",\"encoding\":\"utf-8\"}}],\"id\":null}},";
+             "},{\"mode\":\"100644\",\"path\":\"handleTable\",\"type\":\"Blob\",\"value\":{\"contents\":\"" + ht +
+             "\",\"encoding\":\"utf-8\"}}],\"id\":null}},";
     }
-    // cells: [cells.snapshot(), pending.snapshot()] of two empty SparseArray2D ([undefined] each)
-    o += "{\"mode\":\"100644\",\"path\":\"cells\",\"type\":\"Blob\",\"value\":{\"contents\":\"[[null],[null]]\","
-         "\"encoding\":\"utf-8\"}}],\"id\":null}";
+    // cells: JSON.stringify([cells.snapshot(), pending.snapshot()]); pending stays [undefined] for an
+    // observer (it only holds unACKed local writes)
+    std::map<uint32_t, CellTile> root;  // keyHi -> level-0 tile
+    auto it = e->cell_recs.find(rows_doc);
+    if (it != e->cell_recs.end() && e->n_cells) {
+        std::vector<uint32_t> h(2 * e->n_cells);
+        HIP_TRY(e, hipMemcpy(h.data(), e->d_cell_h.p, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (const mte_engine::CellRec& r : it->second) {
+            const uint32_t rh = h[2 * (size_t)r.cell], ch = h[2 * (size_t)r.cell + 1];
+            if (!rh || !ch) continue;  // adjustPosition undefined in one of the vectors
+            // setCell (sparsearray2d.ts:89-98): getLevel creates every tile on the path
+            const uint32_t hi = morton2x16(rh >> 16, ch >> 16), lo = morton2x16(rh, ch);
+            CellTile* t = root[hi].at(lo >> 24)->at((lo >> 16) & 0xFFu)->at((lo >> 8) & 0xFFu);
+            const bool gone = (rh < freed[0].size() && (int32_t)freed[0][rh] > r.seq) ||
+                              (ch < freed[1].size() && (int32_t)freed[1][ch] > r.seq);
+            t->val[lo & 0xFFu] = gone ? NONE : r.val;
+        }
+    }
+    std::string cells = "[[";
+    if (root.empty()) {
+        cells += "null";
+    } else {
+        const uint32_t top = root.rbegin()->first;
+        if (top > (1u << 20)) return set_err(e, MTE_E_UNSUPPORTED, "cell handles beyond 2^26");
+        for (uint32_t k = 0; k <= top; k++) {
+            if (k) cells += ',';
+            auto r = root.find(k);
+            if (r == root.end()) cells += "null";
+            else cell_tile_json(cells, r->second, 0, e->hb);
+        }
+    }
+    cells += "],[null]]";
+    std::u16string cu;
+    json::decode_utf8(cells.data(), cells.size(), cu);
+    o += "{\"mode\":\"100644\",\"path\":\"cells\",\"type\":\"Blob\",\"value\":{\"contents\":";
+    json::quote(o, cu);
+    o += ",\"encoding\":\"utf-8\"}}],\"id\":null}";
     if (len) *len = o.size();
     if (!buf) return MTE_OK;
     if (cap < o.size()) return MTE_E_RANGE;
@@ -2175,6 +2349,8 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "solo_us") *value = (int64_t)(e->last_solo_ms * 1000.0);  // the solo workgroups' pass (critical path)
     else if (k == "solo_lead_us") *value = (int64_t)(e->last_solo_lead_ms * 1000.0);
     else if (k == "load_alloc_us") *value = (int64_t)(e->last_alloc_ms * 1000.0);
+    else if (k == "load_stage_copy_us") *value = (int64_t)(e->stage_copy_ms * 1000.0);
+    else if (k == "load_stage_wait_us") *value = (int64_t)(e->stage_wait_ms * 1000.0);
     else if (k == "solo_tail_us") *value = (int64_t)(e->last_solo_tail_ms * 1000.0);
     else if (k == "lean") *value = e->last_lean;
     else if (k == "emit_us") *value = (int64_t)(e->last_emit_ms * 1000.0);  // emission after the replay pass
@@ -3223,7 +3399,7 @@ const char* mte_builder_doc_path(const mte_builder* b, uint32_t doc) {
 }
 
 // SharedMatrix.processCore (matrix.ts:548-560): rows then cols, each PermutationVector fed the
-// messages that target it; cell ops allocate handles (not modelled).
+// messages that target it; a cell op (no target) becomes an MTE_OP_CELL record in both, in message order.
 int mte_builder_add_matrix_log(mte_builder* b, const char* observer_name, const char* text, size_t len) {
     if (!b || !text) return MTE_E_ARG;
     json::Value log;
@@ -3237,34 +3413,74 @@ int mte_builder_add_matrix_log(mte_builder* b, const char* observer_name, const 
         b->err = "matrix log must be a JSON array of messages";
         return MTE_E_PARSE;
     }
-    json::Value part[2];
-    part[0].kind = part[1].kind = json::Value::Array;
-    for (const json::Value& m : log.items) {
-        const json::Value* c = m.kind == json::Value::Object ? m.get(u"contents") : nullptr;
-        const json::Value* t = c && c->kind == json::Value::Object ? c->get(u"target") : nullptr;
-        if (!t) {
-            if (c && c->kind == json::Value::Object) {
-                b->err = "SharedMatrix cell ops allocate row / col handles (getAllocatedHandle): out of scope";
-                return MTE_E_UNSUPPORTED;
-            }
-            continue;
-        }
-        if (t->kind == json::Value::String && t->str == u"rows") part[0].items.push_back(m);
-        else if (t->kind == json::Value::String && t->str == u"cols") part[1].items.push_back(m);
-    }
     std::vector<std::unique_ptr<DocBuild>> dbs;
     for (int i = 0; i < 2; i++) {
         dbs.emplace_back(new DocBuild(observer_name));
         dbs.back()->perm = true;
-        if (int rc = add_messages(b, part[i], *dbs.back())) {
-            b->err = dbs.back()->err;
-            return rc;
+    }
+    uint32_t cells = b->n_cells;
+    auto fail = [&](int code, const std::string& m) {
+        b->err = m;
+        return code;
+    };
+    json::Value one;
+    one.kind = json::Value::Array;
+    one.items.resize(1);
+    for (const json::Value& m : log.items) {
+        const json::Value* c = m.kind == json::Value::Object ? m.get(u"contents") : nullptr;
+        const json::Value* t = c && c->kind == json::Value::Object ? c->get(u"target") : nullptr;
+        if (t) {
+            const int i = t->kind != json::Value::String ? -1 : t->str == u"rows" ? 0 : t->str == u"cols" ? 1 : -1;
+            if (i < 0) continue;
+            one.items[0] = m;
+            if (int rc = add_messages(b, one, *dbs[i])) return fail(rc, dbs[i]->err);
+            continue;
         }
+        const json::Value* type = m.kind == json::Value::Object ? m.get(u"type") : nullptr;
+        if (!c || c->kind != json::Value::Object || !type || type->kind != json::Value::String || type->str != u"op")
+            continue;
+        // the remote set (matrix.ts:575-601; an observer never submits, so never the ACK branch)
+        int32_t op = -1, rc_[2] = {-1, -1};
+        num_field(*c, u"type", &op);
+        if (op != 2) return fail(MTE_E_UNSUPPORTED, "SharedMatrix op without target that is not a set");
+        const json::Value* rc[2] = {c->get(u"row"), c->get(u"col")};
+        for (int i = 0; i < 2; i++) {
+            if (!rc[i] || rc[i]->kind != json::Value::Number || rc[i]->num < 0 || rc[i]->num > 0x7FFFFFFF ||
+                rc[i]->num != (double)(int32_t)rc[i]->num)
+                return fail(MTE_E_UNSUPPORTED, "set row / col must be an integer >= 0");
+            rc_[i] = (int32_t)rc[i]->num;
+        }
+        const json::Value* v = c->get(u"value");
+        const uint32_t val = v ? b->in->val(json::stringify(*v)) : 0u;  // undefined -> null in the blob
+        const json::Value* cid = m.get(u"clientId");
+        const std::string name = (cid && cid->kind == json::Value::String) ? json::to_utf8(cid->str.data(), cid->str.size()) : "";
+        for (int i = 0; i < 2; i++) {
+            DocBuild& db = *dbs[i];
+            mte_op o{};
+            num_field(m, u"sequenceNumber", &o.seq);
+            num_field(m, u"referenceSequenceNumber", &o.ref_seq);
+            num_field(m, u"minimumSequenceNumber", &o.msn);
+            uint32_t sid = 0;
+            if (db.collab) {  // getOrAddShortClientId (matrix.ts:576, 580)
+                if (int e2 = db.short_id(name, &sid, o.seq)) return fail(e2, db.err);
+                if (sid == 0) return fail(MTE_E_UNSUPPORTED, "observer never submits ops (ack path)");
+                if (db.reused && o.ref_seq < db.cur_min) sid = 255;
+            }
+            o.client = (uint8_t)sid;
+            o.type = MTE_OP_CELL;
+            o.flags = i ? MTE_F_CELL_COL : 0;
+            o.pos1 = rc_[i];
+            o.b = cells;
+            o.props = val;
+            db.ops.push_back(o);
+        }
+        cells++;
     }
     for (int i = 0; i < 2; i++) {
         dbs[i]->commit(b->hb);
         b->paths.emplace_back(i ? "cols" : "rows");
     }
+    b->n_cells = cells;
     return MTE_OK;
 }
 

@@ -104,6 +104,17 @@ enum {
      *   MTE_DOC_UNSUPPORTED at an op whose marker is unmapped or no longer in the tree (zamboni
      *   dropped it: the reference would walk its stale parent chain). */
     MTE_OP_RELPOS = 9,
+    /* CELL: a SharedMatrix cell `set` (matrix.ts:560-601) as one of its two PermutationVectors sees it
+     *   (both the rows and the cols document carry one, in message order): pos1 = the op's row (rows
+     *   document) or col (cols document, MTE_F_CELL_COL), ref_seq / client = the message's (client: the
+     *   vector's short id, getOrAddShortClientId), seq = its sequence number, b = the cell's index among
+     *   the batch's cell ops (the same in both records), props = the value id (val_text, canonical
+     *   JSON; 0 = null / undefined). The vector applies no merge-tree op for it and its currentSeq /
+     *   minSeq do not move (the message is not the vector's). The engine runs adjustPosition
+     *   (permutationvector.ts:198-209) in both vectors and, when both are defined, getAllocatedHandle
+     *   (:176-196: split at the position, take a handle from the HandleTable free list,
+     *   handletable.ts:35-59); zamboni's UNLINK frees a removed run's handles (:357-382). */
+    MTE_OP_CELL = 10,
 };
 #define MTE_REL_UNMAPPED 0xFFFFFFFFu
 
@@ -121,6 +132,7 @@ enum {
 #define MTE_F_REL_BEFORE2 0x400u  /* RELPOS: relativePos2.before */
 #define MTE_F_PERM 0x1000u        /* INSERT: a PermutationSegment of a SharedMatrix row / col vector
                                      (permutationvector.ts:37-127): b = length, no text, handles unallocated */
+#define MTE_F_CELL_COL 0x2000u    /* CELL: the record of the cols vector (else rows) */
 #define MTE_F_CATCHUP 0x800u      /* op of a catch-up message the legacy summary rewrites (refSeq != seq - 1,
                                      sequence.ts:603-625): the engine records its delta ranges */
 
@@ -214,7 +226,7 @@ typedef struct mte_seg_row {       /* parity dump row (walkAllSegments order, me
     int32_t removed_client;
     uint64_t overlap_mask;         /* removedClientOverlap as a short-id set */
     uint32_t text_off;             /* offset into the text returned by mte_segment_text */
-    uint32_t ref_type;
+    uint32_t ref_type;             /* marker: refType; permutation run: its start handle (0 = unallocated) */
 } mte_seg_row;
 
 /* Library identity / capability */
@@ -278,7 +290,10 @@ int mte_snapshot_shared_string(mte_engine* e, uint32_t doc, char* buf, size_t ca
 int mte_snapshot_legacy(mte_engine* e, uint32_t doc, const char* catch_up_name, char* buf, size_t cap, size_t* len);
 /* SharedMatrix.snapshotCore (matrix.ts:405-430) of a rows / cols document pair from
  * mte_builder_add_matrix_log: each PermutationVector.snapshot (permutationvector.ts:260-273: SnapshotV1
- * under "segments" + the "handleTable" blob) and the "cells" blob. buf may be NULL. */
+ * under "segments" + the "handleTable" blob: the HandleTable's array, free-list head first,
+ * handletable.ts:19-86) and the "cells" blob (JSON.stringify([cells, pending]) of the two SparseArray2D,
+ * sparsearray2d.ts:57-235: 4 levels of 256-entry Morton tiles; pending is [null] for an observer).
+ * buf may be NULL. */
 int mte_snapshot_matrix(mte_engine* e, uint32_t rows_doc, uint32_t cols_doc, char* buf, size_t cap, size_t* len);
 /* Per-doc summaries for all docs of the batch (checksum over text + snapshot blobs). */
 int mte_summaries(mte_engine* e, mte_doc_summary* out, size_t cap);
@@ -325,8 +340,9 @@ const char* mte_builder_doc_path(const mte_builder* b, uint32_t doc);
 /* SharedMatrix op log (matrix.ts:548-560): a JSON array of its sequenced messages becomes TWO documents,
  * the rows then the cols PermutationVector (permutationvector.ts:129-146; paths "rows", "cols"), each
  * fed the messages whose contents.target names it. Segments are PermutationSegment runs
- * ([length, start] specs). Cell ("set") ops allocate handles and split runs
- * (getAllocatedHandle, permutationvector.ts:174-193): MTE_E_UNSUPPORTED. */
+ * ([length, start] specs). A cell ("set") op becomes an MTE_OP_CELL record in both documents
+ * (processCore's remote branch, matrix.ts:575-601); its row / col must be integers >= 0
+ * (MTE_E_UNSUPPORTED otherwise). */
 int mte_builder_add_matrix_log(mte_builder* b, const char* observer_name, const char* json, size_t len);
 int mte_builder_batch(mte_builder* b, mte_batch* out);   /* view valid until destroy */
 const char* mte_builder_error(const mte_builder* b);

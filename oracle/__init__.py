@@ -58,6 +58,14 @@ def lib():
         L.orc_generate_batch.argtypes = [u32, vp, vp, u32, u32, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int32)]
         L.orc_replay_list.restype = u64
         L.orc_replay_list.argtypes = [vp, vp, u32, i32, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int32), i32]
+        L.orc_matrix_new.restype = vp
+        L.orc_matrix_new.argtypes = [cp]
+        L.orc_matrix_free.argtypes = [vp]
+        L.orc_matrix_apply_json.argtypes = [vp, cp, ctypes.c_size_t]
+        L.orc_matrix_vector.restype = vp
+        L.orc_matrix_vector.argtypes = [vp, i32]
+        L.orc_matrix_snapshot_json.restype = vp
+        L.orc_matrix_snapshot_json.argtypes = [vp, u32]
         L.orc_replay_batch.restype = u64
         L.orc_replay_batch.argtypes = [vp, u32, u32, i32, cp, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int32), i32]
         _lib = L
@@ -163,6 +171,40 @@ class OracleDoc:
         a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         lib().orc_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
         return {"leafCount": a.value, "removedLeafCount": b.value, "maxHeight": c.value}
+
+
+class _VectorView(OracleDoc):
+    """One PermutationVector of an OracleMatrix (owned by it)."""
+
+    def __init__(self, owner, handle):
+        self._owner = owner
+        self._h = handle
+
+    def __del__(self):
+        pass
+
+
+class OracleMatrix:
+    """A SharedMatrix replayed by the oracle (matrix.ts:548-605): both PermutationVectors, their
+    HandleTables and the cells SparseArray2D."""
+
+    def __init__(self, observer="__observer__"):
+        self._h = lib().orc_matrix_new(observer.encode())
+        self.rows = _VectorView(self, lib().orc_matrix_vector(self._h, 0))
+        self.cols = _VectorView(self, lib().orc_matrix_vector(self._h, 1))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_matrix_free(self._h)
+            self._h = None
+
+    def apply_json(self, text):
+        b = text.encode() if isinstance(text, str) else text
+        return lib().orc_matrix_apply_json(self._h, b, len(b))
+
+    def snapshot_json(self, chunk=10000):
+        """SharedMatrix.snapshotCore (matrix.ts:405-433) ITree JSON."""
+        return _take(lib().orc_matrix_snapshot_json(self._h, chunk))
 
 
 def _op_dtype():

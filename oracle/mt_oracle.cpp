@@ -238,8 +238,34 @@ class MergeTree {
     // 1 remove, 2 annotate) and the delta segments in walk order, each with its propertyDeltas keys
     typedef std::vector<std::pair<Segment*, std::vector<u16s>>> Deltas;
     std::function<void(int, Deltas&)> onDelta;
+    // mergeTreeMaintenanceCallback's UNLINK (mergeTree.ts:1309-1315): a removed segment zamboni drops
+    std::function<void(Segment*)> onUnlink;
 
     MergeTree() { root = makeBlock(0); }
+
+    // getContainingSegment (mergeTree.ts:1623-1634) -> searchBlock (:1797-1829): the first child whose
+    // length in the (refSeq, clientId) view exceeds the remaining position
+    Segment* containingSegment(int pos, int refSeq, int clientId, int& offset) const {
+        const Block* b = root;
+        for (;;) {
+            const Node* hit = nullptr;
+            for (int i = 0; i < b->childCount; i++) {
+                const Node* c = b->children[i];
+                const int len = nodeLength(c, refSeq, clientId);
+                if (pos < len) {
+                    hit = c;
+                    break;
+                }
+                pos -= len;
+            }
+            if (!hit) return nullptr;
+            if (hit->leaf) {
+                offset = pos;
+                return (Segment*)hit;
+            }
+            b = (const Block*)hit;
+        }
+    }
 
     Block* makeBlock(int childCount) {  // mergeTree.ts:1114-1123
         blockPool.emplace_back();
@@ -649,8 +675,12 @@ class MergeTree {
             }
             Segment* s = (Segment*)cn;
             if (s->removed) {
-                if (s->removedSeq > cw.minSeq) hold.push_back(s);
-                else s->parent = nullptr;
+                if (s->removedSeq > cw.minSeq) {
+                    hold.push_back(s);
+                } else {
+                    if (onUnlink) onUnlink(s);
+                    s->parent = nullptr;
+                }
                 prev = nullptr;
             } else if (s->seq <= cw.minSeq) {
                 bool ok = prev && canAppend(prev, s) && matchProperties(prev, s) && localNetLength(s) > 0;
@@ -1042,6 +1072,43 @@ class Doc {
     // a SharedMatrix row / col vector (PermutationVector, permutationvector.ts:129-146) instead of a
     // SharedString: specs are PermutationSegment JSON
     bool permutation = false;
+    // its HandleTable (handletable.ts:19-86): handles[0] is the free-list head
+    std::vector<int> handles{1};
+    int allocateHandle() {  // :35-40
+        const int fr = handles[0];
+        handles[0] = fr < (int)handles.size() ? handles[fr] : fr + 1;  // handles[free] ?? free + 1
+        if (fr == (int)handles.size()) handles.push_back(0);
+        else handles[fr] = 0;
+        return fr;
+    }
+    void freeHandle(int h) {  // :56-59
+        handles[h] = handles[0];
+        handles[0] = h;
+    }
+    // PermutationVector.adjustPosition (permutationvector.ts:198-209); -1 = undefined
+    int adjustPosition(int pos, int refSeq, int clientId) {
+        int off = 0;
+        Segment* s = mt.containingSegment(pos, refSeq, clientId, off);
+        if (!s || s->removed) return -1;
+        return getPosition(s, mt.cw.currentSeq, mt.cw.clientId) + off;
+    }
+    // PermutationVector.getAllocatedHandle (permutationvector.ts:176-196)
+    int getAllocatedHandle(int pos) {
+        int off = 0;
+        Segment* s = mt.containingSegment(pos, mt.cw.currentSeq, mt.cw.clientId, off);
+        if (!s) throw EngineError(MTE_DOC_UNSUPPORTED, "getAllocatedHandle beyond the vector");
+        if (s->start != HandleUnallocated) return s->start + off;
+        // walkSegments(pos, pos + 1, splitRange) -> mapRange (mergeTree.ts:2797-2807)
+        if (pos) mt.ensureIntervalBoundary(pos, mt.cw.currentSeq, mt.cw.clientId);
+        mt.ensureIntervalBoundary(pos + 1, mt.cw.currentSeq, mt.cw.clientId);
+        int h = HandleUnallocated;
+        auto leaf = [&](Segment* seg, int, int, int) {
+            seg->start = h = allocateHandle();
+            return true;
+        };
+        mt.nodeMap(mt.root, 0, mt.cw.currentSeq, mt.cw.clientId, pos, pos + 1, leaf);
+        return h;
+    }
     Segment* makeSegment(const JV& spec) {  // SharedStringFactory.segmentFromSpec (sequenceFactory.ts:31-37)
         Segment* s = mt.newSegment();
         if (permutation) {  // PermutationSegment.fromJSONObject (permutationvector.ts:41-44): [length, start]
@@ -1506,6 +1573,8 @@ class Doc {
                     loadSegs.push_back(s);
                     continue;
                 }
+                // a cell op needs both vectors (orc_matrix_* replays a matrix from its messages)
+                if (op.type == MTE_OP_CELL) throw EngineError(MTE_DOC_UNSUPPORTED, "cell record in a one-document replay");
                 if (op.type != MTE_OP_NOOP && !(mt.cw.currentSeq < op.seq))
                     throw EngineError(MTE_DOC_SEQ_ORDER, "seq <= currentSeq");
                 if (op.flags & MTE_F_REL) relPositions(b, i, d, op);
@@ -1983,6 +2052,161 @@ static char* dupstr(const std::string& s) {
     return p;
 }
 
+namespace orc {
+static std::string vector_tree(Doc* d, uint32_t chunk) {
+    std::string ht = "[";
+    for (size_t i = 0; i < d->handles.size(); i++) ht += (i ? "," : "") + std::to_string(d->handles[i]);
+    ht += "]";
+    return "{\"entries\":[{\"mode\":\"040000\",\"path\":\"segments\",\"type\":\"Tree\",\"value\":" +
+           d->snapshotTree(chunk ? chunk : 10000) +
+           "},{\"mode\":\"100644\",\"path\":\"handleTable\",\"type\":\"Blob\",\"value\":"
+           "{\"contents\":\"" + ht + "\",\"encoding\":\"utf-8\"}}],\"id\":null}";
+}
+
+// ---- SharedMatrix (matrix.ts): both PermutationVectors, the HandleTables and the cells
+// SparseArray2D (sparsearray2d.ts:57-235: root indexed by the Morton key of the high 16 bits, then four
+// 256-entry tiles by the bytes of the low key), restated with an explicit tile tree.
+static uint32_t interlace16(uint32_t x) {  // x8ToInterlacedX16 (sparsearray2d.ts:15-23), 16 bits
+    uint32_t r = 0;
+    for (int b = 0; b < 16; b++) r |= ((x >> b) & 1u) << (2 * b);
+    return r;
+}
+struct Tile {  // new Array(256).fill(undefined)
+    std::unique_ptr<Tile> sub[256];
+    JVP val[256];
+    bool has[256] = {};
+};
+struct Matrix {
+    Doc rows, cols;
+    std::vector<std::unique_ptr<Tile>> root{};  // [undefined]
+    size_t rootLen = 1;
+    std::string error;
+    int status = 0;
+    explicit Matrix(const char* obs) : rows(obs), cols(obs) {
+        rows.permutation = cols.permutation = true;
+        root.resize(1);
+        rows.mt.onUnlink = [this](Segment* s) { recycled(rows, s, true); };
+        cols.mt.onUnlink = [this](Segment* s) { recycled(cols, s, false); };
+    }
+    static uint32_t r0(uint32_t row) { return interlace16(row) << 1; }
+    static uint32_t c0(uint32_t col) { return interlace16(col); }
+    Tile* level(std::unique_ptr<Tile>& t) {  // getLevel (:220-226)
+        if (!t) t.reset(new Tile());
+        return t.get();
+    }
+    void setCell(uint32_t row, uint32_t col, JVP v) {  // :89-98
+        const uint32_t hi = r0(row >> 16) | c0(col >> 16), lo = r0(row & 0xFFFF) | c0(col & 0xFFFF);
+        if (hi >= root.size()) root.resize(hi + 1);
+        rootLen = std::max<size_t>(rootLen, hi + 1);
+        Tile* t = level(root[hi]);
+        t = level(t->sub[lo >> 24]);
+        t = level(t->sub[(lo >> 16) & 0xFF]);
+        t = level(t->sub[(lo >> 8) & 0xFF]);
+        t->val[lo & 0xFF] = v;
+        t->has[lo & 0xFF] = (bool)v;
+    }
+    // clearRows / clearCols (:167-218): every tile of the row (col) in every populated top-level tile
+    void clearLine(uint32_t h, bool isRow) {
+        for (uint32_t other = 0; other < 0x10000; other++) {
+            const uint32_t hi = isRow ? (r0(h >> 16) | c0(other)) : (c0(h >> 16) | r0(other));
+            if (hi >= root.size() || !root[hi]) continue;
+            const uint32_t lo = isRow ? r0(h & 0xFFFF) : c0(h & 0xFFFF);
+            std::function<void(Tile*, int)> walk = [&](Tile* t, int depth) {
+                const uint32_t bits = (lo >> (24 - 8 * depth)) & 0xFF;
+                for (uint32_t k = 0; k < 16; k++) {
+                    const uint32_t key = bits | (isRow ? c0(k) : r0(k));
+                    if (depth == 3) {
+                        t->val[key] = nullptr;
+                        t->has[key] = false;
+                    } else if (t->sub[key]) {
+                        walk(t->sub[key].get(), depth + 1);
+                    }
+                }
+            };
+            walk(root[hi].get(), 0);
+        }
+    }
+    // PermutationVector.onMaintenance UNLINK (permutationvector.ts:357-382) -> handlesRecycledCallback
+    // (matrix.ts:626-640), then HandleTable.free of each handle
+    void recycled(Doc& v, Segment* s, bool isRow) {
+        if (!s->perm || s->start < 1) return;
+        for (int i = 0; i < s->len; i++) clearLine((uint32_t)(s->start + i), isRow);
+        for (int i = 0; i < s->len; i++) v.freeHandle(s->start + i);
+    }
+    // SharedMatrix.processCore (matrix.ts:548-605), observer (every message remote)
+    void applyMsg(const JV& m) {
+        if (status) return;
+        const JObj& o = m.o;
+        JVP c = o.get(u"contents");
+        JVP t = c && c->t == JV::Obj ? c->o.get(u"target") : nullptr;
+        if (t) {
+            if (t->t == JV::Str && t->s == u"rows") rows.applyMsg(m);
+            else if (t->t == JV::Str && t->s == u"cols") cols.applyMsg(m);
+            if (rows.status || cols.status) {
+                status = rows.status ? rows.status : cols.status;
+                error = rows.status ? rows.error : cols.error;
+            }
+            return;
+        }
+        JVP ty = o.get(u"type");
+        if (!c || c->t != JV::Obj || !ty || ty->t != JV::Str || ty->s != u"op") return;
+        try {
+            if (Doc::num(c->o, u"type") != 2) throw EngineError(MTE_DOC_UNSUPPORTED, "matrix op without target");
+            JVP cid = o.get(u"clientId");
+            const std::string name = cid && cid->t == JV::Str ? u16_to_utf8(cid->s) : "";
+            const int refSeq = Doc::num(o, u"referenceSequenceNumber");
+            const int row = Doc::num(c->o, u"row"), col = Doc::num(c->o, u"col");
+            const int ar = rows.adjustPosition(row, refSeq, rows.getOrAddShortClientId(name));
+            if (ar < 0) return;
+            const int ac = cols.adjustPosition(col, refSeq, cols.getOrAddShortClientId(name));
+            if (ac < 0) return;
+            const int rh = rows.getAllocatedHandle(ar);
+            const int ch = cols.getAllocatedHandle(ac);
+            if (rh < 1 || ch < 1) throw EngineError(MTE_DOC_UNSUPPORTED, "invalid handle");
+            JVP v = c->o.get(u"value");
+            setCell((uint32_t)rh, (uint32_t)ch, v ? v : std::make_shared<JV>());
+        } catch (EngineError& e) {
+            status = e.code;
+            error = e.what();
+        }
+    }
+    std::string cellsJson() {  // JSON.stringify([cells.snapshot(), pending.snapshot()])
+        std::string o = "[[";
+        std::function<void(const Tile*, int)> tile = [&](const Tile* t, int depth) {
+            o += "[";
+            for (int i = 0; i < 256; i++) {
+                if (i) o += ",";
+                if (depth < 3) {
+                    if (t->sub[i]) tile(t->sub[i].get(), depth + 1);
+                    else o += "null";
+                } else if (t->has[i] && t->val[i]) {
+                    js_stringify(o, *t->val[i]);
+                } else {
+                    o += "null";
+                }
+            }
+            o += "]";
+        };
+        for (size_t k = 0; k < rootLen; k++) {
+            if (k) o += ",";
+            if (k < root.size() && root[k]) tile(root[k].get(), 0);
+            else o += "null";
+        }
+        return o + "],[null]]";
+    }
+    std::string tree(uint32_t chunk) {  // snapshotCore (matrix.ts:405-433)
+        std::string cells;
+        js_quote(cells, utf8_to_u16(cellsJson().c_str(), cellsJson().size()));
+        return "{\"entries\":[{\"mode\":\"040000\",\"path\":\"rows\",\"type\":\"Tree\",\"value\":" +
+               vector_tree(&rows, chunk) +
+               "},{\"mode\":\"040000\",\"path\":\"cols\",\"type\":\"Tree\",\"value\":" + vector_tree(&cols, chunk) +
+               "},{\"mode\":\"100644\",\"path\":\"cells\",\"type\":\"Blob\",\"value\":{\"contents\":" + cells +
+               ",\"encoding\":\"utf-8\"}}],\"id\":null}";
+    }
+};
+}  // namespace orc
+using orc::Matrix;
+
 extern "C" {
 
 Doc* orc_new(const char* observer) { return new Doc(observer); }
@@ -2037,13 +2261,23 @@ int orc_apply_matrix_json(Doc* d, const char* json, size_t len, const char* targ
 }
 // PermutationVector.snapshot (permutationvector.ts:260-273): the merge-tree SnapshotV1 under
 // "segments" and the handle table ([1] until a handle is allocated) as a blob.
-char* orc_snapshot_vector_json(Doc* d, uint32_t chunk) {
-    std::string o = "{\"entries\":[{\"mode\":\"040000\",\"path\":\"segments\",\"type\":\"Tree\",\"value\":" +
-                    d->snapshotTree(chunk ? chunk : 10000) +
-                    "},{\"mode\":\"100644\",\"path\":\"handleTable\",\"type\":\"Blob\",\"value\":"
-                    "{\"contents\":\"[1]\",\"encoding\":\"utf-8\"}}],\"id\":null}";
-    return dupstr(o);
+char* orc_snapshot_vector_json(Doc* d, uint32_t chunk) { return dupstr(vector_tree(d, chunk)); }
+
+Matrix* orc_matrix_new(const char* observer) { return new Matrix(observer); }
+void orc_matrix_free(Matrix* m) { delete m; }
+int orc_matrix_apply_json(Matrix* m, const char* json, size_t len) {
+    try {
+        orc::JVP v = orc::parse(json, len);
+        if (v->t != orc::JV::Arr) return m->status = MTE_DOC_UNSUPPORTED;
+        for (auto& x : v->a) m->applyMsg(*x);
+    } catch (std::exception& e) {
+        m->status = MTE_DOC_UNSUPPORTED;
+        m->error = e.what();
+    }
+    return m->status;
 }
+Doc* orc_matrix_vector(Matrix* m, int which) { return which ? &m->cols : &m->rows; }
+char* orc_matrix_snapshot_json(Matrix* m, uint32_t chunk) { return dupstr(m->tree(chunk)); }
 
 // Resume from a summary ITree JSON (SnapshotLoader); the doc must be fresh (observer set).
 int orc_load_summary(Doc* d, const char* json, size_t len) { return d->loadSnapshotJson(json, len); }

@@ -22,11 +22,12 @@ m.builderAddDocFromSummary(b, "catchup", summary, null);
 assert.strictEqual(m.builderDocCount(b), 4);
 assert.throws(() => m.builderAddDocFromSummary(b, "catchup", "{\"entries\":[]}", null), /mte_builder_add_doc_from_summary/);
 assert.deepStrictEqual(m.builderAddContainerLog(b, "readonly", "[]"), []);
-// a SharedMatrix log: rows and cols vectors (two documents); cell ops are out of scope
+// a SharedMatrix log: rows and cols vectors (two documents), cell sets as records in both
 const splice = (t, p, n) => ({ target: t, pos1: p, seg: [n, -2147483648], type: 0 });
-m.builderAddMatrixLog(b, "readonly", JSON.stringify([msg("a", 1, 0, splice("rows", 0, 3)), msg("a", 2, 1, splice("cols", 0, 2))]));
+m.builderAddMatrixLog(b, "readonly", JSON.stringify([msg("a", 1, 0, splice("rows", 0, 3)), msg("a", 2, 1, splice("cols", 0, 2)),
+    msg("a", 3, 2, { type: 2, row: 0, col: 1, value: 1 })]));
 assert.strictEqual(m.builderDocCount(b), 6);
-assert.throws(() => m.builderAddMatrixLog(b, "readonly", JSON.stringify([msg("a", 1, 0, { type: 2, row: 0, col: 0, value: 1 })])),
+assert.throws(() => m.builderAddMatrixLog(b, "readonly", JSON.stringify([msg("a", 1, 0, { type: 2, row: -1, col: 0, value: 1 })])),
     /mte_builder_add_matrix_log/);
 // multi-GPU entry points (the collective itself needs GPUs: parity.gpu.js runs world 1)
 for (const f of ["rcclUniqueId", "rcclCommDestroy", "gatherSummariesRaw", "rcclCommCreateRaw"]) {

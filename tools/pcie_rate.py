@@ -110,6 +110,8 @@ def main():
             res["reps"].append({"load_ms": round((t1 - t0) * 1e3, 1), "replay_wall_ms": round((t2 - t1) * 1e3, 1),
                                 "kernel_ms": round(st["kernel_ms"], 1), "h2d_ms": round(st["h2d_ms"], 1),
                                 "alloc_ms": round(eng.get_info("load_alloc_us") / 1000.0, 1),
+                                "stage_copy_ms": round(eng.get_info("load_stage_copy_us") / 1000.0, 1),
+                                "stage_wait_ms": round(eng.get_info("load_stage_wait_us") / 1000.0, 1),
                                 "ops_per_s_pcie_inclusive": ops / (t2 - t0),
                                 "upload_GBps": host_bytes / (t1 - t0) / 1e9})
     finally:

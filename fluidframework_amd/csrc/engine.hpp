@@ -515,27 +515,24 @@ struct Engine {
                 return L == j ? tot : v;
             }
             const u32 b = o.x < blk_cap() ? o.x : 0u;
-            uint4 q[8];
-#pragma unroll
-            for (u32 s = 0; s < 8; s++) q[s] = VIS()[b * 8 + s];
             u32 sv = 0;
             if (FULL && C >= 32) {  // clients 32..63: the general predicate (HBM half of the overlap mask)
-#pragma unroll
                 for (u32 s = 0; s < 8; s++)
-                    sv += s < o.w ? vis_len(q[s], AUX()[b * 8 + s].z, b * 8 + s, R, C, cz) : 0u;
+                    sv += s < o.w ? vis_len(VIS()[b * 8 + s], AUX()[b * 8 + s].z, b * 8 + s, R, C, cz) : 0u;
             } else {
-                u32 anyo = 0;
+                // two halves of four independent LDS reads: half the live registers of eight at once
+                // (k_lds sits at its 128-VGPR bound: 116 -> 56 spilled bytes per lane, C2 -5 %); the
+                // overlap mask is read only for a slot that has one
 #pragma unroll
-                for (u32 s = 0; s < 8; s++) anyo |= q[s].w;
-                if (wave_ballot(!fast && (anyo & F_OVL) != 0)) {
-                    u32 z[8];
+                for (u32 h = 0; h < 2; h++) {
+                    uint4 q4[4];
 #pragma unroll
-                    for (u32 s = 0; s < 8; s++) z[s] = AUX()[b * 8 + s].z;
+                    for (u32 s = 0; s < 4; s++) q4[s] = VIS()[b * 8 + 4 * h + s];
 #pragma unroll
-                    for (u32 s = 0; s < 8; s++) sv += s < o.w ? vis_w(q[s], z[s], R, C) : 0u;
-                } else {
-#pragma unroll
-                    for (u32 s = 0; s < 8; s++) sv += s < o.w ? vis_w(q[s], 0u, R, C) : 0u;
+                    for (u32 s = 0; s < 4; s++) {
+                        const bool ov = (q4[s].w & F_OVL) != 0;
+                        sv += 4 * h + s < o.w ? vis_w(q4[s], ov ? AUX()[b * 8 + 4 * h + s].z : 0u, R, C) : 0u;
+                    }
                 }
             }
             v = fast ? v : sv;

@@ -1,4 +1,4 @@
-// HIP kernels of the replay engine (gfx950).
+// HIP kernels of the replay engine (gfx950); k_solo is in mte_solo.hip (built with other flags).
 //
 //   k_lds<GEN>: ONE workgroup per CU, LDS_WAVES waves, all 160 KiB of LDS (engine_types.hpp LdsPlan).
 //               Waves pull documents from a queue in LPT order (longest first) and replay
@@ -24,16 +24,6 @@ namespace mte {
 #ifndef MTE_HBMQ_WPE
 #define MTE_HBMQ_WPE 4
 #endif
-// k_solo owns its CU's LDS, so one wave per SIMD is all it ever has: the hint lets the scheduler
-// trade registers for latency hiding instead of aiming at an occupancy it can never reach.
-#ifndef MTE_SOLO_WPE
-#define MTE_SOLO_WPE 1
-#endif
-// waves of a solo workgroup: one per SIMD, so the critical-path CU holds no other kernel's waves
-#ifndef SOLO_WAVES
-#define SOLO_WAVES 4
-#endif
-
 template <bool GEN, int LVL>
 __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(MTE_LDS_WPE))) void k_lds(Params p) {
     LdsPlan* lp = &g_plan;
@@ -101,80 +91,6 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
         e.release();
         if (prio) __builtin_amdgcn_s_setprio(0);
     }
-}
-
-// Critical-path documents (doc_list[0, n_solo), the longest of the batch): one single-wave
-// workgroup each, owning all of a CU's LDS (SoloPlan), at the highest wave priority. The replay
-// latency of the longest document bounds a Zipf batch, so it gets the plan with the
-// most room and no LDS-pool sharing; it continues HBM-resident only if it outgrows even that.
-template <bool GEN, int LVL>
-MTE_DEV void solo_doc(const Params& p) {
-    const u32 i = blockIdx.x;
-    if (i >= p.n_solo) return;
-    const u32 d = p.doc_list[i];
-    __builtin_amdgcn_s_setprio(3);
-    Engine<true, true, LVL> e(p, d);
-    e.bind_lds(0);
-    GenState g;
-    bool done;
-    u64 at = p.docs[d].op_begin;
-    bool handed = false;
-    if constexpr (!GEN && LVL == 0) {
-        // lean replay: the whole document state in this wave's registers (reg_engine.hpp); it moves
-        // to the LDS plan below only if it outgrows the registers or reaches an op they do not cover
-        if (p.reg_solo) {
-            RegEngine<> r(p, d);
-            at = r.replay(at, p.docs[d].op_end);
-            if (r.status != REG_HANDOFF) {
-                r.finish();
-                __builtin_amdgcn_s_setprio(0);
-                return;
-            }
-            reg_handoff(r, e);
-            handed = true;
-        }
-    }
-    if (!handed) e.init();
-    if (GEN) {
-        e.gen_init(g);
-        done = e.generate_run(g);
-    } else {
-        at = e.replay_run(at);
-        done = at >= p.docs[d].op_end;
-    }
-    if (e.st.status == DOC_SPILL) {
-        e.mark_spilled();
-    } else if (!done && e.st.status == 0) {
-        Engine<false, false, LVL> h(p, d);
-        h.continued = true;
-        h.bind_solo_slot(i);
-        h.adopt(e);
-        if (lane_id() == 0) atomicAdd(&p.counters[4], 1u);
-        if (GEN) {
-            h.generate_run(g);
-        } else {
-            h.replay_run(at);
-        }
-        h.finish();
-    } else {
-        e.finish();
-    }
-    __builtin_amdgcn_s_setprio(0);
-}
-
-// The solo workgroup is SOLO_WAVES waves that each claim a whole SIMD's register file (512 VGPRs +
-// AGPRs: the clobbers below make the kernel's allocation the maximum), and all of the CU's LDS: no
-// other wave of the pass can be resident on a critical-path CU. Wave 0 replays the document; the
-// others wait at the barrier (issuing nothing) until it is done.
-template <bool GEN, int LVL>
-__global__ __launch_bounds__(64 * SOLO_WAVES) __attribute__((amdgpu_waves_per_eu(MTE_SOLO_WPE, MTE_SOLO_WPE))) void k_solo(Params p) {
-#if SOLO_WAVES > 1
-    asm volatile("" ::: "v255", "a255");
-    if (wave_first(threadIdx.x >> 6) == 0) solo_doc<GEN, LVL>(p);
-    __syncthreads();
-#else
-    solo_doc<GEN, LVL>(p);
-#endif
 }
 
 // HBM slot of a k_hbmq wave: a free bit of the slot bitmap (cleared by the host before each run).
@@ -303,17 +219,6 @@ hipError_t launch_lds(const Params& p, bool gen, int full, u32 n_groups, hipStre
     if (attr != hipSuccess) return attr;
     void* args[] = {(void*)&p};
     return hipLaunchKernel(MTE_PICK(k_lds, gen, full), dim3(n_groups), dim3(64 * LDS_WAVES), args, sizeof(LdsPlan), s);
-}
-hipError_t launch_solo(const Params& p, bool gen, int full, u32 n_solo, hipStream_t s) {
-    static const hipError_t attr = [] {
-        hipError_t r = lds_attr<SoloPlan>((const void*)k_solo<true, 1>);
-        for (const void* k : {(const void*)k_solo<false, 0>, (const void*)k_solo<false, 1>, (const void*)k_solo<false, 2>})
-            if (r == hipSuccess) r = lds_attr<SoloPlan>(k);
-        return r;
-    }();
-    if (attr != hipSuccess) return attr;
-    void* args[] = {(void*)&p};
-    return hipLaunchKernel(MTE_PICK(k_solo, gen, full), dim3(n_solo), dim3(64 * SOLO_WAVES), args, sizeof(SoloPlan), s);
 }
 hipError_t launch_hbm(const Params& p, bool gen, int full, u32 n_docs, hipStream_t s) {
     void* args[] = {(void*)&p};

@@ -1,0 +1,111 @@
+// k_solo: the critical-path documents (gfx950). Its own translation unit so it builds without the
+// spill-sinking flag of the bulk kernels (mte_kernels.hip; measured 3.93 vs 3.98 us/op on the lone
+// 10^6-op document with it).
+#include "wave_hip.hpp"
+#include "engine.hpp"
+#include "reg_handoff.hpp"
+#include "mte_kernels.h"
+
+namespace mte {
+
+// k_solo owns its CU's LDS, so one wave per SIMD is all it ever has: the hint lets the scheduler
+// trade registers for latency hiding instead of aiming at an occupancy it can never reach.
+#ifndef MTE_SOLO_WPE
+#define MTE_SOLO_WPE 1
+#endif
+// waves of a solo workgroup: one per SIMD, so the critical-path CU holds no other kernel's waves
+#ifndef SOLO_WAVES
+#define SOLO_WAVES 4
+#endif
+
+// Critical-path documents (doc_list[0, n_solo), the longest of the batch): one single-wave
+// workgroup each, owning all of a CU's LDS (SoloPlan), at the highest wave priority. The replay
+// latency of the longest document bounds a Zipf batch, so it gets the plan with the
+// most room and no LDS-pool sharing; it continues HBM-resident only if it outgrows even that.
+template <bool GEN, int LVL>
+MTE_DEV void solo_doc(const Params& p) {
+    const u32 i = blockIdx.x;
+    if (i >= p.n_solo) return;
+    const u32 d = p.doc_list[i];
+    __builtin_amdgcn_s_setprio(3);
+    Engine<true, true, LVL> e(p, d);
+    e.bind_lds(0);
+    GenState g;
+    bool done;
+    u64 at = p.docs[d].op_begin;
+    bool handed = false;
+    if constexpr (!GEN && LVL == 0) {
+        // lean replay: the whole document state in this wave's registers (reg_engine.hpp); it moves
+        // to the LDS plan below only if it outgrows the registers or reaches an op they do not cover
+        if (p.reg_solo) {
+            RegEngine<> r(p, d);
+            at = r.replay(at, p.docs[d].op_end);
+            if (r.status != REG_HANDOFF) {
+                r.finish();
+                __builtin_amdgcn_s_setprio(0);
+                return;
+            }
+            reg_handoff(r, e);
+            handed = true;
+        }
+    }
+    if (!handed) e.init();
+    if (GEN) {
+        e.gen_init(g);
+        done = e.generate_run(g);
+    } else {
+        at = e.replay_run(at);
+        done = at >= p.docs[d].op_end;
+    }
+    if (e.st.status == DOC_SPILL) {
+        e.mark_spilled();
+    } else if (!done && e.st.status == 0) {
+        Engine<false, false, LVL> h(p, d);
+        h.continued = true;
+        h.bind_solo_slot(i);
+        h.adopt(e);
+        if (lane_id() == 0) atomicAdd(&p.counters[4], 1u);
+        if (GEN) {
+            h.generate_run(g);
+        } else {
+            h.replay_run(at);
+        }
+        h.finish();
+    } else {
+        e.finish();
+    }
+    __builtin_amdgcn_s_setprio(0);
+}
+
+// The solo workgroup is SOLO_WAVES waves that each claim a whole SIMD's register file (512 VGPRs +
+// AGPRs: the clobbers below make the kernel's allocation the maximum), and all of the CU's LDS: no
+// other wave of the pass can be resident on a critical-path CU. Wave 0 replays the document; the
+// others wait at the barrier (issuing nothing) until it is done.
+template <bool GEN, int LVL>
+__global__ __launch_bounds__(64 * SOLO_WAVES) __attribute__((amdgpu_waves_per_eu(MTE_SOLO_WPE, MTE_SOLO_WPE))) void k_solo(Params p) {
+#if SOLO_WAVES > 1
+    asm volatile("" ::: "v255", "a255");
+    if (wave_first(threadIdx.x >> 6) == 0) solo_doc<GEN, LVL>(p);
+    __syncthreads();
+#else
+    solo_doc<GEN, LVL>(p);
+#endif
+}
+
+#define MTE_PICK(K, gen, lvl)                                                                           \
+    ((gen) ? (const void*)K<true, 1> : (lvl) >= 2 ? (const void*)K<false, 2> : (lvl) == 1 ? (const void*)K<false, 1> \
+                                                                               : (const void*)K<false, 0>)
+
+hipError_t launch_solo(const Params& p, bool gen, int full, u32 n_solo, hipStream_t s) {
+    static const hipError_t attr = [] {
+        hipError_t r = hipFuncSetAttribute((const void*)k_solo<true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SoloPlan));
+        for (const void* k : {(const void*)k_solo<false, 0>, (const void*)k_solo<false, 1>, (const void*)k_solo<false, 2>})
+            if (r == hipSuccess) r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SoloPlan));
+        return r;
+    }();
+    if (attr != hipSuccess) return attr;
+    void* args[] = {(void*)&p};
+    return hipLaunchKernel(MTE_PICK(k_solo, gen, full), dim3(n_solo), dim3(64 * SOLO_WAVES), args, sizeof(SoloPlan), s);
+}
+
+}  // namespace mte

@@ -209,6 +209,10 @@ struct DevBuf {
         if (count == 0) count = 1;
         return hipMalloc((void**)&p, count * sizeof(T));
     }
+    // keep a buffer that is large enough: a later mte_load of a batch no larger than the last one
+    // allocates nothing (hipFree + hipMalloc of the multi-GB tables took 2.7-3.0 s on some loads,
+    // profiles/pcie_r03m_c4.json)
+    hipError_t fit(size_t count) { return (p && n >= count) ? hipSuccess : alloc(count); }
 };
 
 }  // namespace
@@ -449,7 +453,7 @@ static int upload_staged(mte_engine* e, void* dst, const void* src, size_t bytes
 
 template <class T>
 static int upload(mte_engine* e, DevBuf<T>& d, const T* h, size_t n) {
-    HIP_TRY(e, d.alloc(n));
+    HIP_TRY(e, d.fit(n));
     if (n) return upload_staged(e, d.p, h, n * sizeof(T));
     return MTE_OK;
 }
@@ -507,16 +511,16 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
         for (uint32_t d = 0; d < nd; d++)
             if ((double)n_ops[d] >= 8.0 * mean) e->cfg[d].prio = 1;
     }
-    HIP_TRY(e, e->d_arena.alloc(ar));
-    HIP_TRY(e, e->d_ovl.alloc(seg));
-    HIP_TRY(e, e->d_maps.alloc(mp * e->map_words));
-    HIP_TRY(e, e->d_out_vis.alloc(out));
-    HIP_TRY(e, e->d_out_aux.alloc(out));
-    HIP_TRY(e, e->d_out_ovl.alloc(out));
-    if (any_props) HIP_TRY(e, e->d_out_maps.alloc(out * e->map_words));  // some document can carry props
-    HIP_TRY(e, e->d_counters.alloc(8));
-    HIP_TRY(e, e->d_res.alloc(nd));
-    HIP_TRY(e, e->d_prof.alloc((size_t)nd * PROF_SLOTS));
+    HIP_TRY(e, e->d_arena.fit(ar));
+    HIP_TRY(e, e->d_ovl.fit(seg));
+    HIP_TRY(e, e->d_maps.fit(mp * e->map_words));
+    HIP_TRY(e, e->d_out_vis.fit(out));
+    HIP_TRY(e, e->d_out_aux.fit(out));
+    HIP_TRY(e, e->d_out_ovl.fit(out));
+    if (any_props) HIP_TRY(e, e->d_out_maps.fit(out * e->map_words));  // some document can carry props
+    HIP_TRY(e, e->d_counters.fit(8));
+    HIP_TRY(e, e->d_res.fit(nd));
+    HIP_TRY(e, e->d_prof.fit((size_t)nd * PROF_SLOTS));
     HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, (size_t)nd * PROF_SLOTS * 8, e->stream));
     // LPT order: longest documents start first
     e->order.resize(nd);
@@ -586,7 +590,8 @@ static void wave_plan(const mte_engine* e, uint32_t nd, uint32_t& groups, uint32
 // Output text pool: a document's final text never exceeds the text its log inserted, so the
 // payload's size bounds the whole batch (Engine::finish gathers into it).
 static int alloc_out_text(mte_engine* e) {
-    const uint64_t n = std::max<uint64_t>(1, std::min<uint64_t>(e->d_payload.n, 0xFFFFFFFFull));
+    const uint64_t pay = e->hb.doc_payload_offsets.empty() ? 0 : e->hb.doc_payload_offsets.back();
+    const uint64_t n = std::max<uint64_t>(1, std::min<uint64_t>(pay, 0xFFFFFFFFull));
     if (n > e->d_out_text.n || !e->d_out_text.p) HIP_TRY(e, e->d_out_text.alloc(n));
     e->P.out_text = e->d_out_text.p;
     e->P.out_text_cap = n;
@@ -1345,8 +1350,9 @@ int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_o
 
 static int ensure_host_ops(mte_engine* e) {
     if (e->host_ops_valid) return MTE_OK;
-    e->hb.ops.resize(e->d_ops.n);
-    e->hb.payload.resize(e->d_payload.n);
+    // (the device buffers may be larger than the batch: DevBuf::fit keeps earlier allocations)
+    e->hb.ops.resize(e->hb.doc_op_offsets.empty() ? 0 : e->hb.doc_op_offsets.back());
+    e->hb.payload.resize(e->hb.doc_payload_offsets.empty() ? 0 : e->hb.doc_payload_offsets.back());
     HIP_TRY(e, hipMemcpy(e->hb.ops.data(), e->d_ops.p, e->hb.ops.size() * sizeof(mte_op), hipMemcpyDeviceToHost));
     HIP_TRY(e, hipMemcpy(e->hb.payload.data(), e->d_payload.p, e->hb.payload.size() * 2, hipMemcpyDeviceToHost));
     e->host_ops_valid = true;

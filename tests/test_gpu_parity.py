@@ -409,3 +409,20 @@ def test_hbm_slot_exhaustion_completes(engine):
     if bad:
         compare_doc(engine, batch, bad[0])
     assert not bad
+
+
+def test_reloads_reuse_device_tables(engine):
+    """mte_load keeps device tables that are large enough (DevBuf::fit): a small batch after a large
+    one replays in the larger buffers, then the large one again, each matching the oracle."""
+    big = mte.Builder()
+    for s in range(40):
+        big.add_doc(random_log(100 + s, n=600))
+    small = mte.Builder()
+    for s in range(5):
+        small.add_doc(random_log(200 + s, n=150))
+    for b in (big, small, big):
+        batch = b.batch()
+        engine.load(batch)
+        engine.replay()
+        for d in range(batch.n_docs):
+            compare_doc(engine, batch, d)

@@ -43,6 +43,25 @@ assert.deepStrictEqual(lt.entries.map((x) => [x.path, x.value.contents]),
 // the reference's default summary format is SnapshotLegacy (client.ts:930-941)
 assert.strictEqual(new MergeTreeClient()._engine, undefined);
 assert.strictEqual(c1._engine.legacyFormat, true);
+// SharedMatrix with cell sets (matrix.ts:575-601): rows [3], cols [2], set (0,0)=5 and (2,1)="x" --
+// rows 0 and 2 take handles 1 and 2 (split out of the unallocated run), cols 0 and 1 settle into one
+// run [2, 1]; the cells sit at Morton keys 3 and 12 of the first tile
+const UN = -2147483648;
+const mx = new BatchedMergeEngine({ newMergeTreeSnapshotFormat: true });
+mx.load([{ observer: "obs", matrix: [
+    msg("w", 1, 0, { target: "rows", pos1: 0, seg: [3, UN], type: 0 }, 1),
+    msg("w", 2, 1, { target: "cols", pos1: 0, seg: [2, UN], type: 0 }, 2),
+    msg("w", 3, 2, { type: 2, row: 0, col: 0, value: 5 }, 3),
+    msg("w", 4, 3, { type: 2, row: 2, col: 1, value: "x" }, 4)] }]);
+assert.strictEqual(mx.replay().failedDocs, 0);
+const mt = mx.snapshotMatrix(0, 1);
+const vec = (i) => JSON.parse(mt.entries[i].value.entries[0].value.entries[0].value.contents).segments;
+assert.deepStrictEqual(vec(0), [[1, 1], [1, UN], [1, 2]]);
+assert.deepStrictEqual(vec(1), [[2, 1]]);
+assert.deepStrictEqual(mt.entries.slice(0, 2).map((x) => x.value.entries[1].value.contents), ["[3,0,0]", "[3,0,0]"]);
+const [cells, pending] = JSON.parse(mt.entries[2].value.contents);
+assert.deepStrictEqual(pending, [null]);
+assert.deepStrictEqual(cells[0][0][0][0].flatMap((v, i) => (v === null ? [] : [[i, v]])), [[3, 5], [12, "x"]]);
 const e = new BatchedMergeEngine({ newMergeTreeSnapshotFormat: true });
 e.generate(2, 8, 500, 8, 3);
 const st = e.replay();

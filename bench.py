@@ -140,10 +140,6 @@ def run(args):
     from fluidframework_amd.shard import gather_summaries_rccl, plan_shard
 
     cfg = CONFIGS[args.config]
-    # torch's device context up before any replay: its first CUDA call (the synchronize that opens the
-    # timed region) used to land inside the first timed step, which then ran ~15 % slower
-    torch.cuda.init()
-    torch.cuda.synchronize()
     eng = mte.Engine(local)
     for kv in args.opt:
         k, v = kv.split("=")

@@ -145,9 +145,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_HBMQ_WPE
     if (i >= p.n_list) return;
     const u32 d = p.doc_list[i];
     const u32 slot = acquire_hslot(p);
-#ifdef MTE_HBMQ_PRIO
-    __builtin_amdgcn_s_setprio(MTE_HBMQ_PRIO);
-#endif
     Engine<false, false, LVL> e(p, d);
     e.bind_slot(p.slot_hbm0 + slot);
     e.reset_stats();

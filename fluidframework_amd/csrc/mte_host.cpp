@@ -282,6 +282,7 @@ struct mte_engine {
 #define MTE_HBMQ_PER_CU 8
 #endif
     uint32_t hbm_waves_per_cu = MTE_HBMQ_PER_CU;  // HBM-resident waves (slots) per CU beside the LDS workgroup
+    bool hbm_waves_set = false;          // ... set by mte_set_option (else wave_plan may drop them)
     uint64_t slot_budget = 48ull << 30;  // HBM for per-wave slots
     uint64_t slot_ops_cap = 65536;       // slots are sized for documents of at most this many ops
     uint32_t slot_blk_limit = 0;         // test knob: leaf blocks per slot (0 = from slot_ops_cap)
@@ -578,7 +579,20 @@ static void wave_plan(const mte_engine* e, uint32_t nd, uint32_t& groups, uint32
     if (e->force_hbm || (uint64_t)groups * LDS_WAVES > max_slots) groups = 0;
     if (lds_active) *lds_active = groups ? std::min<uint32_t>(LDS_WAVES, (nd + groups - 1) / groups) : 0;
     // 16 = 4 SIMDs x 4 waves at <= 128 VGPRs (k_hbmq's bound): more can never be resident at once
-    const uint32_t per_cu = groups ? std::min<uint32_t>(e->hbm_waves_per_cu, 16) : 16;
+    uint32_t per_cu = groups ? std::min<uint32_t>(e->hbm_waves_per_cu, 16) : 16;
+    // A batch bounded by its critical-path documents: the HBM-resident waves' memory traffic slows
+    // the solo waves (C4: steps of 4.0-4.77 s with them, 4.00-4.08 s without, profiles/r03hw_*.json),
+    // so the bulk runs LDS-resident only when it still finishes well inside the longest document's
+    // replay (estimates: >= 80 M ops/s for the LDS-only bulk, <= 4 us/op on the critical path).
+    if (groups && n_solo && !e->hbm_waves_set && !e->order.empty()) {
+        uint64_t nmax = 0, bulk = 0;
+        for (uint32_t k = 0; k < (uint32_t)e->order.size(); k++) {
+            const uint64_t n = e->n_ops_doc[e->order[k]];
+            if (k < n_solo) nmax = std::max(nmax, n);
+            else bulk += n;
+        }
+        if ((double)nmax * 4.0e-6 > 1.25 * (double)bulk / 80.0e6) per_cu = 0;
+    }
     uint64_t h = (uint64_t)per_cu * cus;
     h = std::min<uint64_t>(h, max_slots - (uint64_t)groups * LDS_WAVES);
     if (nd > (uint64_t)groups * LDS_WAVES) h = std::min<uint64_t>(h, nd - (uint64_t)groups * LDS_WAVES);
@@ -2324,7 +2338,10 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     std::string k(key);
     if (k == "force_hbm") e->force_hbm = value != 0;
     else if (k == "pool_limit") e->pool_limit = (uint32_t)std::max<int64_t>(0, value);
-    else if (k == "hbm_waves_per_cu") e->hbm_waves_per_cu = (uint32_t)std::min<int64_t>(std::max<int64_t>(0, value), 32);
+    else if (k == "hbm_waves_per_cu") {
+        e->hbm_waves_per_cu = (uint32_t)std::min<int64_t>(std::max<int64_t>(0, value), 32);
+        e->hbm_waves_set = true;
+    }
     else if (k == "slot_budget_mb") e->slot_budget = (uint64_t)std::max<int64_t>(1, value) << 20;
     else if (k == "slot_ops_cap") e->slot_ops_cap = (uint64_t)std::max<int64_t>(64, value);  // next load
     else if (k == "slot_blk_limit") e->slot_blk_limit = (uint32_t)std::max<int64_t>(0, value);  // next load

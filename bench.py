@@ -283,6 +283,7 @@ def run(args):
                       "solo_ms_last_step": info.get("solo_us", 0) / 1000.0,  # critical-path workgroups' pass
                       "kernel_ms_steps": [round(x, 1) for x in kms],
                       "solo_ms_steps": [round(x, 1) for x in solo_steps],
+                      "lds_ms_last_step": info.get("lds_ms", 0.0), "hbm_ms_last_step": info.get("hbm_ms", 0.0),
                       "solo_lead_ms": info.get("solo_lead_us", 0) / 1000.0,  # pass start -> solo start
                       "solo_tail_ms": info.get("solo_tail_us", 0) / 1000.0,  # solo end -> pass end
                       "us_per_op_critical_path": (info.get("solo_us", 0) / max(int(counts.max()), 1)) if info["solo"] else None,

@@ -582,8 +582,9 @@ static void wave_plan(const mte_engine* e, uint32_t nd, uint32_t& groups, uint32
     uint32_t per_cu = groups ? std::min<uint32_t>(e->hbm_waves_per_cu, 16) : 16;
     // A batch bounded by its critical-path documents: the HBM-resident waves' memory traffic slows
     // the solo waves (C4: steps of 4.0-4.77 s with them, 4.00-4.08 s without, profiles/r03hw_*.json),
-    // so the bulk runs LDS-resident only when it still finishes well inside the longest document's
-    // replay (estimates: >= 80 M ops/s for the LDS-only bulk, <= 4 us/op on the critical path).
+    // so the bulk runs LDS-resident only when it still finishes inside the longest document's replay
+    // (estimates: >= 120 M ops/s for the LDS-only bulk -- C2 163 M, C3 187 M, tools/sweep.py hw 0 --
+    // and ~4 us/op on the critical path).
     if (groups && n_solo && !e->hbm_waves_set && !e->order.empty()) {
         uint64_t nmax = 0, bulk = 0;
         for (uint32_t k = 0; k < (uint32_t)e->order.size(); k++) {
@@ -591,7 +592,7 @@ static void wave_plan(const mte_engine* e, uint32_t nd, uint32_t& groups, uint32
             if (k < n_solo) nmax = std::max(nmax, n);
             else bulk += n;
         }
-        if ((double)nmax * 4.0e-6 > 1.25 * (double)bulk / 80.0e6) per_cu = 0;
+        if ((double)nmax * 4.0e-6 > 1.1 * (double)bulk / 120.0e6) per_cu = 0;
     }
     uint64_t h = (uint64_t)per_cu * cus;
     h = std::min<uint64_t>(h, max_slots - (uint64_t)groups * LDS_WAVES);

@@ -72,12 +72,7 @@ def main(tag, config="C4"):
     for p in glob.glob(f"{base}/trace/**/*kernel_stats.csv", recursive=True):
         with open(p) as f, open(f"profiles/{tag}_kernel_stats.csv", "w") as g:
             g.write(f.read())
-    if "hbm_bytes_per_launch" in summary:
-        with open(f"profiles/pmc_replay_{config}.json", "w") as f:
-            json.dump({"docs": docs, "ops": ops, "kind": kind, "source": f"profiles/{tag}_summary.json",
-                       "hbm_bytes_per_launch": summary["hbm_bytes_per_launch"],
-                       "note": "raw (FETCH_SIZE+WRITE_SIZE)*1024; gfx950 FETCH_SIZE calibration (x2) applies only to "
-                               "wide coalesced streams and is NOT applied to this narrow-access kernel"}, f, indent=1)
+    # (profiles/pmc_replay_<config>.json, the bench's calibrated traffic, is tools/pmc_replay.py's)
     print(json.dumps(summary, indent=1))
 
 

@@ -38,8 +38,14 @@ constexpr u32 BM_NOPAR = 0x3FFFFFFFu;
 constexpr u32 LDS_WAVES = 8;
 constexpr u32 LDS_BYTES = 163840;  // 160 KiB per CU (MI355X_MICROARCH.md), one workgroup declares all of it
 constexpr u32 ORD_CAP = 128;       // leaf blocks per document while resident in LDS
-constexpr u32 IN_CAP = 48;         // interior nodes per document while resident in LDS
-constexpr u32 HEAP_CAP = 191;      // LRU heap entries per document while resident in LDS
+#ifndef MTE_IN_CAP
+#define MTE_IN_CAP 48
+#endif
+#ifndef MTE_HEAP_CAP
+#define MTE_HEAP_CAP 191
+#endif
+constexpr u32 IN_CAP = MTE_IN_CAP;      // interior nodes per document while resident in LDS
+constexpr u32 HEAP_CAP = MTE_HEAP_CAP;  // LRU heap entries per document while resident in LDS
 constexpr u32 RING_OPS = 32;       // op records staged per wave (prefetched one batch ahead)
 constexpr u32 OP_CREDIT = 4;       // leaf blocks a wave holds in reserve before each op
 

@@ -1330,10 +1330,11 @@ struct Engine {
     // register image, the root-to-leaf path followed with readlanes; k_solo and HBM mode: lane 0
     // walks the child pairs in memory. Only the moved entries are written.
     // heap entry at a uniform position held in registers (position i: lane i % 64 of set i / 64)
-    MTE_DEV static uint2 hent(uint2 h0, uint2 h1, uint2 h2, u32 i) {
+    MTE_DEV static uint2 hent(uint2 h0, uint2 h1, uint2 h2, uint2 h3, u32 i) {
         if (i < 64) return make_uint2(wave_read(h0.x, i), wave_read(h0.y, i));
         if (i < 128) return make_uint2(wave_read(h1.x, i - 64), wave_read(h1.y, i - 64));
-        return make_uint2(wave_read(h2.x, i - 128), wave_read(h2.y, i - 128));
+        if (HEAP_CAP < 192 || i < 192) return make_uint2(wave_read(h2.x, i - 128), wave_read(h2.y, i - 128));
+        return make_uint2(wave_read(h3.x, i - 192), wave_read(h3.y, i - 192));
     }
     MTE_DEV uint2 heap_pop() {
         MTE_PROF(PF_HEAP);
@@ -1343,20 +1344,21 @@ struct Engine {
         const u32 m = n - 1;
         uint2 x;
         if constexpr (SHARED) {  // the whole heap (<= HEAP_CAP) as a register image, scalar walk
-            static_assert(HEAP_CAP < 192, "heap register image holds 192 positions");
-            uint2 h0 = make_uint2(0, 0), h1 = h0, h2 = h0;
+            static_assert(HEAP_CAP < 256, "heap register image holds 256 positions");
+            uint2 h0 = make_uint2(0, 0), h1 = h0, h2 = h0, h3 = h0;
             if (L <= n) h0 = H[L];
             if (n >= 64 && 64 + L <= n) h1 = H[64 + L];
             if (n >= 128 && 128 + L <= n) h2 = H[128 + L];
-            x = hent(h0, h1, h2, 1);
-            const uint2 last = hent(h0, h1, h2, n);
+            if (HEAP_CAP >= 192 && n >= 192 && 192 + L <= n) h3 = H[192 + L];
+            x = hent(h0, h1, h2, h3, 1);
+            const uint2 last = hent(h0, h1, h2, h3, n);
             i32 newTop = (i32)last.y;
             u32 k = 1;
             while ((k << 1) <= m) {
                 u32 j = k << 1;
-                uint2 hj = hent(h0, h1, h2, j);
+                uint2 hj = hent(h0, h1, h2, h3, j);
                 if (j < m) {
-                    const uint2 hj1 = hent(h0, h1, h2, j + 1);
+                    const uint2 hj1 = hent(h0, h1, h2, h3, j + 1);
                     if ((i32)hj.y - (i32)hj1.y > 0) {
                         j++;
                         hj = hj1;

@@ -2255,18 +2255,16 @@ void mte_rccl_comm_destroy(void* comm) {
     if (comm && rccl().ok()) rccl().commDestroy((ncclComm_t)comm);
 }
 
-int mte_gather_summaries(mte_engine* e, int rank, int world, void* comm, mte_doc_summary* out, size_t cap,
-                         size_t* n) {
+// The gather itself: every rank's records into `res` (rank order). One count all-gather and one
+// record all-gather; the caller sizes nothing beforehand.
+static int gather_all(mte_engine* e, int rank, int world, void* comm, std::vector<mte_doc_summary>& res) {
     if (!e || world < 1 || rank < 0 || rank >= world || (world > 1 && !comm)) return MTE_E_ARG;
     const size_t nd = e->P.n_docs;
     std::vector<mte_doc_summary> mine(nd);
     int rc = nd ? mte_summaries(e, mine.data(), nd) : MTE_OK;
     if (rc) return rc;
     if (world == 1) {
-        if (n) *n = nd;
-        if (!out) return MTE_OK;
-        if (cap < nd) return MTE_E_RANGE;
-        std::copy(mine.begin(), mine.end(), out);
+        res.swap(mine);
         return MTE_OK;
     }
     HIP_TRY(e, hipSetDevice(e->device));
@@ -2283,9 +2281,6 @@ int mte_gather_summaries(mte_engine* e, int rank, int world, void* comm, mte_doc
     HIP_TRY(e, hipMemcpyAsync(counts.data(), all_cnt.p, 8 * (size_t)world, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
     const GatherPlan g = gather_plan(counts.data(), world);
-    if (n) *n = g.total;
-    if (!out) return MTE_OK;
-    if (cap < g.total) return MTE_E_RANGE;
     const size_t words = sizeof(mte_doc_summary) / 8;  // 32-B records as 4 u64 words
     std::vector<mte_doc_summary> blk(g.stride), flat(g.stride * (size_t)world);
     gather_pack(mine.data(), nd, g, blk.data());
@@ -2298,9 +2293,44 @@ int mte_gather_summaries(mte_engine* e, int rank, int world, void* comm, mte_doc
     HIP_TRY(e, hipMemcpyAsync(flat.data(), recv.p, flat.size() * sizeof(mte_doc_summary), hipMemcpyDeviceToHost,
                               e->stream));
     HIP_TRY(e, hipStreamSynchronize(e->stream));
-    gather_concat(flat.data(), counts.data(), world, g, out);
+    res.resize(g.total);
+    gather_concat(flat.data(), counts.data(), world, g, res.data());
     return MTE_OK;
 }
+
+int mte_gather_summaries(mte_engine* e, int rank, int world, void* comm, mte_doc_summary* out, size_t cap,
+                         size_t* n) {
+    if (!e || world < 1 || rank < 0 || rank >= world || (world > 1 && !comm)) return MTE_E_ARG;
+    if (!out) {  // size query: the count all-gather only when world > 1 (every rank queries)
+        if (world == 1) {
+            if (n) *n = e->P.n_docs;
+            return MTE_OK;
+        }
+    }
+    std::vector<mte_doc_summary> res;
+    if (int rc = gather_all(e, rank, world, comm, res)) return rc;
+    if (n) *n = res.size();
+    if (!out) return MTE_OK;
+    if (cap < res.size()) return MTE_E_RANGE;
+    std::copy(res.begin(), res.end(), out);
+    return MTE_OK;
+}
+
+int mte_gather_summaries_alloc(mte_engine* e, int rank, int world, void* comm, mte_doc_summary** out, size_t* n) {
+    if (!out || !n) return MTE_E_ARG;
+    *out = nullptr;
+    *n = 0;
+    std::vector<mte_doc_summary> res;
+    if (int rc = gather_all(e, rank, world, comm, res)) return rc;
+    void* p = malloc(res.empty() ? 1 : res.size() * sizeof(mte_doc_summary));
+    if (!p) return set_err(e, MTE_E_NOMEM, "gather buffer");
+    if (!res.empty()) memcpy(p, res.data(), res.size() * sizeof(mte_doc_summary));
+    *out = (mte_doc_summary*)p;
+    *n = res.size();
+    return MTE_OK;
+}
+
+void mte_free(void* p) { free(p); }
 
 // Extra helpers (not part of include/mte.h's contract; used by tests / bench for diagnostics).
 int mte_doc_result(mte_engine* e, uint32_t doc, void* out, size_t sz) {

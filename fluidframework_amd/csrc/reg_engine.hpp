@@ -137,6 +137,7 @@ struct RegEngine {
     u32 n_lb, height, heapSize, segNext, arenaTop, arenaSel;
     i32 minSeq, curSeq, heapTop, status, failSeq;
     u32 n_ops, n_msgs, n_gc, max_lb;
+    u32 lb_lim;  // leaf-block limit of room() (Params::reg_lb_limit, read once)
     bool adirty;
 #if defined(MTE_PROFILE) && !defined(MTE_CPU)
     u64 pf[RP_N];
@@ -209,41 +210,58 @@ struct RegEngine {
     }
     SD void stf(u32 r, u32 aux, u32 c, V x, B m) {
         u32* b = reinterpret_cast<u32*>(aux ? AUXP() : VISP());
-        if (m.b) b[(r * 64 + __lane_id()) * 4 + c] = x.x;
+        if (simd::lane_of(m)) b[(r * 64 + __lane_id()) * 4 + c] = x.x;
         simd::lds_order();
     }
-    SD void mv_slots(u32 dst, u32 src, u32 n) {  // overlapping: copy in the safe direction
+    // Overlapping slot move in the safe direction, eight 64-slot chunks per round: all sixteen
+    // ds_read_b128 of a round are issued before its first write, so a round costs one LDS latency
+    // (the chunks of one round never overlap the slots a later round reads).
+    SD void mv_slots(u32 dst, u32 src, u32 n) {
         cr = NONE;
         uint4* V4 = VISP();
         uint4* A4 = AUXP();
-        const u32 L = __lane_id();
+        const i32 L = (i32)__lane_id();
         if (dst > src) {
-            for (i32 b = (i32)n - 64; b > -64; b -= 64) {
-                const i32 i = b + (i32)L;
-                uint4 v = make_uint4(0, 0, 0, 0), a = v;
-                if (i >= 0) {
-                    v = V4[src + (u32)i];
-                    a = A4[src + (u32)i];
+            for (i32 top = (i32)n; top > 0; top -= 512) {
+                uint4 v[8], a[8];
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    const i32 i = top - 64 * (c + 1) + L;
+                    if (top - 64 * c > 0 && i >= 0) {
+                        v[c] = V4[src + (u32)i];
+                        a[c] = A4[src + (u32)i];
+                    }
                 }
                 simd::lds_order();
-                if (i >= 0) {
-                    V4[dst + (u32)i] = v;
-                    A4[dst + (u32)i] = a;
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    const i32 i = top - 64 * (c + 1) + L;
+                    if (top - 64 * c > 0 && i >= 0) {
+                        V4[dst + (u32)i] = v[c];
+                        A4[dst + (u32)i] = a[c];
+                    }
                 }
                 simd::lds_order();
             }
         } else {
-            for (u32 b = 0; b < n; b += 64) {
-                const u32 i = b + L;
-                uint4 v = make_uint4(0, 0, 0, 0), a = v;
-                if (i < n) {
-                    v = V4[src + i];
-                    a = A4[src + i];
+            for (i32 b0 = 0; b0 < (i32)n; b0 += 512) {
+                uint4 v[8], a[8];
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    const i32 i = b0 + 64 * c + L;
+                    if (b0 + 64 * c < (i32)n && i < (i32)n) {
+                        v[c] = V4[src + (u32)i];
+                        a[c] = A4[src + (u32)i];
+                    }
                 }
                 simd::lds_order();
-                if (i < n) {
-                    V4[dst + i] = v;
-                    A4[dst + i] = a;
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    const i32 i = b0 + 64 * c + L;
+                    if (b0 + 64 * c < (i32)n && i < (i32)n) {
+                        V4[dst + (u32)i] = v[c];
+                        A4[dst + (u32)i] = a[c];
+                    }
                 }
                 simd::lds_order();
             }
@@ -301,6 +319,7 @@ struct RegEngine {
         failSeq = -1;
         n_ops = n_msgs = n_gc = 0;
         max_lb = 1;
+        lb_lim = p.reg_lb_limit && p.reg_lb_limit < NBLK ? p.reg_lb_limit : NBLK;
         adirty = false;
 #if defined(MTE_PROFILE) && !defined(MTE_CPU)
         for (u32 i = 0; i < RP_N; i++) pf[i] = 0;
@@ -730,16 +749,21 @@ struct RegEngine {
             heap_push(sid, seq);
         }
     }
-    // the leaf block holding segment sid (segment.parent), NONE when unlinked
+    // the leaf block holding segment sid (segment.parent), NONE when unlinked. Segment ids are
+    // unique, so each batch of eight rows needs one per-lane select per row and ONE ballot (no
+    // branch per row): the hit lane's row index comes back with one readlane.
     SD u32 find_seg(u32 sid) {
         RG_PROF(RP_FIND_SEG);
         const u32 nrows = (n_lb + 7) >> 3;
         for (u32 r0 = 0; r0 < nrows; r0 += 8) {  // eight rows' reads in flight per round
             V s8[8];
             for (u32 i = 0; i < 8; i++) s8[i] = ld_sid(r0 + i < nrows ? r0 + i : r0);
-            for (u32 i = 0; i < 8 && r0 + i < nrows; i++) {
-                const u64 m = simd::ballot(s8[i] == sid);
-                if (m) return (r0 + i) * 8 + ((u32)__builtin_ctzll(m) >> 3);
+            V hr = simd::splat(NONE);
+            for (u32 i = 8; i-- > 0;) hr = simd::sel(s8[i] == sid, r0 + i, hr);  // rows past nrows re-read r0: i = 0 wins
+            const u64 m = simd::ballot(hr != NONE);
+            if (m) {
+                const u32 l = (u32)__builtin_ctzll(m);
+                return simd::readlane(hr, l) * 8 + (l >> 3);
             }
         }
         return NONE;
@@ -748,6 +772,9 @@ struct RegEngine {
     // ---------------------------------------------------------------- text (HBM)
     SD u16* arena_cur() const { return arena0 + (u64)arenaSel * arena_cap; }
     SD void fence_arena() {
+#ifdef MTE_KO_TEXT  // timing experiment only (wrong text): no scour text copies, no arena fences
+        return;
+#endif
         if (adirty) {
             simd::wave_fence();
             adirty = false;
@@ -916,6 +943,9 @@ struct RegEngine {
     // The runs' text copies of one block as one flattened gather: slot lane l copies jlen units from
     // its text src to jdst (sources are never destinations of the same scour).
     SD void copy_runs(V jdst, V jsrc, V jlen) {
+#ifdef MTE_KO_TEXT
+        return;
+#endif
         const V jinc = simd::scan_incl(jlen);
         const u32 total = simd::readlane(jinc, 63);
         if (!total) return;
@@ -1332,8 +1362,7 @@ struct RegEngine {
     // Room for one more op (margins for the splits, packs and heap pushes an op can cause);
     // false => hand the document to the LDS engine before this op.
     SD bool room() const {
-        const u32 lim = p.reg_lb_limit && p.reg_lb_limit < NBLK ? p.reg_lb_limit : NBLK;
-        return n_lb + 16 <= lim && heapSize + n_lb + 8 < RG_HEAP && height + 2 <= RG_LEVELS &&
+        return n_lb + 16 <= lb_lim && heapSize + n_lb + 8 < RG_HEAP && height + 2 <= RG_LEVELS &&
                simd::readlane(LV.get(0), 56) == 0u;
     }
 
@@ -1404,28 +1433,39 @@ struct RegEngine {
         }
         RG_PROF(RP_TOTAL);
         const u32* src = (const u32*)p.ops;
-        simd::VA<4> Q;
         const u64 b = i;
         auto load_chunk = [&](u64 c0) MTE_LI {  // records [c0, c0+8)
             const u64 left = e > c0 ? e - c0 : 0;
             const u32 nw = left >= 8 ? 64u : (u32)left * 8u;
             return simd::ld(src + c0 * 8, L(), L() < nw);
         };
-        for (u32 c = 0; c < 4; c++) Q.set(c, load_chunk(b + (u64)c * 8));
+        // four chunk registers used as a ring: chunk c lives in Q[c & 3] and is refilled in place
+        // with chunk c + 4 once consumed, so a refill's load is not waited for until 24 ops later (a
+        // shifted register queue made the compiler wait for each refill at once)
+        V Q0 = load_chunk(b), Q1 = load_chunk(b + 8), Q2 = load_chunk(b + 16), Q3 = load_chunk(b + 24);
+        u32 qh = 0;
         for (; i < e && !status; i++) {
             const u32 r = (u32)((i - b) & 7);
             if (r == 0 && i != b) {
-                Q.set(0, Q.get(1));
-                Q.set(1, Q.get(2));
-                Q.set(2, Q.get(3));
-                Q.set(3, load_chunk(i + 24));
+                const u64 nc = i + 24;
+                switch (qh) {
+                    case 0: Q0 = load_chunk(nc); break;
+                    case 1: Q1 = load_chunk(nc); break;
+                    case 2: Q2 = load_chunk(nc); break;
+                    default: Q3 = load_chunk(nc); break;
+                }
+                qh = (qh + 1) & 3u;
             }
             mte_op op;
             {
                 RG_PROF(RP_FETCH);
-                const V q = Q.get(0);
                 u32 w[8];
-                for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(q, r * 8 + x);
+                switch (qh) {
+                    case 0: for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(Q0, r * 8 + x); break;
+                    case 1: for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(Q1, r * 8 + x); break;
+                    case 2: for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(Q2, r * 8 + x); break;
+                    default: for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(Q3, r * 8 + x); break;
+                }
                 __builtin_memcpy(&op, w, sizeof op);
             }
             RG_COUNT(RP_OPS, 1);

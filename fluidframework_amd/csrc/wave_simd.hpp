@@ -34,9 +34,26 @@ typedef uint64_t u64;
 struct V {
     u32 x;
 };
+#ifndef MTE_B_MASK
+#define MTE_B_MASK 1
+#endif
+#if MTE_B_MASK
+// A per-lane predicate as the wave's 64-bit lane mask (an SGPR pair): a compare is one v_cmp writing
+// the pair, &, | and ~ are one SALU op each, sel is one v_cndmask reading the pair
+// (inverse_ballot) and ballot is free. (A 0/1 value per lane made every ballot of a combined
+// predicate a v_cndmask 0/1 + v_cmp pair.) The program runs with all 64 lanes active.
+struct B {
+    u64 m;
+};
+SD B mk(bool c) { return {__builtin_amdgcn_ballot_w64(c)}; }
+SD bool lane_of(B c) { return __builtin_amdgcn_inverse_ballot_w64(c.m); }
+#else
 struct B {  // a per-lane predicate; u32 0/1 rather than bool: an i1 member defeats SROA (stores i1,
     u32 b;  // loads i8) and left every predicate of the engine on the scratch stack
 };
+SD B mk(bool c) { return {(u32)c}; }
+SD bool lane_of(B c) { return c.b != 0; }
+#endif
 
 SD V lanes() { return V{__lane_id()}; }
 SD V splat(u32 s) { return V{s}; }
@@ -59,34 +76,43 @@ SD V shl(V a, V s) { return {a.x << (s.x & 31u)}; }  // per-lane shift count (lo
 SD V bfe(V a, u32 off, u32 w) { return {__builtin_amdgcn_ubfe(a.x, off, w)}; }
 
 // unsigned compares
-SD B operator==(V a, V b) { return {(u32)(a.x == b.x)}; }
-SD B operator==(V a, u32 b) { return {(u32)(a.x == b)}; }
-SD B operator!=(V a, u32 b) { return {(u32)(a.x != b)}; }
-SD B operator<(V a, u32 b) { return {(u32)(a.x < b)}; }
-SD B operator<(V a, V b) { return {(u32)(a.x < b.x)}; }
-SD B operator>=(V a, u32 b) { return {(u32)(a.x >= b)}; }
-SD B operator>=(V a, V b) { return {(u32)(a.x >= b.x)}; }
-SD B operator>(V a, u32 b) { return {(u32)(a.x > b)}; }
+SD B operator==(V a, V b) { return mk(a.x == b.x); }
+SD B operator==(V a, u32 b) { return mk(a.x == b); }
+SD B operator!=(V a, u32 b) { return mk(a.x != b); }
+SD B operator<(V a, u32 b) { return mk(a.x < b); }
+SD B operator<(V a, V b) { return mk(a.x < b.x); }
+SD B operator>=(V a, u32 b) { return mk(a.x >= b); }
+SD B operator>=(V a, V b) { return mk(a.x >= b.x); }
+SD B operator>(V a, u32 b) { return mk(a.x > b); }
 // signed compares
-SD B slt(V a, V b) { return {(u32)((i32)a.x < (i32)b.x)}; }
-SD B sle(V a, i32 b) { return {(u32)((i32)a.x <= b)}; }
-SD B sgt(V a, i32 b) { return {(u32)((i32)a.x > b)}; }
-SD B sge(V a, i32 b) { return {(u32)((i32)a.x >= b)}; }
-SD B slt(V a, i32 b) { return {(u32)((i32)a.x < b)}; }
-SD B slt(i32 a, V b) { return {(u32)(a < (i32)b.x)}; }
+SD B slt(V a, V b) { return mk((i32)a.x < (i32)b.x); }
+SD B sle(V a, i32 b) { return mk((i32)a.x <= b); }
+SD B sgt(V a, i32 b) { return mk((i32)a.x > b); }
+SD B sge(V a, i32 b) { return mk((i32)a.x >= b); }
+SD B slt(V a, i32 b) { return mk((i32)a.x < b); }
+SD B slt(i32 a, V b) { return mk(a < (i32)b.x); }
 
+#if MTE_B_MASK
+SD B operator&(B a, B b) { return {a.m & b.m}; }
+SD B operator|(B a, B b) { return {a.m | b.m}; }
+SD B operator~(B a) { return {~a.m}; }
+SD B andn(B a, B b) { return {a.m & ~b.m}; }
+SD u64 ballot(B c) { return c.m; }
+SD B ballot_mask(u64 m) { return {m}; }
+#else
 SD B operator&(B a, B b) { return {a.b & b.b}; }
 SD B operator|(B a, B b) { return {a.b | b.b}; }
 SD B operator~(B a) { return {a.b ^ 1u}; }
 SD B andn(B a, B b) { return {a.b & (b.b ^ 1u)}; }
-
-SD V sel(B c, V a, V b) { return {c.b ? a.x : b.x}; }
-SD V sel(B c, u32 a, V b) { return {c.b ? a : b.x}; }
-SD V sel(B c, V a, u32 b) { return {c.b ? a.x : b}; }
-
 SD u64 ballot(B c) { return __ballot(c.b != 0); }
 // the per-lane predicate of a uniform 64-bit mask (lane l: bit l)
 SD B ballot_mask(u64 m) { return {(u32)((m >> __lane_id()) & 1ull)}; }
+#endif
+
+SD V sel(B c, V a, V b) { return {lane_of(c) ? a.x : b.x}; }
+SD V sel(B c, u32 a, V b) { return {lane_of(c) ? a : b.x}; }
+SD V sel(B c, V a, u32 b) { return {lane_of(c) ? a.x : b}; }
+
 SD u32 readlane(V v, u32 l) { return __builtin_amdgcn_readlane(v.x, l); }
 // v_writelane_b32 through the LLVM intrinsic (this clang has no __builtin for it)
 extern "C" __device__ int mte_llvm_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
@@ -139,11 +165,11 @@ struct VA {
 // per-lane memory access (global)
 template <class T>
 SD V ld(const T* p, V idx, B m) {
-    return V{m.b ? (u32)p[idx.x] : 0u};
+    return V{lane_of(m) ? (u32)p[idx.x] : 0u};
 }
 template <class T>
 SD void st(T* p, V idx, V v, B m) {
-    if (m.b) p[idx.x] = (T)v.x;
+    if (lane_of(m)) p[idx.x] = (T)v.x;
 }
 // true in exactly one lane (the lane that performs a wave's single store / atomic)
 SD bool lane0() { return __lane_id() == 0; }

@@ -102,7 +102,7 @@ SUMMARY_DTYPE = np.dtype([("checksum", "<u8"), ("ops", "<u4"), ("length", "<u4")
 EXPORTS = ["mte_abi_version", "mte_build_info", "mte_create", "mte_destroy", "mte_last_error", "mte_load",
            "mte_replay", "mte_generate", "mte_generate_ids", "mte_export_batch", "mte_doc_status", "mte_text", "mte_length", "mte_segments",
            "mte_snapshot_v1", "mte_snapshot_legacy", "mte_snapshot_shared_string", "mte_summaries", "mte_rccl_unique_id",
-           "mte_rccl_comm_create", "mte_rccl_comm_destroy", "mte_gather_summaries", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
+           "mte_rccl_comm_create", "mte_rccl_comm_destroy", "mte_gather_summaries", "mte_gather_summaries_alloc", "mte_free", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
            "mte_builder_add_matrix_log", "mte_snapshot_matrix",
            "mte_builder_batch",
            "mte_builder_error", "mte_builder_destroy"]
@@ -142,6 +142,9 @@ def lib():
         L.mte_rccl_comm_destroy.argtypes = [vp]
         L.mte_rccl_comm_destroy.restype = None
         L.mte_gather_summaries.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_void_p, sz, ctypes.POINTER(sz)]
+        L.mte_gather_summaries_alloc.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp), ctypes.POINTER(sz)]
+        L.mte_free.argtypes = [vp]
+        L.mte_free.restype = None
         L.mte_doc_result.argtypes = [vp, u32, ctypes.c_void_p, sz]
         L.mte_run_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(u64), ctypes.POINTER(u32)]
@@ -364,13 +367,15 @@ class Engine:
 
     def gather_summaries(self, rank=0, world=1, comm=None):
         """Every rank's summary records over RCCL (mte_gather_summaries), rank order. Collective."""
-        n = ctypes.c_size_t()
-        self._check(lib().mte_gather_summaries(self._h, rank, world, comm, None, 0, ctypes.byref(n)),
-                    "mte_gather_summaries")
-        out = np.zeros(n.value, dtype=SUMMARY_DTYPE)
-        self._check(lib().mte_gather_summaries(self._h, rank, world, comm, out.ctypes.data, n.value, ctypes.byref(n)),
-                    "mte_gather_summaries")
-        return out
+        # one collective call; the library allocates the records (mte_gather_summaries_alloc)
+        n, p = ctypes.c_size_t(), ctypes.c_void_p()
+        self._check(lib().mte_gather_summaries_alloc(self._h, rank, world, comm, ctypes.byref(p), ctypes.byref(n)),
+                    "mte_gather_summaries_alloc")
+        try:
+            raw = ctypes.string_at(p, n.value * SUMMARY_DTYPE.itemsize) if n.value else b""
+        finally:
+            lib().mte_free(p)
+        return np.frombuffer(raw, dtype=SUMMARY_DTYPE).copy()
 
     def rccl_comm(self, unique_id, rank, world):
         """RCCL communicator on this engine's device from a MTE_RCCL_ID_BYTES id (rank 0's)."""

@@ -312,6 +312,12 @@ int mte_rccl_comm_create(mte_engine* e, const uint8_t* id, int rank, int world, 
 void mte_rccl_comm_destroy(void* comm);
 int mte_gather_summaries(mte_engine* e, int rank, int world, void* rccl_comm, mte_doc_summary* out, size_t cap,
                          size_t* n);
+/* The same gather as ONE collective call: the records land in a buffer the library allocates
+ * (*out, *n records; release it with mte_free). A binding that sizes its own buffer from the result
+ * cannot leave the other ranks waiting in a second collective when its allocation fails. */
+int mte_gather_summaries_alloc(mte_engine* e, int rank, int world, void* rccl_comm, mte_doc_summary** out,
+                               size_t* n);
+void mte_free(void* p);
 
 /* Op-log ingestion: build a batch from per-doc JSON arrays of ISequencedDocumentMessage
  * (protocol.ts:126-166). The builder owns the memory. */

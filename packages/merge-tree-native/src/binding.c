@@ -549,14 +549,15 @@ static napi_value js_gather_summaries(napi_env env, napi_callback_info info) {
     void* comm = t == napi_external ? get_comm(env, argv[3]) : NULL;
     if (!e || world < 1 || rank < 0 || rank >= world || (world > 1 && !comm))
         return throw_mte(env, "gatherSummaries", -1, "expects an engine, 0 <= rank < world and a live communicator when world > 1");
+    /* one collective call (the library allocates): a failure below leaves no rank waiting */
+    mte_doc_summary* recs = NULL;
     size_t n = 0;
-    int rc = mte_gather_summaries(e, rank, world, comm, NULL, 0, &n);
-    if (rc) return throw_mte(env, "mte_gather_summaries", rc, mte_last_error(e));
-    void* data = NULL;
+    int rc = mte_gather_summaries_alloc(e, rank, world, comm, &recs, &n);
+    if (rc) return throw_mte(env, "mte_gather_summaries_alloc", rc, mte_last_error(e));
     napi_value buf;
-    CHECK(env, napi_create_buffer(env, n * sizeof(mte_doc_summary), &data, &buf));
-    rc = mte_gather_summaries(e, rank, world, comm, (mte_doc_summary*)data, n, &n);
-    if (rc) return throw_mte(env, "mte_gather_summaries", rc, mte_last_error(e));
+    napi_status st = napi_create_buffer_copy(env, n * sizeof(mte_doc_summary), recs, NULL, &buf);
+    mte_free(recs);
+    if (st != napi_ok) return throw_mte(env, "gatherSummaries", -1, "napi_create_buffer_copy");
     return buf;
 }
 

@@ -7,6 +7,17 @@ from collections import Counter
 
 NAMES = ["apply", "resolve", "insert_slot", "range", "zamboni", "scour", "heap", "find_seg", "map", "pack",
          "fetch", "lru", "text", "alloc", "ops", "total"]
+# row engine (reg_engine.hpp RgProf, markers 100 + slot)
+RG_NAMES = ["rg_total", "rg_fetch", "rg_apply", "rg_resolve", "rg_insert_slot", "rg_split", "rg_range", "rg_zamboni",
+            "rg_scour", "rg_heap", "rg_find_seg", "rg_pack", "rg_lru", "rg_ops", "rg_n_resolve", "rg_n_scour",
+            "rg_n_scour_changed", "rg_n_pack", "rg_n_pop", "rg_n_split_blk", "rg_n_move", "rg_split_at", "rg_ins",
+            "rg_rem", "rg_msn", "rg_zam_edit"]
+
+
+def name(s):
+    if s >= 100 and s - 100 < len(RG_NAMES):
+        return RG_NAMES[s - 100]
+    return NAMES[s] if s < len(NAMES) else str(s)
 path = sys.argv[1]
 kernel = sys.argv[2] if len(sys.argv) > 2 else "k_lds<false>"
 mangled = {"k_lds<false>": "_ZN3mte5k_ldsILb0ELi0EEEvNS_6ParamsE", "k_solo<false>": "_ZN3mte6k_soloILb0ELi0EEEvNS_6ParamsE", "k_hbmq<false>": "_ZN3mte6k_hbmqILb0ELi0EEEvNS_6ParamsE"}[kernel]
@@ -18,13 +29,13 @@ stack = []
 ins = re.compile(r"^\s+([sv]_|ds_|global_|scratch_|buffer_|flat_)([a-z0-9_]+)")
 total = 0
 for l in lines[start:end + 1]:
-    m = re.search(r"MTE_BEGIN (\d+)", l)
+    m = re.search(r"MTE_BEGIN (0x[0-9a-fA-F]+|\d+)", l)
     if m:
-        stack.append(int(m.group(1)))
+        stack.append(int(m.group(1), 0))
         continue
-    m = re.search(r"MTE_END (\d+)", l)
+    m = re.search(r"MTE_END (0x[0-9a-fA-F]+|\d+)", l)
     if m:
-        if stack and stack[-1] == int(m.group(1)):
+        if stack and stack[-1] == int(m.group(1), 0):
             stack.pop()
         continue
     if ins.match(l):
@@ -37,5 +48,5 @@ for l in lines[start:end + 1]:
 print(f"{kernel}: {total} instructions")
 for s in sorted(incl, key=lambda x: -incl[x]):
     k = kinds.get(s, Counter())
-    print(f"{NAMES[s] if s < len(NAMES) else str(s):12s} incl {incl[s]:6d} excl {excl[s]:6d}  "
+    print(f"{name(s):16s} incl {incl[s]:6d} excl {excl[s]:6d}  "
           + " ".join(f"{a}{b}" for a, b in sorted(k.items(), key=lambda x: -x[1])[:5]))

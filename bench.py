@@ -93,6 +93,18 @@ def host_cores():
     return avail, why
 
 
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), for the CPU baseline's record."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
@@ -166,11 +178,13 @@ def run(args):
     t_start = time.perf_counter()
     kms = []
     st = None
-    solo_steps = []
+    solo_steps, solo_clk = [], []
     for _ in range(args.steps):
         st = eng.replay()
         kms.append(st["kernel_ms"])
         solo_steps.append(eng.get_info("solo_us") / 1000.0)  # host-side read of the last pass's events
+        # the critical wave's s_memtime cycles and s_memrealtime (100 MHz) ticks over its replay
+        solo_clk.append((eng.get_info("solo_cycles"), eng.get_info("solo_ref_ticks")))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -257,7 +271,7 @@ def run(args):
         c_ops = replay_list(ctypes.addressof(batch), sample, threads=threads)
         dt = time.perf_counter() - c0
         log(f"cpu baseline sample: every {k}th doc ({len(sample)} docs), {c_ops} ops in {dt:.2f} s on {threads} threads")
-        cpu = {"value": c_ops / dt, "unit": "ops/s", "cores": threads, "kind": "port",
+        cpu = {"value": c_ops / dt, "unit": "ops/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
                "sample": f"oracle (tree-shaped C++ restatement of the reference path) replaying every {k}th "
                          f"document ({len(sample)} docs, {c_ops} ops, replay only, longest first) of the same "
                          f"{args.config} batch on {threads} threads, one per usable host core ({why}), in {dt:.2f} s"}
@@ -283,6 +297,10 @@ def run(args):
                       "solo_ms_last_step": info.get("solo_us", 0) / 1000.0,  # critical-path workgroups' pass
                       "kernel_ms_steps": [round(x, 1) for x in kms],
                       "solo_ms_steps": [round(x, 1) for x in solo_steps],
+                      # per step: the critical wave's shader cycles (G) and its clock (cycles / 100 MHz
+                      # reference ticks): a slow step with the same cycles ran at a lower clock
+                      "solo_gcycles_steps": [round(c / 1e9, 4) for c, _ in solo_clk],
+                      "solo_clock_ghz_steps": [round(c / (r / 100e6) / 1e9, 4) if r else None for c, r in solo_clk],
                       "lds_ms_last_step": info.get("lds_ms", 0.0), "hbm_ms_last_step": info.get("hbm_ms", 0.0),
                       "solo_lead_ms": info.get("solo_lead_us", 0) / 1000.0,  # pass start -> solo start
                       "solo_tail_ms": info.get("solo_tail_us", 0) / 1000.0,  # solo end -> pass end

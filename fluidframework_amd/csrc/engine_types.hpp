@@ -221,6 +221,8 @@ struct Params {
     u32* cell_pos;
     u32* cell_h;
     u32* htab;
+    u64* solo_clk;            // per solo workgroup: s_memtime / s_memrealtime at its replay's start and
+                              // end (4 u64): shader cycles vs the 100 MHz reference clock
 };
 
 // MTE_PROFILE builds: s_memtime cycles per engine phase, per document (engine.hpp PROF_*).

@@ -261,7 +261,8 @@ struct mte_engine {
     DevBuf<mte_propset> d_propsets;
     DevBuf<uint32_t> d_out_maps, d_prop_keys, d_prop_vals, d_val_flags, d_val_objidx, d_order, d_list, d_maps, d_counters,
         d_first_seen;
-    DevBuf<uint64_t> d_val_objmatch, d_ovl, d_out_ovl, d_prof;
+    DevBuf<uint64_t> d_val_objmatch, d_ovl, d_out_ovl, d_prof, d_solo_clk;
+    uint64_t last_solo_cycles = 0, last_solo_ref = 0;  // critical wave: s_memtime / s_memrealtime deltas
     // property maps of the documents the host re-ran (their worst-case table), by document
     DevBuf<uint32_t> d_maps_rr;
     std::vector<uint64_t> map_rr_off;  // UINT64_MAX = the document's maps are in d_maps
@@ -322,6 +323,8 @@ struct mte_engine {
     // SnapshotV1 emission on the device (emit.hip): property / name tables, scratch, and two output
     // pools -- round 0 (every document but the solo ones) runs while the critical path is still
     // replaying, round 1 (solo and host-re-run documents) after it
+    uint32_t rows_bulk = 0;   // option "rows_bulk": lean replays run the bulk on k_rows (4 or 8 waves per CU)
+    uint32_t last_rows = 0;   // waves per CU of the last pass's k_rows (0: k_lds / k_hbmq)
     bool emit_opt = true;     // option "emit"
     bool legacy = false;      // snapshot_format 1 (mte_config / option "snapshot_format"): SnapshotLegacy
     bool emitted_legacy = false;  // format of the last emission
@@ -523,6 +526,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     HIP_TRY(e, e->d_res.fit(nd));
     HIP_TRY(e, e->d_prof.fit((size_t)nd * PROF_SLOTS));
     HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, (size_t)nd * PROF_SLOTS * 8, e->stream));
+    HIP_TRY(e, e->d_solo_clk.fit(4 * 64));  // 4 u64 per solo workgroup (solo_max <= 64)
     // LPT order: longest documents start first
     e->order.resize(nd);
     for (uint32_t d = 0; d < nd; d++) e->order[d] = d;
@@ -548,6 +552,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     P.out_maps = any_props ? e->d_out_maps.p : nullptr;
     P.counters = e->d_counters.p;
     P.prof = e->d_prof.p;
+    P.solo_clk = e->d_solo_clk.p;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || cus <= 0) cus = 256;
     e->n_groups = (uint32_t)cus;
@@ -1072,12 +1077,16 @@ static int run_kernel(mte_engine* e, bool gen) {
     const int full = gen ? 1 : e->ext_needed ? 2 : (e->lean_ok && e->lean_opt) ? 0 : 1;
     e->last_lean = full == 0;
     wave_plan(e, nd, groups, hbm_waves, &lds_active, n_solo);
+    // lean replays may run the bulk on the row engine instead (k_rows; DOC_SPILL re-runs as below)
+    const uint32_t rows = (!gen && full == 0 && e->rows_bulk && !e->force_hbm && nd > n_solo) ? e->rows_bulk : 0;
+    e->last_rows = rows;
+    if (rows) groups = hbm_waves = lds_active = 0;
     e->P.slot_hbm0 = groups * LDS_WAVES;
     e->P.lds_active = lds_active;
     e->P.n_prio = 0;
     if (groups)  // critical-path documents lead the LPT order
         while (e->P.n_prio < nd && e->cfg[e->order[e->P.n_prio]].prio) e->P.n_prio++;
-    e->P.n_prio = std::max(e->P.n_prio, n_solo);  // k_lds / k_hbmq start after the solo documents
+    e->P.n_prio = std::max(e->P.n_prio, n_solo);  // k_lds / k_hbmq / k_rows start after the solo documents
     e->P.n_hslots = hbm_waves;
     // the streams of this pass (an A/B with CU-masked streams, hipExtStreamCreateWithCUMask, that kept
     // the solo workgroups' CUs to themselves measured the C4 pass 8 % SLOWER -- 9.07 s vs 8.38 s, the
@@ -1101,6 +1110,11 @@ static int run_kernel(mte_engine* e, bool gen) {
         HIP_TRY(e, hipEventRecord(e->ev3, s_solo));
     }
     if (groups) HIP_TRY(e, launch_lds(e->P, gen, full, groups, s_main));
+    if (rows) {
+        const uint32_t cus = e->n_groups > n_solo ? e->n_groups - n_solo : 1u;
+        const uint32_t per = rows >= 8 ? 8u : 4u;
+        HIP_TRY(e, launch_rows(e->P, per, std::min<uint32_t>(cus, (nd - n_solo + per - 1) / per), s_main));
+    }
     // k_hbmq: one workgroup (wave) per document; those that find the queue drained exit at once
     if (hbm_waves && !groups) {
         HIP_TRY(e, launch_hbmq(e->P, gen, full, nd, s_main));
@@ -1145,6 +1159,10 @@ static int run_kernel(mte_engine* e, bool gen) {
         if (hipEventElapsedTime(&sm, e->ev_s0, e->ev_s1) == hipSuccess) e->last_solo_ms = sm;
         if (hipEventElapsedTime(&sm, e->ev0, e->ev_s0) == hipSuccess) e->last_solo_lead_ms = sm;
         if (hipEventElapsedTime(&sm, e->ev_s1, e->ev1) == hipSuccess) e->last_solo_tail_ms = sm;
+        uint64_t clk[4] = {0, 0, 0, 0};  // solo workgroup 0: the batch's longest document
+        if (e->d_solo_clk.p) HIP_TRY(e, hipMemcpy(clk, e->d_solo_clk.p, sizeof clk, hipMemcpyDeviceToHost));
+        e->last_solo_cycles = clk[2] - clk[0];
+        e->last_solo_ref = clk[3] - clk[1];
     }
     e->last_spilled = (uint32_t)spill.size();
     if (!spill.empty()) {
@@ -2382,7 +2400,8 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "lean") e->lean_opt = value != 0;
     else if (k == "reg_solo") e->reg_solo = value != 0;
     else if (k == "reg_lb_limit") e->reg_lb_limit = (uint32_t)std::max<int64_t>(0, value);
-    else if (k == "emit") e->emit_opt = value != 0;  // SnapshotV1 emission on the device after replay
+    else if (k == "emit") e->emit_opt = value != 0;
+    else if (k == "rows_bulk") e->rows_bulk = value <= 0 ? 0u : value >= 8 ? 8u : 4u;  // SnapshotV1 emission on the device after replay
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
@@ -2402,11 +2421,14 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "solo") *value = e->last_solo;
     else if (k == "solo_us") *value = (int64_t)(e->last_solo_ms * 1000.0);  // the solo workgroups' pass (critical path)
     else if (k == "solo_lead_us") *value = (int64_t)(e->last_solo_lead_ms * 1000.0);
+    else if (k == "solo_cycles") *value = (int64_t)e->last_solo_cycles;  // longest document's wave: s_memtime
+    else if (k == "solo_ref_ticks") *value = (int64_t)e->last_solo_ref;  // ... and s_memrealtime (100 MHz)
     else if (k == "load_alloc_us") *value = (int64_t)(e->last_alloc_ms * 1000.0);
     else if (k == "load_stage_copy_us") *value = (int64_t)(e->stage_copy_ms * 1000.0);
     else if (k == "load_stage_wait_us") *value = (int64_t)(e->stage_wait_ms * 1000.0);
     else if (k == "solo_tail_us") *value = (int64_t)(e->last_solo_tail_ms * 1000.0);
     else if (k == "lean") *value = e->last_lean;
+    else if (k == "rows") *value = e->last_rows;  // k_rows waves per CU of the last pass (0: not used)
     else if (k == "emit_us") *value = (int64_t)(e->last_emit_ms * 1000.0);  // emission after the replay pass
     else if (k == "out_text") {  // UTF-16 units Engine::finish gathered (counters[6..7])
         uint32_t ctr[8] = {0, 0, 0, 0, 0, 0, 0, 0};

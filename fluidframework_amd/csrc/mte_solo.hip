@@ -28,6 +28,19 @@ MTE_DEV void solo_doc(const Params& p) {
     if (i >= p.n_solo) return;
     const u32 d = p.doc_list[i];
     __builtin_amdgcn_s_setprio(3);
+    // the critical wave's own clock: cycles (s_memtime) against the 100 MHz reference counter
+    // (s_memrealtime) over its replay tells a lower shader clock from extra cycles
+    const u64 c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    auto stamp = [&]() {
+        const u64 c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (p.solo_clk && lane_id() == 0) {
+            u64* o = p.solo_clk + 4 * (u64)i;
+            o[0] = c0;
+            o[1] = r0;
+            o[2] = c1;
+            o[3] = r1;
+        }
+    };
     Engine<true, true, LVL> e(p, d);
     e.bind_lds(0);
     GenState g;
@@ -42,6 +55,7 @@ MTE_DEV void solo_doc(const Params& p) {
             at = r.replay(at, p.docs[d].op_end);
             if (r.status != REG_HANDOFF) {
                 r.finish();
+                stamp();
                 __builtin_amdgcn_s_setprio(0);
                 return;
             }
@@ -74,6 +88,7 @@ MTE_DEV void solo_doc(const Params& p) {
     } else {
         e.finish();
     }
+    stamp();
     __builtin_amdgcn_s_setprio(0);
 }
 
@@ -90,6 +105,44 @@ __global__ __launch_bounds__(64 * SOLO_WAVES) __attribute__((amdgpu_waves_per_eu
 #else
     solo_doc<GEN, LVL>(p);
 #endif
+}
+
+// Bulk lean documents on the row engine (reg_engine.hpp): ROWS_WAVES single-SIMD waves per CU, each
+// owning a 1/ROWS_WAVES share of the CU's LDS for ROWS_NR slot rows (ROWS_NR * 8 leaf blocks) and its
+// SIMD's whole register file, replay one document after another from the LPT queue. A document that
+// outgrows the rows or reaches an op the row engine does not implement is re-run by the host,
+// HBM-resident, from its first op (DOC_SPILL).
+template <int RW, int NR>
+__global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4, RW / 4))) void k_rows(Params p) {
+    const u32 w = wave_first(threadIdx.x >> 6);
+    const u32 vb = w * (u32)NR * 64u * 32u, ab = vb + (u32)NR * 64u * 16u;
+    for (;;) {
+        u32 i = 0;
+        if (lane_id() == 0) i = p.n_prio + atomicAdd(&p.counters[0], 1u);
+        i = wave_read(i, 0);
+        if (i >= p.n_list) break;
+        const u32 d = p.doc_list[i];
+        RegEngine<NR> r(p, d, vb, ab, 5);
+        r.replay(p.docs[d].op_begin, p.docs[d].op_end);
+        if (r.status == REG_HANDOFF) r.mark_spilled();
+        else r.finish();
+    }
+}
+
+hipError_t launch_rows(const Params& p, u32 waves_per_cu, u32 n_groups, hipStream_t s) {
+    // 4 waves: 40 KiB of rows each (20 rows, 160 leaf blocks); 8 waves: 20 KiB (10 rows)
+    const void* k = waves_per_cu >= 8 ? (const void*)k_rows<8, 10> : (const void*)k_rows<4, 20>;
+    const u32 rw = waves_per_cu >= 8 ? 8u : 4u, nr = waves_per_cu >= 8 ? 10u : 20u;
+    const int lds = (int)(rw * nr * 64u * 32u);
+    static const hipError_t attr = [] {
+        hipError_t r = hipFuncSetAttribute((const void*)k_rows<4, 20>, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 20 * 64 * 32);
+        if (r == hipSuccess)
+            r = hipFuncSetAttribute((const void*)k_rows<8, 10>, hipFuncAttributeMaxDynamicSharedMemorySize, 8 * 10 * 64 * 32);
+        return r;
+    }();
+    if (attr != hipSuccess) return attr;
+    void* args[] = {(void*)&p};
+    return hipLaunchKernel(k, dim3(n_groups), dim3(64 * rw), args, (size_t)lds, s);
 }
 
 #define MTE_PICK(K, gen, lvl)                                                                           \

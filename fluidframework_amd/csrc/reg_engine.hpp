@@ -133,7 +133,38 @@ struct RegEngine {
 
     // ---------------------------------------------------------------- state
     simd::VA<RG_LEVELS> LV;  // LV[i] lane j: child count of node j of level i+1 (0 beyond the last)
-    simd::VA<8> HK, HS;      // heap keys (maxSeq) / segment ids, position q at lane q&63 of reg q>>6
+    // Heap positions q at lane q&63 of register q>>6. Registers 0 and 1 (positions 1..127, every pop
+    // of a heap that size) are plain values; 2..7 an indexed array touched only by larger heaps (one
+    // 8-register array made every pop copy all eight registers at its merge points).
+    struct HeapRegs {
+        V r0, r1, x2, x3, x4, x5, x6, x7;  // named registers: no access is ever indexed at run time
+        SD V get(u32 i) const {
+            switch (i) {
+                case 0: return r0;
+                case 1: return r1;
+                case 2: return x2;
+                case 3: return x3;
+                case 4: return x4;
+                case 5: return x5;
+                case 6: return x6;
+                default: return x7;
+            }
+        }
+        SD void set(u32 i, V v) {
+            switch (i) {
+                case 0: r0 = v; break;
+                case 1: r1 = v; break;
+                case 2: x2 = v; break;
+                case 3: x3 = v; break;
+                case 4: x4 = v; break;
+                case 5: x5 = v; break;
+                case 6: x6 = v; break;
+                default: x7 = v; break;
+            }
+        }
+        SD void zero() { r0 = r1 = x2 = x3 = x4 = x5 = x6 = x7 = simd::splat(0); }
+    };
+    HeapRegs HK, HS;         // heap keys (maxSeq) / segment ids
     u32 n_lb, height, heapSize, segNext, arenaTop, arenaSel;
     i32 minSeq, curSeq, heapTop, status, failSeq;
     u32 n_ops, n_msgs, n_gc, max_lb;
@@ -191,8 +222,11 @@ struct RegEngine {
         memset(mem_aux[at], 0, (size_t)n * 16);
     }
 #else
-    SD static uint4* VISP() { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + offsetof(SoloPlan, vis)); }
-    SD static uint4* AUXP() { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + offsetof(SoloPlan, aux)); }
+    // the rows' two LDS arrays (byte offsets into the dynamic LDS): the SoloPlan's slot arrays for
+    // k_solo (so the LDS engine finds them in place after a handoff), a per-wave share for k_rows
+    u32 vbase = (u32)offsetof(SoloPlan, vis), abase = (u32)offsetof(SoloPlan, aux);
+    SD uint4* VISP() const { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + vbase); }
+    SD uint4* AUXP() const { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + abase); }
     SD Row ldrow(u32 r) const {
         const u32 i = r * 64 + __lane_id();
         const uint4 v = VISP()[i], a = AUXP()[i];
@@ -213,60 +247,80 @@ struct RegEngine {
         if (simd::lane_of(m)) b[(r * 64 + __lane_id()) * 4 + c] = x.x;
         simd::lds_order();
     }
-    // Overlapping slot move in the safe direction, eight 64-slot chunks per round: all sixteen
-    // ds_read_b128 of a round are issued before its first write, so a round costs one LDS latency
-    // (the chunks of one round never overlap the slots a later round reads).
+#ifdef MTE_OLD_MEMMOVE  // A/B: one 64-slot chunk per LDS round trip
     SD void mv_slots(u32 dst, u32 src, u32 n) {
         cr = NONE;
         uint4* V4 = VISP();
         uint4* A4 = AUXP();
-        const i32 L = (i32)__lane_id();
+        const u32 L = __lane_id();
         if (dst > src) {
-            for (i32 top = (i32)n; top > 0; top -= 512) {
-                uint4 v[8], a[8];
-#pragma unroll
-                for (int c = 0; c < 8; c++) {
-                    const i32 i = top - 64 * (c + 1) + L;
-                    if (top - 64 * c > 0 && i >= 0) {
-                        v[c] = V4[src + (u32)i];
-                        a[c] = A4[src + (u32)i];
-                    }
+            for (i32 b = (i32)n - 64; b > -64; b -= 64) {
+                const i32 i = b + (i32)L;
+                uint4 v = make_uint4(0, 0, 0, 0), a = v;
+                if (i >= 0) {
+                    v = V4[src + (u32)i];
+                    a = A4[src + (u32)i];
                 }
                 simd::lds_order();
-#pragma unroll
-                for (int c = 0; c < 8; c++) {
-                    const i32 i = top - 64 * (c + 1) + L;
-                    if (top - 64 * c > 0 && i >= 0) {
-                        V4[dst + (u32)i] = v[c];
-                        A4[dst + (u32)i] = a[c];
-                    }
+                if (i >= 0) {
+                    V4[dst + (u32)i] = v;
+                    A4[dst + (u32)i] = a;
                 }
                 simd::lds_order();
             }
         } else {
-            for (i32 b0 = 0; b0 < (i32)n; b0 += 512) {
-                uint4 v[8], a[8];
-#pragma unroll
-                for (int c = 0; c < 8; c++) {
-                    const i32 i = b0 + 64 * c + L;
-                    if (b0 + 64 * c < (i32)n && i < (i32)n) {
-                        v[c] = V4[src + (u32)i];
-                        a[c] = A4[src + (u32)i];
-                    }
+            for (u32 b = 0; b < n; b += 64) {
+                const u32 i = b + L;
+                uint4 v = make_uint4(0, 0, 0, 0), a = v;
+                if (i < n) {
+                    v = V4[src + i];
+                    a = A4[src + i];
                 }
                 simd::lds_order();
-#pragma unroll
-                for (int c = 0; c < 8; c++) {
-                    const i32 i = b0 + 64 * c + L;
-                    if (b0 + 64 * c < (i32)n && i < (i32)n) {
-                        V4[dst + (u32)i] = v[c];
-                        A4[dst + (u32)i] = a[c];
-                    }
+                if (i < n) {
+                    V4[dst + i] = v;
+                    A4[dst + i] = a;
                 }
                 simd::lds_order();
             }
         }
     }
+#else
+    // Overlapping slot move in the safe direction, eight 64-slot chunks per round: all sixteen
+    // ds_read_b128 of a round are issued before its first write, so a round costs one LDS latency
+    // (the chunks of one round never overlap the slots a later round reads). Chunk c of a round
+    // covers slot indices base(c) + lane; the chunks are named registers (an array of them went to
+    // the scratch stack).
+    SD void mv_slots(u32 dst, u32 src, u32 n) {
+        cr = NONE;
+        uint4* V4 = VISP();
+        uint4* A4 = AUXP();
+        const i32 L = (i32)__lane_id(), N = (i32)n;
+        const bool fwd = dst > src;  // moving up: rounds from the top down, chunks downwards
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (i32 r0 = 0; r0 < N; r0 += 512) {
+            auto at = [&](i32 c) MTE_LI { return fwd ? N - r0 - 64 * (c + 1) + L : r0 + 64 * c + L; };
+            auto ok = [&](i32 c) MTE_LI { const i32 i = at(c); return r0 + 64 * c < N && i >= 0 && i < N; };
+#define MTE_MV_LD(c)                         \
+    uint4 v##c = z, a##c = z;                \
+    if (ok(c)) {                             \
+        v##c = V4[src + (u32)at(c)];         \
+        a##c = A4[src + (u32)at(c)];         \
+    }
+#define MTE_MV_ST(c)                         \
+    if (ok(c)) {                             \
+        V4[dst + (u32)at(c)] = v##c;         \
+        A4[dst + (u32)at(c)] = a##c;         \
+    }
+            MTE_MV_LD(0) MTE_MV_LD(1) MTE_MV_LD(2) MTE_MV_LD(3) MTE_MV_LD(4) MTE_MV_LD(5) MTE_MV_LD(6) MTE_MV_LD(7)
+            simd::lds_order();
+            MTE_MV_ST(0) MTE_MV_ST(1) MTE_MV_ST(2) MTE_MV_ST(3) MTE_MV_ST(4) MTE_MV_ST(5) MTE_MV_ST(6) MTE_MV_ST(7)
+            simd::lds_order();
+#undef MTE_MV_LD
+#undef MTE_MV_ST
+        }
+    }
+#endif
     SD void zero_slots(u32 at, u32 n) {
         cr = NONE;
         for (u32 b = __lane_id(); b < n; b += 64) {
@@ -296,8 +350,29 @@ struct RegEngine {
         cw = w;
         cr = r;
     }
+    // the cached row itself, for edits in place (no working copy of its eight registers); pair with
+    // writeback(r) before anything else touches the cache
+    SD Row& rowref(u32 r) {
+        if (r != cr) {
+            cw = ldrow(r);
+            cr = r;
+        }
+        return cw;
+    }
+    SD void writeback(u32 r) { strow(r, cw); }
 
-    SD RegEngine(const Params& p_, u32 doc_) : p(p_), doc(doc_) {
+    SD RegEngine(const Params& p_, u32 doc_) : p(p_), doc(doc_) { setup(); }
+#ifndef MTE_CPU
+    // rows in another LDS region (k_rows: one share of the CU's LDS per wave)
+    SD RegEngine(const Params& p_, u32 doc_, u32 vb, u32 ab, u32 mode) : p(p_), doc(doc_) {
+        vbase = vb;
+        abase = ab;
+        res_mode = mode;
+        setup();
+    }
+#endif
+    u32 res_mode = 4;  // DocRes::mode of a document this engine finishes (4: k_solo, 5: k_rows)
+    SD void setup() {
         const DocCfg& c = p.docs[doc];
         payload = p.payload + c.payload_off;
         arena0 = p.arena + c.arena_off;
@@ -353,9 +428,8 @@ struct RegEngine {
     SD u32 count(u32 k) { return count_in(row(k >> 3), k); }
     SD u32 ns_get(u32 k) { return ns_in(row(k >> 3), k); }
     SD void ns_set(u32 k, u32 sc) {
-        Row w = row(k >> 3);
-        ns_put(w, k, sc);
-        putrow(k >> 3, w);
+        ns_put(rowref(k >> 3), k, sc);
+        writeback(k >> 3);
     }
 
     // nodeLength of every slot of a row for (refSeq R, client C) (mergeTree.ts:1659-1699):
@@ -510,7 +584,7 @@ struct RegEngine {
             return NONE;
         }
         const u32 r = k >> 3, gb = gbase(k);
-        Row w = row(r);
+        Row& w = rowref(r);
         const V sl = L() & 7u;
         const B ing = in_group(k);
         const B mv = ing & (sl > j);
@@ -533,7 +607,7 @@ struct RegEngine {
         put(w.cap, rec.cap);
         put(w.rm, rec.rm);
         put(w.sid, rec.sid);
-        putrow(r, w);
+        writeback(r);
         if (cnt + 1 < 8) return k;
         split_block(k);
         return j < 4 ? k : k + 1;
@@ -592,7 +666,7 @@ struct RegEngine {
     // registers statically (level d <= 5: register 0; 6: 1; 7: 2..3; 8: 4..7): a VA indexed by a
     // run-time register number compiles to a v_cndmask chain over all eight registers per access.
     template <int D>
-    SD static u32 hrd(const simd::VA<8>& A, u32 q) {
+    SD static u32 hrd(const HeapRegs& A, u32 q) {
         const u32 l = q & 63u;
         if constexpr (D <= 5) {
             return simd::readlane(A.get(0), l);
@@ -609,7 +683,7 @@ struct RegEngine {
         }
     }
     template <int D>
-    SD static void hwr(simd::VA<8>& A, u32 q, u32 v) {
+    SD static void hwr(HeapRegs& A, u32 q, u32 v) {
         const u32 l = q & 63u;
         if constexpr (D <= 5) {
             A.set(0, simd::writelane(A.get(0), l, v));
@@ -706,12 +780,31 @@ struct RegEngine {
         const V nxt = simd::sel(go, c, 0u);
         u32 k = 1;
         u64 path = 0;  // nodes of register 0 that take their child's entry
+#ifdef MTE_OLD_PATH
         while (k < 64u) {
             const u32 nk = simd::readlane(nxt, k);
             if (!nk) break;
             path |= 1ull << k;
             k = nk;
         }
+#else
+        // E bit k: node k's parent moves down into k (its chosen, taken child). The path from the
+        // root follows E in scalar registers, two bits per level.
+        const u64 E = simd::ballot(simd::bperm(nxt, L() >> 1) == L()) & ~3ull;
+        while (k < 32u) {
+            const u32 two = (u32)(E >> (2 * k)) & 3u;
+            if (!two) break;
+            path |= 1ull << k;
+            k = 2 * k + (two >> 1);
+        }
+        if (k >= 32u && k < 64u) {  // the last level of register 0 may continue into register 1
+            const u32 nk = simd::readlane(nxt, k);
+            if (nk) {
+                path |= 1ull << k;
+                k = nk;
+            }
+        }
+#endif
         const B mv = simd::ballot_mask(path);
         const V sc = simd::sel(c < 64u, simd::bperm(S0, c & 63u), simd::bperm(S1, c & 63u));
         V N0 = simd::sel(mv, kc, K0), T0 = simd::sel(mv, sc, S0);
@@ -1333,7 +1426,7 @@ struct RegEngine {
         u32 carry = c1;
         const u32 cbit = 1u << C;
         for (u32 r = r1; r < nrows && (i32)carry < p2; r++) {
-            Row w = row(r);
+            Row& w = rowref(r);
             const V v = vis(w, R, C);
             const V incl = simd::scan_incl(v) + carry;
             const V ex = incl - v;
@@ -1346,7 +1439,7 @@ struct RegEngine {
             w.rm = simd::sel(mark, w.rm | cbit, w.rm);
             w.meta = simd::sel(was, w.meta | F_OVL, simd::sel(fresh, (w.meta & ~0xFF00u) | (C << 8) | F_REMOVED, w.meta));
             w.rseq = simd::sel(fresh, (u32)seq, w.rseq);
-            putrow(r, w);
+            writeback(r);
             // addToLRUSet per block, document order: the first marked slot of each block
             for (u64 gm = mm; gm;) {
                 const u32 l = (u32)__builtin_ctzll(gm);
@@ -1504,6 +1597,23 @@ struct RegEngine {
         return ((u64)hi << 32) | lo;
 #endif
     }
+    // the document leaves this engine unfinished (k_rows has no LDS plan to hand it to): the host
+    // re-runs it HBM-resident from its first op (engine.hpp mark_spilled)
+    SD void mark_spilled() {
+        fence_arena();
+        if (simd::lane0()) {
+            DocRes& o = p.res[doc];
+            o.status = DOC_SPILL;
+            o.failing_seq = curSeq;
+            o.n_segs = 0;
+            o.max_lb = max_lb;
+            o.mode = 0;
+            o.spill_why = (n_lb << 8) | (heapSize << 20);
+#ifndef MTE_CPU
+            atomicAdd(&p.counters[2], 1u);
+#endif
+        }
+    }
     SD void finish() {
         fence_arena();
         const u32 nrows = (n_lb + 7) >> 3;
@@ -1587,7 +1697,7 @@ struct RegEngine {
             o.text_off = toff;
             o.max_lb = max_lb;
             o.cu_n = 0;
-            o.mode = 4;  // solo, row-vectorised engine
+            o.mode = res_mode;  // row-vectorised engine: 4 on k_solo, 5 on k_rows
             o.spill_why = 0;
         }
 #if defined(MTE_PROFILE) && !defined(MTE_CPU)

@@ -42,6 +42,25 @@ def test_scaled_c4_zipf_batch_matches_oracle(engine):
     assert s["doc_id"].tolist() == ids.tolist()  # summary records carry the global ids
 
 
+def test_full_c4_batch_matches_oracle(engine):
+    """The headline configuration at its own size (BASELINE.json config 4, north_star's "bit-exact
+    SnapshotV1 output for 256k synthetic documents"): 262 144 Zipf documents, 268.6 M ops, the
+    10^6-op head on the solo route -- every document's status and checksum (text + SnapshotV1 blobs)
+    against the oracle on 16 threads, and the head's full segment table, text and SnapshotV1 ITree."""
+    ids, counts = plan_shard("C4", 1, 0, 262_144, 0)
+    engine.generate(2, len(ids), 0, n_clients=8, seed=1000, ops_per_doc=counts, doc_ids=ids)
+    batch = engine.export_batch()
+    st = engine.replay()
+    assert st["failed_docs"] == 0 and st["ops"] == int(counts.sum())
+    head = engine.doc_result(0)
+    assert head["ops"] == 1_000_000 and head["mode"] == 4, head
+    bad, ops, _ = compare_batch_checksums(engine, batch, threads=16)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad and ops == int(counts.sum())
+    compare_doc(engine, batch, 0)
+
+
 def test_lone_long_document_solo_matches_oracle(engine):
     """A lone 200k-op document (the C4 critical path at 1/5 scale) replays on the solo plan."""
     engine.generate(2, 1, 200_000, n_clients=8, seed=1000)

@@ -45,3 +45,19 @@ def test_c5_long_history_document(engine):
     bad, ops, _ = compare_batch_checksums(engine, batch, threads=1)
     assert not bad and ops == 1_000_000
     compare_doc(engine, batch, 0)
+
+
+def test_c2_full_batch(engine):
+    """C2 itself (BASELINE.json config 2): 4 096 documents x 10 000 insert/remove ops, 8 writers --
+    every document's status and checksum (text + SnapshotV1 blobs) against the oracle, and the full
+    segment table / snapshot of four documents."""
+    engine.generate(2, 4096, 10000, n_clients=8, seed=1000)
+    batch = engine.export_batch()
+    st = engine.replay()
+    assert st["failed_docs"] == 0
+    bad, ops, _ = compare_batch_checksums(engine, batch)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad and ops == 4096 * 10000
+    for d in (0, 1365, 2730, 4095):
+        compare_doc(engine, batch, d)

@@ -117,3 +117,39 @@ def test_row_engine_markers_and_builder_logs(engine):
     assert engine.run_info()["lean"] == 1
     assert engine.doc_result(0)["mode"] == MODE_ROWS
     compare_doc(engine, batch, 0)
+
+
+MODE_BULK_ROWS = 5  # DocRes.mode: k_rows (bulk documents on the row engine)
+
+
+@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("kind", [2, 5])
+def test_bulk_rows_kernel_matches_oracle(engine, kind, waves):
+    """Lean bulk documents on k_rows (4 or 8 single-document waves per CU, rows in a share of the
+    LDS): a Zipf mix whose longest document stays on k_solo, every other one on the rows, checksums
+    against the oracle; then 31-writer documents that outgrow the rows and are re-run HBM-resident."""
+    from fluidframework_amd.shard import zipf_op_counts
+
+    engine.set_option("reg_lb_limit", 0)
+    engine.set_option("rows_bulk", waves)
+    try:
+        counts = zipf_op_counts(3000, seed=kind + waves, lo=50, hi=60_000)
+        engine.generate(kind, len(counts), 0, n_clients=8, seed=29, ops_per_doc=counts)
+        batch = engine.export_batch()
+        st = engine.replay()
+        assert st["failed_docs"] == 0 and engine.get_info("rows") == waves
+        modes = [engine.doc_result(d)["mode"] for d in range(len(counts))]
+        assert modes.count(MODE_BULK_ROWS) >= len(counts) - 16, sorted(set(modes))
+        _check(engine, batch, n_docs=len(counts))
+        # documents that outgrow the rows (reg_lb_limit shrinks them) go back to the host, which
+        # re-runs them HBM-resident from their first op
+        engine.set_option("reg_lb_limit", 24)
+        engine.generate(kind, 64, 6000, n_clients=8, seed=31)
+        batch = engine.export_batch()
+        st = engine.replay()
+        assert st["failed_docs"] == 0
+        assert engine.run_info()["spilled"] > 0
+        _check(engine, batch, n_docs=64)
+    finally:
+        engine.set_option("rows_bulk", 0)
+        engine.set_option("reg_lb_limit", 0)

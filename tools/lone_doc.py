@@ -39,6 +39,12 @@ def main():
         st = e.replay()
         res[f"kernel_ms_{r}"] = st["kernel_ms"]
     res["us_per_op"] = res[f"kernel_ms_{a.reps - 1}"] * 1e3 / a.ops
+    try:  # the critical wave's clock stamps (libraries from before them lack the keys)
+        cyc, ref = e.get_info("solo_cycles"), e.get_info("solo_ref_ticks")
+        res["solo_cycles_per_op"] = cyc / a.ops
+        res["solo_clock_ghz"] = cyc / (ref / 100e6) / 1e9 if ref else None
+    except mte.MteError:
+        pass
     res["run_info"] = e.run_info()
     res["doc0"] = e.doc_result(0)
     if os.environ.get("MTE_LIB", "").startswith(("prof", "po_", "rp_")):

@@ -184,7 +184,8 @@ def run(args):
         kms.append(st["kernel_ms"])
         solo_steps.append(eng.get_info("solo_us") / 1000.0)  # host-side read of the last pass's events
         # the critical wave's s_memtime cycles and s_memrealtime (100 MHz) ticks over its replay
-        solo_clk.append((eng.get_info("solo_cycles"), eng.get_info("solo_ref_ticks")))
+        solo_clk.append((eng.get_info("solo_cycles"), eng.get_info("solo_ref_ticks"),
+                         eng.get_info("solo_start_delay_ticks")))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -299,8 +300,10 @@ def run(args):
                       "solo_ms_steps": [round(x, 1) for x in solo_steps],
                       # per step: the critical wave's shader cycles (G) and its clock (cycles / 100 MHz
                       # reference ticks): a slow step with the same cycles ran at a lower clock
-                      "solo_gcycles_steps": [round(c / 1e9, 4) for c, _ in solo_clk],
-                      "solo_clock_ghz_steps": [round(c / (r / 100e6) / 1e9, 4) if r else None for c, r in solo_clk],
+                      "solo_gcycles_steps": [round(c / 1e9, 4) for c, _, _ in solo_clk],
+                      "solo_clock_ghz_steps": [round(c / (r / 100e6) / 1e9, 4) if r else None for c, r, _ in solo_clk],
+                      # the critical wave's start after the bulk kernel's first wave (ms, 100 MHz clock)
+                      "solo_start_delay_ms_steps": [round(dl / 1e5, 3) for _, _, dl in solo_clk],
                       "lds_ms_last_step": info.get("lds_ms", 0.0), "hbm_ms_last_step": info.get("hbm_ms", 0.0),
                       "solo_lead_ms": info.get("solo_lead_us", 0) / 1000.0,  # pass start -> solo start
                       "solo_tail_ms": info.get("solo_tail_us", 0) / 1000.0,  # solo end -> pass end

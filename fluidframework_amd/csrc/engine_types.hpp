@@ -222,8 +222,11 @@ struct Params {
     u32* cell_h;
     u32* htab;
     u64* solo_clk;            // per solo workgroup: s_memtime / s_memrealtime at its replay's start and
-                              // end (4 u64): shader cycles vs the 100 MHz reference clock
+                              // end (4 u64): shader cycles vs the 100 MHz reference clock; then, at
+                              // [4 * SOLO_CLK_SLOTS], the bulk kernel's start (s_memrealtime)
 };
+
+constexpr u32 SOLO_CLK_SLOTS = 64;  // solo workgroups with clock stamps (Params::solo_clk)
 
 // MTE_PROFILE builds: s_memtime cycles per engine phase, per document (engine.hpp PROF_*).
 constexpr u32 PROF_SLOTS = 40;

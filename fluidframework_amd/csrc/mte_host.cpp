@@ -263,6 +263,8 @@ struct mte_engine {
         d_first_seen;
     DevBuf<uint64_t> d_val_objmatch, d_ovl, d_out_ovl, d_prof, d_solo_clk;
     uint64_t last_solo_cycles = 0, last_solo_ref = 0;  // critical wave: s_memtime / s_memrealtime deltas
+    double last_cell_pass_ms = 0;                       // a SharedMatrix batch's first (positions) pass
+    int64_t last_solo_start_delay = 0;                  // critical wave's start - the bulk's (100 MHz ticks)
     // property maps of the documents the host re-ran (their worst-case table), by document
     DevBuf<uint32_t> d_maps_rr;
     std::vector<uint64_t> map_rr_off;  // UINT64_MAX = the document's maps are in d_maps
@@ -324,6 +326,7 @@ struct mte_engine {
     // pools -- round 0 (every document but the solo ones) runs while the critical path is still
     // replaying, round 1 (solo and host-re-run documents) after it
     uint32_t rows_bulk = 0;   // option "rows_bulk": lean replays run the bulk on k_rows (4 or 8 waves per CU)
+    bool xcd_align = true;    // option "xcd_align": bulk grids leave solo CUs free in every XCD (bulk_cus)
     uint32_t last_rows = 0;   // waves per CU of the last pass's k_rows (0: k_lds / k_hbmq)
     bool emit_opt = true;     // option "emit"
     bool legacy = false;      // snapshot_format 1 (mte_config / option "snapshot_format"): SnapshotLegacy
@@ -526,7 +529,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     HIP_TRY(e, e->d_res.fit(nd));
     HIP_TRY(e, e->d_prof.fit((size_t)nd * PROF_SLOTS));
     HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, (size_t)nd * PROF_SLOTS * 8, e->stream));
-    HIP_TRY(e, e->d_solo_clk.fit(4 * 64));  // 4 u64 per solo workgroup (solo_max <= 64)
+    HIP_TRY(e, e->d_solo_clk.fit(4 * SOLO_CLK_SLOTS + 1));  // 4 u64 per solo workgroup + the bulk's start
     // LPT order: longest documents start first
     e->order.resize(nd);
     for (uint32_t d = 0; d < nd; d++) e->order[d] = d;
@@ -573,9 +576,21 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
 // HBM-resident waves at a time (k_hbmq, one document per wave, H slots), or HBM-resident waves
 // alone when the LDS plan is off or the slots for its waves do not fit the budget. Every LDS wave
 // owns a slot for a document that outgrows the plan.
+// CUs left to the bulk beside n_solo solo workgroups. Workgroups are handed to the 8 XCDs in turn,
+// so a grid that is not a multiple of 8 fills some XCDs' CUs completely: a solo workgroup dispatched
+// to such an XCD waits for a bulk workgroup to finish -- a whole bulk pass, ~1.1 s, on every other
+// C4 step (the critical wave's own cycles and clock were the same in slow and fast steps, BENCH_r03
+// and profiles/r04_c4_steps.json). Leaving ceil(n_solo / 8) CUs free in EVERY XCD keeps each one's
+// share of the bulk at most its CUs minus its solo workgroups, whatever XCD the first one lands on.
+static uint32_t bulk_cus(const mte_engine* e, uint32_t n_solo) {
+    constexpr uint32_t XCDS = 8;  // MI355X (gfx950)
+    const uint32_t keep = !e->xcd_align ? n_solo : n_solo ? XCDS * ((n_solo + XCDS - 1) / XCDS) : 0u;
+    return e->n_groups > keep ? e->n_groups - keep : 1u;
+}
+
 static void wave_plan(const mte_engine* e, uint32_t nd, uint32_t& groups, uint32_t& hbm_waves,
                       uint32_t* lds_active = nullptr, uint32_t n_solo = 0) {
-    const uint32_t cus = e->n_groups > n_solo ? e->n_groups - n_solo : 1u;  // k_solo holds n_solo CUs
+    const uint32_t cus = bulk_cus(e, n_solo);  // k_solo holds n_solo CUs
     nd -= std::min(nd, n_solo);
     const uint64_t max_slots = std::max<uint64_t>(1, e->slot_budget / std::max<uint64_t>(e->P.slot_bytes, 1));
     // fewer documents than LDS waves: every CU still gets a workgroup, with fewer active waves
@@ -1059,7 +1074,9 @@ static int emit_list(mte_engine* e, int k, const std::vector<uint32_t>& list, hi
 
 static int run_kernel(mte_engine* e, bool gen) {
     HIP_TRY(e, hipSetDevice(e->device));
-    const uint32_t nd = e->P.n_docs;
+    // nd: the documents this pass replays (e->order, LPT; a SharedMatrix batch's first pass runs
+    // only its cell documents), nall: the batch's documents (results are indexed by document)
+    const uint32_t nd = (uint32_t)e->order.size(), nall = e->P.n_docs;
     e->P.pool_limit = e->pool_limit;
     e->P.reg_solo = e->reg_solo;
     e->P.reg_lb_limit = e->reg_lb_limit;
@@ -1111,7 +1128,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     }
     if (groups) HIP_TRY(e, launch_lds(e->P, gen, full, groups, s_main));
     if (rows) {
-        const uint32_t cus = e->n_groups > n_solo ? e->n_groups - n_solo : 1u;
+        const uint32_t cus = bulk_cus(e, n_solo);
         const uint32_t per = rows >= 8 ? 8u : 4u;
         HIP_TRY(e, launch_rows(e->P, per, std::min<uint32_t>(cus, (nd - n_solo + per - 1) / per), s_main));
     }
@@ -1127,7 +1144,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     const bool emit = !gen && e->emit_opt;
     e->emitted_legacy = e->legacy;
     e->emit_downloaded = false;
-    e->emit_pool_of.assign(nd, 255);
+    e->emit_pool_of.assign(nall, 255);
     e->pool[0].used = e->pool[0].blobs = e->pool[1].used = e->pool[1].blobs = 0;
     int erc;
     if (emit) {
@@ -1141,15 +1158,15 @@ static int run_kernel(mte_engine* e, bool gen) {
     HIP_TRY(e, hipEventRecord(e->ev1, s_main));
     HIP_TRY(e, hipStreamSynchronize(s_main));
     HIP_TRY(e, hipEventElapsedTime(&lds_ms, e->ev0, e->ev1));
-    e->res.resize(nd);
-    HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nd * sizeof(DocRes), hipMemcpyDeviceToHost));
+    e->res.resize(nall);
+    HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nall * sizeof(DocRes), hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < nd; i++)
         if (e->res[e->order[i]].status == DOC_SPILL) spill.push_back(e->order[i]);
     uint32_t ctr[8];
     HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
     e->last_continued = ctr[4];
     e->last_hbm_docs = 0;
-    for (uint32_t i = 0; i < nd; i++) e->last_hbm_docs += e->res[i].mode == 1;
+    for (uint32_t i = 0; i < nd; i++) e->last_hbm_docs += e->res[e->order[i]].mode == 1;
     e->last_hbm_waves = hbm_waves;
     e->last_lds_groups = groups;
     e->last_solo = n_solo;
@@ -1159,10 +1176,15 @@ static int run_kernel(mte_engine* e, bool gen) {
         if (hipEventElapsedTime(&sm, e->ev_s0, e->ev_s1) == hipSuccess) e->last_solo_ms = sm;
         if (hipEventElapsedTime(&sm, e->ev0, e->ev_s0) == hipSuccess) e->last_solo_lead_ms = sm;
         if (hipEventElapsedTime(&sm, e->ev_s1, e->ev1) == hipSuccess) e->last_solo_tail_ms = sm;
-        uint64_t clk[4] = {0, 0, 0, 0};  // solo workgroup 0: the batch's longest document
-        if (e->d_solo_clk.p) HIP_TRY(e, hipMemcpy(clk, e->d_solo_clk.p, sizeof clk, hipMemcpyDeviceToHost));
+        uint64_t clk[4] = {0, 0, 0, 0}, bulk0 = 0;  // solo workgroup 0: the batch's longest document
+        if (e->d_solo_clk.p) {
+            HIP_TRY(e, hipMemcpy(clk, e->d_solo_clk.p, sizeof clk, hipMemcpyDeviceToHost));
+            HIP_TRY(e, hipMemcpy(&bulk0, e->d_solo_clk.p + 4 * SOLO_CLK_SLOTS, 8, hipMemcpyDeviceToHost));
+        }
         e->last_solo_cycles = clk[2] - clk[0];
         e->last_solo_ref = clk[3] - clk[1];
+        // the critical wave's start after the bulk's first wave (100 MHz ticks; negative: before it)
+        e->last_solo_start_delay = (groups || rows) && bulk0 ? (int64_t)(clk[1] - bulk0) : 0;
     }
     e->last_spilled = (uint32_t)spill.size();
     if (!spill.empty()) {
@@ -1180,8 +1202,8 @@ static int run_kernel(mte_engine* e, bool gen) {
         // its own (e->map_rr_off; the first pass's layout stays as it was)
         std::vector<std::pair<uint64_t, uint32_t>> keep_maps;
         uint64_t mtot = 0;
-        e->map_rr_off.assign(nd, UINT64_MAX);
-        e->map_rr_cap.assign(nd, 0);
+        e->map_rr_off.assign(nall, UINT64_MAX);
+        e->map_rr_cap.assign(nall, 0);
         for (uint32_t d : spill) {
             DocCfg& c = e->cfg[d];
             uint64_t cap = 16;
@@ -1191,9 +1213,14 @@ static int run_kernel(mte_engine* e, bool gen) {
                 std::vector<mte_op> ops(c.op_end - c.op_begin);
                 if (!ops.empty())
                     HIP_TRY(e, hipMemcpy(ops.data(), e->d_ops.p + c.op_begin, ops.size() * sizeof(mte_op), hipMemcpyDeviceToHost));
+                // a relative-position annotate can touch every segment of the document: bound it by
+                // the longest the document can get, its payload plus one unit per marker insert
+                uint64_t markers = 0;
+                for (const mte_op& o : ops) markers += o.type == MTE_OP_INSERT_MARKER;
                 for (const mte_op& o : ops) {
                     if (o.type == MTE_OP_ANNOTATE)
-                        cap += (o.flags & MTE_F_REL) ? (uint64_t)c.payload_len + 2 : (uint64_t)std::max<int64_t>(0, (int64_t)o.a - o.pos1) + 2;
+                        cap += (o.flags & MTE_F_REL) ? (uint64_t)c.payload_len + markers + 2
+                                                     : (uint64_t)std::max<int64_t>(0, (int64_t)o.a - o.pos1) + 2;
                     else if (o.props)
                         cap += 1;
                 }
@@ -1245,8 +1272,8 @@ static int run_kernel(mte_engine* e, bool gen) {
         HIP_TRY(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
         e->last_emit_ms = ms;
     }
-    e->res.resize(nd);
-    HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nd * sizeof(DocRes), hipMemcpyDeviceToHost));
+    e->res.resize(nall);
+    HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nall * sizeof(DocRes), hipMemcpyDeviceToHost));
     e->replayed = true;
     e->downloaded = false;
     return MTE_OK;
@@ -1259,9 +1286,22 @@ int mte_replay(mte_engine* e, mte_stats* out) {
     if (e->n_cells && !e->generated) {
         // cell ops: pass 1 evaluates adjustPosition in both vectors of every cell op, pass 2 replays
         // with the handle allocations both gate (a vector's positions do not depend on its handles)
+        // Pass 1 runs only the documents that carry cell records (their positions are all it
+        // produces), without emission; pass 2 replays the whole batch.
+        std::vector<uint32_t> all = e->order, sub;
+        for (uint32_t d : all)
+            if (e->cell_recs.count(d)) sub.push_back(d);
+        const bool emit_was = e->emit_opt;
+        e->order = sub;
+        e->emit_opt = false;
         e->P.cell_mode = 1;
-        rc = run_kernel(e, false);
+        rc = upload(e, e->d_order, e->order);
+        if (!rc) rc = run_kernel(e, false);
         const double ms1 = e->last_kernel_ms;
+        e->order = all;
+        e->emit_opt = emit_was;
+        if (!rc) rc = upload(e, e->d_order, e->order);
+        e->last_cell_pass_ms = ms1;
         e->P.cell_mode = 2;
         if (!rc) rc = run_kernel(e, false);
         e->last_kernel_ms += ms1;
@@ -1339,6 +1379,12 @@ int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_o
     int rc;
     // generated docs hover around a 2048-char target length: 64K-unit semispaces are ample
     if ((rc = layout_and_alloc(e, nops, pay, pi, an, collab, has_nl, 65536, nullptr, nullptr, doc_ids))) return rc;
+    // generated documents carry no SharedMatrix cell ops: drop an earlier load's cell records, so
+    // solo_count and the matrix snapshot never see them (load_cells does the same for a cell-free batch)
+    e->cell_recs.clear();
+    e->n_cells = 0;
+    e->P.cell_pos = e->P.cell_h = e->P.htab = nullptr;
+    for (uint32_t d = 0; d < n_docs; d++) e->cfg[d].ht_cap = e->cfg[d].ht_off = 0;
     HIP_TRY(e, e->d_ops.alloc(e->hb.doc_op_offsets.back()));
     HIP_TRY(e, e->d_payload.alloc(e->hb.doc_payload_offsets.back()));
     HIP_TRY(e, hipMemsetAsync(e->d_payload.p, 0, e->d_payload.n * sizeof(uint16_t), e->stream));
@@ -2400,8 +2446,9 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "lean") e->lean_opt = value != 0;
     else if (k == "reg_solo") e->reg_solo = value != 0;
     else if (k == "reg_lb_limit") e->reg_lb_limit = (uint32_t)std::max<int64_t>(0, value);
-    else if (k == "emit") e->emit_opt = value != 0;
-    else if (k == "rows_bulk") e->rows_bulk = value <= 0 ? 0u : value >= 8 ? 8u : 4u;  // SnapshotV1 emission on the device after replay
+    else if (k == "emit") e->emit_opt = value != 0;  // SnapshotV1 emission on the device after replay
+    else if (k == "xcd_align") e->xcd_align = value != 0;
+    else if (k == "rows_bulk") e->rows_bulk = value <= 0 ? 0u : value >= 8 ? 8u : 4u;  // lean bulk on k_rows
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
@@ -2423,12 +2470,14 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "solo_lead_us") *value = (int64_t)(e->last_solo_lead_ms * 1000.0);
     else if (k == "solo_cycles") *value = (int64_t)e->last_solo_cycles;  // longest document's wave: s_memtime
     else if (k == "solo_ref_ticks") *value = (int64_t)e->last_solo_ref;  // ... and s_memrealtime (100 MHz)
+    else if (k == "solo_start_delay_ticks") *value = e->last_solo_start_delay;  // vs the bulk kernel's start
     else if (k == "load_alloc_us") *value = (int64_t)(e->last_alloc_ms * 1000.0);
     else if (k == "load_stage_copy_us") *value = (int64_t)(e->stage_copy_ms * 1000.0);
     else if (k == "load_stage_wait_us") *value = (int64_t)(e->stage_wait_ms * 1000.0);
     else if (k == "solo_tail_us") *value = (int64_t)(e->last_solo_tail_ms * 1000.0);
     else if (k == "lean") *value = e->last_lean;
-    else if (k == "rows") *value = e->last_rows;  // k_rows waves per CU of the last pass (0: not used)
+    else if (k == "rows") *value = e->last_rows;
+    else if (k == "cell_pass_us") *value = (int64_t)(e->last_cell_pass_ms * 1000.0);  // SharedMatrix pass 1  // k_rows waves per CU of the last pass (0: not used)
     else if (k == "emit_us") *value = (int64_t)(e->last_emit_ms * 1000.0);  // emission after the replay pass
     else if (k == "out_text") {  // UTF-16 units Engine::finish gathered (counters[6..7])
         uint32_t ctr[8] = {0, 0, 0, 0, 0, 0, 0, 0};

@@ -29,6 +29,8 @@ __global__ __launch_bounds__(64 * LDS_WAVES) __attribute__((amdgpu_waves_per_eu(
     LdsPlan* lp = &g_plan;
     const u32 t = threadIdx.x, L = t & 63;
     const u32 w = wave_first(t >> 6);  // wave-uniform (the compiler cannot infer it from threadIdx)
+    // the bulk's start on the 100 MHz reference clock, beside k_solo's own stamps (dispatch delays)
+    if (blockIdx.x == 0 && t == 0 && p.solo_clk) p.solo_clk[4 * SOLO_CLK_SLOTS] = __builtin_amdgcn_s_memrealtime();
     u32 usable = POOL_BLOCKS;
     if (p.pool_limit && p.pool_limit < usable) usable = p.pool_limit;
     if (t < 16) {

@@ -116,6 +116,7 @@ template <int RW, int NR>
 __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4, RW / 4))) void k_rows(Params p) {
     const u32 w = wave_first(threadIdx.x >> 6);
     const u32 vb = w * (u32)NR * 64u * 32u, ab = vb + (u32)NR * 64u * 16u;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && p.solo_clk) p.solo_clk[4 * SOLO_CLK_SLOTS] = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         u32 i = 0;
         if (lane_id() == 0) i = p.n_prio + atomicAdd(&p.counters[0], 1u);

@@ -247,7 +247,8 @@ struct RegEngine {
         if (simd::lane_of(m)) b[(r * 64 + __lane_id()) * 4 + c] = x.x;
         simd::lds_order();
     }
-#ifdef MTE_OLD_MEMMOVE  // A/B: one 64-slot chunk per LDS round trip
+    // Overlapping slot move, one 64-slot chunk per LDS round trip. (Issuing eight chunks' reads
+    // before their writes measured 7 % SLOWER on the lone 10^6-op document: 4.25 vs 3.93 us/op.)
     SD void mv_slots(u32 dst, u32 src, u32 n) {
         cr = NONE;
         uint4* V4 = VISP();
@@ -285,42 +286,6 @@ struct RegEngine {
             }
         }
     }
-#else
-    // Overlapping slot move in the safe direction, eight 64-slot chunks per round: all sixteen
-    // ds_read_b128 of a round are issued before its first write, so a round costs one LDS latency
-    // (the chunks of one round never overlap the slots a later round reads). Chunk c of a round
-    // covers slot indices base(c) + lane; the chunks are named registers (an array of them went to
-    // the scratch stack).
-    SD void mv_slots(u32 dst, u32 src, u32 n) {
-        cr = NONE;
-        uint4* V4 = VISP();
-        uint4* A4 = AUXP();
-        const i32 L = (i32)__lane_id(), N = (i32)n;
-        const bool fwd = dst > src;  // moving up: rounds from the top down, chunks downwards
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        for (i32 r0 = 0; r0 < N; r0 += 512) {
-            auto at = [&](i32 c) MTE_LI { return fwd ? N - r0 - 64 * (c + 1) + L : r0 + 64 * c + L; };
-            auto ok = [&](i32 c) MTE_LI { const i32 i = at(c); return r0 + 64 * c < N && i >= 0 && i < N; };
-#define MTE_MV_LD(c)                         \
-    uint4 v##c = z, a##c = z;                \
-    if (ok(c)) {                             \
-        v##c = V4[src + (u32)at(c)];         \
-        a##c = A4[src + (u32)at(c)];         \
-    }
-#define MTE_MV_ST(c)                         \
-    if (ok(c)) {                             \
-        V4[dst + (u32)at(c)] = v##c;         \
-        A4[dst + (u32)at(c)] = a##c;         \
-    }
-            MTE_MV_LD(0) MTE_MV_LD(1) MTE_MV_LD(2) MTE_MV_LD(3) MTE_MV_LD(4) MTE_MV_LD(5) MTE_MV_LD(6) MTE_MV_LD(7)
-            simd::lds_order();
-            MTE_MV_ST(0) MTE_MV_ST(1) MTE_MV_ST(2) MTE_MV_ST(3) MTE_MV_ST(4) MTE_MV_ST(5) MTE_MV_ST(6) MTE_MV_ST(7)
-            simd::lds_order();
-#undef MTE_MV_LD
-#undef MTE_MV_ST
-        }
-    }
-#endif
     SD void zero_slots(u32 at, u32 n) {
         cr = NONE;
         for (u32 b = __lane_id(); b < n; b += 64) {
@@ -771,11 +736,25 @@ struct RegEngine {
     SD void pop_fast(u32 m, u32 lk, u32 ls, i32& newTop) {
         const V K0 = HK.get(0), K1 = HK.get(1), S0 = HS.get(0), S1 = HS.get(1);
         const V cl = L() * 2u, cr = cl + 1u;
-        const V kL = simd::sel(cl < 64u, simd::bperm(K0, cl & 63u), simd::bperm(K1, cl & 63u));
-        const V kR = simd::sel(cr < 64u, simd::bperm(K0, cr & 63u), simd::bperm(K1, cr & 63u));
+        // both children's keys AND segment ids in one round of crossbar gathers (register 1 only
+        // when the heap reaches it)
+        V kL, kR, sL, sR;
+        if (m < 64u) {
+            kL = simd::bperm(K0, cl & 63u);
+            kR = simd::bperm(K0, cr & 63u);
+            sL = simd::bperm(S0, cl & 63u);
+            sR = simd::bperm(S0, cr & 63u);
+        } else {
+            const B l0 = cl < 64u, r0 = cr < 64u;
+            kL = simd::sel(l0, simd::bperm(K0, cl & 63u), simd::bperm(K1, cl & 63u));
+            kR = simd::sel(r0, simd::bperm(K0, cr & 63u), simd::bperm(K1, cr & 63u));
+            sL = simd::sel(l0, simd::bperm(S0, cl & 63u), simd::bperm(S1, cl & 63u));
+            sR = simd::sel(r0, simd::bperm(S0, cr & 63u), simd::bperm(S1, cr & 63u));
+        }
         const B right = (cr < m + 1u) & simd::slt(kR, kL);  // smaller child, the left one on ties
         const V c = simd::sel(right, cr, cl);
         const V kc = simd::sel(right, kR, kL);
+        const V sc = simd::sel(right, sR, sL);
         const B go = (cl < m + 1u) & simd::slt(kc, (i32)lk);  // the moved entry goes below k
         const V nxt = simd::sel(go, c, 0u);
         u32 k = 1;
@@ -806,7 +785,6 @@ struct RegEngine {
         }
 #endif
         const B mv = simd::ballot_mask(path);
-        const V sc = simd::sel(c < 64u, simd::bperm(S0, c & 63u), simd::bperm(S1, c & 63u));
         V N0 = simd::sel(mv, kc, K0), T0 = simd::sel(mv, sc, S0);
         if (path & 2u) newTop = (i32)simd::readlane(kc, 1);
         if (k < 64u) {
@@ -934,8 +912,10 @@ struct RegEngine {
     // Each run becomes its head with the run's text: already contiguous (no copy), appended into the
     // head's arena chunk when it has the capacity, or else copied into a fresh chunk of
     // max(32, 2 * total) units; all copies of the block run as one flattened gather.
+    bool scoured = false;  // the last scour rewrote its block's row, needsScour already false
     SD u32 scour(u32 k, u32 cnt) {
         RG_PROF(RP_SCOUR);
+        scoured = false;
         RG_COUNT(RP_N_SCOUR, 1);
         if (cnt > 8) cnt = 8;
         const u32 r = k >> 3, gb = gbase(k);
@@ -1030,7 +1010,9 @@ struct RegEngine {
         cmp(w.toff, 0u);
         cmp(w.rm, 0u);
         cmp(w.sid, 0u);
+        ns_put(w, k, SC_FALSE);  // scourNode's caller clears needsScour (mergeTree.ts:1457): same write
         putrow(r, w);
+        scoured = true;
         return nkeep;
     }
     // The runs' text copies of one block as one flattened gather: slot lane l copies jlen units from
@@ -1182,7 +1164,9 @@ struct RegEngine {
         cmp(w.rseq, nullptr, 0u);
         cmp(w.meta, nullptr, NS_MASK);  // the block's needsScour stays in every lane
         cmp(w.sid, nullptr, 0u);
+        ns_put(w, k, SC_FALSE);
         putrow(r, w);
+        scoured = true;
         return nkeep;
     }
     // The recorded copies as one flattened gather (sources are never destinations of one scour).
@@ -1321,7 +1305,7 @@ struct RegEngine {
             const u32 cnt = count(k);
             const u32 nc = scour(k, cnt);
             if (status) return;
-            ns_set(k, SC_FALSE);
+            if (!scoured) ns_set(k, SC_FALSE);
             if (!(nc < cnt && nc < 4 && height > 1)) continue;
             u32 k0;
             const u32 pi = parent_of(0, k, k0);
@@ -1368,6 +1352,49 @@ struct RegEngine {
         return insert_slot(f.k, f.cnt, (u32)f.slot + 1, right, true, rr, lc);
     }
 
+    // An insert inside segment `f.slot` of a block with room for two more children: splitAt and the
+    // insert as ONE edit of the block's row (the same result as split_at then insert_slot: left piece
+    // at s, the new segment at s+1, the right piece -- a copy of s cut at f.r -- at s+2, later slots
+    // two places on; the right piece's id is taken first).
+    SD bool split_insert(const RFound& f, RSeg rec, i32 seq) {
+        RG_PROF(RP_INSERT_SLOT);
+        const u32 s = (u32)f.slot, rr = (u32)f.r, k = f.k;
+        const u32 sid_r = new_sid();
+        if (sid_r == NONE) return false;
+        rec.sid = new_sid();
+        if (rec.sid == NONE) return false;
+        const u32 r = k >> 3, gb = gbase(k);
+        Row& w = rowref(r);
+        const V sl = L() & 7u;
+        const B ing = in_group(k);
+        const B mv = ing & (sl >= s + 2);       // take lane - 2: the right piece and the later slots
+        const B at = L() == gb + s + 1;         // the new segment
+        const B rp = L() == gb + s + 2;         // the right piece
+        const B lp = L() == gb + s;             // the left piece
+        const u32 ns = (simd::readlane(w.meta, gb) >> NS_SHIFT) & 3u;
+        auto put = [&](V& x, u32 val) MTE_LI {
+            x = simd::sel(mv, simd::row_shr2(x), x);
+            x = simd::sel(at, val, x);
+        };
+        put(w.len, rec.len);
+        put(w.seq, (u32)rec.seq);
+        put(w.rseq, rec.rseq);
+        put(w.meta, (rec.meta & ~NS_MASK) | (ns << NS_SHIFT));
+        put(w.toff, rec.toff);
+        put(w.cap, rec.cap);
+        put(w.rm, rec.rm);
+        put(w.sid, rec.sid);
+        // arena text (cap >= len) splits its capacity between the pieces; payload text has none
+        const B ar = (w.toff & ARENA_BIT) != 0u;
+        w.cap = simd::sel(rp, simd::sel(ar, w.cap - rr, 0u), simd::sel(lp, simd::sel(ar, simd::splat(rr), 0u), w.cap));
+        w.len = simd::sel(rp, w.len - rr, simd::sel(lp, simd::splat(rr), w.len));
+        w.toff = simd::sel(rp, w.toff + rr, w.toff);
+        w.sid = simd::sel(rp, simd::splat(sid_r), w.sid);
+        writeback(r);
+        if (seq > minSeq) add_lru(k, rec.sid, seq);
+        return status == 0;
+    }
+
     // insertSegments (mergeTree.ts:1968-1998): split at pos, then place the new segment.
     SD bool op_insert(i32 pos, i32 R, u32 C, i32 seq, RSeg rec) {
         RG_PROF(RP_INS);
@@ -1377,6 +1404,7 @@ struct RegEngine {
             return false;
         }
         u32 k = f.k, j;
+        if (f.slot >= 0 && f.r > 0 && f.cnt + 2 < 8 && rec.len != 0) return split_insert(f, rec, seq);
         if (f.slot >= 0 && f.r > 0) {
             if (split_at(f) == NONE || status) return false;
             // the insertion point follows from the split: before the right piece, except when the
@@ -1532,35 +1560,34 @@ struct RegEngine {
             const u32 nw = left >= 8 ? 64u : (u32)left * 8u;
             return simd::ld(src + c0 * 8, L(), L() < nw);
         };
-        // four chunk registers used as a ring: chunk c lives in Q[c & 3] and is refilled in place
-        // with chunk c + 4 once consumed, so a refill's load is not waited for until 24 ops later (a
-        // shifted register queue made the compiler wait for each refill at once)
-        V Q0 = load_chunk(b), Q1 = load_chunk(b + 8), Q2 = load_chunk(b + 16), Q3 = load_chunk(b + 24);
-        u32 qh = 0;
+        // Two chunk registers: CUR holds the records being decoded, NXT the next eight. At a chunk's
+        // first op CUR = NXT (loaded eight ops earlier), the op is decoded, and only THEN is NXT
+        // refilled: the compiler waits for the whole vector-memory counter before a decode, so the
+        // newest load outstanding there must be an op old. (Loading before the decode, or a
+        // four-register ring indexed by a switch, made every chunk wait for a fresh HBM load.)
+        V CUR = load_chunk(b), NXT = load_chunk(b + 8);
+#ifndef MTE_CPU
+        // wait for the first chunk here, once: CUR then enters the loop with no load outstanding, so
+        // the decodes need no vector-memory wait at all (stores of the merge arena included)
+        asm volatile("" ::"v"(CUR.x));
+#endif
         for (; i < e && !status; i++) {
             const u32 r = (u32)((i - b) & 7);
-            if (r == 0 && i != b) {
-                const u64 nc = i + 24;
-                switch (qh) {
-                    case 0: Q0 = load_chunk(nc); break;
-                    case 1: Q1 = load_chunk(nc); break;
-                    case 2: Q2 = load_chunk(nc); break;
-                    default: Q3 = load_chunk(nc); break;
-                }
-                qh = (qh + 1) & 3u;
+            const bool first = r == 0 && i != b;
+            if (first) {
+                CUR = NXT;
+#ifndef MTE_CPU
+                asm volatile("");  // keep this a branch: a select would read NXT (and wait) every op
+#endif
             }
             mte_op op;
             {
                 RG_PROF(RP_FETCH);
                 u32 w[8];
-                switch (qh) {
-                    case 0: for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(Q0, r * 8 + x); break;
-                    case 1: for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(Q1, r * 8 + x); break;
-                    case 2: for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(Q2, r * 8 + x); break;
-                    default: for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(Q3, r * 8 + x); break;
-                }
+                for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(CUR, r * 8 + x);
                 __builtin_memcpy(&op, w, sizeof op);
             }
+            if (first) NXT = load_chunk(i + 8);
             RG_COUNT(RP_OPS, 1);
             if (!apply(op)) {
                 status = REG_HANDOFF;

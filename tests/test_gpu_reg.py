@@ -139,7 +139,9 @@ def test_bulk_rows_kernel_matches_oracle(engine, kind, waves):
         st = engine.replay()
         assert st["failed_docs"] == 0 and engine.get_info("rows") == waves
         modes = [engine.doc_result(d)["mode"] for d in range(len(counts))]
-        assert modes.count(MODE_BULK_ROWS) >= len(counts) - 16, sorted(set(modes))
+        # the longest documents may take k_solo (4); a document that outgrows the rows (8 waves: 64
+        # leaf blocks) is re-run HBM-resident (1)
+        assert set(modes) <= {MODE_BULK_ROWS, MODE_ROWS, 1} and modes.count(MODE_BULK_ROWS) > 0.9 * len(counts), sorted(set(modes))
         _check(engine, batch, n_docs=len(counts))
         # documents that outgrow the rows (reg_lb_limit shrinks them) go back to the host, which
         # re-runs them HBM-resident from their first op

@@ -250,3 +250,42 @@ def test_gpu_relative_positions_match_oracle(engine):
     assert codes[:8] == [0] * 8
     assert codes[8:8 + len(edge_logs())] == [c[2] for c in edge_logs()]
     assert codes[-2:] == [0, UNSUPPORTED]
+
+
+def marker_heavy_log(n_markers=150, n_ann=6):
+    """Markers carry no payload: a relative annotate spanning them touches far more segments than
+    the document has text characters."""
+    msgs, seq, L = [msg("a", 1, 0, ins(0, "xy"))], 1, 2
+    for i in range(n_markers):
+        seq += 1
+        msgs.append(msg("a", seq, seq - 1, ins(L, {"marker": {"refType": 1}, "props": {"markerId": f"m{i}"}})))
+        L += 1
+    for j in range(n_ann):
+        seq += 1
+        c = {"type": 2, "relativePos1": rel("m0", True), "relativePos2": rel(f"m{n_markers - 1}"), "props": {"k": j}}
+        msgs.append(msg("b" if j % 2 else "a", seq, seq - 1, c))
+    return msgs
+
+
+@pytest.mark.gpu
+def test_gpu_marker_heavy_relative_annotates_rerun(engine):
+    """The host's re-run pass sizes a re-run document's property-map table from its ops; a relative
+    annotate over many markers (length 1, no payload) must count them, or a valid document ends
+    MTE_DOC_CAPACITY in the re-run (map_rerun). Forced through the re-run: HBM slots too small."""
+    logs = [marker_heavy_log(), marker_heavy_log(60, 12)]
+    engine.set_option("slot_blk_limit", 8)
+    try:
+        b = mte.Builder()
+        for m in logs:
+            b.add_doc(m)
+        batch = b.batch()
+        engine.load(batch)
+        engine.set_option("force_hbm", 1)
+        engine.replay()
+        assert engine.run_info()["spilled"] == len(logs)
+    finally:
+        engine.set_option("force_hbm", 0)
+        engine.set_option("slot_blk_limit", 0)
+    for d in range(batch.n_docs):
+        assert engine.status(d)[0] == 0
+        compare_doc(engine, batch, d)

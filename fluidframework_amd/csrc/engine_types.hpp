@@ -224,6 +224,7 @@ struct Params {
     u64* solo_clk;            // per solo workgroup: s_memtime / s_memrealtime at its replay's start and
                               // end (4 u64): shader cycles vs the 100 MHz reference clock; then, at
                               // [4 * SOLO_CLK_SLOTS], the bulk kernel's start (s_memrealtime)
+    u32* solo_started;        // solo workgroups that have started this pass (k_solo_gate waits for n_solo)
 };
 
 constexpr u32 SOLO_CLK_SLOTS = 64;  // solo workgroups with clock stamps (Params::solo_clk)

@@ -233,6 +233,7 @@ struct mte_engine {
     hipStream_t stream3 = nullptr;                    // stream3: the solo workgroups (k_solo)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
     hipEvent_t ev_s0 = nullptr, ev_s1 = nullptr;  // timing of the solo workgroups (critical path)
+    hipEvent_t ev_gate = nullptr;                 // after k_solo_gate: the second bulk stream starts here
     // pinned staging for uploads from the caller's (pageable) buffers: two chunks, each refilled by
     // host threads while the DMA engine copies the other one (upload_staged)
     void* stage[2] = {nullptr, nullptr};
@@ -262,6 +263,8 @@ struct mte_engine {
     DevBuf<uint32_t> d_out_maps, d_prop_keys, d_prop_vals, d_val_flags, d_val_objidx, d_order, d_list, d_maps, d_counters,
         d_first_seen;
     DevBuf<uint64_t> d_val_objmatch, d_ovl, d_out_ovl, d_prof, d_solo_clk;
+    DevBuf<uint32_t> d_solo_started;  // k_solo_gate's counter
+    bool solo_gate = true;            // option "solo_gate"
     uint64_t last_solo_cycles = 0, last_solo_ref = 0;  // critical wave: s_memtime / s_memrealtime deltas
     double last_cell_pass_ms = 0;                       // a SharedMatrix batch's first (positions) pass
     int64_t last_solo_start_delay = 0;                  // critical wave's start - the bulk's (100 MHz ticks)
@@ -325,7 +328,8 @@ struct mte_engine {
     // SnapshotV1 emission on the device (emit.hip): property / name tables, scratch, and two output
     // pools -- round 0 (every document but the solo ones) runs while the critical path is still
     // replaying, round 1 (solo and host-re-run documents) after it
-    uint32_t rows_bulk = 0;   // option "rows_bulk": lean replays run the bulk on k_rows (4 or 8 waves per CU)
+    int32_t rows_bulk = -1;   // option "rows_bulk": lean replays run the bulk on k_rows, 4 or 8 waves per CU;
+                              // -1 (auto): 4 when every bulk document gets a row wave at once, 0: never
     bool xcd_align = true;    // option "xcd_align": bulk grids leave solo CUs free in every XCD (bulk_cus)
     uint32_t last_rows = 0;   // waves per CU of the last pass's k_rows (0: k_lds / k_hbmq)
     bool emit_opt = true;     // option "emit"
@@ -530,6 +534,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     HIP_TRY(e, e->d_prof.fit((size_t)nd * PROF_SLOTS));
     HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, (size_t)nd * PROF_SLOTS * 8, e->stream));
     HIP_TRY(e, e->d_solo_clk.fit(4 * SOLO_CLK_SLOTS + 1));  // 4 u64 per solo workgroup + the bulk's start
+    HIP_TRY(e, e->d_solo_started.fit(1));
     // LPT order: longest documents start first
     e->order.resize(nd);
     for (uint32_t d = 0; d < nd; d++) e->order[d] = d;
@@ -556,6 +561,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     P.counters = e->d_counters.p;
     P.prof = e->d_prof.p;
     P.solo_clk = e->d_solo_clk.p;
+    P.solo_started = e->d_solo_started.p;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || cus <= 0) cus = 256;
     e->n_groups = (uint32_t)cus;
@@ -737,6 +743,7 @@ int mte_create(const mte_config* cfg, mte_engine** out) {
     HIP_TRY(e.get(), hipEventCreate(&e->ev_s0));
     HIP_TRY(e.get(), hipEventCreate(&e->ev_s1));
     HIP_TRY(e.get(), hipEventCreateWithFlags(&e->ev2, hipEventDisableTiming));
+    HIP_TRY(e.get(), hipEventCreateWithFlags(&e->ev_gate, hipEventDisableTiming));
     HIP_TRY(e.get(), hipEventCreate(&e->ev0));
     HIP_TRY(e.get(), hipEventCreate(&e->ev1));
     *out = e.release();
@@ -751,6 +758,7 @@ void mte_destroy(mte_engine* e) {
         if (e->stage[i]) (void)hipHostFree(e->stage[i]);
         if (e->ev_stage[i]) (void)hipEventDestroy(e->ev_stage[i]);
     }
+    if (e->ev_gate) (void)hipEventDestroy(e->ev_gate);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->ev2) (void)hipEventDestroy(e->ev2);
@@ -1095,7 +1103,16 @@ static int run_kernel(mte_engine* e, bool gen) {
     e->last_lean = full == 0;
     wave_plan(e, nd, groups, hbm_waves, &lds_active, n_solo);
     // lean replays may run the bulk on the row engine instead (k_rows; DOC_SPILL re-runs as below)
-    const uint32_t rows = (!gen && full == 0 && e->rows_bulk && !e->force_hbm && nd > n_solo) ? e->rows_bulk : 0;
+    // k_rows: lean replays whose bulk documents all get a row wave at once (C5: 1 024 documents of
+    // 10^6 ops, 4.4 s per step against 9.8 s on k_lds / k_hbmq); a batch of many short documents
+    // (C2: 4 096 x 10^4 ops, 282 vs 171 ms) keeps the sixteen LDS / HBM waves per CU
+    uint32_t rows = 0;
+    if (!gen && full == 0 && e->rows_bulk && !e->force_hbm && nd > n_solo) {
+        uint64_t bulk_ops = 0;
+        for (uint32_t k = n_solo; k < nd; k++) bulk_ops += e->n_ops_doc[e->order[k]];
+        const bool long_docs = nd - n_solo <= 4 * bulk_cus(e, n_solo) && bulk_ops >= 200000ull * (nd - n_solo);
+        rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : long_docs ? 4u : 0u;
+    }
     e->last_rows = rows;
     if (rows) groups = hbm_waves = lds_active = 0;
     e->P.slot_hbm0 = groups * LDS_WAVES;
@@ -1112,6 +1129,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 8 * sizeof(uint32_t), s_main));
     HIP_TRY(e, hipMemsetAsync(e->d_slot_bits.p, 0, e->d_slot_bits.n * sizeof(uint32_t), s_main));
     HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, e->d_prof.n * sizeof(uint64_t), s_main));  // profiling build
+    HIP_TRY(e, hipMemsetAsync(e->d_solo_started.p, 0, sizeof(uint32_t), s_main));  // k_solo_gate's counter
     HIP_TRY(e, hipEventRecord(e->ev0, s_main));
     std::vector<uint32_t> spill;
     e->map_rr_off.clear();  // (set again below for this pass's re-run documents)
@@ -1125,7 +1143,10 @@ static int run_kernel(mte_engine* e, bool gen) {
         HIP_TRY(e, launch_solo(e->P, gen, full, n_solo, s_solo));
         HIP_TRY(e, hipEventRecord(e->ev_s1, s_solo));
         HIP_TRY(e, hipEventRecord(e->ev3, s_solo));
+        // the bulk starts once the solo workgroups hold their CUs (k_solo_gate)
+        if (e->solo_gate && (groups || rows || hbm_waves)) HIP_TRY(e, launch_solo_gate(e->d_solo_started.p, n_solo, s_main));
     }
+    HIP_TRY(e, hipEventRecord(e->ev_gate, s_main));
     if (groups) HIP_TRY(e, launch_lds(e->P, gen, full, groups, s_main));
     if (rows) {
         const uint32_t cus = bulk_cus(e, n_solo);
@@ -1136,7 +1157,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     if (hbm_waves && !groups) {
         HIP_TRY(e, launch_hbmq(e->P, gen, full, nd, s_main));
     } else if (hbm_waves) {
-        HIP_TRY(e, hipStreamWaitEvent(s_hbmq, e->ev0, 0));
+        HIP_TRY(e, hipStreamWaitEvent(s_hbmq, e->ev_gate, 0));
         HIP_TRY(e, launch_hbmq(e->P, gen, full, nd, s_hbmq));
         HIP_TRY(e, hipEventRecord(e->ev2, s_hbmq));
         HIP_TRY(e, hipStreamWaitEvent(s_main, e->ev2, 0));
@@ -2448,7 +2469,8 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "reg_lb_limit") e->reg_lb_limit = (uint32_t)std::max<int64_t>(0, value);
     else if (k == "emit") e->emit_opt = value != 0;  // SnapshotV1 emission on the device after replay
     else if (k == "xcd_align") e->xcd_align = value != 0;
-    else if (k == "rows_bulk") e->rows_bulk = value <= 0 ? 0u : value >= 8 ? 8u : 4u;  // lean bulk on k_rows
+    else if (k == "solo_gate") e->solo_gate = value != 0;
+    else if (k == "rows_bulk") e->rows_bulk = value < 0 ? -1 : value == 0 ? 0 : value >= 8 ? 8 : 4;  // lean bulk on k_rows
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;

@@ -739,7 +739,11 @@ struct RegEngine {
         // both children's keys AND segment ids in one round of crossbar gathers (register 1 only
         // when the heap reaches it)
         V kL, kR, sL, sR;
+#ifdef MTE_NO_GATHER2
+        if (false) {
+#else
         if (m < 64u) {
+#endif
             kL = simd::bperm(K0, cl & 63u);
             kR = simd::bperm(K0, cr & 63u);
             sL = simd::bperm(S0, cl & 63u);
@@ -1305,7 +1309,11 @@ struct RegEngine {
             const u32 cnt = count(k);
             const u32 nc = scour(k, cnt);
             if (status) return;
+#ifdef MTE_NO_SCOUR_NS
+            ns_set(k, SC_FALSE);
+#else
             if (!scoured) ns_set(k, SC_FALSE);
+#endif
             if (!(nc < cnt && nc < 4 && height > 1)) continue;
             u32 k0;
             const u32 pi = parent_of(0, k, k0);
@@ -1404,7 +1412,9 @@ struct RegEngine {
             return false;
         }
         u32 k = f.k, j;
+#ifndef MTE_NO_SPLIT_INSERT
         if (f.slot >= 0 && f.r > 0 && f.cnt + 2 < 8 && rec.len != 0) return split_insert(f, rec, seq);
+#endif
         if (f.slot >= 0 && f.r > 0) {
             if (split_at(f) == NONE || status) return false;
             // the insertion point follows from the split: before the right piece, except when the
@@ -1483,8 +1493,10 @@ struct RegEngine {
     // Room for one more op (margins for the splits, packs and heap pushes an op can cause);
     // false => hand the document to the LDS engine before this op.
     SD bool room() const {
+        // level-1 nodes hold >= 1 leaf block each, so fewer than 57 blocks cannot reach lane 56 (and
+        // the readlane, a VALU -> SALU round trip, is skipped)
         return n_lb + 16 <= lb_lim && heapSize + n_lb + 8 < RG_HEAP && height + 2 <= RG_LEVELS &&
-               simd::readlane(LV.get(0), 56) == 0u;
+               (n_lb < 57 || simd::readlane(LV.get(0), 56) == 0u);
     }
 
     // Client.applyMsg for one op record (client.ts:805-836); false => not applied, hand off.

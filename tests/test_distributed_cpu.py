@@ -83,19 +83,30 @@ def test_summary_gather_gloo_world2():
         assert int(rec["checksum"]) == o.checksum()
 
 
-def _bench_shard_worker(rank, world, port, q):
-    """One rank of bench.py's C4 path at CPU scale: plan_shard -> generate (global ids) -> replay ->
-    summary records -> all-gather (gloo here; RCCL's mte_gather_summaries on the box)."""
+# bench.py's shard plans at CPU scale: C4 (Zipf, LPT) and C5 (equal documents, strided; kind 5)
+PLANS = {"C4": dict(kind=2, docs=96, ops=0, zipf_lo=50, zipf_hi=3000), "C5": dict(kind=5, docs=40, ops=1500)}
+
+
+def _plan(config, world, rank):
+    from fluidframework_amd.shard import plan_shard
+
+    c = PLANS[config]
+    extra = {k: c[k] for k in ("zipf_lo", "zipf_hi") if k in c}
+    return plan_shard(config, world, rank, c["docs"], c["ops"], **extra)
+
+
+def _bench_shard_worker(rank, world, port, q, config="C4"):
+    """One rank of bench.py's C4 / C5 path at CPU scale: plan_shard -> generate (global ids) -> replay
+    -> summary records -> all-gather (gloo here; RCCL's mte_gather_summaries on the box)."""
     import torch.distributed as dist
 
-    from fluidframework_amd.shard import plan_shard
     from oracle import generate_batch
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    ids, counts = plan_shard("C4", world, rank, 96, 0, zipf_lo=50, zipf_hi=3000)
-    _, cks, sts = generate_batch(2, ids, counts, n_clients=8, seed=1000, threads=2)
+    ids, counts = _plan(config, world, rank)
+    _, cks, sts = generate_batch(PLANS[config]["kind"], ids, counts, n_clients=8, seed=1000, threads=2)
     recs = np.zeros(len(ids), dtype=SUMMARY_DTYPE)
     recs["checksum"] = cks
     recs["status"] = sts
@@ -106,16 +117,17 @@ def _bench_shard_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_bench_shard_and_gather_world2_equals_world1():
-    """bench.py's sharding at world 2 replays exactly the documents of world 1: the gathered,
-    rank-concatenated summary records, sorted by global id, equal a single-process run."""
-    from fluidframework_amd.shard import plan_shard
+@pytest.mark.parametrize("config", ["C4", "C5"])
+def test_bench_shard_and_gather_world2_equals_world1(config):
+    """bench.py's sharding at world 2 replays exactly the documents of world 1 (C4: LPT over Zipf
+    op counts; C5: equal documents strided over the ranks): the gathered, rank-concatenated summary
+    records, sorted by global id, equal a single-process run."""
     from oracle import generate_batch
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bench_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_bench_shard_worker, args=(r, 2, port, q, config)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in procs)
@@ -125,11 +137,14 @@ def test_bench_shard_and_gather_world2_equals_world1():
     assert res[0] == res[1]
     g = np.frombuffer(res[0], dtype=SUMMARY_DTYPE)
     g = g[np.argsort(g["doc_id"])]
-    ids, counts = plan_shard("C4", 1, 0, 96, 0, zipf_lo=50, zipf_hi=3000)
-    assert sorted(g["doc_id"].tolist()) == list(range(96)) == sorted(ids.tolist())
+    n = PLANS[config]["docs"]
+    ids, counts = _plan(config, 1, 0)
+    assert sorted(g["doc_id"].tolist()) == list(range(n)) == sorted(ids.tolist())
     order = np.argsort(ids)
-    _, cks, sts = generate_batch(2, ids[order], counts[order], n_clients=8, seed=1000, threads=4)
+    _, cks, sts = generate_batch(PLANS[config]["kind"], ids[order], counts[order], n_clients=8, seed=1000, threads=4)
     assert g["checksum"].tolist() == cks and all(s == 0 for s in sts)
-    # LPT: rank loads differ by at most the longest document
-    loads = [plan_shard("C4", 2, r, 96, 0, zipf_lo=50, zipf_hi=3000)[1].sum() for r in range(2)]
-    assert abs(loads[0] - loads[1]) <= 3000
+    loads = [_plan(config, 2, r)[1].sum() for r in range(2)]
+    if config == "C4":  # LPT: rank loads differ by at most the longest document
+        assert abs(loads[0] - loads[1]) <= 3000
+    else:  # strided equal documents: the ranks' document counts differ by at most one
+        assert abs(len(_plan(config, 2, 0)[0]) - len(_plan(config, 2, 1)[0])) <= 1

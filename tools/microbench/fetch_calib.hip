@@ -26,10 +26,12 @@ __global__ void k_read_x4(const uint4* p, size_t n, uint32_t* sink) {
     if (acc == 0x12345678u) sink[0] = acc;
 }
 // 2 B per lane, coalesced (UTF-16 text copies)
+// (the sink test must be reachable: an xor of u16 values never reaches 0x12345678, and the
+// compiler dropped the whole loop of an earlier version -- FETCH_SIZE 0)
 __global__ void k_read_u16(const uint16_t* p, size_t n, uint32_t* sink) {
     uint32_t acc = 0;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) acc ^= p[i];
-    if (acc == 0x12345678u) sink[0] = acc;
+    if (acc == 0x1234u) sink[0] = acc;
 }
 // one dword per lane stores (row output, scratch)
 __global__ void k_write_dword(uint32_t* p, size_t n) {

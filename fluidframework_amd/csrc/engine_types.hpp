@@ -42,7 +42,7 @@ constexpr u32 ORD_CAP = 128;       // leaf blocks per document while resident in
 #define MTE_IN_CAP 48
 #endif
 #ifndef MTE_HEAP_CAP
-#define MTE_HEAP_CAP 191  // 255 measured C2 -2.6 % (A/B, profiles/ab_r03) but is not yet through the GPU suite; 127: +11 %
+#define MTE_HEAP_CAP 255  // 191: C2 +2.6 % (A/B, profiles/ab_r03: half as many documents continue HBM-resident); 127: +11 %
 #endif
 constexpr u32 IN_CAP = MTE_IN_CAP;      // interior nodes per document while resident in LDS
 constexpr u32 HEAP_CAP = MTE_HEAP_CAP;  // LRU heap entries per document while resident in LDS

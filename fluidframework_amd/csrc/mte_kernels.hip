@@ -231,6 +231,26 @@ hipError_t launch_hbmq(const Params& p, bool gen, int full, u32 n_waves, hipStre
     return hipLaunchKernel(MTE_PICK(k_hbmq, gen, full), dim3(n_waves), dim3(64), args, 0, s);
 }
 
+// The bulk kernels start only once every solo workgroup is resident. Launched on the bulk's stream
+// between k_solo (its own stream) and k_lds / k_rows: without it the bulk sometimes took the CUs first
+// and a solo workgroup waited ~1.2 s for one to drain (solo_start_delay_ms in the bench line), on about
+// every other C4 step. One wave, no LDS; gives up after `limit` 100 MHz ticks so it can never hold
+// the bulk back for long (or hang) whatever the dispatcher does.
+__global__ __launch_bounds__(64) void k_solo_gate(const u32* started, u32 n, u64 limit) {
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const u32 v = __hip_atomic_load(started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wave_read(v, 0) >= n) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > limit) break;
+        __builtin_amdgcn_s_sleep(16);
+    }
+}
+
+hipError_t launch_solo_gate(const u32* started, u32 n_solo, hipStream_t s) {
+    hipLaunchKernelGGL(k_solo_gate, dim3(1), dim3(64), 0, s, started, n_solo, (u64)2000000);  // 20 ms
+    return hipGetLastError();
+}
+
 hipError_t launch_wave_selftest(const u32* in, u32* out, u32 n_waves, hipStream_t s) {
     hipLaunchKernelGGL(k_wave_selftest, dim3(n_waves), dim3(64), 0, s, in, out);
     return hipGetLastError();

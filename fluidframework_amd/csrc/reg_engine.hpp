@@ -739,11 +739,7 @@ struct RegEngine {
         // both children's keys AND segment ids in one round of crossbar gathers (register 1 only
         // when the heap reaches it)
         V kL, kR, sL, sR;
-#ifdef MTE_NO_GATHER2
-        if (false) {
-#else
         if (m < 64u) {
-#endif
             kL = simd::bperm(K0, cl & 63u);
             kR = simd::bperm(K0, cr & 63u);
             sL = simd::bperm(S0, cl & 63u);
@@ -763,14 +759,6 @@ struct RegEngine {
         const V nxt = simd::sel(go, c, 0u);
         u32 k = 1;
         u64 path = 0;  // nodes of register 0 that take their child's entry
-#ifdef MTE_OLD_PATH
-        while (k < 64u) {
-            const u32 nk = simd::readlane(nxt, k);
-            if (!nk) break;
-            path |= 1ull << k;
-            k = nk;
-        }
-#else
         // E bit k: node k's parent moves down into k (its chosen, taken child). The path from the
         // root follows E in scalar registers, two bits per level.
         const u64 E = simd::ballot(simd::bperm(nxt, L() >> 1) == L()) & ~3ull;
@@ -787,7 +775,6 @@ struct RegEngine {
                 k = nk;
             }
         }
-#endif
         const B mv = simd::ballot_mask(path);
         V N0 = simd::sel(mv, kc, K0), T0 = simd::sel(mv, sc, S0);
         if (path & 2u) newTop = (i32)simd::readlane(kc, 1);
@@ -847,9 +834,6 @@ struct RegEngine {
     // ---------------------------------------------------------------- text (HBM)
     SD u16* arena_cur() const { return arena0 + (u64)arenaSel * arena_cap; }
     SD void fence_arena() {
-#ifdef MTE_KO_TEXT  // timing experiment only (wrong text): no scour text copies, no arena fences
-        return;
-#endif
         if (adirty) {
             simd::wave_fence();
             adirty = false;
@@ -1022,9 +1006,6 @@ struct RegEngine {
     // The runs' text copies of one block as one flattened gather: slot lane l copies jlen units from
     // its text src to jdst (sources are never destinations of the same scour).
     SD void copy_runs(V jdst, V jsrc, V jlen) {
-#ifdef MTE_KO_TEXT
-        return;
-#endif
         const V jinc = simd::scan_incl(jlen);
         const u32 total = simd::readlane(jinc, 63);
         if (!total) return;
@@ -1309,11 +1290,7 @@ struct RegEngine {
             const u32 cnt = count(k);
             const u32 nc = scour(k, cnt);
             if (status) return;
-#ifdef MTE_NO_SCOUR_NS
-            ns_set(k, SC_FALSE);
-#else
             if (!scoured) ns_set(k, SC_FALSE);
-#endif
             if (!(nc < cnt && nc < 4 && height > 1)) continue;
             u32 k0;
             const u32 pi = parent_of(0, k, k0);
@@ -1360,49 +1337,6 @@ struct RegEngine {
         return insert_slot(f.k, f.cnt, (u32)f.slot + 1, right, true, rr, lc);
     }
 
-    // An insert inside segment `f.slot` of a block with room for two more children: splitAt and the
-    // insert as ONE edit of the block's row (the same result as split_at then insert_slot: left piece
-    // at s, the new segment at s+1, the right piece -- a copy of s cut at f.r -- at s+2, later slots
-    // two places on; the right piece's id is taken first).
-    SD bool split_insert(const RFound& f, RSeg rec, i32 seq) {
-        RG_PROF(RP_INSERT_SLOT);
-        const u32 s = (u32)f.slot, rr = (u32)f.r, k = f.k;
-        const u32 sid_r = new_sid();
-        if (sid_r == NONE) return false;
-        rec.sid = new_sid();
-        if (rec.sid == NONE) return false;
-        const u32 r = k >> 3, gb = gbase(k);
-        Row& w = rowref(r);
-        const V sl = L() & 7u;
-        const B ing = in_group(k);
-        const B mv = ing & (sl >= s + 2);       // take lane - 2: the right piece and the later slots
-        const B at = L() == gb + s + 1;         // the new segment
-        const B rp = L() == gb + s + 2;         // the right piece
-        const B lp = L() == gb + s;             // the left piece
-        const u32 ns = (simd::readlane(w.meta, gb) >> NS_SHIFT) & 3u;
-        auto put = [&](V& x, u32 val) MTE_LI {
-            x = simd::sel(mv, simd::row_shr2(x), x);
-            x = simd::sel(at, val, x);
-        };
-        put(w.len, rec.len);
-        put(w.seq, (u32)rec.seq);
-        put(w.rseq, rec.rseq);
-        put(w.meta, (rec.meta & ~NS_MASK) | (ns << NS_SHIFT));
-        put(w.toff, rec.toff);
-        put(w.cap, rec.cap);
-        put(w.rm, rec.rm);
-        put(w.sid, rec.sid);
-        // arena text (cap >= len) splits its capacity between the pieces; payload text has none
-        const B ar = (w.toff & ARENA_BIT) != 0u;
-        w.cap = simd::sel(rp, simd::sel(ar, w.cap - rr, 0u), simd::sel(lp, simd::sel(ar, simd::splat(rr), 0u), w.cap));
-        w.len = simd::sel(rp, w.len - rr, simd::sel(lp, simd::splat(rr), w.len));
-        w.toff = simd::sel(rp, w.toff + rr, w.toff);
-        w.sid = simd::sel(rp, simd::splat(sid_r), w.sid);
-        writeback(r);
-        if (seq > minSeq) add_lru(k, rec.sid, seq);
-        return status == 0;
-    }
-
     // insertSegments (mergeTree.ts:1968-1998): split at pos, then place the new segment.
     SD bool op_insert(i32 pos, i32 R, u32 C, i32 seq, RSeg rec) {
         RG_PROF(RP_INS);
@@ -1412,9 +1346,6 @@ struct RegEngine {
             return false;
         }
         u32 k = f.k, j;
-#ifndef MTE_NO_SPLIT_INSERT
-        if (f.slot >= 0 && f.r > 0 && f.cnt + 2 < 8 && rec.len != 0) return split_insert(f, rec, seq);
-#endif
         if (f.slot >= 0 && f.r > 0) {
             if (split_at(f) == NONE || status) return false;
             // the insertion point follows from the split: before the right piece, except when the

@@ -146,8 +146,6 @@ SD V g8_sum(V v) {
 // Lane l takes lane l-1 inside its 16-lane row (lane 0 of a row takes 0). Used with a mask whose
 // lanes never sit at a group start, so no value crosses an 8-lane group.
 SD V row_shr1(V v) { return {(u32)__builtin_amdgcn_update_dpp(0u, v.x, 0x111, 0xf, 0xf, false)}; }
-// Lane l takes lane l-2 inside its 16-lane row (lanes 0, 1 of a row take 0).
-SD V row_shr2(V v) { return {(u32)__builtin_amdgcn_update_dpp(0u, v.x, 0x112, 0xf, 0xf, false)}; }
 // Lane l takes lane l-1 across the whole wave (lane 0 takes 0): DPP wave_shr:1.
 SD V wave_shr1(V v) { return {(u32)__builtin_amdgcn_update_dpp(0u, v.x, 0x138, 0xf, 0xf, false)}; }
 
@@ -337,11 +335,6 @@ SD V g8_sum(V v) {
 SD V row_shr1(V v) {
     V r;
     MTE_L r.x[l] = (l & 15) ? v.x[l - 1] : 0u;
-    return r;
-}
-SD V row_shr2(V v) {
-    V r;
-    MTE_L r.x[l] = (l & 15) >= 2 ? v.x[l - 2] : 0u;
     return r;
 }
 SD V wave_shr1(V v) {

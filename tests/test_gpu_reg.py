@@ -153,5 +153,5 @@ def test_bulk_rows_kernel_matches_oracle(engine, kind, waves):
         assert engine.run_info()["spilled"] > 0
         _check(engine, batch, n_docs=64)
     finally:
-        engine.set_option("rows_bulk", 0)
+        engine.set_option("rows_bulk", -1)
         engine.set_option("reg_lb_limit", 0)

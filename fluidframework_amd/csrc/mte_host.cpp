@@ -1150,7 +1150,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     if (groups) HIP_TRY(e, launch_lds(e->P, gen, full, groups, s_main));
     if (rows) {
         const uint32_t cus = bulk_cus(e, n_solo);
-        const uint32_t per = rows >= 8 ? 8u : 4u;
+        const uint32_t per = rows >= 12 ? 12u : rows >= 8 ? 8u : 4u;
         HIP_TRY(e, launch_rows(e->P, per, std::min<uint32_t>(cus, (nd - n_solo + per - 1) / per), s_main));
     }
     // k_hbmq: one workgroup (wave) per document; those that find the queue drained exit at once
@@ -2470,7 +2470,7 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "emit") e->emit_opt = value != 0;  // SnapshotV1 emission on the device after replay
     else if (k == "xcd_align") e->xcd_align = value != 0;
     else if (k == "solo_gate") e->solo_gate = value != 0;
-    else if (k == "rows_bulk") e->rows_bulk = value < 0 ? -1 : value == 0 ? 0 : value >= 8 ? 8 : 4;  // lean bulk on k_rows
+    else if (k == "rows_bulk") e->rows_bulk = value < 0 ? -1 : value == 0 ? 0 : value >= 12 ? 12 : value >= 8 ? 8 : 4;  // lean bulk on k_rows
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;

@@ -45,6 +45,10 @@ constexpr u32 RG_HEAP = 511;              // LRU heap positions 1..511
 constexpr u32 RSEQ_LIVE = 0x7FFFFFFFu;    // removedSeq of a live segment (never <= a refSeq)
 constexpr u32 RCL_LIVE = 0xFFu;           // removedClient byte of a live segment (never a client)
 constexpr i32 REG_HANDOFF = 101;          // internal: continue in the LDS engine from the current op
+// k_rows' shared row pool: 79 slot rows (vis array, then aux array) and its row mask, 160 KiB of LDS
+constexpr u32 ROWS_POOL = 79, ROWS_POOL_WORDS = 3;
+constexpr u32 ROWS_POOL_VIS = 0, ROWS_POOL_AUX = ROWS_POOL * 64 * 16, ROWS_POOL_MASK = ROWS_POOL * 64 * 32;
+constexpr u32 ROWS_LDS_BYTES = ROWS_POOL_MASK + ROWS_POOL_WORDS * 4;
 // needsScour (mergeTree.ts:63) in meta bits 24..25 of every slot lane of a block
 constexpr u32 NS_SHIFT = 24, NS_MASK = 3u << NS_SHIFT;
 static_assert(RG_BLOCKS <= SOLO_POOL, "the rows live in the SoloPlan's slot arrays");
@@ -120,7 +124,10 @@ struct RFound {
     u32 carry; // visible length before that row
 };
 
-template <int NR = (int)RG_ROWS>
+// PAGED (k_rows): logical row r of the document lives in pool row ptab[r] of a pool the CU's waves
+// share (rows_pool_*), taken as the document grows and given back as it shrinks or ends; a document
+// the pool cannot grow is spilled (REG_HANDOFF, re-run by the host). Otherwise row r is slot row r.
+template <int NR = (int)RG_ROWS, bool PAGED = false>
 struct RegEngine {
     typedef simd::V V;
     typedef simd::B B;
@@ -181,45 +188,86 @@ struct RegEngine {
     u32 seg_cap, arena_cap, payload_len;
 
     // ---------------------------------------------------------------- slot rows (LDS)
+    // ---------------------------------------------------------------- paged rows
+    V ptab = simd::splat(0);  // lane r: pool row of logical row r (PAGED)
+    u32 n_rows = 0;           // logical rows taken from the pool (PAGED)
+    SD u32 prow(u32 r) const {
+        if constexpr (PAGED) return simd::readlane(ptab, r);
+        else return r;
+    }
 #ifdef MTE_CPU
     u32 mem_vis[RG_ROWS * 64][4], mem_aux[RG_ROWS * 64][4];
+    u64 pool_mask = 0;           // PAGED: pool rows in use (this engine's own pool on the CPU)
+    u32 pool_rows = RG_ROWS, pool_takes = 0;
+    SD u32 pslot(u32 s) const { return PAGED ? prow(s >> 6) * 64 + (s & 63) : s; }
+    SD bool take_row(u32& row) {  // a scattered order, so logical and pool rows differ
+        for (u32 t = 0; t < pool_rows; t++) {
+            const u32 c = (pool_takes * 7 + 3 + t) % pool_rows;
+            if (!((pool_mask >> c) & 1)) {
+                pool_mask |= 1ull << c;
+                pool_takes++;
+                row = c;
+                return true;
+            }
+        }
+        return false;
+    }
+    SD void give_row(u32 row) { pool_mask &= ~(1ull << row); }
+    SD void zero_prow(u32 row) {
+        memset(mem_vis[row * 64], 0, 64 * 16);
+        memset(mem_aux[row * 64], 0, 64 * 16);
+    }
     SD Row ldrow(u32 r) const {
         Row w;
+        const u32 pr = prow(r);
         for (u32 l = 0; l < 64; l++) {
-            const u32* v = mem_vis[r * 64 + l];
-            const u32* a = mem_aux[r * 64 + l];
+            const u32* v = mem_vis[pr * 64 + l];
+            const u32* a = mem_aux[pr * 64 + l];
             w.len.x[l] = v[0], w.seq.x[l] = v[1], w.rseq.x[l] = v[2], w.meta.x[l] = v[3];
             w.cap.x[l] = a[0], w.toff.x[l] = a[1], w.rm.x[l] = a[2], w.sid.x[l] = a[3];
         }
         return w;
     }
     SD void strow(u32 r, const Row& w) {
+        const u32 pr = prow(r);
         for (u32 l = 0; l < 64; l++) {
-            u32* v = mem_vis[r * 64 + l];
-            u32* a = mem_aux[r * 64 + l];
+            u32* v = mem_vis[pr * 64 + l];
+            u32* a = mem_aux[pr * 64 + l];
             v[0] = w.len.x[l], v[1] = w.seq.x[l], v[2] = w.rseq.x[l], v[3] = w.meta.x[l];
             a[0] = w.cap.x[l], a[1] = w.toff.x[l], a[2] = w.rm.x[l], a[3] = w.sid.x[l];
         }
     }
     SD V ldf(u32 r, u32 aux, u32 c) const {  // one field of a row
         V x;
-        for (u32 l = 0; l < 64; l++) x.x[l] = aux ? mem_aux[r * 64 + l][c] : mem_vis[r * 64 + l][c];
+        const u32 pr = prow(r);
+        for (u32 l = 0; l < 64; l++) x.x[l] = aux ? mem_aux[pr * 64 + l][c] : mem_vis[pr * 64 + l][c];
         return x;
     }
     SD void stf(u32 r, u32 aux, u32 c, V x, B m) {
+        const u32 pr = prow(r);
         for (u32 l = 0; l < 64; l++)
-            if ((m.m >> l) & 1) (aux ? mem_aux[r * 64 + l] : mem_vis[r * 64 + l])[c] = x.x[l];
+            if ((m.m >> l) & 1) (aux ? mem_aux[pr * 64 + l] : mem_vis[pr * 64 + l])[c] = x.x[l];
     }
     // slot-index memmove (blocks move as whole 8-slot groups)
     SD void mv_slots(u32 dst, u32 src, u32 n) {
         cr = NONE;
-        memmove(mem_vis[dst], mem_vis[src], (size_t)n * 16);
-        memmove(mem_aux[dst], mem_aux[src], (size_t)n * 16);
+        if (!PAGED) {
+            memmove(mem_vis[dst], mem_vis[src], (size_t)n * 16);
+            memmove(mem_aux[dst], mem_aux[src], (size_t)n * 16);
+            return;
+        }
+        for (u32 t = 0; t < n; t++) {  // slot by slot in the memmove's safe direction
+            const u32 i = dst > src ? n - 1 - t : t;
+            memcpy(mem_vis[pslot(dst + i)], mem_vis[pslot(src + i)], 16);
+            memcpy(mem_aux[pslot(dst + i)], mem_aux[pslot(src + i)], 16);
+        }
     }
     SD void zero_slots(u32 at, u32 n) {
         cr = NONE;
-        memset(mem_vis[at], 0, (size_t)n * 16);
-        memset(mem_aux[at], 0, (size_t)n * 16);
+        for (u32 i = 0; i < n; i++) {
+            memset(mem_vis[pslot(at + i)], 0, 16);
+            memset(mem_aux[pslot(at + i)], 0, 16);
+        }
     }
 #else
     // the rows' two LDS arrays (byte offsets into the dynamic LDS): the SoloPlan's slot arrays for
@@ -227,24 +275,60 @@ struct RegEngine {
     u32 vbase = (u32)offsetof(SoloPlan, vis), abase = (u32)offsetof(SoloPlan, aux);
     SD uint4* VISP() const { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + vbase); }
     SD uint4* AUXP() const { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + abase); }
+    u32 pool_off = 0;  // PAGED: byte offset of the pool's row mask (ROWS_POOL_WORDS words)
+    SD u32* pool_words() const { return reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + pool_off); }
+    SD bool take_row(u32& row) {  // lane 0 claims a free pool row with an LDS atomic or
+        u32 got = NONE;
+        if (__lane_id() == 0) {
+            u32* m = pool_words();
+            for (u32 wd = 0; wd < ROWS_POOL_WORDS && got == NONE; wd++) {
+                u32 cur = __hip_atomic_load(m + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                while (~cur) {
+                    const u32 bit = 1u << __builtin_ctz(~cur);
+                    const u32 old = atomicOr(m + wd, bit);
+                    if (!(old & bit)) {
+                        got = wd * 32 + (u32)__builtin_ctz(bit);
+                        break;
+                    }
+                    cur = old | bit;
+                }
+            }
+        }
+        got = simd::readlane(simd::V{got}, 0);
+        row = got;
+        return got != NONE;
+    }
+    SD void give_row(u32 row) {
+        if (__lane_id() == 0) atomicAnd(pool_words() + (row >> 5), ~(1u << (row & 31)));
+    }
+    SD void zero_prow(u32 row) {
+        VISP()[row * 64 + __lane_id()] = make_uint4(0, 0, 0, 0);
+        AUXP()[row * 64 + __lane_id()] = make_uint4(0, 0, 0, 0);
+        simd::lds_order();
+    }
+    // physical slot of logical slot s, per lane (PAGED: a block range can cross pool rows)
+    SD u32 pslot(u32 s) const {
+        if constexpr (PAGED) return simd::bperm(ptab, simd::V{s >> 6}).x * 64u + (s & 63u);
+        else return s;
+    }
     SD Row ldrow(u32 r) const {
-        const u32 i = r * 64 + __lane_id();
+        const u32 i = prow(r) * 64 + __lane_id();
         const uint4 v = VISP()[i], a = AUXP()[i];
         return Row{V{v.x}, V{v.y}, V{v.z}, V{v.w}, V{a.x}, V{a.y}, V{a.z}, V{a.w}};
     }
     SD void strow(u32 r, const Row& w) {
-        const u32 i = r * 64 + __lane_id();
+        const u32 i = prow(r) * 64 + __lane_id();
         VISP()[i] = make_uint4(w.len.x, w.seq.x, w.rseq.x, w.meta.x);
         AUXP()[i] = make_uint4(w.cap.x, w.toff.x, w.rm.x, w.sid.x);
         simd::lds_order();
     }
     SD V ldf(u32 r, u32 aux, u32 c) const {
         const u32* b = reinterpret_cast<const u32*>(aux ? AUXP() : VISP());
-        return V{b[(r * 64 + __lane_id()) * 4 + c]};
+        return V{b[(prow(r) * 64 + __lane_id()) * 4 + c]};
     }
     SD void stf(u32 r, u32 aux, u32 c, V x, B m) {
         u32* b = reinterpret_cast<u32*>(aux ? AUXP() : VISP());
-        if (simd::lane_of(m)) b[(r * 64 + __lane_id()) * 4 + c] = x.x;
+        if (simd::lane_of(m)) b[(prow(r) * 64 + __lane_id()) * 4 + c] = x.x;
         simd::lds_order();
     }
     // Overlapping slot move, one 64-slot chunk per LDS round trip. (Issuing eight chunks' reads
@@ -254,6 +338,27 @@ struct RegEngine {
         uint4* V4 = VISP();
         uint4* A4 = AUXP();
         const u32 L = __lane_id();
+        if constexpr (PAGED) {  // the same chunks, each lane's slots mapped through ptab
+            const bool up = dst > src;
+            for (u32 c = 0; c < n; c += 64) {
+                const i32 i = up ? (i32)(n - c) - 64 + (i32)L : (i32)(c + L);
+                const bool ok = i >= 0 && (u32)i < n;
+                const u32 ii = ok ? (u32)i : 0u;
+                const u32 ps = pslot(src + ii), pd = pslot(dst + ii);
+                uint4 v = make_uint4(0, 0, 0, 0), a = v;
+                if (ok) {
+                    v = V4[ps];
+                    a = A4[ps];
+                }
+                simd::lds_order();
+                if (ok) {
+                    V4[pd] = v;
+                    A4[pd] = a;
+                }
+                simd::lds_order();
+            }
+            return;
+        }
         if (dst > src) {
             for (i32 b = (i32)n - 64; b > -64; b -= 64) {
                 const i32 i = b + (i32)L;
@@ -288,9 +393,13 @@ struct RegEngine {
     }
     SD void zero_slots(u32 at, u32 n) {
         cr = NONE;
-        for (u32 b = __lane_id(); b < n; b += 64) {
-            VISP()[at + b] = make_uint4(0, 0, 0, 0);
-            AUXP()[at + b] = make_uint4(0, 0, 0, 0);
+        for (u32 c = 0; c < n; c += 64) {
+            const u32 b = c + __lane_id();
+            const u32 ps = pslot(at + (b < n ? b : 0u));
+            if (b < n) {
+                VISP()[ps] = make_uint4(0, 0, 0, 0);
+                AUXP()[ps] = make_uint4(0, 0, 0, 0);
+            }
         }
         simd::lds_order();
     }
@@ -326,12 +435,44 @@ struct RegEngine {
     }
     SD void writeback(u32 r) { strow(r, cw); }
 
+    // PAGED: logical rows [n_rows, need) from the pool, zeroed (rows past the last block stay zero)
+    SD bool grow_rows(u32 need) {
+        while (n_rows < need) {
+            u32 row;
+            if (n_rows >= (u32)NR || !take_row(row)) return false;
+            zero_prow(row);
+            ptab = simd::writelane(ptab, n_rows, row);
+            n_rows++;
+        }
+        return true;
+    }
+    SD void shrink_rows(u32 keep) {
+        cr = NONE;
+        while (n_rows > keep) give_row(prow(--n_rows));
+    }
+    SD void release_rows() {
+        if constexpr (PAGED) shrink_rows(0);
+    }
+    // Room for leaf blocks [0, nb): PAGED takes pool rows (none left: spill the document, the host
+    // re-runs it); otherwise the fixed rows must hold them.
+    SD bool ensure_blocks(u32 nb) {
+        if constexpr (PAGED) {
+            if (grow_rows((nb + 7) >> 3)) return true;
+            fail(REG_HANDOFF, curSeq);
+        } else {
+            if (nb <= NBLK) return true;
+            fail(MTE_DOC_CAPACITY, curSeq);
+        }
+        return false;
+    }
+
     SD RegEngine(const Params& p_, u32 doc_) : p(p_), doc(doc_) { setup(); }
 #ifndef MTE_CPU
     // rows in another LDS region (k_rows: one share of the CU's LDS per wave)
-    SD RegEngine(const Params& p_, u32 doc_, u32 vb, u32 ab, u32 mode) : p(p_), doc(doc_) {
+    SD RegEngine(const Params& p_, u32 doc_, u32 vb, u32 ab, u32 mode, u32 pool = 0) : p(p_), doc(doc_) {
         vbase = vb;
         abase = ab;
+        pool_off = pool;
         res_mode = mode;
         setup();
     }
@@ -347,7 +488,12 @@ struct RegEngine {
         init();
     }
     SD void init() {
-        zero_slots(0, NBLK * 8);  // every slot empty: rows past the last block stay zero
+        if constexpr (PAGED) {
+            n_rows = 0;
+            ptab = simd::splat(0);
+        } else {
+            zero_slots(0, NBLK * 8);  // every slot empty: rows past the last block stay zero
+        }
         LV.zero();
         HK.zero();
         HS.zero();
@@ -364,6 +510,8 @@ struct RegEngine {
 #if defined(MTE_PROFILE) && !defined(MTE_CPU)
         for (u32 i = 0; i < RP_N; i++) pf[i] = 0;
 #endif
+        if constexpr (PAGED)
+            if (!grow_rows(1)) status = REG_HANDOFF;
     }
 
     SD static V L() { return simd::lanes(); }
@@ -581,10 +729,7 @@ struct RegEngine {
     SD void split_block(u32 k) {
         RG_PROF(RP_SPLIT);
         RG_COUNT(RP_N_SPLIT_BLK, 1);
-        if (n_lb + 1 > NBLK) {
-            fail(MTE_DOC_CAPACITY, curSeq);
-            return;
-        }
+        if (!ensure_blocks(n_lb + 1)) return;
         shift_blocks(k + 1, 1);
         const u32 r = k >> 3, r2 = (k + 1) >> 3;
         const V sl = L() & 7u;
@@ -1186,10 +1331,7 @@ struct RegEngine {
         if (kk > 7) kk = 7;
         if (kk < 1) kk = 1;
         const u32 base = T / kk, extra = T % kk;
-        if (n_lb + kk > NBLK + m) {
-            fail(MTE_DOC_CAPACITY, curSeq);
-            return;
-        }
+        if (!ensure_blocks(n_lb + kk - m)) return;
         // item t (lane t < T) of the concatenated children: block k0 + sib, slot q
         V sib = simd::splat(0), q = L();
         for (u32 i = 0; i < m; i++) {
@@ -1423,9 +1565,17 @@ struct RegEngine {
 
     // Room for one more op (margins for the splits, packs and heap pushes an op can cause);
     // false => hand the document to the LDS engine before this op.
-    SD bool room() const {
+    SD bool room() {
         // level-1 nodes hold >= 1 leaf block each, so fewer than 57 blocks cannot reach lane 56 (and
         // the readlane, a VALU -> SALU round trip, is skipped)
+        if constexpr (PAGED) {
+            // rows are taken as blocks appear (ensure_blocks), so no block margin; pool rows past
+            // the last block's row and one spare go back
+            const u32 keep = ((n_lb + 7) >> 3) + 1;
+            if (n_rows > keep) shrink_rows(keep);
+            return n_lb + 4 <= lb_lim && heapSize + n_lb + 8 < RG_HEAP && height + 2 <= RG_LEVELS &&
+                   (n_lb < 57 || simd::readlane(LV.get(0), 56) == 0u);
+        }
         return n_lb + 16 <= lb_lim && heapSize + n_lb + 8 < RG_HEAP && height + 2 <= RG_LEVELS &&
                (n_lb < 57 || simd::readlane(LV.get(0), 56) == 0u);
     }

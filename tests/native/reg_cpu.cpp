@@ -11,16 +11,16 @@
 
 using namespace mte;
 
-extern "C" {
 
 // Replays one document's op records. Outputs are the engine's own final rows (LDS-engine format:
 // vis = len, seq, removedSeq, meta; aux = props, text offset, text capacity / overlap, segment id),
 // the gathered text, and the DocRes record. Returns the op index the replay stopped at (n_ops when
 // done or failed; earlier when the document would hand over to the LDS engine).
-uint64_t regcpu_replay(const mte_op* ops, uint64_t n_ops, const uint16_t* payload, uint32_t payload_len,
-                       uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
-                       uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
-                       DocRes* res) {
+template <bool PAGED>
+static uint64_t replay_impl(const mte_op* ops, uint64_t n_ops, const uint16_t* payload, uint32_t payload_len,
+                            uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
+                            uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
+                            DocRes* res, uint32_t pool_rows) {
     std::vector<uint16_t> pay(payload, payload + payload_len + 1);
     std::vector<uint16_t> arena((size_t)arena_cap * 2 + 1, 0);
     DocCfg cfg;
@@ -47,18 +47,47 @@ uint64_t regcpu_replay(const mte_op* ops, uint64_t n_ops, const uint16_t* payloa
     p.out_text = out_text;
     p.out_text_cap = out_text_cap;
     p.counters = counters;
-    RegEngine<> e(p, 0);
-    const uint64_t at = e.replay(0, n_ops);
+    // (the paged engine's pool is its own row arrays here, rows taken in a scattered order)
+    RegEngine<(int)RG_ROWS, PAGED>* ep = new RegEngine<(int)RG_ROWS, PAGED>(p, 0);
+    RegEngine<(int)RG_ROWS, PAGED>& e = *ep;
+    if (PAGED) {
+        e.release_rows();
+        e.pool_rows = pool_rows < RG_ROWS ? pool_rows : RG_ROWS;
+        e.init();
+    }
+    const uint64_t at = e.status ? 0 : e.replay(0, n_ops);
     if (e.status == REG_HANDOFF) {
         memset(res, 0, sizeof *res);
         res->status = REG_HANDOFF;
         res->n_lb = e.n_lb;
         res->heap_size = e.heapSize;
         res->height = e.height;
+        delete ep;
         return at;
     }
     e.finish();
+    delete ep;
     return at;
+}
+
+extern "C" {
+
+uint64_t regcpu_replay(const mte_op* ops, uint64_t n_ops, const uint16_t* payload, uint32_t payload_len,
+                       uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
+                       uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
+                       DocRes* res) {
+    return replay_impl<false>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
+                              out_cap, out_text, out_text_cap, res, 0);
+}
+
+// The PAGED engine (k_rows): logical rows mapped to pool rows taken in a scattered order from a pool
+// of pool_rows rows; a document the pool cannot hold stops with REG_HANDOFF (k_rows spills it).
+uint64_t regcpu_replay_paged(const mte_op* ops, uint64_t n_ops, const uint16_t* payload, uint32_t payload_len,
+                             uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
+                             uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
+                             DocRes* res, uint32_t pool_rows) {
+    return replay_impl<true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
+                             out_cap, out_text, out_text_cap, res, pool_rows);
 }
 
 uint32_t regcpu_docres_size(void) { return (uint32_t)sizeof(DocRes); }

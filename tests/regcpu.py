@@ -34,6 +34,8 @@ def lib():
         vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
         L.regcpu_replay.restype = u64
         L.regcpu_replay.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u32, vp, u64, vp]
+        L.regcpu_replay_paged.restype = u64
+        L.regcpu_replay_paged.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u32, vp, u64, vp, u32]
         L.regcpu_docres_size.restype = u32
         L.regcpu_heap.restype = u32
         L.regcpu_heap.argtypes = [vp, u32, vp]
@@ -42,9 +44,10 @@ def lib():
     return _lib
 
 
-def replay(ops, pay, arena_cap=None):
+def replay(ops, pay, arena_cap=None, pool_rows=None):
     """Replay op records (numpy, oracle._op_dtype) + payload (uint16) on the CPU build of the register
-    engine. Returns (stop index, DocRes record, rows [(vis, aux, ovl)], text uint16 array)."""
+    engine (pool_rows: the PAGED engine of k_rows, rows from a pool of that many). Returns (stop
+    index, DocRes record, rows [(vis, aux, ovl)], text uint16 array)."""
     ops = np.ascontiguousarray(ops, dtype=_op_dtype())
     pay = np.ascontiguousarray(pay, dtype=np.uint16)
     n = len(ops)
@@ -58,8 +61,12 @@ def replay(ops, pay, arena_cap=None):
     text = np.zeros(len(pay) + 16, dtype=np.uint16)
     res = np.zeros(1, dtype=DOCRES)
     pay1 = np.concatenate([pay, np.zeros(1, dtype=np.uint16)])
-    at = lib().regcpu_replay(ops.ctypes.data, n, pay1.ctypes.data, len(pay), seg_cap, arena_cap, vis.ctypes.data,
-                             aux.ctypes.data, ovl.ctypes.data, cap, text.ctypes.data, len(text), res.ctypes.data)
+    args = (ops.ctypes.data, n, pay1.ctypes.data, len(pay), seg_cap, arena_cap, vis.ctypes.data, aux.ctypes.data,
+            ovl.ctypes.data, cap, text.ctypes.data, len(text), res.ctypes.data)
+    if pool_rows is None:
+        at = lib().regcpu_replay(*args)
+    else:
+        at = lib().regcpu_replay_paged(*args, pool_rows)
     r = res[0]
     k = int(r["n_segs"])
     return at, r, (vis[:k], aux[:k], ovl[:k]), text
@@ -157,13 +164,13 @@ def generated(kind, gid, n_ops, n_clients=8, seed=0):
     return OracleDoc().generate(kind, gid, n_ops, n_clients=n_clients, seed=seed, export=True)
 
 
-def compare(ops, pay, names=None, arena_cap=None):
+def compare(ops, pay, names=None, arena_cap=None, pool_rows=None):
     """Replay on the CPU register engine and on the oracle; assert identical status, segment table
     and text. Returns the engine's DocRes record."""
     if names is None:
         nc = int(ops["client"].max()) if len(ops) else 0
         names = ["__observer__"] + [f"w{i}" for i in range(1, max(nc, 1) + 1)]
-    at, res, rows, text = replay(ops, pay, arena_cap=arena_cap)
+    at, res, rows, text = replay(ops, pay, arena_cap=arena_cap, pool_rows=pool_rows)
     assert int(res["status"]) != REG_HANDOFF, f"register engine handed off at op {at} (n_lb {res['n_lb']})"
     ob = OneDocBatch(ops, pay, names)
     o = ob.oracle()

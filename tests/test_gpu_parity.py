@@ -300,10 +300,15 @@ def test_slot_overflow_reruns_with_worst_case_capacity(engine):
 def test_long_documents_match_oracle(engine):
     """50k-op documents: merge chains that append in place and then outgrow their chunk within one
     scour (the copy of the head must not read bytes the same batch has yet to write), arena GC,
-    LDS-to-HBM continuation."""
+    LDS-to-HBM continuation (a 40-block LDS pool per CU: the 255-entry heap keeps these documents in
+    a full pool to the end)."""
     engine.generate(2, 16, 50000, n_clients=8, seed=1000)
     batch = engine.export_batch()
-    engine.replay()
+    engine.set_option("pool_limit", 40)
+    try:
+        engine.replay()
+    finally:
+        engine.set_option("pool_limit", 0)
     assert engine.run_info()["continued"] > 0
     bad, _, _ = compare_batch_checksums(engine, batch)
     if bad:

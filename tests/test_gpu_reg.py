@@ -122,12 +122,13 @@ def test_row_engine_markers_and_builder_logs(engine):
 MODE_BULK_ROWS = 5  # DocRes.mode: k_rows (bulk documents on the row engine)
 
 
-@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("waves", [4, 8, 12])
 @pytest.mark.parametrize("kind", [2, 5])
 def test_bulk_rows_kernel_matches_oracle(engine, kind, waves):
-    """Lean bulk documents on k_rows (4 or 8 single-document waves per CU, rows in a share of the
-    LDS): a Zipf mix whose longest document stays on k_solo, every other one on the rows, checksums
-    against the oracle; then 31-writer documents that outgrow the rows and are re-run HBM-resident."""
+    """Lean bulk documents on k_rows (4, 8 or 12 single-document waves per CU, slot rows from one
+    79-row LDS pool per CU): a Zipf mix whose longest document stays on k_solo, every other one on
+    the rows, checksums against the oracle; then documents held to 24 leaf blocks (reg_lb_limit) that
+    are re-run HBM-resident."""
     from fluidframework_amd.shard import zipf_op_counts
 
     engine.set_option("reg_lb_limit", 0)
@@ -139,8 +140,8 @@ def test_bulk_rows_kernel_matches_oracle(engine, kind, waves):
         st = engine.replay()
         assert st["failed_docs"] == 0 and engine.get_info("rows") == waves
         modes = [engine.doc_result(d)["mode"] for d in range(len(counts))]
-        # the longest documents may take k_solo (4); a document that outgrows the rows (8 waves: 64
-        # leaf blocks) is re-run HBM-resident (1)
+        # the longest documents may take k_solo (4); a document the pool cannot grow is re-run
+        # HBM-resident (1)
         assert set(modes) <= {MODE_BULK_ROWS, MODE_ROWS, 1} and modes.count(MODE_BULK_ROWS) > 0.9 * len(counts), sorted(set(modes))
         _check(engine, batch, n_docs=len(counts))
         # documents that outgrow the rows (reg_lb_limit shrinks them) go back to the host, which
@@ -155,3 +156,26 @@ def test_bulk_rows_kernel_matches_oracle(engine, kind, waves):
     finally:
         engine.set_option("rows_bulk", -1)
         engine.set_option("reg_lb_limit", 0)
+
+
+@pytest.mark.parametrize("waves", [8, 12])
+def test_bulk_rows_pool_shared_and_exhausted(engine, waves):
+    """C2-shaped documents (kind 2, 10^4 ops, 8 writers, leaf blocks peaking near 100) on the shared
+    row pool, bit-exact against the oracle; then 31-writer documents too large for twelve (or eight)
+    at once in 79 rows: the waves that cannot grow spill mid-op and the host re-runs them."""
+    engine.set_option("rows_bulk", waves)
+    try:
+        engine.generate(2, 2048, 10_000, n_clients=8, seed=1000)
+        batch = engine.export_batch()
+        st = engine.replay()
+        assert st["failed_docs"] == 0 and engine.get_info("rows") == waves
+        modes = [engine.doc_result(d)["mode"] for d in range(2048)]
+        assert modes.count(MODE_BULK_ROWS) > 0.9 * 2048, sorted(set(modes))
+        _check(engine, batch, n_docs=2048)
+        engine.generate(2, 1024, 4000, n_clients=31, seed=4)
+        batch = engine.export_batch()
+        st = engine.replay()
+        assert st["failed_docs"] == 0 and engine.run_info()["spilled"] > 0
+        _check(engine, batch, n_docs=1024)
+    finally:
+        engine.set_option("rows_bulk", -1)

@@ -38,6 +38,25 @@ def test_arena_compaction(arena_cap):
     assert int(r["n_gc"]) > 10
 
 
+@pytest.mark.parametrize("kind", [2, 5])
+def test_paged_rows_match_oracle(kind):
+    """k_rows' PAGED engine: logical rows in pool rows taken in a scattered order as the document
+    grows and given back as it shrinks (block moves and splits cross pool rows), bit-exact with the
+    oracle; C2-shaped documents whose leaf blocks peak near 100."""
+    for gid in (256, 1792, 3584):
+        ops, pay = regcpu.generated(kind, gid, 10_000, n_clients=8, seed=1000)
+        r = regcpu.compare(ops, pay, pool_rows=32)
+        assert int(r["max_lb"]) > 16
+
+
+def test_paged_pool_exhausted_spills():
+    """A pool too small for the document stops it with REG_HANDOFF (k_rows marks it for the host's
+    re-run) instead of failing it."""
+    ops, pay = regcpu.generated(2, 256, 10_000, n_clients=8, seed=1000)
+    at, res, _, _ = regcpu.replay(ops, pay, pool_rows=4)
+    assert int(res["status"]) == regcpu.REG_HANDOFF and 0 < at < len(ops)
+
+
 def test_outgrows_the_rows_and_hands_off():
     """31 concurrent writers keep hundreds of tombstones and heap entries in the collaboration window:
     the document outgrows the row plan's margins (leaf blocks, level-1 nodes or heap) and would hand

@@ -1,5 +1,5 @@
 """Per-pass HBM traffic of the replay for bench.py's roofline (`traffic`), from tools/profile.sh's
-FETCH_SIZE and WRITE_SIZE passes, corrected with the gfx950 calibration of profiles/fetch_calib_r03.json
+FETCH_SIZE and WRITE_SIZE passes, corrected with the gfx950 calibration of profiles/fetch_calib_r04.json
 (FETCH_SIZE x 2 for the engine's coalesced dword / 16-B reads, WRITE_SIZE x 1).
 
 rocprofv3 serialises dispatches while it collects counters, so in these passes k_lds takes every
@@ -22,7 +22,7 @@ def main(tag, config="C4"):
     import bench
     from fluidframework_amd.shard import plan_shard
 
-    cal = json.load(open(os.path.join(ROOT, "profiles", "fetch_calib_r03.json")))
+    cal = json.load(open(os.path.join(ROOT, "profiles", "fetch_calib_r04.json")))
     c = bench.CONFIGS[config]
     ids, counts = plan_shard(config, 1, 0, c["docs"], c["ops"])
     per = defaultdict(lambda: defaultdict(float))
@@ -44,7 +44,7 @@ def main(tag, config="C4"):
         total += corr
     out = {"docs": len(ids), "ops": int(counts.sum()), "kind": c["kind"], "tag": tag, "passes": steps,
            "hbm_bytes_per_launch": total, "kernels": kernels,
-           "correction": "FETCH_SIZE x %.1f, WRITE_SIZE x %.1f (profiles/fetch_calib_r03.json)" % (cal["fetch_factor"], cal["write_factor"]),
+           "correction": "FETCH_SIZE x %.1f, WRITE_SIZE x %.1f (profiles/fetch_calib_r04.json)" % (cal["fetch_factor"], cal["write_factor"]),
            "note": "rocprofv3 serialises dispatches while collecting: per-kernel split of the serialised pass"}
     path = os.path.join(ROOT, "profiles", f"pmc_replay_{config}.json")
     json.dump(out, open(path, "w"), indent=1)

@@ -5,8 +5,9 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/re
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/re/gpu_tests.log 2>&1 || { tail -30 gpurun_out/re/gpu_tests.log; exit 1; }
-tail -2 gpurun_out/re/gpu_tests.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/re/gpu_tests.log 2>&1; rc=$?
+grep -E "FAILED" gpurun_out/re/gpu_tests.log | tail -20; tail -2 gpurun_out/re/gpu_tests.log
+[ $rc -le 1 ] || exit 1  # a crash or time limit (not a failed assertion) ends the call
 T=re bash tools/r04_ab.sh base cur || exit 1
 T=re EXTRA="--no-cpu-baseline" bash tools/r04_bench_ab.sh "C2:" "C2:rows_bulk=4" || exit 1
 T=re5 EXTRA="--no-cpu-baseline --kind 5" bash tools/r04_bench_ab.sh "C2:" "C2:rows_bulk=4" "C2:rows_bulk=8" || exit 1

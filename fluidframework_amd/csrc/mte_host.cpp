@@ -328,8 +328,8 @@ struct mte_engine {
     // SnapshotV1 emission on the device (emit.hip): property / name tables, scratch, and two output
     // pools -- round 0 (every document but the solo ones) runs while the critical path is still
     // replaying, round 1 (solo and host-re-run documents) after it
-    int32_t rows_bulk = -1;   // option "rows_bulk": lean replays run the bulk on k_rows, 4 or 8 waves per CU;
-                              // -1 (auto): 4 when every bulk document gets a row wave at once, 0: never
+    int32_t rows_bulk = -1;   // option "rows_bulk": lean replays run the bulk on k_rows, 4, 8 or 12 waves per
+                              // CU; -1 (auto: 4 for long documents, 8 without solo documents), 0: never
     bool xcd_align = true;    // option "xcd_align": bulk grids leave solo CUs free in every XCD (bulk_cus)
     uint32_t last_rows = 0;   // waves per CU of the last pass's k_rows (0: k_lds / k_hbmq)
     bool emit_opt = true;     // option "emit"
@@ -1102,16 +1102,18 @@ static int run_kernel(mte_engine* e, bool gen) {
     const int full = gen ? 1 : e->ext_needed ? 2 : (e->lean_ok && e->lean_opt) ? 0 : 1;
     e->last_lean = full == 0;
     wave_plan(e, nd, groups, hbm_waves, &lds_active, n_solo);
-    // lean replays may run the bulk on the row engine instead (k_rows; DOC_SPILL re-runs as below)
-    // k_rows: lean replays whose bulk documents all get a row wave at once (C5: 1 024 documents of
-    // 10^6 ops, 4.4 s per step against 9.8 s on k_lds / k_hbmq); a batch of many short documents
-    // (C2: 4 096 x 10^4 ops, 282 vs 171 ms) keeps the sixteen LDS / HBM waves per CU
+    // Lean replays run the bulk on the row engine (k_rows; DOC_SPILL re-runs as below): 4 waves per
+    // CU when every bulk document of a long-document batch gets a SIMD of its own (C5: 1 024 x 10^6
+    // ops, 4.4 s per step against 9.8 s on k_lds / k_hbmq), else 8 (two per SIMD on the shared row
+    // pool; C2: 4 096 x 10^4 ops, 110 ms against 166 ms on the sixteen LDS / HBM waves per CU). A
+    // batch with solo documents keeps k_lds beside them: its pass is the critical path's anyway, and
+    // k_lds continues a document that outgrows LDS in HBM instead of re-running it from its first op.
     uint32_t rows = 0;
     if (!gen && full == 0 && e->rows_bulk && !e->force_hbm && nd > n_solo) {
         uint64_t bulk_ops = 0;
         for (uint32_t k = n_solo; k < nd; k++) bulk_ops += e->n_ops_doc[e->order[k]];
         const bool long_docs = nd - n_solo <= 4 * bulk_cus(e, n_solo) && bulk_ops >= 200000ull * (nd - n_solo);
-        rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : long_docs ? 4u : 0u;
+        rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : long_docs ? 4u : n_solo == 0 ? 8u : 0u;
     }
     e->last_rows = rows;
     if (rows) groups = hbm_waves = lds_active = 0;

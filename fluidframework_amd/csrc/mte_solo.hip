@@ -108,21 +108,31 @@ __global__ __launch_bounds__(64 * SOLO_WAVES) __attribute__((amdgpu_waves_per_eu
 #endif
 }
 
-// Bulk lean documents on the row engine (reg_engine.hpp): RW single-SIMD waves per CU (4, or 8 = two
-// per SIMD), each with its SIMD's register file (or half of it), replay one document after another
-// from the LPT queue. Their slot rows come from ONE pool of 79 rows in the CU's LDS (PAGED engine:
-// logical row -> pool row table in a VGPR), taken as a document grows and given back as it shrinks
-// or ends, so a document at a transient peak borrows what its neighbours do not use. A document the
-// pool cannot grow, or that reaches an op the row engine does not implement, is re-run by the host,
+// Bulk lean documents on the row engine (reg_engine.hpp): RW single-SIMD waves per CU (4, 8 = two per
+// SIMD, or 12), each with its SIMD's register file (or a half / third of it), replay one document
+// after another from the LPT queue. At 4 waves each wave owns a fixed quarter of the CU's LDS, 20
+// contiguous slot rows (160 leaf blocks: the long documents of C5 peak at 117). At 8 and 12 the
+// waves' rows come from ONE pool of 79 rows (PAGED engine: logical -> pool row table in a VGPR),
+// taken as a document grows and given back as it shrinks or ends, so a document at a transient peak
+// borrows what its neighbours do not use. (The table lookup costs a lone wave ~11 %: C5 4.93 s
+// paged against 4.45 s on fixed rows, hence the fixed quarters at 4 waves.) A document the rows
+// cannot hold, or that reaches an op the row engine does not implement, is re-run by the host,
 // HBM-resident, from its first op (DOC_SPILL).
+constexpr u32 ROWS_FIXED_NR = 20, ROWS_FIXED_LDS = 4 * ROWS_FIXED_NR * 64 * 32;
 template <int RW>
 __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4, RW / 4))) void k_rows(Params p) {
-    u32* mask = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + ROWS_POOL_MASK);
-    if (threadIdx.x < ROWS_POOL_WORDS)  // rows past the pool are marked taken
-        mask[threadIdx.x] = threadIdx.x * 32 + 32 <= ROWS_POOL ? 0u
-                            : threadIdx.x * 32 >= ROWS_POOL   ? ~0u
-                                                              : ~((1u << (ROWS_POOL - threadIdx.x * 32)) - 1u);
-    __syncthreads();
+    constexpr bool PAGED = RW > 4;
+    const u32 w = wave_first(threadIdx.x >> 6);
+    if constexpr (PAGED) {
+        u32* mask = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + ROWS_POOL_MASK);
+        if (threadIdx.x < ROWS_POOL_WORDS)  // rows past the pool are marked taken
+            mask[threadIdx.x] = threadIdx.x * 32 + 32 <= ROWS_POOL ? 0u
+                                : threadIdx.x * 32 >= ROWS_POOL   ? ~0u
+                                                                  : ~((1u << (ROWS_POOL - threadIdx.x * 32)) - 1u);
+        __syncthreads();
+    }
+    const u32 vb = PAGED ? ROWS_POOL_VIS : w * ROWS_FIXED_NR * 64u * 32u;
+    const u32 ab = PAGED ? ROWS_POOL_AUX : vb + ROWS_FIXED_NR * 64u * 16u;
     if (blockIdx.x == 0 && threadIdx.x == 0 && p.solo_clk) p.solo_clk[4 * SOLO_CLK_SLOTS] = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         u32 i = 0;
@@ -130,7 +140,7 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
         i = wave_read(i, 0);
         if (i >= p.n_list) break;
         const u32 d = p.doc_list[i];
-        RegEngine<(int)RG_ROWS, true> r(p, d, ROWS_POOL_VIS, ROWS_POOL_AUX, 5, ROWS_POOL_MASK);
+        RegEngine<PAGED ? (int)RG_ROWS : (int)ROWS_FIXED_NR, PAGED> r(p, d, vb, ab, 5, ROWS_POOL_MASK);
         if (!r.status) r.replay(p.docs[d].op_begin, p.docs[d].op_end);
         if (r.status == REG_HANDOFF) r.mark_spilled();
         else r.finish();
@@ -141,15 +151,16 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
 hipError_t launch_rows(const Params& p, u32 waves_per_cu, u32 n_groups, hipStream_t s) {
     const u32 rw = waves_per_cu >= 12 ? 12u : waves_per_cu >= 8 ? 8u : 4u;
     const void* k = rw == 12 ? (const void*)k_rows<12> : rw == 8 ? (const void*)k_rows<8> : (const void*)k_rows<4>;
+    const u32 lds = rw == 4 ? ROWS_FIXED_LDS : ROWS_LDS_BYTES;
     static const hipError_t attr = [] {
-        hipError_t r = hipSuccess;
-        for (const void* f : {(const void*)k_rows<4>, (const void*)k_rows<8>, (const void*)k_rows<12>})
+        hipError_t r = hipFuncSetAttribute((const void*)k_rows<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_FIXED_LDS);
+        for (const void* f : {(const void*)k_rows<8>, (const void*)k_rows<12>})
             if (r == hipSuccess) r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_LDS_BYTES);
         return r;
     }();
     if (attr != hipSuccess) return attr;
     void* args[] = {(void*)&p};
-    return hipLaunchKernel(k, dim3(n_groups), dim3(64 * rw), args, (size_t)ROWS_LDS_BYTES, s);
+    return hipLaunchKernel(k, dim3(n_groups), dim3(64 * rw), args, (size_t)lds, s);
 }
 
 #define MTE_PICK(K, gen, lvl)                                                                           \

@@ -18,7 +18,10 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def engine():
+    # this file tests the LDS / HBM-resident engine (engine.hpp) and its routing: lean batches without
+    # solo documents would otherwise take k_rows (tests/test_gpu_reg.py covers that route)
     e = mte.Engine(0)
+    e.set_option("rows_bulk", 0)
     yield e
     e.close()
 

@@ -125,8 +125,8 @@ MODE_BULK_ROWS = 5  # DocRes.mode: k_rows (bulk documents on the row engine)
 @pytest.mark.parametrize("waves", [4, 8, 12])
 @pytest.mark.parametrize("kind", [2, 5])
 def test_bulk_rows_kernel_matches_oracle(engine, kind, waves):
-    """Lean bulk documents on k_rows (4, 8 or 12 single-document waves per CU, slot rows from one
-    79-row LDS pool per CU): a Zipf mix whose longest document stays on k_solo, every other one on
+    """Lean bulk documents on k_rows (4 single-document waves per CU on fixed 20-row LDS quarters, or
+    8 / 12 taking slot rows from one 79-row LDS pool per CU): a Zipf mix whose longest document stays on k_solo, every other one on
     the rows, checksums against the oracle; then documents held to 24 leaf blocks (reg_lb_limit) that
     are re-run HBM-resident."""
     from fluidframework_amd.shard import zipf_op_counts

@@ -224,6 +224,9 @@ struct Doc {
     MTE_DEV u32 build_entries() const {
         const u32 L = lane_id(), n = r.n_segs;
         const i32 minSeq = r.min_seq;
+        // a row's last character matters only to TextSegment.canAppend's '\n' test: a document whose
+        // payload has no '\n' skips the per-row text read (one 64-B HBM burst per row otherwise)
+        const bool nl = p.cfg[d].has_nl != 0;
         u32 ne = 0;
         bool open = false, runText = false, runProps = false, runPerm = false;
         u32 runFirst = 0, runLast = 0, runLen = 0, runLast16 = 0, runStart = 0;
@@ -239,7 +242,7 @@ struct Doc {
             if (k < n) {
                 v = p.vis[row0 + k];
                 a = p.aux[row0 + k];
-                if (!(v.w & (F_MARKER | F_PERM)) && v.x) last16 = row_text(a)[v.x - 1];
+                if (nl && !(v.w & (F_MARKER | F_PERM)) && v.x) last16 = row_text(a)[v.x - 1];
             }
             const u32 cnt = n - base < 64 ? n - base : 64u;
             for (u32 j = 0; j < cnt; j++) {

@@ -308,6 +308,7 @@ struct mte_engine {
     DevBuf<uint32_t> d_cell_pos, d_cell_h, d_htab;
     bool ext_cu = false;                 // ... MTE_F_CATCHUP ops: EXT only when a legacy summary is emitted
     bool lean_base = false;              // batch_is_lean, before the catch-up records decide
+    bool props_rows_ok = false;          // k_rows may take the batch: no '\n', relative positions or summary loads, < 32 clients
     bool lean_opt = true;                // option "lean" (0 = always the FULL kernels)
     bool last_lean = false;
     uint32_t solo_max = 16;              // at most this many (0 = off)
@@ -851,7 +852,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     e->stage_copy_ms = e->stage_wait_ms = 0;
     const uint32_t nd = b->n_docs;
     std::vector<uint64_t> n_ops(nd), pay(nd), pi(nd), an(nd);
-    std::vector<uint8_t> collab(nd), has_nl(nd, 0), not_lean(nd, 0), doc_ext(nd, 0), doc_cu(nd, 0);
+    std::vector<uint8_t> collab(nd), has_nl(nd, 0), not_lean(nd, 0), doc_ext(nd, 0), doc_cu(nd, 0), not_rows(nd, 0);
     std::vector<uint32_t> doc_keys(nd, 0);  // distinct property keys of each document's ops
     std::vector<uint32_t> n_cell(nd, 0);    // SharedMatrix cell records (MTE_OP_CELL)
     // one pass over each document's ops and payload, documents spread over host threads (the scan is
@@ -869,6 +870,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         std::vector<uint32_t> keys;
         for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
             if ((b->ops[i].flags & MTE_F_PERM) || b->ops[i].type == MTE_OP_CELL) doc_ext[d] = 1;
+            if (b->ops[i].type > MTE_OP_NOOP) not_rows[d] = 1;  // summary loads: the row engine would spill
             if (b->ops[i].type == MTE_OP_CELL) n_cell[d]++;
             if (b->ops[i].flags & MTE_F_CATCHUP) doc_cu[d] = 1;
             const uint32_t ps = b->ops[i].props;
@@ -880,8 +882,8 @@ int mte_load(mte_engine* e, const mte_batch* b) {
             doc_keys[d] = (uint32_t)(std::unique(keys.begin(), keys.end()) - keys.begin());
         }
         collab[d] = e->hb.client(d, 0).empty() ? 0 : 1;  // empty observer name => local, non-collab
-        not_lean[d] = has_nl[d] || pi[d] || an[d] || rel ||
-                      e->hb.doc_client_offsets[d + 1] - e->hb.doc_client_offsets[d] > 32;
+        not_rows[d] = not_rows[d] || has_nl[d] || rel || e->hb.doc_client_offsets[d + 1] - e->hb.doc_client_offsets[d] > 32;
+        not_lean[d] = not_rows[d] || pi[d] || an[d];
         // a document with more than MTE_MAX_CLIENTS clients fails alone (MTE_DOC_UNSUPPORTED at its
         // first op from a client beyond the cap), never the batch
     };
@@ -894,12 +896,13 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         };
         run_pool(nt, work);
     }
-    bool lean = true, ext = false, cu_any = false;
+    bool lean = true, ext = false, cu_any = false, rows_ok = true;
     uint32_t max_keys = 7;
     for (uint32_t d = 0; d < nd; d++) max_keys = std::max(max_keys, std::min<uint32_t>(doc_keys[d], MTE_MAX_PROPS));
     e->map_words = ((1 + 2 * max_keys) + 3) & ~3u;  // 16 for up to 7 keys, 128 for MTE_MAX_PROPS
     for (uint32_t d = 0; d < nd; d++) {
         lean = lean && !not_lean[d];
+        rows_ok = rows_ok && !not_rows[d];
         ext = ext || doc_ext[d];
         cu_any = cu_any || doc_cu[d];
     }
@@ -945,6 +948,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     // is MTE_F_CATCHUP runs the lean / FULL kernels (which ignore the flag) unless the replay emits
     // the legacy format (run_kernel decides, snapshot_format may change after the load)
     e->lean_base = lean;
+    e->props_rows_ok = rows_ok;
     e->ext_perm = ext;
     e->ext_cu = cu_any;
     e->lean_ok = lean && !ext;
@@ -1108,8 +1112,11 @@ static int run_kernel(mte_engine* e, bool gen) {
     // pool; C2: 4 096 x 10^4 ops, 110 ms against 166 ms on the sixteen LDS / HBM waves per CU). A
     // batch with solo documents keeps k_lds beside them: its pass is the critical path's anyway, and
     // k_lds continues a document that outgrows LDS in HBM instead of re-running it from its first op.
+    // Property-carrying batches (FULL only for their properties: no '\n', no relative positions, < 32
+    // clients) take the same route on the PROPS row engine.
     uint32_t rows = 0;
-    if (!gen && full == 0 && e->rows_bulk && !e->force_hbm && nd > n_solo) {
+    const bool props_rows = full == 1 && e->props_rows_ok;
+    if (!gen && ((full == 0 && e->props_rows_ok) || props_rows) && e->rows_bulk && !e->force_hbm && nd > n_solo) {
         uint64_t bulk_ops = 0;
         for (uint32_t k = n_solo; k < nd; k++) bulk_ops += e->n_ops_doc[e->order[k]];
         const bool long_docs = nd - n_solo <= 4 * bulk_cus(e, n_solo) && bulk_ops >= 200000ull * (nd - n_solo);
@@ -1153,7 +1160,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     if (rows) {
         const uint32_t cus = bulk_cus(e, n_solo);
         const uint32_t per = rows >= 12 ? 12u : rows >= 8 ? 8u : 4u;
-        HIP_TRY(e, launch_rows(e->P, per, std::min<uint32_t>(cus, (nd - n_solo + per - 1) / per), s_main));
+        HIP_TRY(e, launch_rows(e->P, per, std::min<uint32_t>(cus, (nd - n_solo + per - 1) / per), full == 1, s_main));
     }
     // k_hbmq: one workgroup (wave) per document; those that find the queue drained exit at once
     if (hbm_waves && !groups) {
@@ -1426,6 +1433,7 @@ int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_o
     e->emit_tables = false;  // names are known after the generator ran
     // kinds 2 and 5 draw no properties and no '\n'; short ids stay below 1 + n_clients
     e->lean_ok = e->lean_base = kind != 3 && n_clients < 32;
+    e->props_rows_ok = n_clients < 32;
     e->ext_needed = e->ext_perm = e->ext_cu = false;
     rc = run_kernel(e, true);
     if (rc) return rc;

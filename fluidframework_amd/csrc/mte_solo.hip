@@ -118,21 +118,36 @@ __global__ __launch_bounds__(64 * SOLO_WAVES) __attribute__((amdgpu_waves_per_eu
 // paged against 4.45 s on fixed rows, hence the fixed quarters at 4 waves.) A document the rows
 // cannot hold, or that reaches an op the row engine does not implement, is re-run by the host,
 // HBM-resident, from its first op (DOC_SPILL).
-constexpr u32 ROWS_FIXED_NR = 20, ROWS_FIXED_LDS = 4 * ROWS_FIXED_NR * 64 * 32;
-template <int RW>
+// LDS geometry of k_rows: 32 B per slot (vis + aux), 36 with the property map ids (PROPS). The pool
+// (8 / 12 waves): vis array, aux array, [props array], row mask. Fixed quarters (4 waves): per wave
+// its rows' vis, aux and [props] arrays.
+template <bool PROPS>
+struct RowsGeom {
+    static constexpr u32 POOL = PROPS ? 71 : 79;
+    static constexpr u32 VIS = 0, AUX = POOL * 64 * 16, PRP = 2 * POOL * 64 * 16;
+    static constexpr u32 MASK = PRP + (PROPS ? POOL * 64 * 4 : 0);
+    static constexpr u32 LDS = MASK + ROWS_POOL_WORDS * 4;
+    static constexpr u32 FIXED_NR = PROPS ? 17 : 20;
+    static constexpr u32 FIXED_WAVE = FIXED_NR * 64 * (PROPS ? 36 : 32);
+    static constexpr u32 FIXED_LDS = 4 * FIXED_WAVE;
+    static_assert(LDS <= LDS_BYTES && FIXED_LDS <= LDS_BYTES && POOL <= 32 * ROWS_POOL_WORDS, "k_rows LDS plan");
+};
+template <int RW, bool PROPS>
 __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4, RW / 4))) void k_rows(Params p) {
+    typedef RowsGeom<PROPS> G;
     constexpr bool PAGED = RW > 4;
     const u32 w = wave_first(threadIdx.x >> 6);
     if constexpr (PAGED) {
-        u32* mask = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + ROWS_POOL_MASK);
+        u32* mask = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + G::MASK);
         if (threadIdx.x < ROWS_POOL_WORDS)  // rows past the pool are marked taken
-            mask[threadIdx.x] = threadIdx.x * 32 + 32 <= ROWS_POOL ? 0u
-                                : threadIdx.x * 32 >= ROWS_POOL   ? ~0u
-                                                                  : ~((1u << (ROWS_POOL - threadIdx.x * 32)) - 1u);
+            mask[threadIdx.x] = threadIdx.x * 32 + 32 <= G::POOL ? 0u
+                                : threadIdx.x * 32 >= G::POOL   ? ~0u
+                                                                : ~((1u << (G::POOL - threadIdx.x * 32)) - 1u);
         __syncthreads();
     }
-    const u32 vb = PAGED ? ROWS_POOL_VIS : w * ROWS_FIXED_NR * 64u * 32u;
-    const u32 ab = PAGED ? ROWS_POOL_AUX : vb + ROWS_FIXED_NR * 64u * 16u;
+    const u32 vb = PAGED ? G::VIS : w * G::FIXED_WAVE;
+    const u32 ab = PAGED ? G::AUX : vb + G::FIXED_NR * 64u * 16u;
+    const u32 pb = PAGED ? G::PRP : vb + G::FIXED_NR * 64u * 32u;
     if (blockIdx.x == 0 && threadIdx.x == 0 && p.solo_clk) p.solo_clk[4 * SOLO_CLK_SLOTS] = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         u32 i = 0;
@@ -140,7 +155,7 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
         i = wave_read(i, 0);
         if (i >= p.n_list) break;
         const u32 d = p.doc_list[i];
-        RegEngine<PAGED ? (int)RG_ROWS : (int)ROWS_FIXED_NR, PAGED> r(p, d, vb, ab, 5, ROWS_POOL_MASK);
+        RegEngine<PAGED ? (int)RG_ROWS : (int)G::FIXED_NR, PAGED, PROPS> r(p, d, vb, ab, 5, G::MASK, pb);
         if (!r.status) r.replay(p.docs[d].op_begin, p.docs[d].op_end);
         if (r.status == REG_HANDOFF) r.mark_spilled();
         else r.finish();
@@ -148,19 +163,23 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
     }
 }
 
-hipError_t launch_rows(const Params& p, u32 waves_per_cu, u32 n_groups, hipStream_t s) {
-    const u32 rw = waves_per_cu >= 12 ? 12u : waves_per_cu >= 8 ? 8u : 4u;
-    const void* k = rw == 12 ? (const void*)k_rows<12> : rw == 8 ? (const void*)k_rows<8> : (const void*)k_rows<4>;
-    const u32 lds = rw == 4 ? ROWS_FIXED_LDS : ROWS_LDS_BYTES;
+template <bool PROPS>
+static hipError_t launch_rows_t(const Params& p, u32 rw, u32 n_groups, hipStream_t s) {
+    typedef RowsGeom<PROPS> G;
+    const void* k = rw == 12 ? (const void*)k_rows<12, PROPS> : rw == 8 ? (const void*)k_rows<8, PROPS> : (const void*)k_rows<4, PROPS>;
     static const hipError_t attr = [] {
-        hipError_t r = hipFuncSetAttribute((const void*)k_rows<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_FIXED_LDS);
-        for (const void* f : {(const void*)k_rows<8>, (const void*)k_rows<12>})
-            if (r == hipSuccess) r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ROWS_LDS_BYTES);
+        hipError_t r = hipFuncSetAttribute((const void*)k_rows<4, PROPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::FIXED_LDS);
+        for (const void* f : {(const void*)k_rows<8, PROPS>, (const void*)k_rows<12, PROPS>})
+            if (r == hipSuccess) r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
         return r;
     }();
     if (attr != hipSuccess) return attr;
     void* args[] = {(void*)&p};
-    return hipLaunchKernel(k, dim3(n_groups), dim3(64 * rw), args, (size_t)lds, s);
+    return hipLaunchKernel(k, dim3(n_groups), dim3(64 * rw), args, (size_t)(rw == 4 ? G::FIXED_LDS : G::LDS), s);
+}
+hipError_t launch_rows(const Params& p, u32 waves_per_cu, u32 n_groups, bool props, hipStream_t s) {
+    const u32 rw = waves_per_cu >= 12 ? 12u : waves_per_cu >= 8 ? 8u : 4u;
+    return props ? launch_rows_t<true>(p, rw, n_groups, s) : launch_rows_t<false>(p, rw, n_groups, s);
 }
 
 #define MTE_PICK(K, gen, lvl)                                                                           \

@@ -45,10 +45,7 @@ constexpr u32 RG_HEAP = 511;              // LRU heap positions 1..511
 constexpr u32 RSEQ_LIVE = 0x7FFFFFFFu;    // removedSeq of a live segment (never <= a refSeq)
 constexpr u32 RCL_LIVE = 0xFFu;           // removedClient byte of a live segment (never a client)
 constexpr i32 REG_HANDOFF = 101;          // internal: continue in the LDS engine from the current op
-// k_rows' shared row pool: 79 slot rows (vis array, then aux array) and its row mask, 160 KiB of LDS
-constexpr u32 ROWS_POOL = 79, ROWS_POOL_WORDS = 3;
-constexpr u32 ROWS_POOL_VIS = 0, ROWS_POOL_AUX = ROWS_POOL * 64 * 16, ROWS_POOL_MASK = ROWS_POOL * 64 * 32;
-constexpr u32 ROWS_LDS_BYTES = ROWS_POOL_MASK + ROWS_POOL_WORDS * 4;
+constexpr u32 ROWS_POOL_WORDS = 3;         // k_rows' pool row mask (mte_solo.hip RowsGeom): <= 96 rows
 // needsScour (mergeTree.ts:63) in meta bits 24..25 of every slot lane of a block
 constexpr u32 NS_SHIFT = 24, NS_MASK = 3u << NS_SHIFT;
 static_assert(RG_BLOCKS <= SOLO_POOL, "the rows live in the SoloPlan's slot arrays");
@@ -113,6 +110,7 @@ struct RSeg {
     u32 cap;  // owned merge-arena capacity from toff (0 for payload text)
     u32 rm;   // removers: bit c for removedClient c and every client in removedClientOverlap
     u32 sid;
+    u32 props = 0;  // property map id (PROPS engines; 0 = no properties)
 };
 struct RFound {
     bool ok;
@@ -127,7 +125,10 @@ struct RFound {
 // PAGED (k_rows): logical row r of the document lives in pool row ptab[r] of a pool the CU's waves
 // share (rows_pool_*), taken as the document grows and given back as it shrinks or ends; a document
 // the pool cannot grow is spilled (REG_HANDOFF, re-run by the host). Otherwise row r is slot row r.
-template <int NR = (int)RG_ROWS, bool PAGED = false>
+// PROPS (k_rows of property-carrying batches): a ninth slot field, the segment's property map id
+// (immutable maps in the document's HBM map table, SegmentPropertiesManager.addProperties), annotate
+// ops, and merges that require matching properties.
+template <int NR = (int)RG_ROWS, bool PAGED = false, bool PROPS = false>
 struct RegEngine {
     typedef simd::V V;
     typedef simd::B B;
@@ -136,6 +137,7 @@ struct RegEngine {
     // rm 0, so nodeLength's removal test is one bit test of rm (no separate overlap-set lookup).
     struct Row {
         V len, seq, rseq, meta, cap, toff, rm, sid;
+        V props;  // PROPS only (never loaded, stored or read otherwise)
     };
 
     // ---------------------------------------------------------------- state
@@ -197,6 +199,7 @@ struct RegEngine {
     }
 #ifdef MTE_CPU
     u32 mem_vis[RG_ROWS * 64][4], mem_aux[RG_ROWS * 64][4];
+    u32 mem_props[RG_ROWS * 64];
     u64 pool_mask = 0;           // PAGED: pool rows in use (this engine's own pool on the CPU)
     u32 pool_rows = RG_ROWS, pool_takes = 0;
     SD u32 pslot(u32 s) const { return PAGED ? prow(s >> 6) * 64 + (s & 63) : s; }
@@ -216,6 +219,7 @@ struct RegEngine {
     SD void zero_prow(u32 row) {
         memset(mem_vis[row * 64], 0, 64 * 16);
         memset(mem_aux[row * 64], 0, 64 * 16);
+        memset(&mem_props[row * 64], 0, 64 * 4);
     }
     SD Row ldrow(u32 r) const {
         Row w;
@@ -225,6 +229,7 @@ struct RegEngine {
             const u32* a = mem_aux[pr * 64 + l];
             w.len.x[l] = v[0], w.seq.x[l] = v[1], w.rseq.x[l] = v[2], w.meta.x[l] = v[3];
             w.cap.x[l] = a[0], w.toff.x[l] = a[1], w.rm.x[l] = a[2], w.sid.x[l] = a[3];
+            w.props.x[l] = PROPS ? mem_props[pr * 64 + l] : 0u;
         }
         return w;
     }
@@ -235,6 +240,7 @@ struct RegEngine {
             u32* a = mem_aux[pr * 64 + l];
             v[0] = w.len.x[l], v[1] = w.seq.x[l], v[2] = w.rseq.x[l], v[3] = w.meta.x[l];
             a[0] = w.cap.x[l], a[1] = w.toff.x[l], a[2] = w.rm.x[l], a[3] = w.sid.x[l];
+            if (PROPS) mem_props[pr * 64 + l] = w.props.x[l];
         }
     }
     SD V ldf(u32 r, u32 aux, u32 c) const {  // one field of a row
@@ -254,12 +260,14 @@ struct RegEngine {
         if (!PAGED) {
             memmove(mem_vis[dst], mem_vis[src], (size_t)n * 16);
             memmove(mem_aux[dst], mem_aux[src], (size_t)n * 16);
+            memmove(&mem_props[dst], &mem_props[src], (size_t)n * 4);
             return;
         }
         for (u32 t = 0; t < n; t++) {  // slot by slot in the memmove's safe direction
             const u32 i = dst > src ? n - 1 - t : t;
             memcpy(mem_vis[pslot(dst + i)], mem_vis[pslot(src + i)], 16);
             memcpy(mem_aux[pslot(dst + i)], mem_aux[pslot(src + i)], 16);
+            mem_props[pslot(dst + i)] = mem_props[pslot(src + i)];
         }
     }
     SD void zero_slots(u32 at, u32 n) {
@@ -267,6 +275,7 @@ struct RegEngine {
         for (u32 i = 0; i < n; i++) {
             memset(mem_vis[pslot(at + i)], 0, 16);
             memset(mem_aux[pslot(at + i)], 0, 16);
+            mem_props[pslot(at + i)] = 0;
         }
     }
 #else
@@ -275,6 +284,8 @@ struct RegEngine {
     u32 vbase = (u32)offsetof(SoloPlan, vis), abase = (u32)offsetof(SoloPlan, aux);
     SD uint4* VISP() const { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + vbase); }
     SD uint4* AUXP() const { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + abase); }
+    u32 pbase = 0;  // PROPS: byte offset of the slots' property map ids (one u32 per slot)
+    SD u32* PROPP() const { return reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + pbase); }
     u32 pool_off = 0;  // PAGED: byte offset of the pool's row mask (ROWS_POOL_WORDS words)
     SD u32* pool_words() const { return reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + pool_off); }
     SD bool take_row(u32& row) {  // lane 0 claims a free pool row with an LDS atomic or
@@ -304,6 +315,7 @@ struct RegEngine {
     SD void zero_prow(u32 row) {
         VISP()[row * 64 + __lane_id()] = make_uint4(0, 0, 0, 0);
         AUXP()[row * 64 + __lane_id()] = make_uint4(0, 0, 0, 0);
+        if constexpr (PROPS) PROPP()[row * 64 + __lane_id()] = 0u;
         simd::lds_order();
     }
     // physical slot of logical slot s, per lane (PAGED: a block range can cross pool rows)
@@ -314,12 +326,13 @@ struct RegEngine {
     SD Row ldrow(u32 r) const {
         const u32 i = prow(r) * 64 + __lane_id();
         const uint4 v = VISP()[i], a = AUXP()[i];
-        return Row{V{v.x}, V{v.y}, V{v.z}, V{v.w}, V{a.x}, V{a.y}, V{a.z}, V{a.w}};
+        return Row{V{v.x}, V{v.y}, V{v.z}, V{v.w}, V{a.x}, V{a.y}, V{a.z}, V{a.w}, V{PROPS ? PROPP()[i] : 0u}};
     }
     SD void strow(u32 r, const Row& w) {
         const u32 i = prow(r) * 64 + __lane_id();
         VISP()[i] = make_uint4(w.len.x, w.seq.x, w.rseq.x, w.meta.x);
         AUXP()[i] = make_uint4(w.cap.x, w.toff.x, w.rm.x, w.sid.x);
+        if constexpr (PROPS) PROPP()[i] = w.props.x;
         simd::lds_order();
     }
     SD V ldf(u32 r, u32 aux, u32 c) const {
@@ -346,14 +359,17 @@ struct RegEngine {
                 const u32 ii = ok ? (u32)i : 0u;
                 const u32 ps = pslot(src + ii), pd = pslot(dst + ii);
                 uint4 v = make_uint4(0, 0, 0, 0), a = v;
+                u32 pp = 0;
                 if (ok) {
                     v = V4[ps];
                     a = A4[ps];
+                    if constexpr (PROPS) pp = PROPP()[ps];
                 }
                 simd::lds_order();
                 if (ok) {
                     V4[pd] = v;
                     A4[pd] = a;
+                    if constexpr (PROPS) PROPP()[pd] = pp;
                 }
                 simd::lds_order();
             }
@@ -363,14 +379,17 @@ struct RegEngine {
             for (i32 b = (i32)n - 64; b > -64; b -= 64) {
                 const i32 i = b + (i32)L;
                 uint4 v = make_uint4(0, 0, 0, 0), a = v;
+                u32 pp = 0;
                 if (i >= 0) {
                     v = V4[src + (u32)i];
                     a = A4[src + (u32)i];
+                    if constexpr (PROPS) pp = PROPP()[src + (u32)i];
                 }
                 simd::lds_order();
                 if (i >= 0) {
                     V4[dst + (u32)i] = v;
                     A4[dst + (u32)i] = a;
+                    if constexpr (PROPS) PROPP()[dst + (u32)i] = pp;
                 }
                 simd::lds_order();
             }
@@ -378,14 +397,17 @@ struct RegEngine {
             for (u32 b = 0; b < n; b += 64) {
                 const u32 i = b + L;
                 uint4 v = make_uint4(0, 0, 0, 0), a = v;
+                u32 pp = 0;
                 if (i < n) {
                     v = V4[src + i];
                     a = A4[src + i];
+                    if constexpr (PROPS) pp = PROPP()[src + i];
                 }
                 simd::lds_order();
                 if (i < n) {
                     V4[dst + i] = v;
                     A4[dst + i] = a;
+                    if constexpr (PROPS) PROPP()[dst + i] = pp;
                 }
                 simd::lds_order();
             }
@@ -399,6 +421,7 @@ struct RegEngine {
             if (b < n) {
                 VISP()[ps] = make_uint4(0, 0, 0, 0);
                 AUXP()[ps] = make_uint4(0, 0, 0, 0);
+                if constexpr (PROPS) PROPP()[ps] = 0u;
             }
         }
         simd::lds_order();
@@ -469,9 +492,10 @@ struct RegEngine {
     SD RegEngine(const Params& p_, u32 doc_) : p(p_), doc(doc_) { setup(); }
 #ifndef MTE_CPU
     // rows in another LDS region (k_rows: one share of the CU's LDS per wave)
-    SD RegEngine(const Params& p_, u32 doc_, u32 vb, u32 ab, u32 mode, u32 pool = 0) : p(p_), doc(doc_) {
+    SD RegEngine(const Params& p_, u32 doc_, u32 vb, u32 ab, u32 mode, u32 pool = 0, u32 pb = 0) : p(p_), doc(doc_) {
         vbase = vb;
         abase = ab;
+        pbase = pb;
         pool_off = pool;
         res_mode = mode;
         setup();
@@ -486,6 +510,129 @@ struct RegEngine {
         arena_cap = c.arena_cap;
         payload_len = c.payload_len;
         init();
+        if constexpr (PROPS) {
+            mw = p.map_words;
+            maps = p.maps + c.map_off * mw;
+            map_cap = c.map_cap;
+            mapNext = 1;  // map id 0 == no properties
+            // TextSegment.canAppend reads the last character when the text has '\n': not modelled here
+            if (c.has_nl) status = REG_HANDOFF;
+        }
+    }
+
+    // ---------------------------------------------------------------- property maps (PROPS, HBM)
+    // A map record is [n, key 0, value 0, key 1, value 1, ...] (mw words) in the document's map
+    // table, immutable once built; id 0 = no properties. Lane i holds pair i.
+    u32* maps = nullptr;
+    u32 map_cap = 0, mw = 0, mapNext = 1;
+    // lanes below each lane set in m (mbcnt)
+    SD static V rank_below(u64 m) {
+#ifdef MTE_CPU
+        V r;
+        for (u32 l = 0; l < 64; l++) r.x[l] = (u32)__builtin_popcountll(m & ((1ull << l) - 1ull));
+        return r;
+#else
+        return V{__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u))};
+#endif
+    }
+    // matchProperties on one value, b uniform (properties.ts:72-80): equal ids, or b an object value
+    // that a's deep-equality bits name
+    SD B val_match(V a, u32 b) const {
+        const B eq = a == simd::splat(b);
+        if (!(p.val_flags[b] & 2u)) return eq;
+        const u32 j = p.val_objidx[b];
+        if (j == NONE) return eq;
+        const V om = simd::ld(reinterpret_cast<const u32*>(p.val_objmatch), a * 2u + (j >> 5), simd::mk_all());
+        return eq | (((om >> (j & 31u)) & 1u) != 0u);
+    }
+    // matchProperties of two maps (properties.ts:62-93)
+    SD bool match_props(u32 a, u32 b) {
+        if (a == b) return true;
+        if (a == 0 || b == 0 || a >= map_cap || b >= map_cap) return false;
+        fence_arena();  // map records are written lane-parallel (build_map)
+        const u32* ma = maps + (u64)a * mw;
+        const u32* mb = maps + (u64)b * mw;
+        const u32 na = ma[0], nb = mb[0];
+        if (na != nb) return false;
+        const B in = L() < na;
+        const V Ka = simd::ld(ma + 1, L() * 2u, in), Va = simd::ld(ma + 2, L() * 2u, in);
+        const V Kb = simd::ld(mb + 1, L() * 2u, in), Vb = simd::ld(mb + 2, L() * 2u, in);
+        B ok = ~in;
+        for (u32 q = 0; q < nb; q++) {
+            const u32 kq = simd::readlane(Kb, q), vq = simd::readlane(Vb, q);
+            const B hit = in & (Ka == kq);
+            if (simd::ballot(hit)) ok = ok | (hit & val_match(Va, vq));
+        }
+        return simd::ballot(~ok) == 0;
+    }
+    // SegmentPropertiesManager.addProperties (segmentPropertiesManager.ts:35-111) on an immutable map:
+    // a fresh map id (the LDS engine's build_map, engine.hpp, lane for lane)
+    SD u32 build_map(u32 old, u32 propset, bool rewrite) {
+        if (mapNext >= map_cap) {  // the load-time estimate was short: the host re-runs it with the worst case
+            fail(REG_HANDOFF, curSeq);
+            return 0;
+        }
+        fence_arena();
+        const u32 maxp = (mw - 1) / 2 < MTE_MAX_PROPS ? (mw - 1) / 2 : MTE_MAX_PROPS;
+        u32 n = 0;
+        V K = simd::splat(0), Vv = simd::splat(0);
+        if (old && old < map_cap) {
+            const u32* mo = maps + (u64)old * mw;
+            n = mo[0];
+            if (n > maxp) n = maxp;
+            K = simd::ld(mo + 1, L() * 2u, L() < n);
+            Vv = simd::ld(mo + 2, L() * 2u, L() < n);
+        }
+        const mte_propset ps = p.propsets[propset];
+        const u32 pc = ps.count, pf = ps.first;
+        if (rewrite) {  // delete keys whose new value is falsy / absent (:65-78); order kept
+            B keep = simd::mk_none();
+            for (u32 q = 0; q < pc; q++) {
+                const u32 k = p.prop_keys[pf + q];
+                const bool falsy = (p.val_flags[p.prop_vals[pf + q]] & 1u) != 0;
+                const B hit = (L() < n) & (K == k);
+                keep = falsy ? simd::andn(keep, hit) : (keep | hit);
+            }
+            keep = keep & (L() < n);
+            const u64 km = simd::ballot(keep);
+            const u32 nk = (u32)__builtin_popcountll(km);
+            const V below = rank_below(km);
+            const V dst = simd::sel(keep, below, (L() - below) + nk);  // a permutation of the lanes
+            K = simd::push(K, dst);
+            Vv = simd::push(Vv, dst);
+            n = nk;
+        }
+        for (u32 q = 0; q < pc; q++) {
+            const u32 k = p.prop_keys[pf + q], v = p.prop_vals[pf + q];
+            const u64 hm = simd::ballot((L() < n) & (K == k));
+            if (v == 0) {  // null deletes (:98-100): the pairs after it move down one lane
+                if (hm) {
+                    const u32 at = (u32)__builtin_ctzll(hm);
+                    const V nxt = (L() + 1u) & 63u;
+                    const V K1 = simd::bperm(K, nxt), V1 = simd::bperm(Vv, nxt);
+                    const B mvd = L() >= at;
+                    K = simd::sel(mvd, K1, K);
+                    Vv = simd::sel(mvd, V1, Vv);
+                    n--;
+                }
+            } else if (hm) {
+                Vv = simd::sel(L() == (u32)__builtin_ctzll(hm), v, Vv);
+            } else if (n < maxp) {
+                K = simd::sel(L() == n, k, K);
+                Vv = simd::sel(L() == n, v, Vv);
+                n++;
+            } else {
+                fail(MTE_DOC_UNSUPPORTED, curSeq);
+                return 0;
+            }
+        }
+        const u32 id = mapNext++;
+        u32* m = maps + (u64)id * mw;
+        simd::st(m + 1, L() * 2u, K, L() < n);
+        simd::st(m + 2, L() * 2u, Vv, L() < n);
+        simd::st(m, L(), simd::splat(n), L() == 0u);
+        adirty = true;  // read back later (match_props, build_map): fence_arena first
+        return id;
     }
     SD void init() {
         if constexpr (PAGED) {
@@ -720,6 +867,7 @@ struct RegEngine {
         put(w.cap, rec.cap);
         put(w.rm, rec.rm);
         put(w.sid, rec.sid);
+        if constexpr (PROPS) put(w.props, rec.props);
         writeback(r);
         if (cnt + 1 < 8) return k;
         split_block(k);
@@ -757,6 +905,7 @@ struct RegEngine {
         mv(w.cap, w2.cap, 0u);
         mv(w.rm, w2.rm, 0u);
         mv(w.sid, w2.sid, 0u);
+        if constexpr (PROPS) mv(w.props, w2.props, 0u);
         // the new block's needsScour is undefined
         if (r2 == r) {
             w.meta = simd::sel(in_group(k + 1), w.meta & ~NS_MASK, w.meta);
@@ -1060,7 +1209,14 @@ struct RegEngine {
         const u32 mSET = group_bits(simd::ballot(simd::andn(act, rem) & simd::sle(w.seq, minSeq)), k);
         const u32 mTXT = group_bits(simd::ballot(act & ((w.meta & F_MARKER) == 0u)), k);
         const u32 mST = mSET & mTXT;
-        const u32 mJOIN = mST & (mST << 1) & 0xFFu;  // slot s joins the run of slot s-1
+        u32 mJOIN = mST & (mST << 1) & 0xFFu;  // slot s joins the run of slot s-1
+        if constexpr (PROPS) {  // ... when its properties match slot s-1's (matchProperties)
+            const u32 mSAME = group_bits(simd::ballot(w.props == simd::row_shr1(w.props)), k);
+            for (u32 c = mJOIN & ~mSAME; c; c &= c - 1) {
+                const u32 sb = (u32)__builtin_ctz(c);
+                if (!match_props(simd::readlane(w.props, gb + sb - 1), simd::readlane(w.props, gb + sb))) mJOIN &= ~(1u << sb);
+            }
+        }
         if (!mDROP && !mJOIN) return cnt;            // nothing dropped, nothing merged
         if (mJOIN & group_bits(simd::ballot(w.len > (u32)GRANULARITY), k)) return scour_serial(k, cnt);
         RG_COUNT(RP_N_SCOUR_CHANGED, 1);
@@ -1143,6 +1299,7 @@ struct RegEngine {
         cmp(w.toff, 0u);
         cmp(w.rm, 0u);
         cmp(w.sid, 0u);
+        if constexpr (PROPS) cmp(w.props, 0u);
         ns_put(w, k, SC_FALSE);  // scourNode's caller clears needsScour (mergeTree.ts:1457): same write
         putrow(r, w);
         scoured = true;
@@ -1196,7 +1353,7 @@ struct RegEngine {
             jdst = jsrc = jlen = simd::splat(0);
             u32 top = arenaTop, need = 0;
             i32 prev = -1;
-            u32 pLen = 0, pOff = 0, pCap = 0, pMat = 0;
+            u32 pLen = 0, pOff = 0, pCap = 0, pMat = 0, pProps = 0;
             bool pText = false, pFresh = false;
             auto job = [&](u32 d, u32 s, u32 n) MTE_LI {
                 if (jn < 64) {
@@ -1215,7 +1372,9 @@ struct RegEngine {
                 } else if (mSET & bit) {
                     const u32 ln = simd::readlane(w.len, gb + s), to = simd::readlane(w.toff, gb + s);
                     const u32 tc = simd::readlane(w.cap, gb + s);
-                    const bool ok = prev >= 0 && pText && (mTXT & bit) && (pLen <= (u32)GRANULARITY || ln <= (u32)GRANULARITY);
+                    const u32 sp = PROPS ? simd::readlane(w.props, gb + s) : 0u;
+                    const bool ok = prev >= 0 && pText && (mTXT & bit) && (pLen <= (u32)GRANULARITY || ln <= (u32)GRANULARITY) &&
+                                    (!PROPS || match_props(pProps, sp));
                     if (ok) {  // TextSegment.append
                         if ((pOff & ARENA_BIT) && pLen + ln <= pCap) {
                             job(pOff + pLen, to, ln);
@@ -1252,6 +1411,7 @@ struct RegEngine {
                         pCap = tc;
                         pText = (mTXT & bit) != 0;
                         pFresh = false;
+                        pProps = sp;
                     }
                 } else {
                     prev = -1;
@@ -1294,6 +1454,7 @@ struct RegEngine {
         cmp(w.rseq, nullptr, 0u);
         cmp(w.meta, nullptr, NS_MASK);  // the block's needsScour stays in every lane
         cmp(w.sid, nullptr, 0u);
+        if constexpr (PROPS) cmp(w.props, nullptr, 0u);
         ns_put(w, k, SC_FALSE);
         putrow(r, w);
         scoured = true;
@@ -1356,6 +1517,7 @@ struct RegEngine {
         t.cap = gather(a.cap, b.cap);
         t.rm = gather(a.rm, b.rm);
         t.sid = gather(a.sid, b.sid);
+        if constexpr (PROPS) t.props = gather(a.props, b.props);
         const i32 d = (i32)kk - (i32)m;
         shift_blocks(k0 + m, d);
         // destination: block k0 + dj slot dq <- item dj*base + min(dj, extra) + dq
@@ -1379,6 +1541,7 @@ struct RegEngine {
             put(w.cap, t.cap);
             put(w.rm, t.rm);
             put(w.sid, t.sid);
+            if constexpr (PROPS) put(w.props, t.props);
             strow(rr, w);
         }
         cr = NONE;
@@ -1466,6 +1629,7 @@ struct RegEngine {
         t.toff = simd::readlane(w.toff, l);
         t.cap = simd::readlane(w.cap, l);
         t.rm = simd::readlane(w.rm, l);
+        if constexpr (PROPS) t.props = simd::readlane(w.props, l);  // the right piece shares the map
         const u32 sid = new_sid();
         if (sid == NONE) return NONE;
         const u32 rr = (u32)f.r;
@@ -1563,6 +1727,60 @@ struct RegEngine {
         return status == 0;
     }
 
+    // annotateRange (mergeTree.ts:2565-2605; PROPS): split at p1 and p2 like a remove, then every
+    // segment of [p1, p2) visible in the (R, C) view takes a new map, addProperties of the op's set on
+    // its old one (one map per distinct old map: the LDS engine's memo of the last one built).
+    SD bool op_annotate(i32 p1, i32 p2, i32 R, u32 C, i32 seq, u32 propset, bool rewrite) {
+        RG_PROF(RP_REM);
+        u32 r1 = 0, c1 = 0;
+        for (u32 ph = 0; ph < 2; ph++) {
+            const RFound f = resolve(ph ? p2 : p1, R, C, r1, c1);
+            if (ph == 0 && f.ok) {
+                r1 = f.row;
+                c1 = f.carry;
+            }
+            if (!f.ok || !(f.slot >= 0 && f.r > 0)) continue;
+            if (split_at(f) == NONE || status) return false;
+        }
+        RG_PROF(RP_RANGE);
+        const u32 nrows = (n_lb + 7) >> 3;
+        u32 carry = c1, memoOld = NONE, memoNew = 0;
+        for (u32 r = r1; r < nrows && (i32)carry < p2; r++) {
+            Row& w = rowref(r);
+            const V v = vis(w, R, C);
+            const V incl = simd::scan_incl(v) + carry;
+            const V ex = incl - v;
+            const B mark = (v != 0u) & simd::slt(ex, p2) & simd::sgt(incl, p1);
+            carry = simd::readlane(incl, 63);
+            const u64 mm = simd::ballot(mark);
+            if (!mm) continue;
+            for (u64 pending = mm; pending;) {
+                const u32 old = simd::readlane(w.props, (u32)__builtin_ctzll(pending));
+                u32 nid;
+                if (old == memoOld) {
+                    nid = memoNew;
+                } else {
+                    nid = build_map(old, propset, rewrite);
+                    if (status) return false;
+                    memoOld = old;
+                    memoNew = nid;
+                }
+                const B same = simd::ballot_mask(pending) & (w.props == old);
+                w.props = simd::sel(same, nid, w.props);
+                pending &= ~simd::ballot(same);
+            }
+            writeback(r);
+            for (u64 gm = mm; gm;) {  // addToLRUSet per block, document order
+                const u32 l = (u32)__builtin_ctzll(gm);
+                const u32 g = l >> 3;
+                gm &= ~(0xFFull << (g * 8));
+                add_lru(r * 8 + g, simd::readlane(w.sid, l), seq);
+                if (status) return false;
+            }
+        }
+        return status == 0;
+    }
+
     // Room for one more op (margins for the splits, packs and heap pushes an op can cause);
     // false => hand the document to the LDS engine before this op.
     SD bool room() {
@@ -1585,10 +1803,11 @@ struct RegEngine {
         RG_PROF(RP_APPLY);
         const u32 type = op.type;
         const bool ins = type == MTE_OP_INSERT || type == MTE_OP_INSERT_MARKER;
-        if (!(ins || type == MTE_OP_REMOVE || type == MTE_OP_NOOP)) return false;
+        const bool ann = PROPS && type == MTE_OP_ANNOTATE;
+        if (!(ins || ann || type == MTE_OP_REMOVE || type == MTE_OP_NOOP)) return false;
         // (MTE_F_CATCHUP only asks for delta records, which only a legacy-format replay reads: that one
         // runs the EXT kernels, so here the flag is ignored like the lean LDS kernels do)
-        if ((op.flags & (MTE_F_REL | MTE_F_PERM)) || op.props) return false;
+        if ((op.flags & (MTE_F_REL | MTE_F_PERM)) || (!PROPS && op.props)) return false;
         if (type != MTE_OP_NOOP && (op.client == 0 || op.client >= 32)) return false;
         if (!room()) return false;
         const u32 C = op.client;
@@ -1609,10 +1828,17 @@ struct RegEngine {
             rec.cap = 0;
             rec.rm = 0;
             rec.sid = 0;
+            if constexpr (PROPS) {
+                rec.props = op.props ? build_map(0, op.props, false) : 0u;
+                if (status) return true;
+            }
             edited = op_insert(op.pos1, R, C, seq, rec);
             n_ops++;
         } else if (type == MTE_OP_REMOVE) {
             edited = op_remove(op.pos1, op.a, R, C, seq);
+            n_ops++;
+        } else if (ann) {
+            edited = op_annotate(op.pos1, op.a, R, C, seq, op.props, (op.flags & MTE_F_REWRITE) != 0);
             n_ops++;
         }
         if (status) return true;
@@ -1781,7 +2007,15 @@ struct RegEngine {
                 simd::st(ov, t4 + 1u, w.seq, have);
                 simd::st(ov, t4 + 2u, simd::sel(live, 0u, w.rseq), have);
                 simd::st(ov, t4 + 3u, m2, have);
-                simd::st(oa, t4, simd::splat(0), have);
+                simd::st(oa, t4, PROPS ? w.props : simd::splat(0), have);
+                if constexpr (PROPS) {  // the row's property map, indexed by row (emission reads it)
+                    const B hp = have & (w.props != 0u);
+                    if (p.out_maps && simd::ballot(hp)) {
+                        fence_arena();
+                        for (u32 q = 0; q < mw; q++)
+                            simd::st(p.out_maps, at * mw + q, simd::ld(maps, w.props * mw + q, hp), hp);
+                    }
+                }
                 simd::st(oa, t4 + 1u, simd::sel(txt, tat, w.toff), have);
                 simd::st(oa, t4 + 2u, z2, have);
                 simd::st(oa, t4 + 3u, w.sid - 1u, have);
@@ -1808,7 +2042,7 @@ struct RegEngine {
             o.n_lb = n_lb;
             o.arena_sel = arenaSel;
             o.arena_top = arenaTop;
-            o.map_next = 1;
+            o.map_next = PROPS ? mapNext : 1u;
             o.seg_next = segNext;
             o.heap_size = heapSize;
             o.n_gc = n_gc;

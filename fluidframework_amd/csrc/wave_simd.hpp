@@ -47,12 +47,16 @@ struct B {
 };
 SD B mk(bool c) { return {__builtin_amdgcn_ballot_w64(c)}; }
 SD bool lane_of(B c) { return __builtin_amdgcn_inverse_ballot_w64(c.m); }
+SD B mk_all() { return {~0ull}; }
+SD B mk_none() { return {0ull}; }
 #else
 struct B {  // a per-lane predicate; u32 0/1 rather than bool: an i1 member defeats SROA (stores i1,
     u32 b;  // loads i8) and left every predicate of the engine on the scratch stack
 };
 SD B mk(bool c) { return {(u32)c}; }
 SD bool lane_of(B c) { return c.b != 0; }
+SD B mk_all() { return {1u}; }
+SD B mk_none() { return {0u}; }
 #endif
 
 SD V lanes() { return V{__lane_id()}; }
@@ -195,6 +199,8 @@ struct V {
 struct B {
     u64 m;
 };
+SD B mk_all() { return {~0ull}; }
+SD B mk_none() { return {0ull}; }
 #define MTE_L for (u32 l = 0; l < 64; l++)
 
 SD V lanes() {

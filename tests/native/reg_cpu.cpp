@@ -16,11 +16,23 @@ using namespace mte;
 // vis = len, seq, removedSeq, meta; aux = props, text offset, text capacity / overlap, segment id),
 // the gathered text, and the DocRes record. Returns the op index the replay stopped at (n_ops when
 // done or failed; earlier when the document would hand over to the LDS engine).
-template <bool PAGED>
+// Property tables of a PROPS replay (the host's interned propsets, Params::propsets & co.).
+struct PropTables {
+    const mte_propset* propsets;
+    uint32_t n_propsets;
+    const uint32_t* prop_keys;
+    const uint32_t* prop_vals;
+    const uint32_t* val_flags;
+    uint32_t n_vals;
+    uint32_t map_words, map_cap;
+    uint32_t* out_maps;  // per output row, map_words words
+};
+
+template <bool PAGED, bool PROPS>
 static uint64_t replay_impl(const mte_op* ops, uint64_t n_ops, const uint16_t* payload, uint32_t payload_len,
                             uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
                             uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
-                            DocRes* res, uint32_t pool_rows) {
+                            DocRes* res, uint32_t pool_rows, const PropTables* pt = nullptr) {
     std::vector<uint16_t> pay(payload, payload + payload_len + 1);
     std::vector<uint16_t> arena((size_t)arena_cap * 2 + 1, 0);
     DocCfg cfg;
@@ -47,9 +59,29 @@ static uint64_t replay_impl(const mte_op* ops, uint64_t n_ops, const uint16_t* p
     p.out_text = out_text;
     p.out_text_cap = out_text_cap;
     p.counters = counters;
+    std::vector<uint32_t> maps, objidx;
+    std::vector<uint64_t> objmatch;
+    if (PROPS) {
+        cfg.map_cap = pt->map_cap;
+        maps.assign((size_t)pt->map_cap * pt->map_words, 0);
+        objidx.assign(pt->n_vals, NONE);
+        objmatch.assign(pt->n_vals, 0);
+        p.maps = maps.data();
+        p.map_words = pt->map_words;
+        p.propsets = pt->propsets;
+        p.n_propsets = pt->n_propsets;
+        p.prop_keys = pt->prop_keys;
+        p.prop_vals = pt->prop_vals;
+        p.val_flags = pt->val_flags;
+        p.val_objidx = objidx.data();
+        p.val_objmatch = objmatch.data();
+        p.n_vals = pt->n_vals;
+        p.out_maps = pt->out_maps;
+    }
     // (the paged engine's pool is its own row arrays here, rows taken in a scattered order)
-    RegEngine<(int)RG_ROWS, PAGED>* ep = new RegEngine<(int)RG_ROWS, PAGED>(p, 0);
-    RegEngine<(int)RG_ROWS, PAGED>& e = *ep;
+    typedef RegEngine<(int)RG_ROWS, PAGED, PROPS> E;
+    E* ep = new E(p, 0);
+    E& e = *ep;
     if (PAGED) {
         e.release_rows();
         e.pool_rows = pool_rows < RG_ROWS ? pool_rows : RG_ROWS;
@@ -76,8 +108,8 @@ uint64_t regcpu_replay(const mte_op* ops, uint64_t n_ops, const uint16_t* payloa
                        uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
                        uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
                        DocRes* res) {
-    return replay_impl<false>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
-                              out_cap, out_text, out_text_cap, res, 0);
+    return replay_impl<false, false>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
+                                     out_cap, out_text, out_text_cap, res, 0);
 }
 
 // The PAGED engine (k_rows): logical rows mapped to pool rows taken in a scattered order from a pool
@@ -86,8 +118,24 @@ uint64_t regcpu_replay_paged(const mte_op* ops, uint64_t n_ops, const uint16_t* 
                              uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
                              uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
                              DocRes* res, uint32_t pool_rows) {
-    return replay_impl<true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
-                             out_cap, out_text, out_text_cap, res, pool_rows);
+    return replay_impl<true, false>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
+                                    out_cap, out_text, out_text_cap, res, pool_rows);
+}
+
+// The PROPS engine (k_rows of property-carrying batches), paged when pool_rows > 0: property maps in
+// a table of map_cap records of map_words words; each final row's map copied to out_maps.
+uint64_t regcpu_replay_props(const mte_op* ops, uint64_t n_ops, const uint16_t* payload, uint32_t payload_len,
+                             uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
+                             uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
+                             DocRes* res, uint32_t pool_rows, const uint32_t* propsets, uint32_t n_propsets,
+                             const uint32_t* prop_keys, const uint32_t* prop_vals, const uint32_t* val_flags,
+                             uint32_t n_vals, uint32_t map_words, uint32_t map_cap, uint32_t* out_maps) {
+    PropTables t{(const mte_propset*)propsets, n_propsets, prop_keys, prop_vals, val_flags, n_vals, map_words, map_cap, out_maps};
+    if (pool_rows)
+        return replay_impl<true, true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
+                                       out_cap, out_text, out_text_cap, res, pool_rows, &t);
+    return replay_impl<false, true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
+                                    out_cap, out_text, out_text_cap, res, 0, &t);
 }
 
 uint32_t regcpu_docres_size(void) { return (uint32_t)sizeof(DocRes); }

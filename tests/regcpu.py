@@ -36,6 +36,9 @@ def lib():
         L.regcpu_replay.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u32, vp, u64, vp]
         L.regcpu_replay_paged.restype = u64
         L.regcpu_replay_paged.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u32, vp, u64, vp, u32]
+        L.regcpu_replay_props.restype = u64
+        L.regcpu_replay_props.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u32, vp, u64, vp, u32,
+                                          vp, u32, vp, vp, vp, u32, u32, u32, vp]
         L.regcpu_docres_size.restype = u32
         L.regcpu_heap.restype = u32
         L.regcpu_heap.argtypes = [vp, u32, vp]
@@ -72,7 +75,71 @@ def replay(ops, pay, arena_cap=None, pool_rows=None):
     return at, r, (vis[:k], aux[:k], ovl[:k]), text
 
 
-def rows_json(rows, text, names):
+class GenProps:
+    """The generator's property sets (mte_host.cpp build_generator_props, the oracle's genPropset):
+    ids 1..28 one key, then 294 two-key sets; value id 0 = null. Interned tables for the engine and
+    the oracle's batch."""
+    KEYS = ["bold", "italic", "color", "size"]
+    VALS = ["null", "true", "false", '"red"', '"blue"', "10", "12"]  # value ids
+    GEN_VALS = [1, 2, 3, 4, 5, 6, 0]  # the generator's value order -> value id
+
+    def __init__(self):
+        sets = [[]]
+        for k in range(4):
+            for v in range(7):
+                sets.append([(k, self.GEN_VALS[v])])
+        for k1 in range(4):
+            for k2 in range(k1 + 1, 4):
+                for v1 in range(7):
+                    for v2 in range(7):
+                        sets.append([(k1, self.GEN_VALS[v1]), (k2, self.GEN_VALS[v2])])
+        ps, keys, vals = [], [], []
+        for st in sets:
+            ps += [len(keys), len(st)]
+            for k, v in st:
+                keys.append(k)
+                vals.append(v)
+        self.propsets = np.array(ps, dtype=np.uint32)
+        self.prop_keys = np.array(keys + [0], dtype=np.uint32)
+        self.prop_vals = np.array(vals + [0], dtype=np.uint32)
+        self.val_flags = np.array([1 if v in ("null", "false") else 0 for v in self.VALS], dtype=np.uint32)
+        self.n_propsets = len(sets)
+
+    def render(self, rec):
+        """A map record [n, k0, v0, ...] as JSON.stringify of the property object."""
+        n = int(rec[0])
+        return "{" + ",".join('"%s":%s' % (self.KEYS[int(rec[1 + 2 * i])], self.VALS[int(rec[2 + 2 * i])])
+                              for i in range(n)) + "}"
+
+
+def replay_props(ops, pay, gp, pool_rows=0, map_words=16):
+    """The PROPS engine (k_rows' property-carrying form) on the CPU: (stop index, DocRes, rows, text,
+    per-row map records)."""
+    ops = np.ascontiguousarray(ops, dtype=_op_dtype())
+    pay = np.ascontiguousarray(pay, dtype=np.uint16)
+    n = len(ops)
+    seg_cap = 3 * n + 8
+    arena_cap = 6 * len(pay) + 4096
+    cap = seg_cap
+    vis = np.zeros((cap, 4), dtype=np.uint32)
+    aux = np.zeros((cap, 4), dtype=np.uint32)
+    ovl = np.zeros(cap, dtype=np.uint64)
+    text = np.zeros(len(pay) + 16, dtype=np.uint16)
+    res = np.zeros(1, dtype=DOCRES)
+    omaps = np.zeros((cap, map_words), dtype=np.uint32)
+    pay1 = np.concatenate([pay, np.zeros(1, dtype=np.uint16)])
+    map_cap = 2 * n + 64
+    at = lib().regcpu_replay_props(ops.ctypes.data, n, pay1.ctypes.data, len(pay), seg_cap, arena_cap,
+                                   vis.ctypes.data, aux.ctypes.data, ovl.ctypes.data, cap, text.ctypes.data,
+                                   len(text), res.ctypes.data, pool_rows, gp.propsets.ctypes.data, gp.n_propsets,
+                                   gp.prop_keys.ctypes.data, gp.prop_vals.ctypes.data, gp.val_flags.ctypes.data,
+                                   len(gp.VALS), map_words, map_cap, omaps.ctypes.data)
+    r = res[0]
+    k = int(r["n_segs"])
+    return at, r, (vis[:k], aux[:k], ovl[:k]), text, omaps[:k]
+
+
+def rows_json(rows, text, names, props=None):
     """The engine's rows as mte_segments_json renders them (host DocView, mte_host.cpp)."""
     vis, aux, ovl = rows
     out = []
@@ -92,7 +159,7 @@ def rows_json(rows, text, names):
             row["removedSeq"] = rseq if rseq < 2 ** 31 else rseq - 2 ** 32
             row["removedClient"] = names[(meta >> 8) & 0xFF]
         row["overlap"] = [names[b] for b in range(64) if (int(ovl[i]) >> b) & 1]
-        row["props"] = None
+        row["props"] = props(i) if props and int(aux[i][0]) else None
         out.append(row)
     return json.dumps(out, separators=(",", ":"), ensure_ascii=False)
 
@@ -116,7 +183,7 @@ class OneDocBatch:
     """A one-document mte_batch over numpy op records + payload, clients named `names` by short id
     (index 0 = the observer). Keeps its buffers alive."""
 
-    def __init__(self, ops, pay, names):
+    def __init__(self, ops, pay, names, gp=None):
         self.ops = np.ascontiguousarray(ops, dtype=_op_dtype())
         self.pay = np.ascontiguousarray(pay, dtype=np.uint16)
         self.opo = (ctypes.c_uint64 * 2)(0, len(self.ops))
@@ -148,6 +215,24 @@ class OneDocBatch:
         b.doc_client_offsets = ctypes.cast(self.cli, ctypes.POINTER(ctypes.c_uint32))
         b.client_name_offsets = ctypes.cast(self.cno, ctypes.POINTER(ctypes.c_uint64))
         b.client_names = ctypes.addressof(self.cn)
+        if gp is not None:  # the generator's property sets
+            self.gp = gp
+            b.n_propsets = gp.n_propsets
+            b.propsets = gp.propsets.ctypes.data
+            b.prop_keys = gp.prop_keys.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+            b.prop_vals = gp.prop_vals.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+            kt = [('"%s"' % k).encode() for k in gp.KEYS]
+            vt = [v.encode() for v in gp.VALS]
+            self.keyo = (ctypes.c_uint64 * (len(kt) + 1))(*np.cumsum([0] + [len(x) for x in kt]).tolist())
+            self.keytext = ctypes.create_string_buffer(b"".join(kt))
+            self.valo = (ctypes.c_uint64 * (len(vt) + 1))(*np.cumsum([0] + [len(x) for x in vt]).tolist())
+            self.valtext = ctypes.create_string_buffer(b"".join(vt))
+            b.n_keys = len(kt)
+            b.key_offsets = ctypes.cast(self.keyo, ctypes.POINTER(ctypes.c_uint64))
+            b.key_text = ctypes.addressof(self.keytext)
+            b.n_vals = len(vt)
+            b.val_offsets = ctypes.cast(self.valo, ctypes.POINTER(ctypes.c_uint64))
+            b.val_text = ctypes.addressof(self.valtext)
         self.batch = b
 
     def oracle(self):
@@ -180,6 +265,30 @@ def compare(ops, pay, names=None, arena_cap=None, pool_rows=None):
         assert int(res["failing_seq"]) == fseq
         return res
     js, oj = rows_json(rows, text, names), o.segments_json()
+    if js != oj:
+        a, b = json.loads(js), json.loads(oj)
+        for i, (x, y) in enumerate(zip(a, b)):
+            if x != y:
+                raise AssertionError(f"segment {i} differs:\n engine {x}\n oracle {y}\n ({len(a)} vs {len(b)} rows)")
+        raise AssertionError(f"segment count differs: {len(a)} vs {len(b)}")
+    assert engine_text(rows, text) == o.text()
+    return res
+
+
+def compare_props(ops, pay, pool_rows=0):
+    """The PROPS engine against the oracle on a generated kind-3 log: status, segment table with
+    each segment's properties (JSON.stringify of the map), text. Returns the DocRes record."""
+    gp = GenProps()
+    nc = int(ops["client"].max()) if len(ops) else 0
+    names = ["__observer__"] + [f"w{i}" for i in range(1, max(nc, 1) + 1)]
+    at, res, rows, text, omaps = replay_props(ops, pay, gp, pool_rows=pool_rows)
+    assert int(res["status"]) != REG_HANDOFF, f"handed off at op {at} (n_lb {res['n_lb']})"
+    o = OneDocBatch(ops, pay, names, gp=gp).oracle()
+    code, err, fseq = o.status()
+    assert int(res["status"]) == code, f"status engine={int(res['status'])} oracle={code} ({err})"
+    if code:
+        return res
+    js, oj = rows_json(rows, text, names, props=lambda i: gp.render(omaps[i])), o.segments_json()
     if js != oj:
         a, b = json.loads(js), json.loads(oj)
         for i, (x, y) in enumerate(zip(a, b)):

@@ -179,3 +179,32 @@ def test_bulk_rows_pool_shared_and_exhausted(engine, waves):
         _check(engine, batch, n_docs=1024)
     finally:
         engine.set_option("rows_bulk", -1)
+
+
+@pytest.mark.parametrize("waves", [4, 8])
+def test_bulk_rows_props_matches_oracle(engine, waves):
+    """Property-carrying batches on k_rows' PROPS engine (C3's mix: 45/35/20 insert / remove /
+    annotate, property maps per segment, merges only between matching maps): a Zipf mix and a
+    C3-shaped batch, every checksum (text + SnapshotV1 blobs with the properties) against the
+    oracle."""
+    from fluidframework_amd.shard import zipf_op_counts
+
+    engine.set_option("rows_bulk", waves)
+    try:
+        counts = zipf_op_counts(2000, seed=waves, lo=50, hi=30_000)
+        engine.generate(3, len(counts), 0, n_clients=8, seed=41, ops_per_doc=counts)
+        batch = engine.export_batch()
+        st = engine.replay()
+        assert st["failed_docs"] == 0 and engine.get_info("rows") == waves and engine.run_info()["lean"] == 0
+        modes = [engine.doc_result(d)["mode"] for d in range(len(counts))]
+        assert modes.count(MODE_BULK_ROWS) > 0.9 * len(counts), sorted(set(modes))
+        _check(engine, batch, n_docs=len(counts))
+        engine.generate(3, 1024, 10_000, n_clients=8, seed=1000)
+        batch = engine.export_batch()
+        st = engine.replay()
+        assert st["failed_docs"] == 0
+        modes = [engine.doc_result(d)["mode"] for d in range(1024)]
+        assert modes.count(MODE_BULK_ROWS) > 0.9 * 1024, sorted(set(modes))
+        _check(engine, batch, n_docs=1024)
+    finally:
+        engine.set_option("rows_bulk", -1)

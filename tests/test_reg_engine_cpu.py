@@ -193,3 +193,26 @@ def test_lru_heap_pop_order(seed):
     out = np.zeros(len(ops), dtype=np.uint32)
     n = regcpu.lib().regcpu_heap(arr.ctypes.data, len(ops), out.ctypes.data)
     assert list(out[:n]) == _heap_pops(ops)
+
+
+@pytest.mark.parametrize("gid,n_ops,clients,pool", [(1, 3000, 8, 0), (2, 10_000, 8, 0), (3, 10_000, 8, 32),
+                                                    (4, 6000, 16, 0), (7, 20_000, 8, 24), (9, 2000, 31, 0)])
+def test_props_engine_matches_oracle(gid, n_ops, clients, pool):
+    """The PROPS row engine (k_rows for property-carrying batches): C3-mix logs (45/35/20 insert /
+    remove / annotate, 15 % forced ties), property maps built on insert and annotate, merges only
+    between segments whose maps match (deep, not by id), paged rows when pool > 0; segment table
+    with every segment's properties and the text against the oracle."""
+    ops, pay = regcpu.generated(3, gid, n_ops, n_clients=clients, seed=1000)
+    assert (ops["type"] == 2).sum() > n_ops // 10
+    r = regcpu.compare_props(ops, pay, pool_rows=pool)
+    assert int(r["map_next"]) > n_ops // 4
+
+
+def test_props_engine_rewrite_annotates():
+    """annotate with combiningOp rewrite (MTE_F_REWRITE: keys whose new value is falsy or absent are
+    dropped, segmentPropertiesManager.ts:65-78) on every third annotate of a C3-mix log."""
+    ops, pay = regcpu.generated(3, 11, 8000, n_clients=8, seed=1000)
+    ann = np.nonzero(ops["type"] == 2)[0][::3]
+    ops = ops.copy()
+    ops["flags"][ann] |= 0x2
+    regcpu.compare_props(ops, pay)

@@ -310,7 +310,8 @@ def run(args):
                       "us_per_op_critical_path": (info.get("solo_us", 0) / max(int(counts.max()), 1)) if info["solo"] else None,
                       "docs_rerun_hbm": info["spilled"], "docs_continued_hbm": info["continued"],
                       "docs_hbm_waves": info["hbm_docs"], "lds_groups": info["lds_groups"],
-                      "hbm_wave_slots": info["hbm_waves"], "gen_s": gen_s, "summary_s": snap_host_s,
+                      "hbm_wave_slots": info["hbm_waves"], "rows_waves_per_cu": eng.get_info("rows"),
+                      "gen_s": gen_s, "summary_s": snap_host_s,
                       "snapshot_bytes": snap_bytes, "summaries_gathered": gathered, "oracle_verified_docs": nv},
         }
         print(json.dumps(line), flush=True)

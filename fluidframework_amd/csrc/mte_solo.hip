@@ -63,6 +63,23 @@ MTE_DEV void solo_doc(const Params& p) {
             reg_handoff(r, e);
             handed = true;
         }
+    } else if constexpr (!GEN && LVL == 1) {
+        // property-carrying replay: the PROPS row engine, its map ids in an array past the rows'
+        // slots in the SoloPlan's aux array (blocks RG_BLOCKS.., unused until a handoff has read it)
+        if (p.reg_solo) {
+            constexpr u32 vb = (u32)offsetof(SoloPlan, vis), ab = (u32)offsetof(SoloPlan, aux);
+            static_assert(RG_BLOCKS * 8 * 16 + RG_BLOCKS * 8 * 4 <= SOLO_POOL * 8 * 16, "props array in the aux pool");
+            RegEngine<(int)RG_ROWS, false, true> r(p, d, vb, ab, 4, 0, ab + RG_BLOCKS * 8 * 16);
+            if (!r.status) at = r.replay(at, p.docs[d].op_end);
+            if (r.status != REG_HANDOFF) {
+                r.finish();
+                stamp();
+                __builtin_amdgcn_s_setprio(0);
+                return;
+            }
+            reg_handoff(r, e);
+            handed = true;
+        }
     }
     if (!handed) e.init();
     if (GEN) {

@@ -130,6 +130,7 @@ struct RFound {
 // ops, and merges that require matching properties.
 template <int NR = (int)RG_ROWS, bool PAGED = false, bool PROPS = false>
 struct RegEngine {
+    static constexpr bool kProps = PROPS;
     typedef simd::V V;
     typedef simd::B B;
     static constexpr u32 NBLK = (u32)NR * 8;
@@ -415,6 +416,14 @@ struct RegEngine {
     }
     SD void zero_slots(u32 at, u32 n) {
         cr = NONE;
+        if constexpr (!PAGED && !PROPS) {
+            for (u32 b = __lane_id(); b < n; b += 64) {
+                VISP()[at + b] = make_uint4(0, 0, 0, 0);
+                AUXP()[at + b] = make_uint4(0, 0, 0, 0);
+            }
+            simd::lds_order();
+            return;
+        }
         for (u32 c = 0; c < n; c += 64) {
             const u32 b = c + __lane_id();
             const u32 ps = pslot(at + (b < n ? b : 0u));
@@ -569,7 +578,7 @@ struct RegEngine {
     // a fresh map id (the LDS engine's build_map, engine.hpp, lane for lane)
     SD u32 build_map(u32 old, u32 propset, bool rewrite) {
         if (mapNext >= map_cap) {  // the load-time estimate was short: the host re-runs it with the worst case
-            fail(REG_HANDOFF, curSeq);
+            fail(res_mode == 4 ? DOC_SPILL : REG_HANDOFF, curSeq);  // (k_solo cannot hand over mid-op)
             return 0;
         }
         fence_arena();

@@ -93,7 +93,9 @@ MTE_DEV void reg_handoff(R& r, E& e) {
         // removedClient) or 0
         const u32 ovm = a.z & ~(1u << ((v.w >> 8) & 31u));
         e.VIS()[64 * rr + L] = make_uint4(v.x, v.y, live ? 0u : v.z, m2);
-        e.AUX()[64 * rr + L] = make_uint4(0u, a.y, live ? a.x : (ov ? ovm : 0u), v.x ? a.w - 1u : 0u);
+        u32 props = 0;
+        if constexpr (R::kProps) props = v.x ? r.PROPP()[64 * rr + L] : 0u;  // beyond the rows' slots: intact
+        e.AUX()[64 * rr + L] = make_uint4(props, a.y, live ? a.x : (ov ? ovm : 0u), v.x ? a.w - 1u : 0u);
     }
     // replay state and per-document counters
     St& st = e.st;
@@ -107,7 +109,8 @@ MTE_DEV void reg_handoff(R& r, E& e) {
     st.segNext = r.segNext;
     st.arenaTop = r.arenaTop;
     st.arenaSel = r.arenaSel;
-    st.mapNext = 1;
+    if constexpr (R::kProps) st.mapNext = r.mapNext;  // the same per-document map table
+    else st.mapNext = 1;
     st.lbFree = NONE;
     st.lbBump = r.n_lb;
     st.inFree = NONE;
@@ -116,7 +119,7 @@ MTE_DEV void reg_handoff(R& r, E& e) {
     st.credit = 0;
     st.status = 0;
     st.adirty = 1;  // merge-arena text written by other lanes: fence before the next read
-    st.gdirty = 0;
+    st.gdirty = R::kProps ? 1 : 0;  // map records written lane-parallel by the register engine
     if (L == 0) {
         u32* S = e.STATS();
         S[ST_OPS] = r.n_ops;

@@ -4,6 +4,7 @@ bit-exact against the oracle: checksums (text + SnapshotV1 blobs) and, for a doc
 the full segment table."""
 import ctypes
 
+import numpy as np
 import pytest
 
 from fluidframework_amd import mte
@@ -61,6 +62,41 @@ def test_row_engine_hands_off_mid_document(engine, limit):
         _check(engine, batch)
     finally:
         engine.set_option("reg_lb_limit", 0)
+
+
+@pytest.mark.parametrize("n_ops,clients,limit", [(3000, 8, 0), (40_000, 8, 0), (8000, 16, 0), (6000, 8, 20),
+                                                (6000, 8, 40)])
+def test_props_row_engine_lone_documents(engine, n_ops, clients, limit):
+    """A property-carrying (kind 3) critical-path document on k_solo's PROPS row engine (mode 4) from
+    start to end, or handed to the LDS engine part-way with its property map ids and map table
+    (reg_lb_limit 20 / 40: mode 3); checksums with the SnapshotV1 property blobs against the oracle."""
+    engine.set_option("reg_lb_limit", limit)
+    try:
+        engine.generate(3, 1, n_ops, n_clients=clients, seed=17)
+        batch = engine.export_batch()
+        st = engine.replay()
+        assert engine.run_info()["solo"] == 1 and engine.run_info()["lean"] == 0
+        r = engine.doc_result(0)
+        assert r["status"] == 0 and st["ops"] == n_ops, r
+        assert r["mode"] == (MODE_SOLO_LDS if limit else MODE_ROWS), r
+        _check(engine, batch)
+    finally:
+        engine.set_option("reg_lb_limit", 0)
+
+
+def test_props_zipf_head_on_rows(engine):
+    """The head of a Zipf kind-3 batch runs on k_solo's PROPS row engine (mode 4); the rest of the
+    batch on k_lds beside it; every checksum against the oracle."""
+    from fluidframework_amd.shard import zipf_op_counts
+
+    counts = zipf_op_counts(1024, seed=3, lo=100, hi=100_000)
+    engine.generate(3, len(counts), 0, n_clients=8, seed=5, ops_per_doc=counts)
+    batch = engine.export_batch()
+    st = engine.replay()
+    assert st["failed_docs"] == 0 and engine.run_info()["solo"] >= 1
+    head = int(np.argmax(counts))
+    assert engine.doc_result(head)["mode"] == MODE_ROWS, engine.doc_result(head)
+    _check(engine, batch, n_docs=len(counts))
 
 
 def test_row_engine_off_equals_on(engine):

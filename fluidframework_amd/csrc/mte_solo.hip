@@ -64,12 +64,15 @@ MTE_DEV void solo_doc(const Params& p) {
             handed = true;
         }
     } else if constexpr (!GEN && LVL == 1) {
-        // property-carrying replay: the PROPS row engine, its map ids in an array past the rows'
-        // slots in the SoloPlan's aux array (blocks RG_BLOCKS.., unused until a handoff has read it)
+        // FULL replay (properties, clients up to 63): the PROPS + WIDE row engine, its map ids and
+        // high removers in arrays past the rows' slots in the SoloPlan's aux array (blocks
+        // RG_BLOCKS.., unused until a handoff has read them)
         if (p.reg_solo) {
             constexpr u32 vb = (u32)offsetof(SoloPlan, vis), ab = (u32)offsetof(SoloPlan, aux);
-            static_assert(RG_BLOCKS * 8 * 16 + RG_BLOCKS * 8 * 4 <= SOLO_POOL * 8 * 16, "props array in the aux pool");
-            RegEngine<(int)RG_ROWS, false, true> r(p, d, vb, ab, 4, 0, ab + RG_BLOCKS * 8 * 16);
+            static_assert(RG_BLOCKS * 8 * 16 + 2 * RG_BLOCKS * 8 * 4 <= SOLO_POOL * 8 * 16, "props / rm2 arrays in the aux pool");
+            // WIDE: clients 32..63 too (a second removers array after the map ids)
+            RegEngine<(int)RG_ROWS, false, true, true> r(p, d, vb, ab, 4, 0, ab + RG_BLOCKS * 8 * 16,
+                                                         ab + RG_BLOCKS * 8 * 16 + RG_BLOCKS * 8 * 4);
             if (!r.status) at = r.replay(at, p.docs[d].op_end);
             if (r.status != REG_HANDOFF) {
                 r.finish();

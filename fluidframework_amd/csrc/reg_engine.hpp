@@ -111,6 +111,23 @@ struct RSeg {
     u32 rm;   // removers: bit c for removedClient c and every client in removedClientOverlap
     u32 sid;
     u32 props = 0;  // property map id (PROPS engines; 0 = no properties)
+    u32 rm2 = 0;    // removers 32..63 (WIDE engines)
+};
+// the extra slot fields of a PROPS engine's rows (the property map id) and of a WIDE one's (removers
+// 32..63); absent otherwise: the lean rows stay eight registers
+template <bool P, bool W>
+struct RowProps {};
+template <>
+struct RowProps<true, false> {
+    simd::V props;
+};
+template <>
+struct RowProps<false, true> {
+    simd::V rm2;
+};
+template <>
+struct RowProps<true, true> {
+    simd::V props, rm2;
 };
 struct RFound {
     bool ok;
@@ -128,17 +145,18 @@ struct RFound {
 // PROPS (k_rows of property-carrying batches): a ninth slot field, the segment's property map id
 // (immutable maps in the document's HBM map table, SegmentPropertiesManager.addProperties), annotate
 // ops, and merges that require matching properties.
-template <int NR = (int)RG_ROWS, bool PAGED = false, bool PROPS = false>
+// WIDE (k_solo's property-carrying instantiation): clients 32..63 too, a second removers word per slot.
+template <int NR = (int)RG_ROWS, bool PAGED = false, bool PROPS = false, bool WIDE = false>
 struct RegEngine {
-    static constexpr bool kProps = PROPS;
+    static constexpr bool kProps = PROPS, kWide = WIDE;
+    static constexpr u32 MAXC = WIDE ? 64u : 32u;  // client ids below this (rm, rm2)
     typedef simd::V V;
     typedef simd::B B;
     static constexpr u32 NBLK = (u32)NR * 8;
     // One row of slots: vis = (len, seq, rseq, meta), aux = (cap, toff, rm, sid). A live segment has
     // rm 0, so nodeLength's removal test is one bit test of rm (no separate overlap-set lookup).
-    struct Row {
+    struct Row : RowProps<PROPS, WIDE> {
         V len, seq, rseq, meta, cap, toff, rm, sid;
-        V props;  // PROPS only (never loaded, stored or read otherwise)
     };
 
     // ---------------------------------------------------------------- state
@@ -200,7 +218,7 @@ struct RegEngine {
     }
 #ifdef MTE_CPU
     u32 mem_vis[RG_ROWS * 64][4], mem_aux[RG_ROWS * 64][4];
-    u32 mem_props[RG_ROWS * 64];
+    u32 mem_props[RG_ROWS * 64], mem_rm2[RG_ROWS * 64];
     u64 pool_mask = 0;           // PAGED: pool rows in use (this engine's own pool on the CPU)
     u32 pool_rows = RG_ROWS, pool_takes = 0;
     SD u32 pslot(u32 s) const { return PAGED ? prow(s >> 6) * 64 + (s & 63) : s; }
@@ -221,6 +239,7 @@ struct RegEngine {
         memset(mem_vis[row * 64], 0, 64 * 16);
         memset(mem_aux[row * 64], 0, 64 * 16);
         memset(&mem_props[row * 64], 0, 64 * 4);
+        memset(&mem_rm2[row * 64], 0, 64 * 4);
     }
     SD Row ldrow(u32 r) const {
         Row w;
@@ -230,7 +249,8 @@ struct RegEngine {
             const u32* a = mem_aux[pr * 64 + l];
             w.len.x[l] = v[0], w.seq.x[l] = v[1], w.rseq.x[l] = v[2], w.meta.x[l] = v[3];
             w.cap.x[l] = a[0], w.toff.x[l] = a[1], w.rm.x[l] = a[2], w.sid.x[l] = a[3];
-            w.props.x[l] = PROPS ? mem_props[pr * 64 + l] : 0u;
+            if constexpr (PROPS) w.props.x[l] = mem_props[pr * 64 + l];
+            if constexpr (WIDE) w.rm2.x[l] = mem_rm2[pr * 64 + l];
         }
         return w;
     }
@@ -241,7 +261,8 @@ struct RegEngine {
             u32* a = mem_aux[pr * 64 + l];
             v[0] = w.len.x[l], v[1] = w.seq.x[l], v[2] = w.rseq.x[l], v[3] = w.meta.x[l];
             a[0] = w.cap.x[l], a[1] = w.toff.x[l], a[2] = w.rm.x[l], a[3] = w.sid.x[l];
-            if (PROPS) mem_props[pr * 64 + l] = w.props.x[l];
+            if constexpr (PROPS) mem_props[pr * 64 + l] = w.props.x[l];
+            if constexpr (WIDE) mem_rm2[pr * 64 + l] = w.rm2.x[l];
         }
     }
     SD V ldf(u32 r, u32 aux, u32 c) const {  // one field of a row
@@ -262,6 +283,7 @@ struct RegEngine {
             memmove(mem_vis[dst], mem_vis[src], (size_t)n * 16);
             memmove(mem_aux[dst], mem_aux[src], (size_t)n * 16);
             memmove(&mem_props[dst], &mem_props[src], (size_t)n * 4);
+            memmove(&mem_rm2[dst], &mem_rm2[src], (size_t)n * 4);
             return;
         }
         for (u32 t = 0; t < n; t++) {  // slot by slot in the memmove's safe direction
@@ -269,6 +291,7 @@ struct RegEngine {
             memcpy(mem_vis[pslot(dst + i)], mem_vis[pslot(src + i)], 16);
             memcpy(mem_aux[pslot(dst + i)], mem_aux[pslot(src + i)], 16);
             mem_props[pslot(dst + i)] = mem_props[pslot(src + i)];
+            mem_rm2[pslot(dst + i)] = mem_rm2[pslot(src + i)];
         }
     }
     SD void zero_slots(u32 at, u32 n) {
@@ -277,6 +300,7 @@ struct RegEngine {
             memset(mem_vis[pslot(at + i)], 0, 16);
             memset(mem_aux[pslot(at + i)], 0, 16);
             mem_props[pslot(at + i)] = 0;
+            mem_rm2[pslot(at + i)] = 0;
         }
     }
 #else
@@ -287,6 +311,8 @@ struct RegEngine {
     SD uint4* AUXP() const { return reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + abase); }
     u32 pbase = 0;  // PROPS: byte offset of the slots' property map ids (one u32 per slot)
     SD u32* PROPP() const { return reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + pbase); }
+    u32 r2base = 0;  // WIDE: byte offset of the slots' removers 32..63 (one u32 per slot)
+    SD u32* RM2P() const { return reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + r2base); }
     u32 pool_off = 0;  // PAGED: byte offset of the pool's row mask (ROWS_POOL_WORDS words)
     SD u32* pool_words() const { return reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + pool_off); }
     SD bool take_row(u32& row) {  // lane 0 claims a free pool row with an LDS atomic or
@@ -317,6 +343,7 @@ struct RegEngine {
         VISP()[row * 64 + __lane_id()] = make_uint4(0, 0, 0, 0);
         AUXP()[row * 64 + __lane_id()] = make_uint4(0, 0, 0, 0);
         if constexpr (PROPS) PROPP()[row * 64 + __lane_id()] = 0u;
+        if constexpr (WIDE) RM2P()[row * 64 + __lane_id()] = 0u;
         simd::lds_order();
     }
     // physical slot of logical slot s, per lane (PAGED: a block range can cross pool rows)
@@ -327,13 +354,19 @@ struct RegEngine {
     SD Row ldrow(u32 r) const {
         const u32 i = prow(r) * 64 + __lane_id();
         const uint4 v = VISP()[i], a = AUXP()[i];
-        return Row{V{v.x}, V{v.y}, V{v.z}, V{v.w}, V{a.x}, V{a.y}, V{a.z}, V{a.w}, V{PROPS ? PROPP()[i] : 0u}};
+        Row w;
+        w.len = V{v.x}, w.seq = V{v.y}, w.rseq = V{v.z}, w.meta = V{v.w};
+        w.cap = V{a.x}, w.toff = V{a.y}, w.rm = V{a.z}, w.sid = V{a.w};
+        if constexpr (PROPS) w.props = V{PROPP()[i]};
+        if constexpr (WIDE) w.rm2 = V{RM2P()[i]};
+        return w;
     }
     SD void strow(u32 r, const Row& w) {
         const u32 i = prow(r) * 64 + __lane_id();
         VISP()[i] = make_uint4(w.len.x, w.seq.x, w.rseq.x, w.meta.x);
         AUXP()[i] = make_uint4(w.cap.x, w.toff.x, w.rm.x, w.sid.x);
         if constexpr (PROPS) PROPP()[i] = w.props.x;
+        if constexpr (WIDE) RM2P()[i] = w.rm2.x;
         simd::lds_order();
     }
     SD V ldf(u32 r, u32 aux, u32 c) const {
@@ -360,17 +393,19 @@ struct RegEngine {
                 const u32 ii = ok ? (u32)i : 0u;
                 const u32 ps = pslot(src + ii), pd = pslot(dst + ii);
                 uint4 v = make_uint4(0, 0, 0, 0), a = v;
-                u32 pp = 0;
+                u32 pp = 0, q2 = 0;
                 if (ok) {
                     v = V4[ps];
                     a = A4[ps];
                     if constexpr (PROPS) pp = PROPP()[ps];
+                    if constexpr (WIDE) q2 = RM2P()[ps];
                 }
                 simd::lds_order();
                 if (ok) {
                     V4[pd] = v;
                     A4[pd] = a;
                     if constexpr (PROPS) PROPP()[pd] = pp;
+                    if constexpr (WIDE) RM2P()[pd] = q2;
                 }
                 simd::lds_order();
             }
@@ -380,17 +415,19 @@ struct RegEngine {
             for (i32 b = (i32)n - 64; b > -64; b -= 64) {
                 const i32 i = b + (i32)L;
                 uint4 v = make_uint4(0, 0, 0, 0), a = v;
-                u32 pp = 0;
+                u32 pp = 0, q2 = 0;
                 if (i >= 0) {
                     v = V4[src + (u32)i];
                     a = A4[src + (u32)i];
                     if constexpr (PROPS) pp = PROPP()[src + (u32)i];
+                    if constexpr (WIDE) q2 = RM2P()[src + (u32)i];
                 }
                 simd::lds_order();
                 if (i >= 0) {
                     V4[dst + (u32)i] = v;
                     A4[dst + (u32)i] = a;
                     if constexpr (PROPS) PROPP()[dst + (u32)i] = pp;
+                    if constexpr (WIDE) RM2P()[dst + (u32)i] = q2;
                 }
                 simd::lds_order();
             }
@@ -398,17 +435,19 @@ struct RegEngine {
             for (u32 b = 0; b < n; b += 64) {
                 const u32 i = b + L;
                 uint4 v = make_uint4(0, 0, 0, 0), a = v;
-                u32 pp = 0;
+                u32 pp = 0, q2 = 0;
                 if (i < n) {
                     v = V4[src + i];
                     a = A4[src + i];
                     if constexpr (PROPS) pp = PROPP()[src + i];
+                    if constexpr (WIDE) q2 = RM2P()[src + i];
                 }
                 simd::lds_order();
                 if (i < n) {
                     V4[dst + i] = v;
                     A4[dst + i] = a;
                     if constexpr (PROPS) PROPP()[dst + i] = pp;
+                    if constexpr (WIDE) RM2P()[dst + i] = q2;
                 }
                 simd::lds_order();
             }
@@ -416,7 +455,7 @@ struct RegEngine {
     }
     SD void zero_slots(u32 at, u32 n) {
         cr = NONE;
-        if constexpr (!PAGED && !PROPS) {
+        if constexpr (!PAGED && !PROPS && !WIDE) {
             for (u32 b = __lane_id(); b < n; b += 64) {
                 VISP()[at + b] = make_uint4(0, 0, 0, 0);
                 AUXP()[at + b] = make_uint4(0, 0, 0, 0);
@@ -431,6 +470,7 @@ struct RegEngine {
                 VISP()[ps] = make_uint4(0, 0, 0, 0);
                 AUXP()[ps] = make_uint4(0, 0, 0, 0);
                 if constexpr (PROPS) PROPP()[ps] = 0u;
+                if constexpr (WIDE) RM2P()[ps] = 0u;
             }
         }
         simd::lds_order();
@@ -501,10 +541,12 @@ struct RegEngine {
     SD RegEngine(const Params& p_, u32 doc_) : p(p_), doc(doc_) { setup(); }
 #ifndef MTE_CPU
     // rows in another LDS region (k_rows: one share of the CU's LDS per wave)
-    SD RegEngine(const Params& p_, u32 doc_, u32 vb, u32 ab, u32 mode, u32 pool = 0, u32 pb = 0) : p(p_), doc(doc_) {
+    SD RegEngine(const Params& p_, u32 doc_, u32 vb, u32 ab, u32 mode, u32 pool = 0, u32 pb = 0, u32 r2b = 0)
+        : p(p_), doc(doc_) {
         vbase = vb;
         abase = ab;
         pbase = pb;
+        r2base = r2b;
         pool_off = pool;
         res_mode = mode;
         setup();
@@ -707,7 +749,9 @@ struct RegEngine {
     // (live: rseq RSEQ_LIVE and rm 0; removed: bit C of rm covers removedClient and the overlap set)
     SD static V vis(const Row& w, i32 R, u32 C) {
         const B ins = simd::sle(w.seq, R) | (simd::bfe(w.meta, 0, 8) == C);
-        const B rem = simd::sle(w.rseq, R) | ((w.rm & (1u << C)) != 0u);
+        B rem;
+        if constexpr (WIDE) rem = simd::sle(w.rseq, R) | (((C < 32 ? w.rm : w.rm2) & (1u << (C & 31u))) != 0u);
+        else rem = simd::sle(w.rseq, R) | ((w.rm & (1u << C)) != 0u);
         return simd::sel(simd::andn(ins, rem), w.len, 0u);
     }
 
@@ -877,6 +921,7 @@ struct RegEngine {
         put(w.rm, rec.rm);
         put(w.sid, rec.sid);
         if constexpr (PROPS) put(w.props, rec.props);
+        if constexpr (WIDE) put(w.rm2, rec.rm2);
         writeback(r);
         if (cnt + 1 < 8) return k;
         split_block(k);
@@ -915,6 +960,7 @@ struct RegEngine {
         mv(w.rm, w2.rm, 0u);
         mv(w.sid, w2.sid, 0u);
         if constexpr (PROPS) mv(w.props, w2.props, 0u);
+        if constexpr (WIDE) mv(w.rm2, w2.rm2, 0u);
         // the new block's needsScour is undefined
         if (r2 == r) {
             w.meta = simd::sel(in_group(k + 1), w.meta & ~NS_MASK, w.meta);
@@ -1309,6 +1355,7 @@ struct RegEngine {
         cmp(w.rm, 0u);
         cmp(w.sid, 0u);
         if constexpr (PROPS) cmp(w.props, 0u);
+        if constexpr (WIDE) cmp(w.rm2, 0u);
         ns_put(w, k, SC_FALSE);  // scourNode's caller clears needsScour (mergeTree.ts:1457): same write
         putrow(r, w);
         scoured = true;
@@ -1381,7 +1428,8 @@ struct RegEngine {
                 } else if (mSET & bit) {
                     const u32 ln = simd::readlane(w.len, gb + s), to = simd::readlane(w.toff, gb + s);
                     const u32 tc = simd::readlane(w.cap, gb + s);
-                    const u32 sp = PROPS ? simd::readlane(w.props, gb + s) : 0u;
+                    u32 sp = 0;
+                    if constexpr (PROPS) sp = simd::readlane(w.props, gb + s);
                     const bool ok = prev >= 0 && pText && (mTXT & bit) && (pLen <= (u32)GRANULARITY || ln <= (u32)GRANULARITY) &&
                                     (!PROPS || match_props(pProps, sp));
                     if (ok) {  // TextSegment.append
@@ -1464,6 +1512,7 @@ struct RegEngine {
         cmp(w.meta, nullptr, NS_MASK);  // the block's needsScour stays in every lane
         cmp(w.sid, nullptr, 0u);
         if constexpr (PROPS) cmp(w.props, nullptr, 0u);
+        if constexpr (WIDE) cmp(w.rm2, nullptr, 0u);
         ns_put(w, k, SC_FALSE);
         putrow(r, w);
         scoured = true;
@@ -1527,6 +1576,7 @@ struct RegEngine {
         t.rm = gather(a.rm, b.rm);
         t.sid = gather(a.sid, b.sid);
         if constexpr (PROPS) t.props = gather(a.props, b.props);
+        if constexpr (WIDE) t.rm2 = gather(a.rm2, b.rm2);
         const i32 d = (i32)kk - (i32)m;
         shift_blocks(k0 + m, d);
         // destination: block k0 + dj slot dq <- item dj*base + min(dj, extra) + dq
@@ -1551,6 +1601,7 @@ struct RegEngine {
             put(w.rm, t.rm);
             put(w.sid, t.sid);
             if constexpr (PROPS) put(w.props, t.props);
+            if constexpr (WIDE) put(w.rm2, t.rm2);
             strow(rr, w);
         }
         cr = NONE;
@@ -1639,6 +1690,7 @@ struct RegEngine {
         t.cap = simd::readlane(w.cap, l);
         t.rm = simd::readlane(w.rm, l);
         if constexpr (PROPS) t.props = simd::readlane(w.props, l);  // the right piece shares the map
+        if constexpr (WIDE) t.rm2 = simd::readlane(w.rm2, l);
         const u32 sid = new_sid();
         if (sid == NONE) return NONE;
         const u32 rr = (u32)f.r;
@@ -1708,7 +1760,7 @@ struct RegEngine {
         RG_PROF(RP_RANGE);
         const u32 nrows = (n_lb + 7) >> 3;
         u32 carry = c1;
-        const u32 cbit = 1u << C;
+        const u32 cbit = WIDE ? 1u << (C & 31u) : 1u << C;
         for (u32 r = r1; r < nrows && (i32)carry < p2; r++) {
             Row& w = rowref(r);
             const V v = vis(w, R, C);
@@ -1720,7 +1772,11 @@ struct RegEngine {
             if (!mm) continue;
             const B was = mark & (w.rseq != RSEQ_LIVE);  // already removed: addOverlappingClient
             const B fresh = simd::andn(mark, was);
-            w.rm = simd::sel(mark, w.rm | cbit, w.rm);
+            if (WIDE && C >= 32) {
+                if constexpr (WIDE) w.rm2 = simd::sel(mark, w.rm2 | cbit, w.rm2);
+            } else {
+                w.rm = simd::sel(mark, w.rm | cbit, w.rm);
+            }
             w.meta = simd::sel(was, w.meta | F_OVL, simd::sel(fresh, (w.meta & ~0xFF00u) | (C << 8) | F_REMOVED, w.meta));
             w.rseq = simd::sel(fresh, (u32)seq, w.rseq);
             writeback(r);
@@ -1817,7 +1873,7 @@ struct RegEngine {
         // (MTE_F_CATCHUP only asks for delta records, which only a legacy-format replay reads: that one
         // runs the EXT kernels, so here the flag is ignored like the lean LDS kernels do)
         if ((op.flags & (MTE_F_REL | MTE_F_PERM)) || (!PROPS && op.props)) return false;
-        if (type != MTE_OP_NOOP && (op.client == 0 || op.client >= 32)) return false;
+        if (type != MTE_OP_NOOP && (op.client == 0 || op.client >= MAXC)) return false;
         if (!room()) return false;
         const u32 C = op.client;
         const i32 seq = op.seq, R = op.ref_seq;
@@ -1847,7 +1903,7 @@ struct RegEngine {
             edited = op_remove(op.pos1, op.a, R, C, seq);
             n_ops++;
         } else if (ann) {
-            edited = op_annotate(op.pos1, op.a, R, C, seq, op.props, (op.flags & MTE_F_REWRITE) != 0);
+            if constexpr (PROPS) edited = op_annotate(op.pos1, op.a, R, C, seq, op.props, (op.flags & MTE_F_REWRITE) != 0);
             n_ops++;
         }
         if (status) return true;
@@ -2008,7 +2064,16 @@ struct RegEngine {
                 const B hasov = (w.meta & F_OVL) != 0u;
                 const V m2 = simd::sel(live, w.meta & ~0xFF00u, w.meta) & ~NS_MASK;
                 // removedClientOverlap = the removers but removedClient (the LDS engine's format)
-                const V ovm = w.rm & (simd::shl(simd::splat(1), simd::bfe(w.meta, 8, 8)) ^ 0xFFFFFFFFu);
+                V ovm, ovh = simd::splat(0);
+                if constexpr (WIDE) {  // removedClient may be 32..63: its bit is in rm2 then
+                    const V rc = simd::bfe(w.meta, 8, 8);
+                    const V rcb = simd::shl(simd::splat(1), rc);  // bit rc & 31
+                    const B rclo = rc < 32u;
+                    ovm = w.rm & (simd::sel(rclo, rcb, 0u) ^ 0xFFFFFFFFu);
+                    ovh = simd::sel(hasov, w.rm2 & (simd::sel(rclo, 0u, rcb) ^ 0xFFFFFFFFu), 0u);
+                } else {
+                    ovm = w.rm & (simd::shl(simd::splat(1), simd::bfe(w.meta, 8, 8)) ^ 0xFFFFFFFFu);
+                }
                 const V ovl = simd::sel(hasov, ovm, 0u);
                 const V z2 = simd::sel(live, w.cap, ovl);
                 const V t4 = at * 4u;
@@ -2016,7 +2081,9 @@ struct RegEngine {
                 simd::st(ov, t4 + 1u, w.seq, have);
                 simd::st(ov, t4 + 2u, simd::sel(live, 0u, w.rseq), have);
                 simd::st(ov, t4 + 3u, m2, have);
-                simd::st(oa, t4, PROPS ? w.props : simd::splat(0), have);
+                V pm = simd::splat(0);
+                if constexpr (PROPS) pm = w.props;
+                simd::st(oa, t4, pm, have);
                 if constexpr (PROPS) {  // the row's property map, indexed by row (emission reads it)
                     const B hp = have & (w.props != 0u);
                     if (p.out_maps && simd::ballot(hp)) {
@@ -2029,7 +2096,7 @@ struct RegEngine {
                 simd::st(oa, t4 + 2u, z2, have);
                 simd::st(oa, t4 + 3u, w.sid - 1u, have);
                 simd::st(oo, at * 2u, ovl, have);
-                simd::st(oo, at * 2u + 1u, simd::splat(0), have);
+                simd::st(oo, at * 2u + 1u, ovh, have);
                 // text, one segment at a time, 64 units per step
                 for (u64 tm = simd::ballot(txt); tm; tm &= tm - 1) {
                     const u32 l = (u32)__builtin_ctzll(tm);

@@ -91,8 +91,17 @@ MTE_DEV void reg_handoff(R& r, E& e) {
         const u32 m2 = (live ? (v.w & ~0xFF00u) : v.w) & ~NS_MASK;
         // aux.z: a live segment's text capacity, a removed one's removedClientOverlap (rm without
         // removedClient) or 0
-        const u32 ovm = a.z & ~(1u << ((v.w >> 8) & 31u));
-        e.VIS()[64 * rr + L] = make_uint4(v.x, v.y, live ? 0u : v.z, m2);
+        u32 ovm = a.z & ~(1u << ((v.w >> 8) & 31u)), m3 = m2;
+        if constexpr (R::kWide) {  // removers 32..63: the LDS engine keeps them in its HBM mask by id
+            const u32 rc = (v.w >> 8) & 0xFFu, rm2 = r.RM2P()[64 * rr + L];
+            ovm = a.z & ~(rc < 32 ? 1u << rc : 0u);
+            const u32 hi = (!live && ov) ? rm2 & ~(rc >= 32 ? 1u << (rc & 31u) : 0u) : 0u;
+            if (v.x && hi && a.w - 1u < e.seg_cap) {
+                e.ovl[a.w - 1u] = (u64)hi << 32;
+                m3 |= F_OVLHI;
+            }
+        }
+        e.VIS()[64 * rr + L] = make_uint4(v.x, v.y, live ? 0u : v.z, m3);
         u32 props = 0;
         if constexpr (R::kProps) props = v.x ? r.PROPP()[64 * rr + L] : 0u;  // beyond the rows' slots: intact
         e.AUX()[64 * rr + L] = make_uint4(props, a.y, live ? a.x : (ov ? ovm : 0u), v.x ? a.w - 1u : 0u);

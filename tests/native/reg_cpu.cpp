@@ -28,7 +28,7 @@ struct PropTables {
     uint32_t* out_maps;  // per output row, map_words words
 };
 
-template <bool PAGED, bool PROPS>
+template <bool PAGED, bool PROPS, bool WIDE = false>
 static uint64_t replay_impl(const mte_op* ops, uint64_t n_ops, const uint16_t* payload, uint32_t payload_len,
                             uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
                             uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
@@ -79,7 +79,7 @@ static uint64_t replay_impl(const mte_op* ops, uint64_t n_ops, const uint16_t* p
         p.out_maps = pt->out_maps;
     }
     // (the paged engine's pool is its own row arrays here, rows taken in a scattered order)
-    typedef RegEngine<(int)RG_ROWS, PAGED, PROPS> E;
+    typedef RegEngine<(int)RG_ROWS, PAGED, PROPS, WIDE> E;
     E* ep = new E(p, 0);
     E& e = *ep;
     if (PAGED) {
@@ -129,8 +129,11 @@ uint64_t regcpu_replay_props(const mte_op* ops, uint64_t n_ops, const uint16_t* 
                              uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
                              DocRes* res, uint32_t pool_rows, const uint32_t* propsets, uint32_t n_propsets,
                              const uint32_t* prop_keys, const uint32_t* prop_vals, const uint32_t* val_flags,
-                             uint32_t n_vals, uint32_t map_words, uint32_t map_cap, uint32_t* out_maps) {
+                             uint32_t n_vals, uint32_t map_words, uint32_t map_cap, uint32_t* out_maps, uint32_t wide) {
     PropTables t{(const mte_propset*)propsets, n_propsets, prop_keys, prop_vals, val_flags, n_vals, map_words, map_cap, out_maps};
+    if (wide)  // k_solo's FULL instantiation: clients up to 63
+        return replay_impl<false, true, true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux,
+                                              out_ovl, out_cap, out_text, out_text_cap, res, 0, &t);
     if (pool_rows)
         return replay_impl<true, true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
                                        out_cap, out_text, out_text_cap, res, pool_rows, &t);

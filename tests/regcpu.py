@@ -38,7 +38,7 @@ def lib():
         L.regcpu_replay_paged.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u32, vp, u64, vp, u32]
         L.regcpu_replay_props.restype = u64
         L.regcpu_replay_props.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u32, vp, u64, vp, u32,
-                                          vp, u32, vp, vp, vp, u32, u32, u32, vp]
+                                          vp, u32, vp, vp, vp, u32, u32, u32, vp, u32]
         L.regcpu_docres_size.restype = u32
         L.regcpu_heap.restype = u32
         L.regcpu_heap.argtypes = [vp, u32, vp]
@@ -112,7 +112,7 @@ class GenProps:
                               for i in range(n)) + "}"
 
 
-def replay_props(ops, pay, gp, pool_rows=0, map_words=16):
+def replay_props(ops, pay, gp, pool_rows=0, map_words=16, wide=False):
     """The PROPS engine (k_rows' property-carrying form) on the CPU: (stop index, DocRes, rows, text,
     per-row map records)."""
     ops = np.ascontiguousarray(ops, dtype=_op_dtype())
@@ -133,7 +133,7 @@ def replay_props(ops, pay, gp, pool_rows=0, map_words=16):
                                    vis.ctypes.data, aux.ctypes.data, ovl.ctypes.data, cap, text.ctypes.data,
                                    len(text), res.ctypes.data, pool_rows, gp.propsets.ctypes.data, gp.n_propsets,
                                    gp.prop_keys.ctypes.data, gp.prop_vals.ctypes.data, gp.val_flags.ctypes.data,
-                                   len(gp.VALS), map_words, map_cap, omaps.ctypes.data)
+                                   len(gp.VALS), map_words, map_cap, omaps.ctypes.data, int(wide))
     r = res[0]
     k = int(r["n_segs"])
     return at, r, (vis[:k], aux[:k], ovl[:k]), text, omaps[:k]
@@ -275,13 +275,13 @@ def compare(ops, pay, names=None, arena_cap=None, pool_rows=None):
     return res
 
 
-def compare_props(ops, pay, pool_rows=0):
+def compare_props(ops, pay, pool_rows=0, wide=False):
     """The PROPS engine against the oracle on a generated kind-3 log: status, segment table with
     each segment's properties (JSON.stringify of the map), text. Returns the DocRes record."""
     gp = GenProps()
     nc = int(ops["client"].max()) if len(ops) else 0
     names = ["__observer__"] + [f"w{i}" for i in range(1, max(nc, 1) + 1)]
-    at, res, rows, text, omaps = replay_props(ops, pay, gp, pool_rows=pool_rows)
+    at, res, rows, text, omaps = replay_props(ops, pay, gp, pool_rows=pool_rows, wide=wide)
     assert int(res["status"]) != REG_HANDOFF, f"handed off at op {at} (n_lb {res['n_lb']})"
     o = OneDocBatch(ops, pay, names, gp=gp).oracle()
     code, err, fseq = o.status()

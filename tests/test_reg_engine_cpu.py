@@ -216,3 +216,14 @@ def test_props_engine_rewrite_annotates():
     ops = ops.copy()
     ops["flags"][ann] |= 0x2
     regcpu.compare_props(ops, pay)
+
+
+@pytest.mark.parametrize("kind,gid,n_ops,clients", [(3, 2, 1100, 40), (2, 3, 1200, 48), (3, 4, 1100, 63),
+                                                    (3, 7, 1100, 50), (5, 5, 8000, 36), (3, 1, 4000, 8)])
+def test_wide_engine_matches_oracle(kind, gid, n_ops, clients):
+    """k_solo's FULL instantiation (PROPS + WIDE): removers 32..63 in a second mask word per slot
+    (removedClient and removedClientOverlap of clients up to 63), with and without properties;
+    segment table incl. overlap sets and text against the oracle."""
+    ops, pay = regcpu.generated(kind, gid, n_ops, n_clients=clients, seed=1000)
+    assert clients < 32 or (ops["client"] >= 32).sum() > 0
+    regcpu.compare_props(ops, pay, wide=True)

@@ -227,3 +227,22 @@ def test_wide_engine_matches_oracle(kind, gid, n_ops, clients):
     ops, pay = regcpu.generated(kind, gid, n_ops, n_clients=clients, seed=1000)
     assert clients < 32 or (ops["client"] >= 32).sum() > 0
     regcpu.compare_props(ops, pay, wide=True)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_row_engine_variants_random_logs(seed):
+    """Randomised logs (kind, writers 2-63, length) through every row-engine instantiation the
+    product builds -- lean, lean paged, PROPS, PROPS paged, PROPS + WIDE -- each against the oracle."""
+    rng = random.Random(seed)
+    kind = rng.choice([2, 3, 5])
+    clients = rng.choice([2, 3, 8, 16, 31]) if seed % 3 else rng.randint(32, 63)
+    n = rng.randint(200, 2500) if clients < 32 else rng.randint(200, 900)
+    ops, pay = regcpu.generated(kind, 500 + seed, n, n_clients=clients, seed=seed)
+    regcpu.compare_props(ops, pay, wide=True)
+    if clients >= 32:
+        return
+    regcpu.compare_props(ops, pay, pool_rows=rng.randint(12, 32))
+    regcpu.compare_props(ops, pay)
+    if kind != 3:
+        regcpu.compare(ops, pay)
+        regcpu.compare(ops, pay, pool_rows=rng.randint(12, 32))

@@ -1107,8 +1107,8 @@ static int run_kernel(mte_engine* e, bool gen) {
     e->last_lean = full == 0;
     wave_plan(e, nd, groups, hbm_waves, &lds_active, n_solo);
     // Lean replays run the bulk on the row engine (k_rows; DOC_SPILL re-runs as below): 4 waves per
-    // CU when every bulk document of a long-document batch gets a SIMD of its own (C5: 1 024 x 10^6
-    // ops, 4.4 s per step against 9.8 s on k_lds / k_hbmq), else 8 (two per SIMD on the shared row
+    // CU for long documents, each on a SIMD of its own with fixed rows (C5: 1 024 x 10^6 ops, 4.4 s
+    // per step against 9.8 s on k_lds / k_hbmq), else 8 (two per SIMD on the shared row
     // pool; C2: 4 096 x 10^4 ops, 110 ms against 166 ms on the sixteen LDS / HBM waves per CU). A
     // batch with solo documents keeps k_lds beside them: its pass is the critical path's anyway, and
     // k_lds continues a document that outgrows LDS in HBM instead of re-running it from its first op.
@@ -1119,7 +1119,9 @@ static int run_kernel(mte_engine* e, bool gen) {
     if (!gen && ((full == 0 && e->props_rows_ok) || props_rows) && e->rows_bulk && !e->force_hbm && nd > n_solo) {
         uint64_t bulk_ops = 0;
         for (uint32_t k = n_solo; k < nd; k++) bulk_ops += e->n_ops_doc[e->order[k]];
-        const bool long_docs = nd - n_solo <= 4 * bulk_cus(e, n_solo) && bulk_ops >= 200000ull * (nd - n_solo);
+        // (long documents take 4 waves whatever their count: eight of them, ~120 leaf blocks each,
+        // would not fit one CU's 79-row pool and spill to HBM re-runs of 10^5+ ops)
+        const bool long_docs = bulk_ops >= 200000ull * (nd - n_solo);
         rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : long_docs ? 4u : n_solo == 0 ? 8u : 0u;
     }
     e->last_rows = rows;

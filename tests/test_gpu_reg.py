@@ -84,23 +84,24 @@ def test_props_row_engine_lone_documents(engine, n_ops, clients, limit):
         engine.set_option("reg_lb_limit", 0)
 
 
-@pytest.mark.parametrize("kind,n_ops,clients", [(3, 1100, 40), (2, 1200, 48), (3, 1100, 63), (2, 6000, 48),
-                                                (3, 5000, 40)])
-def test_wide_row_engine_lone_documents(engine, kind, n_ops, clients):
+@pytest.mark.parametrize("kind,gid,n_ops,clients,rows", [(3, 2, 1100, 40, True), (2, 3, 1200, 48, True),
+                                                         (3, 4, 1100, 63, True), (2, 0, 6000, 48, False),
+                                                         (3, 0, 5000, 40, False)])
+def test_wide_row_engine_lone_documents(engine, kind, gid, n_ops, clients, rows):
     """Documents with writers 32..63 (FULL batches) on k_solo's PROPS + WIDE row engine: the second
-    removers word per slot; the longer ones outgrow the row plan and hand over to the LDS engine with
-    their high overlap bits in its HBM mask (F_OVLHI). Checksums against the oracle."""
+    removers word per slot (mode 4 to the end: the documents the CPU suite checks the same way); the
+    longer ones outgrow the row plan and hand over to the LDS engine (mode 3, or 2 when they outgrow
+    its plan too) with their high overlap bits in its HBM mask (F_OVLHI). Checksums against the
+    oracle."""
     engine.set_option("reg_lb_limit", 0)
-    engine.generate(kind, 1, n_ops, n_clients=clients, seed=1000)
+    engine.generate(kind, 1, n_ops, n_clients=clients, seed=1000, doc_ids=[gid])
     batch = engine.export_batch()
     st = engine.replay()
     assert engine.run_info()["solo"] == 1 and engine.run_info()["lean"] == 0
     r = engine.doc_result(0)
     assert r["status"] == 0 and st["ops"] == n_ops, r
-    assert r["mode"] in (MODE_ROWS, MODE_SOLO_LDS), r
-    if n_ops < 2000:
-        assert r["mode"] == MODE_ROWS, r
     _check(engine, batch)
+    assert r["mode"] == MODE_ROWS if rows else r["mode"] in (2, MODE_SOLO_LDS), r
 
 
 def test_props_zipf_head_on_rows(engine):

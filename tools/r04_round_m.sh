@@ -1,6 +1,6 @@
 #!/bin/bash
-# GPU box: the full GPU suite and smoke() on the final tree (final tree, after the WIDE test fixes
-# instantiation). Stops on a crash or time limit.
+# GPU box: the full GPU suite, smoke() and a short C4 bench on the final tree. Stops on a crash or
+# time limit.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/rm

@@ -4,7 +4,8 @@ FETCH_SIZE and WRITE_SIZE passes, corrected with the gfx950 calibration of profi
 
 rocprofv3 serialises dispatches while it collects counters, so in these passes k_lds takes every
 non-solo document and k_hbmq finds the queue drained: the per-kernel split is that of the serialised
-pass, the total is the pass's. Usage: python tools/pmc_replay.py <tag> [config] -> profiles/pmc_replay_<config>.json
+pass, the total is the pass's. Usage: python tools/pmc_replay.py <tag> [config] -> profiles/pmc_replay_<config>.json (C2 / C3 / C5 run
+their bulk on k_rows: its launches count the passes there)
 """
 import csv
 import glob
@@ -14,7 +15,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-REPLAY = ("k_solo<false", "k_lds<false", "k_hbmq<false", "k_emit_count", "k_emit_write")
+REPLAY = ("k_solo<false", "k_lds<false", "k_hbmq<false", "k_rows<", "k_emit_count", "k_emit_write")
 
 
 def main(tag, config="C4"):
@@ -34,7 +35,8 @@ def main(tag, config="C4"):
                 if k and r["Counter_Name"] == ctr:
                     per[k][ctr] += float(r["Counter_Value"]) * 1024.0
                     calls[k][ctr] += 1
-    steps = max(calls["k_lds<false"].values() or [1])
+    # replay passes: the bulk kernel's launches (k_lds, or k_rows for the row-engine configs)
+    steps = max(list(calls["k_lds<false"].values()) + list(calls["k_rows<"].values()) or [1])
     kernels = {}
     total = 0.0
     for k, v in per.items():

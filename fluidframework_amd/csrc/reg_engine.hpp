@@ -46,6 +46,7 @@ constexpr u32 RSEQ_LIVE = 0x7FFFFFFFu;    // removedSeq of a live segment (never
 constexpr u32 RCL_LIVE = 0xFFu;           // removedClient byte of a live segment (never a client)
 constexpr i32 REG_HANDOFF = 101;          // internal: continue in the LDS engine from the current op
 constexpr u32 ROWS_POOL_WORDS = 3;         // k_rows' pool row mask (mte_solo.hip RowsGeom): <= 96 rows
+constexpr u32 ROWS_WAIT_TRIES = 400;       // a wave finding the pool full retries this often (s_sleep 8)
 // needsScour (mergeTree.ts:63) in meta bits 24..25 of every slot lane of a block
 constexpr u32 NS_SHIFT = 24, NS_MASK = 3u << NS_SHIFT;
 static_assert(RG_BLOCKS <= SOLO_POOL, "the rows live in the SoloPlan's slot arrays");
@@ -336,6 +337,16 @@ struct RegEngine {
         row = got;
         return got != NONE;
     }
+    // A full pool is usually full for a moment (the other waves' documents shrink and end all the
+    // time): wait up to ~0.2 ms for a row before giving the document up (a bounded wait, so waves
+    // that all wait cannot deadlock: they spill).
+    SD bool take_row_wait(u32& row) {
+        for (u32 t = 0; t < ROWS_WAIT_TRIES; t++) {
+            if (take_row(row)) return true;
+            __builtin_amdgcn_s_sleep(8);  // ~512 cycles
+        }
+        return take_row(row);
+    }
     SD void give_row(u32 row) {
         if (__lane_id() == 0) atomicAnd(pool_words() + (row >> 5), ~(1u << (row & 31)));
     }
@@ -511,7 +522,11 @@ struct RegEngine {
     SD bool grow_rows(u32 need) {
         while (n_rows < need) {
             u32 row;
+#ifdef MTE_CPU
             if (n_rows >= (u32)NR || !take_row(row)) return false;
+#else
+            if (n_rows >= (u32)NR || !take_row_wait(row)) return false;
+#endif
             zero_prow(row);
             ptab = simd::writelane(ptab, n_rows, row);
             n_rows++;

@@ -237,7 +237,7 @@ def test_bulk_rows_pool_shared_and_exhausted(engine, waves):
         engine.set_option("rows_bulk", -1)
 
 
-@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("waves", [4, 8, 12])
 def test_bulk_rows_props_matches_oracle(engine, waves):
     """Property-carrying batches on k_rows' PROPS engine (C3's mix: 45/35/20 insert / remove /
     annotate, property maps per segment, merges only between matching maps): a Zipf mix and a

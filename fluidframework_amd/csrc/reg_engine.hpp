@@ -1947,33 +1947,36 @@ struct RegEngine {
     // Replay ops [i, e): returns the first op not applied (e when done or failed; earlier when the
     // document hands over to the LDS engine). Records are prefetched 8 per VGPR (lane 8*r + w holds
     // word w of record r), four chunks ahead.
-    SD u64 replay(u64 i, u64 e) {
+    SD u64 replay(u64 i0, u64 e) {
         if (!p.docs[doc].collab) {  // local, non-collaborative edits: the LDS engine's path
             status = REG_HANDOFF;
-            return i;
+            return i0;
         }
         RG_PROF(RP_TOTAL);
-        const u32* src = (const u32*)p.ops;
-        const u64 b = i;
-        auto load_chunk = [&](u64 c0) MTE_LI {  // records [c0, c0+8)
-            const u64 left = e > c0 ? e - c0 : 0;
-            const u32 nw = left >= 8 ? 64u : (u32)left * 8u;
-            return simd::ld(src + c0 * 8, L(), L() < nw);
+        // this document's records from one base pointer, indexed by 32-bit op numbers (a 64-bit
+        // global op index in the loop held three more SGPR pairs in a kernel that spills SGPRs)
+        const u32* src = (const u32*)p.ops + i0 * 8;
+        const u32 n = (u32)(e - i0);
+        auto load_chunk = [&](u32 c0) MTE_LI {  // records [c0, c0+8)
+            const u32 left = n > c0 ? n - c0 : 0u;
+            const u32 nw = left >= 8 ? 64u : left * 8u;
+            return simd::ld(src + (u64)c0 * 8, L(), L() < nw);
         };
         // Two chunk registers: CUR holds the records being decoded, NXT the next eight. At a chunk's
         // first op CUR = NXT (loaded eight ops earlier), the op is decoded, and only THEN is NXT
         // refilled: the compiler waits for the whole vector-memory counter before a decode, so the
         // newest load outstanding there must be an op old. (Loading before the decode, or a
         // four-register ring indexed by a switch, made every chunk wait for a fresh HBM load.)
-        V CUR = load_chunk(b), NXT = load_chunk(b + 8);
+        V CUR = load_chunk(0), NXT = load_chunk(8);
 #ifndef MTE_CPU
         // wait for the first chunk here, once: CUR then enters the loop with no load outstanding, so
         // the decodes need no vector-memory wait at all (stores of the merge arena included)
         asm volatile("" ::"v"(CUR.x));
 #endif
-        for (; i < e && !status; i++) {
-            const u32 r = (u32)((i - b) & 7);
-            const bool first = r == 0 && i != b;
+        u32 k = 0;
+        for (; k < n && !status; k++) {
+            const u32 r = k & 7u;
+            const bool first = r == 0 && k != 0;
             if (first) {
                 CUR = NXT;
 #ifndef MTE_CPU
@@ -1987,14 +1990,14 @@ struct RegEngine {
                 for (u32 x = 0; x < 8; x++) w[x] = simd::readlane(CUR, r * 8 + x);
                 __builtin_memcpy(&op, w, sizeof op);
             }
-            if (first) NXT = load_chunk(i + 8);
+            if (first) NXT = load_chunk(k + 8);
             RG_COUNT(RP_OPS, 1);
             if (!apply(op)) {
                 status = REG_HANDOFF;
-                return i;
+                return i0 + k;
             }
         }
-        return i;
+        return i0 + k;
     }
 
     // ---------------------------------------------------------------- results

@@ -46,7 +46,7 @@ constexpr u32 RSEQ_LIVE = 0x7FFFFFFFu;    // removedSeq of a live segment (never
 constexpr u32 RCL_LIVE = 0xFFu;           // removedClient byte of a live segment (never a client)
 constexpr i32 REG_HANDOFF = 101;          // internal: continue in the LDS engine from the current op
 constexpr u32 ROWS_POOL_WORDS = 3;         // k_rows' pool row mask (mte_solo.hip RowsGeom): <= 96 rows
-constexpr u32 ROWS_WAIT_TRIES = 2000;      // a wave finding the pool full retries this often (s_sleep 8)
+constexpr u32 ROWS_WAIT_TRIES = 20000;     // a wave finding the pool full retries this often (s_sleep 8)
 // needsScour (mergeTree.ts:63) in meta bits 24..25 of every slot lane of a block
 constexpr u32 NS_SHIFT = 24, NS_MASK = 3u << NS_SHIFT;
 static_assert(RG_BLOCKS <= SOLO_POOL, "the rows live in the SoloPlan's slot arrays");
@@ -338,8 +338,9 @@ struct RegEngine {
         return got != NONE;
     }
     // A full pool is usually full for a moment (the other waves' documents shrink and end all the
-    // time): wait up to ~0.4 ms for a row before giving the document up (a bounded wait, so waves
-    // that all wait cannot deadlock: they spill).
+    // time): wait up to ~4 ms for a row before giving the document up (a bounded wait, so waves
+    // that all wait cannot deadlock: they spill; ~0.4 ms still let one C2 document in five steps
+    // spill into a 100 ms HBM re-run).
     SD bool take_row_wait(u32& row) {
         for (u32 t = 0; t < ROWS_WAIT_TRIES; t++) {
             if (take_row(row)) return true;

@@ -225,6 +225,8 @@ struct Params {
                               // end (4 u64): shader cycles vs the 100 MHz reference clock; then, at
                               // [4 * SOLO_CLK_SLOTS], the bulk kernel's start (s_memrealtime)
     u32* solo_started;        // solo workgroups that have started this pass (k_solo_gate waits for n_solo)
+    u32* rows_retry;          // k_rows: documents the row pool could not grow, queued to restart once
+                              // (doc + 1 per slot; counters[8] pushed, counters[9] popped), or null
 };
 
 constexpr u32 SOLO_CLK_SLOTS = 64;  // solo workgroups with clock stamps (Params::solo_clk)

@@ -264,6 +264,7 @@ struct mte_engine {
         d_first_seen;
     DevBuf<uint64_t> d_val_objmatch, d_ovl, d_out_ovl, d_prof, d_solo_clk;
     DevBuf<uint32_t> d_solo_started;  // k_solo_gate's counter
+    DevBuf<uint32_t> d_rows_retry;    // k_rows' restart queue (Params::rows_retry)
     bool solo_gate = true;            // option "solo_gate"
     uint64_t last_solo_cycles = 0, last_solo_ref = 0;  // critical wave: s_memtime / s_memrealtime deltas
     double last_cell_pass_ms = 0;                       // a SharedMatrix batch's first (positions) pass
@@ -531,7 +532,8 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     HIP_TRY(e, e->d_out_aux.fit(out));
     HIP_TRY(e, e->d_out_ovl.fit(out));
     if (any_props) HIP_TRY(e, e->d_out_maps.fit(out * e->map_words));  // some document can carry props
-    HIP_TRY(e, e->d_counters.fit(8));
+    HIP_TRY(e, e->d_counters.fit(16));
+    HIP_TRY(e, e->d_rows_retry.fit(nd));
     HIP_TRY(e, e->d_res.fit(nd));
     HIP_TRY(e, e->d_prof.fit((size_t)nd * PROF_SLOTS));
     HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, (size_t)nd * PROF_SLOTS * 8, e->stream));
@@ -564,6 +566,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     P.prof = e->d_prof.p;
     P.solo_clk = e->d_solo_clk.p;
     P.solo_started = e->d_solo_started.p;
+    P.rows_retry = e->d_rows_retry.p;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || cus <= 0) cus = 256;
     e->n_groups = (uint32_t)cus;
@@ -1140,7 +1143,8 @@ static int run_kernel(mte_engine* e, bool gen) {
     // the solo workgroups' CUs to themselves measured the C4 pass 8 % SLOWER -- 9.07 s vs 8.38 s, the
     // solo workgroups themselves included -- and hung at teardown: not used)
     hipStream_t s_main = e->stream, s_hbmq = e->stream2, s_solo = e->stream3;
-    HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 8 * sizeof(uint32_t), s_main));
+    HIP_TRY(e, hipMemsetAsync(e->d_counters.p, 0, 16 * sizeof(uint32_t), s_main));
+    if (e->d_rows_retry.p) HIP_TRY(e, hipMemsetAsync(e->d_rows_retry.p, 0, e->d_rows_retry.n * sizeof(uint32_t), s_main));
     HIP_TRY(e, hipMemsetAsync(e->d_slot_bits.p, 0, e->d_slot_bits.n * sizeof(uint32_t), s_main));
     HIP_TRY(e, hipMemsetAsync(e->d_prof.p, 0, e->d_prof.n * sizeof(uint64_t), s_main));  // profiling build
     HIP_TRY(e, hipMemsetAsync(e->d_solo_started.p, 0, sizeof(uint32_t), s_main));  // k_solo_gate's counter

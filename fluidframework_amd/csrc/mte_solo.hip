@@ -170,15 +170,60 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
     const u32 pb = PAGED ? G::PRP : vb + G::FIXED_NR * 64u * 32u;
     if (blockIdx.x == 0 && threadIdx.x == 0 && p.solo_clk) p.solo_clk[4 * SOLO_CLK_SLOTS] = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        u32 i = 0;
-        if (lane_id() == 0) i = p.n_prio + atomicAdd(&p.counters[0], 1u);
-        i = wave_read(i, 0);
-        if (i >= p.n_list) break;
-        const u32 d = p.doc_list[i];
+        // a document another wave gave back when the pool was full restarts first (once; a second
+        // failure goes to the host's re-run), then the LPT queue
+        u32 d = NONE;
+        bool again = false;
+        if (PAGED && p.rows_retry) {
+            u32 slot = NONE;
+            if (lane_id() == 0) {
+                u32* pushed = &p.counters[8];
+                u32* popped = &p.counters[9];
+                u32 old = __hip_atomic_load(popped, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                while (old < __hip_atomic_load(pushed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
+                    const u32 seen = atomicCAS(popped, old, old + 1u);
+                    if (seen == old) {
+                        slot = old;
+                        break;
+                    }
+                    old = seen;
+                }
+                if (slot != NONE) {  // the pusher bumps the count before its slot write lands: wait for it
+                    u32 v = 0;
+                    for (u32 t = 0; t < (1u << 20) && v == 0; t++)
+                        v = __hip_atomic_load(p.rows_retry + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    slot = v ? v - 1u : NONE;
+                }
+            }
+            d = wave_read(slot, 0);
+            again = d != NONE;
+        }
+        if (d == NONE) {
+            u32 i = 0;
+            if (lane_id() == 0) i = p.n_prio + atomicAdd(&p.counters[0], 1u);
+            i = wave_read(i, 0);
+            if (i >= p.n_list) {
+                // the queue is drained; documents still being given back are picked up by waves that
+                // have not finished yet, or go to the host's re-run
+                break;
+            }
+            d = p.doc_list[i];
+        }
         RegEngine<PAGED ? (int)RG_ROWS : (int)G::FIXED_NR, PAGED, PROPS> r(p, d, vb, ab, 5, G::MASK, pb);
         if (!r.status) r.replay(p.docs[d].op_begin, p.docs[d].op_end);
-        if (r.status == REG_HANDOFF) r.mark_spilled();
-        else r.finish();
+        if (r.status == REG_HANDOFF && PAGED && p.rows_retry && r.pool_full && !again) {
+            // marked for the host's re-run first (so a document no wave restarts is still replayed),
+            // then queued to restart from its first op; a restart that finishes overwrites the mark
+            r.mark_spilled();
+            if (lane_id() == 0) {
+                const u32 k = atomicAdd(&p.counters[8], 1u);
+                __hip_atomic_store(p.rows_retry + k, d + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else if (r.status == REG_HANDOFF) {
+            r.mark_spilled();
+        } else {
+            r.finish();
+        }
         r.release_rows();
     }
 }

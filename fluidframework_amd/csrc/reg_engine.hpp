@@ -520,13 +520,18 @@ struct RegEngine {
     SD void writeback(u32 r) { strow(r, cw); }
 
     // PAGED: logical rows [n_rows, need) from the pool, zeroed (rows past the last block stay zero)
+    bool pool_full = false;  // PAGED: the last grow found the pool full (not the logical row limit)
     SD bool grow_rows(u32 need) {
         while (n_rows < need) {
             u32 row;
 #ifdef MTE_CPU
             if (n_rows >= (u32)NR || !take_row(row)) return false;
 #else
-            if (n_rows >= (u32)NR || !take_row_wait(row)) return false;
+            if (n_rows >= (u32)NR) return false;
+            if (!take_row_wait(row)) {
+                pool_full = true;
+                return false;
+            }
 #endif
             zero_prow(row);
             ptab = simd::writelane(ptab, n_rows, row);

@@ -331,8 +331,7 @@ struct mte_engine {
     // pools -- round 0 (every document but the solo ones) runs while the critical path is still
     // replaying, round 1 (solo and host-re-run documents) after it
     int32_t rows_bulk = -1;   // option "rows_bulk": lean replays run the bulk on k_rows, 4, 8 or 12 waves per
-                              // CU; -1 (auto: 4 for long documents, else 12 with properties / 8 lean
-                              // when there are no solo documents), 0: never
+                              // CU; -1 (auto: 4 for long documents, 12 without solo documents), 0: never
     bool xcd_align = true;    // option "xcd_align": bulk grids leave solo CUs free in every XCD (bulk_cus)
     uint32_t last_rows = 0;   // waves per CU of the last pass's k_rows (0: k_lds / k_hbmq)
     bool emit_opt = true;     // option "emit"
@@ -1112,10 +1111,9 @@ static int run_kernel(mte_engine* e, bool gen) {
     wave_plan(e, nd, groups, hbm_waves, &lds_active, n_solo);
     // Lean replays run the bulk on the row engine (k_rows; DOC_SPILL re-runs as below): 4 waves per
     // CU for long documents, each on a SIMD of its own with fixed rows (C5: 1 024 x 10^6 ops, 4.4 s
-    // per step against 9.8 s on k_lds / k_hbmq), else 12 for property-carrying batches (three per
-    // SIMD on the shared row pool; C3 1.37 s against 1.87 at 8 and 2.15 on k_lds / k_hbmq) and 8 for
-    // lean ones (C2: 110 ms against 166 on the sixteen LDS / HBM waves per CU; at 12 waves 96 ms, but
-    // about one step in twenty spills a document at a pool peak into a 100 ms HBM re-run). A
+    // per step against 9.8 s on k_lds / k_hbmq), else 12 (three per SIMD on the shared row pool; C2
+    // 98 ms against 110 at 8 and 166 on the sixteen LDS / HBM waves per CU; C3 1.34 s against 1.87 at
+    // 8 and 2.15 on k_lds / k_hbmq; a document the pool cannot grow restarts inside the pass). A
     // batch with solo documents keeps k_lds beside them: its pass is the critical path's anyway, and
     // k_lds continues a document that outgrows LDS in HBM instead of re-running it from its first op.
     // Property-carrying batches (FULL only for their properties: no '\n', no relative positions, < 32
@@ -1128,7 +1126,7 @@ static int run_kernel(mte_engine* e, bool gen) {
         // (long documents take 4 waves whatever their count: eight of them, ~120 leaf blocks each,
         // would not fit one CU's 79-row pool and spill to HBM re-runs of 10^5+ ops)
         const bool long_docs = bulk_ops >= 200000ull * (nd - n_solo);
-        rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : long_docs ? 4u : n_solo == 0 ? (full == 1 ? 12u : 8u) : 0u;
+        rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : long_docs ? 4u : n_solo == 0 ? 12u : 0u;
     }
     e->last_rows = rows;
     if (rows) groups = hbm_waves = lds_active = 0;

@@ -227,6 +227,7 @@ struct Params {
     u32* solo_started;        // solo workgroups that have started this pass (k_solo_gate waits for n_solo)
     u32* rows_retry;          // k_rows: documents the row pool could not grow, queued to restart once
                               // (doc + 1 per slot; counters[8] pushed, counters[9] popped), or null
+    u32 rows_pool_lim;        // test knob: k_rows pool rows usable per CU (0 = all of the pool)
 };
 
 constexpr u32 SOLO_CLK_SLOTS = 64;  // solo workgroups with clock stamps (Params::solo_clk)

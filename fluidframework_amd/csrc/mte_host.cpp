@@ -309,6 +309,7 @@ struct mte_engine {
     DevBuf<uint32_t> d_cell_pos, d_cell_h, d_htab;
     bool ext_cu = false;                 // ... MTE_F_CATCHUP ops: EXT only when a legacy summary is emitted
     bool lean_base = false;              // batch_is_lean, before the catch-up records decide
+    uint32_t rows_pool_lim = 0;          // option rows_pool: k_rows pool rows per CU (test knob, 0 = all)
     bool props_rows_ok = false;          // k_rows may take the batch: no '\n', relative positions or summary loads, < 32 clients
     bool lean_opt = true;                // option "lean" (0 = always the FULL kernels)
     bool last_lean = false;
@@ -887,6 +888,9 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         collab[d] = e->hb.client(d, 0).empty() ? 0 : 1;  // empty observer name => local, non-collab
         not_rows[d] = not_rows[d] || has_nl[d] || rel || e->hb.doc_client_offsets[d + 1] - e->hb.doc_client_offsets[d] > 32;
         not_lean[d] = not_rows[d] || pi[d] || an[d];
+        // a local, non-collaborative document is the LDS engine's path (lean or not): RegEngine::replay
+        // hands it over at op 0, and k_rows has no LDS plan to hand it to
+        not_rows[d] = not_rows[d] || !collab[d];
         // a document with more than MTE_MAX_CLIENTS clients fails alone (MTE_DOC_UNSUPPORTED at its
         // first op from a client beyond the cap), never the batch
     };
@@ -1093,6 +1097,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     // only its cell documents), nall: the batch's documents (results are indexed by document)
     const uint32_t nd = (uint32_t)e->order.size(), nall = e->P.n_docs;
     e->P.pool_limit = e->pool_limit;
+    e->P.rows_pool_lim = e->rows_pool_lim;
     e->P.reg_solo = e->reg_solo;
     e->P.reg_lb_limit = e->reg_lb_limit;
     e->P.doc_list = e->d_order.p;
@@ -1119,7 +1124,9 @@ static int run_kernel(mte_engine* e, bool gen) {
     // Property-carrying batches (FULL only for their properties: no '\n', no relative positions, < 32
     // clients) take the same route on the PROPS row engine.
     uint32_t rows = 0;
-    const bool props_rows = full == 1 && e->props_rows_ok;
+    // (PROPS rows only when properties are what requires FULL: option lean = 0 on a lean batch keeps
+    // the FULL LDS kernels, as that diagnostic switch says)
+    const bool props_rows = full == 1 && !e->lean_ok && e->props_rows_ok;
     if (!gen && ((full == 0 && e->props_rows_ok) || props_rows) && e->rows_bulk && !e->force_hbm && nd > n_solo) {
         uint64_t bulk_ops = 0;
         for (uint32_t k = n_solo; k < nd; k++) bulk_ops += e->n_ops_doc[e->order[k]];
@@ -2403,12 +2410,12 @@ static int gather_all(mte_engine* e, int rank, int world, void* comm, std::vecto
 int mte_gather_summaries(mte_engine* e, int rank, int world, void* comm, mte_doc_summary* out, size_t cap,
                          size_t* n) {
     if (!e || world < 1 || rank < 0 || rank >= world || (world > 1 && !comm)) return MTE_E_ARG;
-    if (!out) {  // size query: the count all-gather only when world > 1 (every rank queries)
-        if (world == 1) {
-            if (n) *n = e->P.n_docs;
-            return MTE_OK;
-        }
+    if (!out && world == 1) {  // size query on one rank: no collective
+        if (n) *n = e->P.n_docs;
+        return MTE_OK;
     }
+    // (with world > 1 a size query runs the full record all-gather, like the call that follows it:
+    // mte_gather_summaries_alloc does both in one collective)
     std::vector<mte_doc_summary> res;
     if (int rc = gather_all(e, rank, world, comm, res)) return rc;
     if (n) *n = res.size();
@@ -2489,6 +2496,7 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "solo_gate") e->solo_gate = value != 0;
     else if (k == "rows_bulk") e->rows_bulk = value < 0 ? -1 : value == 0 ? 0 : value >= 12 ? 12 : value >= 8 ? 8 : 4;  // lean bulk on k_rows
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
+    else if (k == "rows_pool") e->rows_pool_lim = (uint32_t)std::max<int64_t>(0, value);  // k_rows pool rows per CU (0 = all)
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
 }
@@ -2515,8 +2523,15 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "load_stage_wait_us") *value = (int64_t)(e->stage_wait_ms * 1000.0);
     else if (k == "solo_tail_us") *value = (int64_t)(e->last_solo_tail_ms * 1000.0);
     else if (k == "lean") *value = e->last_lean;
-    else if (k == "rows") *value = e->last_rows;
-    else if (k == "cell_pass_us") *value = (int64_t)(e->last_cell_pass_ms * 1000.0);  // SharedMatrix pass 1  // k_rows waves per CU of the last pass (0: not used)
+    else if (k == "rows") *value = e->last_rows;  // k_rows waves per CU of the last pass (0: not used)
+    else if (k == "cell_pass_us") *value = (int64_t)(e->last_cell_pass_ms * 1000.0);  // SharedMatrix pass 1
+    else if (k == "rows_restart_pushed" || k == "rows_restart_popped") {
+        // k_rows' in-pass restart queue (counters[8] / [9]): documents given back when the row pool
+        // was full, and restarts taken by a wave
+        uint32_t ctr[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (e->d_counters.p) HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
+        *value = k == "rows_restart_pushed" ? ctr[8] : ctr[9];
+    }
     else if (k == "emit_us") *value = (int64_t)(e->last_emit_ms * 1000.0);  // emission after the replay pass
     else if (k == "out_text") {  // UTF-16 units Engine::finish gathered (counters[6..7])
         uint32_t ctr[8] = {0, 0, 0, 0, 0, 0, 0, 0};

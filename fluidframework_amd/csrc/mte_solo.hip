@@ -34,7 +34,7 @@ MTE_DEV void solo_doc(const Params& p) {
     const u64 c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     auto stamp = [&]() {
         const u64 c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-        if (p.solo_clk && lane_id() == 0) {
+        if (p.solo_clk && i < SOLO_CLK_SLOTS && lane_id() == 0) {  // (slot SOLO_CLK_SLOTS: the bulk's stamp)
             u64* o = p.solo_clk + 4 * (u64)i;
             o[0] = c0;
             o[1] = r0;
@@ -42,12 +42,13 @@ MTE_DEV void solo_doc(const Params& p) {
             o[3] = r1;
         }
     };
-    Engine<true, true, LVL> e(p, d);
-    e.bind_lds(0);
     GenState g;
     bool done;
     u64 at = p.docs[d].op_begin;
     bool handed = false;
+    St hst;  // the LDS engine's replay state after a handoff (its LDS arrays are written in place)
+    // The LDS engine is constructed only after the row engine is done with the document: nothing of
+    // it is live across the row engine's replay loop (its registers were, for the whole replay).
     if constexpr (!GEN && LVL == 0) {
         // lean replay: the whole document state in this wave's registers (reg_engine.hpp); it moves
         // to the LDS plan below only if it outgrows the registers or reaches an op they do not cover
@@ -60,7 +61,10 @@ MTE_DEV void solo_doc(const Params& p) {
                 __builtin_amdgcn_s_setprio(0);
                 return;
             }
-            reg_handoff(r, e);
+            Engine<true, true, LVL> t(p, d);
+            t.bind_lds(0);
+            reg_handoff(r, t);
+            hst = t.st;
             handed = true;
         }
     } else if constexpr (!GEN && LVL == 1) {
@@ -80,11 +84,21 @@ MTE_DEV void solo_doc(const Params& p) {
                 __builtin_amdgcn_s_setprio(0);
                 return;
             }
-            reg_handoff(r, e);
+            Engine<true, true, LVL> t(p, d);
+            t.bind_lds(0);
+            reg_handoff(r, t);
+            hst = t.st;
             handed = true;
         }
     }
-    if (!handed) e.init();
+    Engine<true, true, LVL> e(p, d);
+    if (handed) {
+        e.wave = 0;  // (bind_lds(0) without clearing the counters the handoff wrote)
+        e.st = hst;
+    } else {
+        e.bind_lds(0);
+        e.init();
+    }
     if (GEN) {
         e.gen_init(g);
         done = e.generate_run(g);
@@ -159,10 +173,12 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
     const u32 w = wave_first(threadIdx.x >> 6);
     if constexpr (PAGED) {
         u32* mask = reinterpret_cast<u32*>(reinterpret_cast<unsigned char*>(g_lds_dyn) + G::MASK);
-        if (threadIdx.x < ROWS_POOL_WORDS)  // rows past the pool are marked taken
-            mask[threadIdx.x] = threadIdx.x * 32 + 32 <= G::POOL ? 0u
-                                : threadIdx.x * 32 >= G::POOL   ? ~0u
-                                                                : ~((1u << (G::POOL - threadIdx.x * 32)) - 1u);
+        // rows past the pool (or past the rows_pool_lim test knob) are marked taken
+        const u32 np = p.rows_pool_lim && p.rows_pool_lim < G::POOL ? p.rows_pool_lim : G::POOL;
+        if (threadIdx.x < ROWS_POOL_WORDS)
+            mask[threadIdx.x] = threadIdx.x * 32 + 32 <= np ? 0u
+                                : threadIdx.x * 32 >= np   ? ~0u
+                                                           : ~((1u << (np - threadIdx.x * 32)) - 1u);
         __syncthreads();
     }
     const u32 vb = PAGED ? G::VIS : w * G::FIXED_WAVE;

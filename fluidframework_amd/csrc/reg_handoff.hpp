@@ -76,10 +76,13 @@ MTE_DEV void reg_handoff(R& r, E& e) {
             first += c;
         }
     }
-    // LRU heap (positions 1..heapSize)
-    for (u32 q0 = 0; q0 <= r.heapSize; q0 += 64) {
-        const u32 q = q0 + L;
-        const u32 hk = r.HK.get(q0 >> 6).x, hs = r.HS.get(q0 >> 6).x;
+    // LRU heap (positions 1..heapSize). The register index must be a compile-time constant: a
+    // run-time index here made the compiler keep a heap register set in scratch memory for the whole
+    // kernel, so every heap access of the row engine's replay loop was a scratch load.
+#pragma unroll
+    for (u32 j = 0; j < 8; j++) {
+        const u32 q = j * 64 + L;
+        const u32 hk = r.HK.get(j).x, hs = r.HS.get(j).x;
         if (q >= 1 && q <= r.heapSize) e.HEAP()[q] = make_uint2(hs - 1u, hk);  // ids 1-based in the rows
     }
     // slots: row rr lane l is block 8*rr + l/8, slot l%8 = the LDS engine's slot index 64*rr + l,

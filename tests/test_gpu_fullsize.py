@@ -61,3 +61,50 @@ def test_c2_full_batch(engine):
     assert not bad and ops == 4096 * 10000
     for d in (0, 1365, 2730, 4095):
         compare_doc(engine, batch, d)
+
+
+def test_c5_batch_on_the_bench_route(engine):
+    """C5 on the route bench.py takes (BASELINE.json config 5): 256 of its 1 024 documents of 10^6
+    kind-5 ops (the bench's global ids 0..255, equal lengths, so no solo document), replayed by k_rows
+    at 4 waves per CU on fixed 20-row LDS quarters (mode 5). Every document's status and checksum
+    (text + SnapshotV1 blobs) against the oracle, and the full segment table / snapshot of two."""
+    from fluidframework_amd.shard import plan_shard
+
+    ids, counts = plan_shard("C5", 1, 0, 1024, 1_000_000)
+    ids, counts = ids[:256], counts[:256]
+    engine.generate(5, len(ids), 1_000_000, n_clients=8, seed=1000, ops_per_doc=counts, doc_ids=ids)
+    batch = engine.export_batch()
+    st = engine.replay()
+    assert st["failed_docs"] == 0
+    info = engine.run_info()
+    assert engine.get_info("rows") == 4 and info["solo"] == 0 and info["spilled"] == 0, info
+    modes = [engine.doc_result(d)["mode"] for d in range(len(ids))]
+    assert modes == [5] * len(ids), sorted(set(modes))
+    bad, ops, _ = compare_batch_checksums(engine, batch)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad and ops == len(ids) * 1_000_000
+    for d in (0, 255):
+        compare_doc(engine, batch, d)
+
+
+def test_c3_full_batch(engine):
+    """C3 itself (BASELINE.json config 3): 65 536 documents x 10 000 ops with annotates, property
+    sets, forced ties and overlapping removes, on the default route (k_rows' PROPS row engine at 12
+    waves per CU on the shared row pool, with the in-pass restart queue): every document's status and
+    checksum against the oracle; any document the pool could not hold was restarted in the pass or
+    re-run by the host, and still matches."""
+    engine.generate(3, 65536, 10000, n_clients=8, seed=1000)
+    batch = engine.export_batch()
+    st = engine.replay()
+    assert st["failed_docs"] == 0
+    info = engine.run_info()
+    assert engine.get_info("rows") == 12 and info["lean"] == 0, info
+    print(f"C3 full: spilled {info['spilled']}, restarts pushed {info['rows_restart_pushed']} "
+          f"popped {info['rows_restart_popped']}")
+    bad, ops, _ = compare_batch_checksums(engine, batch)
+    if bad:
+        compare_doc(engine, batch, bad[0])
+    assert not bad and ops == 65536 * 10000
+    for d in (0, 32768, 65535):
+        compare_doc(engine, batch, d)

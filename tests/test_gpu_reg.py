@@ -198,7 +198,10 @@ def test_bulk_rows_kernel_matches_oracle(engine, kind, waves):
         modes = [engine.doc_result(d)["mode"] for d in range(len(counts))]
         # the longest documents may take k_solo (4); a document the pool cannot grow is re-run
         # HBM-resident (1)
-        assert set(modes) <= {MODE_BULK_ROWS, MODE_ROWS, 1} and modes.count(MODE_BULK_ROWS) > 0.9 * len(counts), sorted(set(modes))
+        # (at most 16 solo documents: every other document stays on the rows)
+        assert set(modes) <= {MODE_BULK_ROWS, MODE_ROWS, 1}, sorted(set(modes))
+        assert modes.count(MODE_BULK_ROWS) >= len(counts) - 16, (modes.count(1), engine.run_info())
+        assert modes.count(1) == engine.run_info()["spilled"]
         _check(engine, batch, n_docs=len(counts))
         # documents that outgrow the rows (reg_lb_limit shrinks them) go back to the host, which
         # re-runs them HBM-resident from their first op
@@ -226,7 +229,7 @@ def test_bulk_rows_pool_shared_and_exhausted(engine, waves):
         st = engine.replay()
         assert st["failed_docs"] == 0 and engine.get_info("rows") == waves
         modes = [engine.doc_result(d)["mode"] for d in range(2048)]
-        assert modes.count(MODE_BULK_ROWS) > 0.9 * 2048, sorted(set(modes))
+        assert modes.count(MODE_BULK_ROWS) >= 2048 - 16, (modes.count(1), engine.run_info())
         _check(engine, batch, n_docs=2048)
         engine.generate(2, 1024, 4000, n_clients=31, seed=4)
         batch = engine.export_batch()
@@ -253,14 +256,75 @@ def test_bulk_rows_props_matches_oracle(engine, waves):
         st = engine.replay()
         assert st["failed_docs"] == 0 and engine.get_info("rows") == waves and engine.run_info()["lean"] == 0
         modes = [engine.doc_result(d)["mode"] for d in range(len(counts))]
-        assert modes.count(MODE_BULK_ROWS) > 0.9 * len(counts), sorted(set(modes))
+        assert modes.count(MODE_BULK_ROWS) >= len(counts) - 16, (modes.count(1), engine.run_info())
         _check(engine, batch, n_docs=len(counts))
         engine.generate(3, 1024, 10_000, n_clients=8, seed=1000)
         batch = engine.export_batch()
         st = engine.replay()
         assert st["failed_docs"] == 0
         modes = [engine.doc_result(d)["mode"] for d in range(1024)]
-        assert modes.count(MODE_BULK_ROWS) > 0.9 * 1024, sorted(set(modes))
+        assert modes.count(MODE_BULK_ROWS) >= 1024 - 16, (modes.count(1), engine.run_info())
         _check(engine, batch, n_docs=1024)
     finally:
         engine.set_option("rows_bulk", -1)
+
+
+@pytest.mark.parametrize("pool", [40, 56])
+def test_bulk_rows_restart_queue(engine, pool):
+    """k_rows' in-pass restart queue, forced: C2-shaped documents (leaf blocks peaking near 100, i.e.
+    up to 13 slot rows) at 12 waves per CU on a pool shrunk to `pool` rows (option rows_pool), so
+    waves find it full at their documents' peaks, give a document up after the bounded wait and queue
+    it to restart from its first op. Asserts that documents were pushed and restarted in the pass
+    (run_info rows_restart_pushed / _popped), that restarts finished on the rows (fewer host re-runs
+    than pushes, every document mode 5 or re-run), and every checksum against the oracle."""
+    engine.set_option("rows_bulk", 12)
+    engine.set_option("rows_pool", pool)
+    try:
+        engine.generate(2, 2048, 10_000, n_clients=8, seed=1000)
+        batch = engine.export_batch()
+        st = engine.replay()
+        info = engine.run_info()
+        print(f"pool {pool}: {info}")
+        assert st["failed_docs"] == 0 and info["rows"] == 12, info
+        pushed, popped = info["rows_restart_pushed"], info["rows_restart_popped"]
+        assert pushed > 0 and popped > 0 and popped <= pushed, info
+        modes = [engine.doc_result(d)["mode"] for d in range(2048)]
+        assert set(modes) <= {MODE_BULK_ROWS, 1} and modes.count(1) == info["spilled"], sorted(set(modes))
+        assert info["spilled"] < pushed, info  # at least one restarted document finished on the rows
+        _check(engine, batch, n_docs=2048)
+    finally:
+        engine.set_option("rows_pool", 0)
+        engine.set_option("rows_bulk", -1)
+
+
+def test_local_documents_keep_the_lds_engine(engine):
+    """A lean batch of local (non-collaborative) documents and no solo document: the row engine does
+    not replay local edits, so the batch must not take k_rows (its waves would hand every document to
+    the host's HBM re-run); it runs on k_lds / k_hbmq with no re-run. Local edits apply in order, so
+    each document's text is checked against the same edits on a Python string (the oracle's record
+    path replays sequenced logs only)."""
+    from tests.oplog import ins, msg, rem
+
+    logs, texts = [], []
+    for d in range(96):
+        ops, text = [], ""
+        for i in range(300 + d):
+            if len(text) > 20 and i % 5 == 4:
+                a = (i * 7) % (len(text) - 5)
+                ops.append(msg("local", 0, 0, rem(a, a + 3)))
+                text = text[:a] + text[a + 3:]
+            else:
+                t, at = f"t{d}.{i} ", (i * 13) % (len(text) + 1)
+                ops.append(msg("local", 0, 0, ins(at, t)))
+                text = text[:at] + t + text[at:]
+        logs.append(ops)
+        texts.append(text)
+    b = mte.Builder()
+    for m in logs:
+        b.add_doc(m, observer="")
+    engine.load(b.batch())
+    st = engine.replay()
+    info = engine.run_info()
+    assert st["failed_docs"] == 0 and info["lean"] == 1 and info["solo"] == 0, info
+    assert engine.get_info("rows") == 0 and info["spilled"] == 0, info
+    assert [engine.text(d) for d in range(96)] == texts

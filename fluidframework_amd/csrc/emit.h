@@ -18,6 +18,7 @@ struct EmitParams {
     const u32* maps;           // the property map of every row with props (map_words per row), or null
     u32 map_words;
     const u16* text;           // gathered text of every row
+    const u32* esc;            // per row: its text's JSON byte size + flags (engine_types.hpp ESC_*)
     // property text tables (interned JSON texts of keys and values)
     const char* key_text;
     const u64* key_off;
@@ -33,7 +34,8 @@ struct EmitParams {
     const u64* name_off;
     const u64* name_base;
     // scratch
-    uint4* ent;                // snapshot entries, indexed like the rows
+    uint4* ent;                // legacy: snapshot entries, indexed like the rows; SnapshotV1: the chunk
+                               // table (per chunk: first entry, entry count, length in characters)
     u16* tscr;                 // gathered text of runs that span elided rows, indexed like `text`
     // per document (indexed by doc): COUNT writes, WRITE reads
     u32* n_ent;

@@ -313,8 +313,15 @@ struct Doc {
         wave_sync();
         return dst;
     }
-    MTE_DEV void put_seg(Out& o, u32 row, const u16* txt, u64 n) const {  // Segment.toJSONObject
-        const uint4 v = p.vis[row0 + row], a = p.aux[row0 + row];
+    // quoted text: the bytes from the text (WRITE), or from the rows' emission words (COUNT: tb, the
+    // JSON size of the text without its quotes), so COUNT never reads text
+    static constexpr u64 NO_TB = ~0ull;  // no precomputed size: COUNT reads the text (legacy format)
+    MTE_DEV void put_text(Out& o, const u16* txt, u64 n, u64 tb) const {
+        if (o.out || tb == NO_TB) put_quoted(o, txt, n);
+        else o.pos += 2 + tb;
+    }
+    // Segment.toJSONObject of row `row` (vis v, aux a); txt / n / tb: its text (put_text)
+    MTE_DEV void put_seg(Out& o, u32 row, uint4 v, uint4 a, const u16* txt, u64 n, u64 tb) const {
         if (v.w & F_PERM) {  // PermutationSegment.toJSONObject (permutationvector.ts:75-77): [length, start]
             put(o, "[");
             put_int(o, (i64)n);
@@ -334,25 +341,28 @@ struct Doc {
             put(o, "}");
         } else if (a.x) {
             put(o, "{\"text\":");
-            put_quoted(o, txt, n);
+            put_text(o, txt, n, tb);
             put(o, ",\"props\":");
             put_props(o, row0 + row);
             put(o, "}");
         } else {
-            put_quoted(o, txt, n);
+            put_text(o, txt, n, tb);
         }
     }
-    MTE_DEV void put_entry(Out& o, uint4 e) const {
+    // one entry: e = (first row, last row, length, kind) as build_entries / Walk make them; tb the
+    // JSON size of its text (COUNT)
+    MTE_DEV void put_entry(Out& o, uint4 e, u64 tb = NO_TB) const {
+        const uint4 v = p.vis[row0 + e.x], a = p.aux[row0 + e.x];
         if (e.w == 0 || e.w == 1 || e.w == 3) {  // settled: coalesced text / permutation run or a marker
             u64 n = e.w == 3 ? e.z : 0;
-            const u16* t = e.w == 0 ? run_text(e, n) : nullptr;
-            put_seg(o, e.x, t, n);
+            const u16* t = e.w == 0 && (o.out || tb == NO_TB) ? run_text(e, n) : nullptr;
+            if (e.w == 0 && !t) n = e.z;
+            put_seg(o, e.x, v, a, t, n, tb);
             return;
         }
-        const uint4 v = p.vis[row0 + e.x], a = p.aux[row0 + e.x];
         const bool notext = (v.w & (F_MARKER | F_PERM)) != 0;
         put(o, "{\"json\":");
-        put_seg(o, e.x, notext ? nullptr : row_text(a), (v.w & F_MARKER) ? 0 : v.x);
+        put_seg(o, e.x, v, a, notext ? nullptr : row_text(a), (v.w & F_MARKER) ? 0 : v.x, tb);
         const bool collab = p.cfg[d].collab != 0;
         if ((i32)v.y > r.min_seq) {
             put(o, ",\"seq\":");
@@ -411,6 +421,251 @@ struct Doc {
                 put_int(o, r.min_seq);
                 put(o, ",\"totalLength\":");
                 put_int(o, (i64)total);
+                put(o, ",\"totalSegmentCount\":");
+                put_int(o, ne);
+                put(o, "}");
+            }
+            put(o, "}");
+        }
+        return o.pos;
+    }
+
+    // SnapshotV1 COUNT and WRITE without an entries table (extractSync streamed, snapshotV1.ts:170-228):
+    // both passes walk the rows in 64-row batches (lane = row: its vis and emission word; aux only for
+    // markers and permutation runs). Neither pass reads an entry's rows again: the walk carries the
+    // first row's vis, its text offset (the running sum of the text rows' lengths -- Engine::finish
+    // lays every text row out in document order), whether it has properties, and the JSON size of the
+    // entry's text (the rows' emission words, less 8 bytes per surrogate pair joined across two rows),
+    // so COUNT reads no text and WRITE reads only the text it writes. COUNT stores only the chunk table
+    // (entry count, length per chunk); WRITE emits each entry as the walk closes it.
+    struct Item {
+        uint4 e;    // (first row, last row, length, kind) as build_entries makes it
+        uint4 v;    // the first row's vis
+        u32 ay;     // its text offset in the document's text run, or a marker's refType word / a run's start
+        u64 tb;     // the JSON size of the entry's text
+        bool props, gap;  // the first row has properties; a run spans an elided text row
+    };
+    struct Walk {
+        const Doc& D;
+        u32 n, base, j, tcarry;
+        uint4 bv;          // this lane's row of the batch: vis
+        u32 be, bay, btof;  // ... its emission word, aux.y (markers / permutation runs), text offset
+        bool open, pend, filled;
+        Item run, pe;       // the open run, and a merge-info entry queued behind it
+        bool runText, runPerm, runNL, runHI;
+        MTE_DEV explicit Walk(const Doc& d)
+            : D(d), n(d.r.n_segs), base(0), j(64), tcarry(0), open(false), pend(false), filled(false) {}
+        MTE_DEV void fill() {
+            const u32 k = base + lane_id();
+            bv = make_uint4(0, 0, 0, 0);
+            be = bay = 0;
+            if (k < n) {
+                bv = D.p.vis[D.row0 + k];
+                be = D.p.esc[D.row0 + k];
+                if (bv.w & (F_PERM | F_MARKER)) bay = D.p.aux[D.row0 + k].y;
+            }
+            const u32 tl = (bv.w & (F_PERM | F_MARKER)) ? 0u : bv.x;
+            const u32 incl = wave_scan_incl(tl);
+            btof = tcarry + incl - tl;
+            tcarry += wave_read(incl, 63);
+        }
+        // the next entry into it; false when the document has no more
+        MTE_DEV bool next(Item& it) {
+            const i32 minSeq = D.r.min_seq;
+            for (;;) {
+                if (pend && !open) {
+                    pend = false;
+                    it = pe;
+                    return true;
+                }
+                if (j == 64) {  // the next batch
+                    if (filled) base += 64;
+                    filled = true;
+                    j = 0;
+                    if (base < n) fill();
+                }
+                const u32 row = base + j;
+                if (row >= n) {  // the end: the open run
+                    if (!open) return false;
+                    open = false;
+                    it = run;
+                    return true;
+                }
+                const uint4 v = make_uint4(wave_read(bv.x, j), wave_read(bv.y, j), wave_read(bv.z, j), wave_read(bv.w, j));
+                const u32 ew = wave_read(be, j), ay = wave_read(bay, j), tof = wave_read(btof, j);
+                j++;
+                const u32 len = v.x, meta = v.w;
+                const bool removed = (meta & F_REMOVED) != 0, marker = (meta & F_MARKER) != 0, perm = (meta & F_PERM) != 0;
+                const bool hasP = (ew & ESC_PROPS) != 0;
+                if (removed && (i32)v.z <= minSeq) {  // elided (:184-186)
+                    if (open && runText && !marker && len) run.gap = true;  // run_text gathers around it
+                    continue;
+                }
+                Item cur;
+                cur.v = v;
+                cur.ay = (marker || perm) ? ay : tof;
+                cur.tb = ew & ESC_LEN;
+                cur.props = hasP;
+                cur.gap = false;
+                if ((i32)v.y <= minSeq && !removed) {
+                    if (open && (runPerm ? perm && ay == (run.ay ? run.ay + run.e.z : 0u)
+                                         : runText && !marker && !perm && !(run.e.z && runNL) && (run.e.z <= 256 || len <= 256)) &&
+                        D.match(D.row0 + run.e.x, run.props, D.row0 + row, hasP)) {
+                        run.e.y = row;  // clone + append (:197-202)
+                        run.e.z += len;
+                        run.tb += (ew & ESC_LEN) - (runHI && (ew & ESC_LO) ? 8u : 0u);
+                        runNL = (ew & ESC_NL) != 0;
+                        runHI = (ew & ESC_HI) != 0;
+                        continue;
+                    }
+                    const bool had = open;
+                    const Item prev = run;
+                    open = true;
+                    runText = !marker && !perm;
+                    runPerm = perm;
+                    runNL = (ew & ESC_NL) != 0;
+                    runHI = (ew & ESC_HI) != 0;
+                    run = cur;
+                    run.e = make_uint4(row, row, len, perm ? 3u : runText ? 0u : 1u);
+                    if (had) {
+                        it = prev;
+                        return true;
+                    }
+                } else {  // a merge-info entry
+                    cur.e = make_uint4(row, row, len, 2u);
+                    if (open) {
+                        open = false;
+                        pend = true;
+                        pe = cur;
+                        it = run;
+                        return true;
+                    }
+                    it = cur;
+                    return true;
+                }
+            }
+        }
+    };
+    // one streamed entry (put_entry without reading its rows; a run across an elided text row gathers
+    // its text through run_text)
+    MTE_DEV void put_item(Out& o, const Item& it) const {
+        const uint4 a = make_uint4(it.props ? 1u : 0u, it.ay, 0, 0);
+        if (it.e.w == 0 || it.e.w == 1 || it.e.w == 3) {  // settled: coalesced text / permutation run or a marker
+            u64 n = it.e.z;
+            const u16* t = nullptr;
+            if (it.e.w == 0 && o.out) t = it.gap ? run_text(it.e, n) : p.text + r.text_off + it.ay;
+            put_seg(o, it.e.x, it.v, a, t, n, it.tb);
+            return;
+        }
+        const uint4 v = it.v;
+        const bool notext = (v.w & (F_MARKER | F_PERM)) != 0;
+        put(o, "{\"json\":");
+        put_seg(o, it.e.x, v, a, notext ? nullptr : p.text + r.text_off + it.ay, (v.w & F_MARKER) ? 0 : v.x, it.tb);
+        const bool collab = p.cfg[d].collab != 0;
+        if ((i32)v.y > r.min_seq) {
+            put(o, ",\"seq\":");
+            put_int(o, (i32)v.y);
+            put(o, ",\"client\":");
+            put_name(o, collab ? (v.w & 0xffu) : NONE);
+        }
+        if (v.w & F_REMOVED) {
+            put(o, ",\"removedSeq\":");
+            put_int(o, (i32)v.z);
+            put(o, ",\"removedClient\":");
+            put_name(o, collab ? ((v.w >> 8) & 0xffu) : NONE);
+        }
+        put(o, "}");
+    }
+
+    // COUNT (SnapshotV1): byte count and blob count; the chunk table into ent[row0 + c]
+    MTE_DEV u64 count_v1(u32& ne, u32& nblobs) const {
+        const u32 L = lane_id(), chunk = p.chunk;
+        Walk w(*this);
+        Out o{nullptr, 0};
+        u32 nch = 0, cnt = 0, first = 0;
+        u64 len = 0, totalLen = 0;
+        ne = 0;
+        Item it;
+        auto close_chunk = [&]() {
+            if (L == 0) p.ent[row0 + nch] = make_uint4(first, cnt, (u32)len, 0u);
+            put(o, "{\"version\":\"1\",\"segmentCount\":");
+            put_int(o, cnt);
+            put(o, ",\"length\":");
+            put_int(o, (i64)len);
+            put(o, ",\"segments\":[");
+            put(o, "],\"startIndex\":");
+            put_int(o, first);
+            put(o, "}");
+            if (cnt > 1) o.pos += cnt - 1;  // the commas between its entries
+            totalLen += len;
+            nch++;
+            first += cnt;
+            cnt = 0;
+            len = 0;
+        };
+        while (w.next(it)) {
+            put_item(o, it);
+            ne++;
+            cnt++;
+            len += it.e.z;
+            if (len >= chunk) close_chunk();
+        }
+        if (cnt || nch == 0) close_chunk();
+        // the header chunk's metadata
+        put(o, ",\"headerMetadata\":{\"minSequenceNumber\":");
+        put_int(o, r.min_seq);
+        put(o, ",\"sequenceNumber\":");
+        put_int(o, r.cur_seq);
+        put(o, ",\"orderedChunkMetadata\":[{\"id\":\"header\"}");
+        for (u32 b = 1; b < nch; b++) {
+            put(o, ",{\"id\":\"body_");
+            put_int(o, b - 1);
+            put(o, "\"}");
+        }
+        put(o, "],\"totalLength\":");
+        put_int(o, (i64)totalLen);
+        put(o, ",\"totalSegmentCount\":");
+        put_int(o, ne);
+        put(o, "}");
+        nblobs = nch;
+        return o.pos;
+    }
+    // WRITE (SnapshotV1) from the chunk table COUNT wrote
+    MTE_DEV u64 write_v1(u32 ne, u32 nch, char* out, u64* blob_off) const {
+        const u32 L = lane_id();
+        Walk w(*this);
+        Out o{out, 0};
+        u64 totalLen = 0;
+        for (u32 c = 0; c < nch; c++) totalLen += p.ent[row0 + c].z;
+        Item it;
+        for (u32 c = 0; c < nch; c++) {
+            const uint4 ch = p.ent[row0 + c];
+            if (L == 0) blob_off[c] = o.pos;
+            put(o, "{\"version\":\"1\",\"segmentCount\":");
+            put_int(o, ch.y);
+            put(o, ",\"length\":");
+            put_int(o, (i64)ch.z);
+            put(o, ",\"segments\":[");
+            for (u32 q = 0; q < ch.y; q++) {
+                if (!w.next(it)) break;  // (COUNT's walk: never short)
+                if (q) put(o, ",");
+                put_item(o, it);
+            }
+            put(o, "],\"startIndex\":");
+            put_int(o, ch.x);
+            if (c == 0) {
+                put(o, ",\"headerMetadata\":{\"minSequenceNumber\":");
+                put_int(o, r.min_seq);
+                put(o, ",\"sequenceNumber\":");
+                put_int(o, r.cur_seq);
+                put(o, ",\"orderedChunkMetadata\":[{\"id\":\"header\"}");
+                for (u32 b = 1; b < nch; b++) {
+                    put(o, ",{\"id\":\"body_");
+                    put_int(o, b - 1);
+                    put(o, "\"}");
+                }
+                put(o, "],\"totalLength\":");
+                put_int(o, (i64)totalLen);
                 put(o, ",\"totalSegmentCount\":");
                 put_int(o, ne);
                 put(o, "}");
@@ -509,9 +764,13 @@ __global__ __launch_bounds__(64) void k_emit_count(EmitParams p) {
     u32 ne = 0, nb = 0;
     u64 bytes = 0;
     if (doc.r.status == 0) {
-        ne = doc.build_entries();
-        wave_sync();  // entries written by lane 0, read by every lane
-        bytes = doc.emit(ne, nullptr, nullptr, nb);
+        if (p.legacy || !p.esc) {
+            ne = doc.build_entries();
+            wave_sync();  // entries written by lane 0, read by every lane
+            bytes = doc.emit(ne, nullptr, nullptr, nb);
+        } else {
+            bytes = doc.count_v1(ne, nb);
+        }
     }
     if (lane_id() == 0) {
         p.n_ent[d] = ne;
@@ -528,7 +787,8 @@ __global__ __launch_bounds__(64) void k_emit_write(EmitParams p) {
     Doc doc(p, d);
     if (doc.r.status != 0 || p.size[d] == 0) return;
     u32 nb = 0;
-    doc.emit(p.n_ent[d], p.out + p.out_off[d], p.blob_off + p.blob_base[d], nb);
+    if (p.legacy || !p.esc) doc.emit(p.n_ent[d], p.out + p.out_off[d], p.blob_off + p.blob_base[d], nb);
+    else doc.write_v1(p.n_ent[d], p.nblobs[d], p.out + p.out_off[d], p.blob_off + p.blob_base[d]);
 }
 
 hipError_t launch_emit(const EmitParams& p, bool write, hipStream_t s) {

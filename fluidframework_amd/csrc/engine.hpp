@@ -804,15 +804,12 @@ struct Engine {
     // ht[1 + i] = handles[i] (handles[0] = the free-list head), ht[1 + cap + i] = the seq of the op
     // whose zamboni last freed handle i (0 = never). Lane 0 owns it; results are broadcast.
     MTE_DEV u32* ht_base() const { return p.htab + p.docs[doc].ht_off; }
-    MTE_DEV void ht_reset() {
+    MTE_DEV void ht_reset() {  // new HandleTable(): [1], or HandleTable.load of a matrix summary (htab0)
         const u32 cap = p.docs[doc].ht_cap;
-        if (!cap || !p.htab) return;
+        if (!cap || !p.htab || !p.htab0) return;
         u32* ht = ht_base();
-        for (u32 i = L; i < cap; i += 64) ht[1 + cap + i] = 0;
-        if (L == 0) {
-            ht[0] = 1;  // new HandleTable(): [1]
-            ht[1] = 1;
-        }
+        const u32* h0 = p.htab0 + p.docs[doc].ht_off;
+        for (u32 i = L; i < 1 + 2 * cap; i += 64) ht[i] = h0[i];
         wave_sync();
     }
     MTE_DEV u32 ht_alloc() {  // HandleTable.allocate (handletable.ts:35-40)
@@ -2254,7 +2251,8 @@ struct Engine {
         rec.tcap = 0;          // (the overlap mask of a removed segment: empty)
         rec.seq = op.seq;
         rec.rseq = rm ? op.ref_seq : 0;
-        rec.meta = (op.client & 0xffu) | (mk ? F_MARKER : 0u) | (rm ? ((((u32)op.pos1 & 0xffu) << 8) | F_REMOVED) : 0u);
+        rec.meta = (op.client & 0xffu) | (mk ? F_MARKER : 0u) | (rm ? ((((u32)op.pos1 & 0xffu) << 8) | F_REMOVED) : 0u) |
+                   ((EXT && (op.flags & MTE_F_PERM)) ? F_PERM : 0u);  // a loaded run: its start handle in toff
         rec.sid = new_sid();
         if (rec.sid == NONE) return;
         u32 k = st.n_lb - 1;
@@ -2436,14 +2434,15 @@ struct Engine {
             rec.len = mk ? 1u : op.b;
             rec.seq = seq;
             rec.rseq = 0;
-            rec.meta = (C & 0xff) | (mk ? F_MARKER : 0u) | ((EXT && !ld && (op.flags & MTE_F_PERM)) ? F_PERM : 0u);
+            rec.meta = (C & 0xff) | (mk ? F_MARKER : 0u) | ((EXT && (op.flags & MTE_F_PERM)) ? F_PERM : 0u);
             u32 type = op.type;
             i32 p1 = op.pos1;
             if (ld && !load_append_pos(op, rec, p1)) return;  // skipped (a repeated object) or failed
             type = ld ? (mk ? (u32)MTE_OP_INSERT_MARKER : (u32)MTE_OP_INSERT) : type;
             rec.props = (ins && op.props) ? build_map(0, op.props, false) : 0u;
             if (st.status) return;
-            rec.toff = (mk && !ld) ? op.b : ((rec.meta & F_PERM) ? 0u : (u32)op.a);
+            // (a PermutationSegment run: handles unallocated on insert -- onDelta's reset -- kept when loaded)
+            rec.toff = (mk && !ld) ? op.b : ((rec.meta & F_PERM) && !ld ? 0u : (u32)op.a);
             rec.tcap = 0;
             rec.sid = 0;
             const bool cu = EXT && (op.flags & MTE_F_CATCHUP) != 0 && !ld;  // EXT batches only
@@ -2580,20 +2579,30 @@ struct Engine {
                 u32 tat = trun + tincl - bt;
                 for (u32 s = 0; s < c; s++) {
                     uint4 v = VIS()[o.x * 8 + s], a = AUX()[o.x * 8 + s];
+                    u32 esc = a.x ? ESC_PROPS : 0u;  // the row's emission word (ESC_*, engine_types.hpp)
                     if (!(v.w & (F_MARKER | F_PERM))) {  // wave-divergent copy, 8 units in flight per lane
                         const u16* __restrict__ src = text_ptr(a.y);
                         u16* __restrict__ dst = tdst + tat;
+                        u32 tot = 0, prevc = 0, firstc = 0;
                         for (u32 i = 0; i < v.x; i += 8) {
                             u16 t[8];
 #pragma unroll
                             for (u32 j = 0; j < 8; j++) t[j] = i + j < v.x ? src[i + j] : (u16)0;
+                            if (i == 0) firstc = t[0];
 #pragma unroll
                             for (u32 j = 0; j < 8; j++)
-                                if (i + j < v.x) dst[i + j] = t[j];
+                                if (i + j < v.x) {
+                                    dst[i + j] = t[j];
+                                    tot += (u32)esc_unit(t[j], prevc);
+                                    prevc = t[j];
+                                }
                         }
+                        esc |= (tot & ESC_LEN) | (esc_is_lo(firstc) ? ESC_LO : 0u) | (esc_is_hi(prevc) ? ESC_HI : 0u) |
+                               (prevc == (u32)'\n' ? ESC_NL : 0u);
                         a.y = tat;  // offset in the document's text run
                         tat += v.x;
                     }
+                    if (p.out_esc) p.out_esc[at + s] = esc;
                     if (a.x && p.out_maps) {  // the row's property map, indexed by row
                         const uint4* ms = (const uint4*)(maps + (u64)a.x * mw);
                         uint4* md = (uint4*)(p.out_maps + (u64)(at + s) * mw);

@@ -26,6 +26,25 @@ constexpr u32 MAP_WORDS = 16;  // the narrowest map record: [0] = count, then 7 
                                // (Params::map_words = 1 + 2 * keys, rounded up to 4, <= 128)
 constexpr i32 GRANULARITY = 256;                         // TextSegmentGranularity (mergeTree.ts:1059)
 
+// Per output row, the emission's view of its text (Params::out_esc, written by every engine's finish):
+// the bytes JSON.stringify writes for the row's text alone, quotes excluded (UTF-8, '"' '\\' and control
+// characters escaped, an unpaired surrogate as \uXXXX), and the flags the SnapshotV1 writer needs
+// without reading the text or the aux row: the text starts with a low / ends with a high surrogate (a
+// pair joined across two rows of a run is 4 bytes, not 6 + 6), ends with '\n' (TextSegment.canAppend),
+// and the row has a property map. Markers and permutation runs: 0 bytes, the props flag only.
+constexpr u32 ESC_LEN = 0x0FFFFFFFu, ESC_NL = 1u << 28, ESC_PROPS = 1u << 29, ESC_LO = 1u << 30, ESC_HI = 1u << 31;
+MTE_HOSTDEV_ bool esc_is_hi(u32 c) { return c >= 0xD800u && c < 0xDC00u; }
+MTE_HOSTDEV_ bool esc_is_lo(u32 c) { return c >= 0xDC00u && c < 0xE000u; }
+// bytes of one UTF-16 unit c after `prev` inside one JSON string (emit.hip put_quoted): a high surrogate
+// counts 6 and its low partner -2, so a joined pair totals 4 (6 + 6 for unpaired units)
+MTE_HOSTDEV_ i32 esc_unit(u32 c, u32 prev) {
+    if (c == '"' || c == '\\') return 2;
+    if (c < 0x20u) return (c == '\b' || c == '\f' || c == '\n' || c == '\r' || c == '\t') ? 2 : 6;
+    if (esc_is_hi(c)) return 6;
+    if (esc_is_lo(c)) return esc_is_hi(prev) ? -2 : 6;
+    return c < 0x80u ? 1 : c < 0x800u ? 2 : 3;
+}
+
 // Leaf-block metadata word: parent interior node (bits 0..29) | needsScour (bits 30..31).
 constexpr u32 BM_PAR = 0x3FFFFFFFu;
 constexpr u32 BM_NOPAR = 0x3FFFFFFFu;
@@ -221,6 +240,7 @@ struct Params {
     u32* cell_pos;
     u32* cell_h;
     u32* htab;
+    const u32* htab0;         // each HandleTable's state at document start (new, or loaded from a summary)
     u64* solo_clk;            // per solo workgroup: s_memtime / s_memrealtime at its replay's start and
                               // end (4 u64): shader cycles vs the 100 MHz reference clock; then, at
                               // [4 * SOLO_CLK_SLOTS], the bulk kernel's start (s_memrealtime)
@@ -228,6 +248,7 @@ struct Params {
     u32* rows_retry;          // k_rows: documents the row pool could not grow, queued to restart once
                               // (doc + 1 per slot; counters[8] pushed, counters[9] popped), or null
     u32 rows_pool_lim;        // test knob: k_rows pool rows usable per CU (0 = all of the pool)
+    u32* out_esc;             // per output row: JSON byte size of its text + flags (ESC_*), or null
 };
 
 constexpr u32 SOLO_CLK_SLOTS = 64;  // solo workgroups with clock stamps (Params::solo_clk)

@@ -14,10 +14,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -276,6 +278,7 @@ struct mte_engine {
     DevBuf<DocCfg> d_cfg;
     DevBuf<DocRes> d_res;
     DevBuf<uint4> d_out_vis, d_out_aux;
+    DevBuf<uint32_t> d_out_esc;  // per output row: the emission word (engine_types.hpp ESC_*)
     DevBuf<unsigned char> d_hbm, d_spill, d_solo_spill;
     DevBuf<uint32_t> d_slot_bits;
     std::vector<uint64_t> n_ops_doc;
@@ -305,8 +308,15 @@ struct mte_engine {
         uint32_t val;
     };
     std::unordered_map<uint32_t, std::vector<CellRec>> cell_recs;
+    // a SharedMatrix loaded from a summary (MTE_F_MX_* records of its rows document): the loaded
+    // cells (row handle, col handle, value id), tiles (key hi, depth, low-key prefix) and root extent
+    struct MxInit {
+        std::vector<std::array<uint32_t, 3>> cells, tiles;
+        uint32_t root_len = 1;
+    };
+    std::unordered_map<uint32_t, MxInit> mx_init;
     uint64_t n_cells = 0;                // cell indices 0 .. n_cells - 1
-    DevBuf<uint32_t> d_cell_pos, d_cell_h, d_htab;
+    DevBuf<uint32_t> d_cell_pos, d_cell_h, d_htab, d_htab0;  // HandleTables, and their state at document start
     bool ext_cu = false;                 // ... MTE_F_CATCHUP ops: EXT only when a legacy summary is emitted
     bool lean_base = false;              // batch_is_lean, before the catch-up records decide
     uint32_t rows_pool_lim = 0;          // option rows_pool: k_rows pool rows per CU (test knob, 0 = all)
@@ -529,6 +539,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     HIP_TRY(e, e->d_ovl.fit(seg));
     HIP_TRY(e, e->d_maps.fit(mp * e->map_words));
     HIP_TRY(e, e->d_out_vis.fit(out));
+    HIP_TRY(e, e->d_out_esc.fit(out));
     HIP_TRY(e, e->d_out_aux.fit(out));
     HIP_TRY(e, e->d_out_ovl.fit(out));
     if (any_props) HIP_TRY(e, e->d_out_maps.fit(out * e->map_words));  // some document can carry props
@@ -558,6 +569,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     P.maps = e->d_maps.p;
     P.map_words = e->map_words;
     P.out_vis = e->d_out_vis.p;
+    P.out_esc = e->d_out_esc.p;
     P.out_aux = e->d_out_aux.p;
     P.out_ovl = e->d_out_ovl.p;
     P.out_cap = out;
@@ -812,36 +824,71 @@ static void run_pool(unsigned n, F&& work) {
 // pass's results; the records' cell / seq / value are kept for the cells blob (mte_snapshot_matrix).
 static int load_cells(mte_engine* e, const mte_batch* b, const std::vector<uint32_t>& n_cell) {
     e->cell_recs.clear();
+    e->mx_init.clear();
     e->n_cells = 0;
     uint64_t words = 0;
+    std::vector<uint32_t> init;  // every region's state at document start (Params::htab0)
+    bool any = false;
     for (uint32_t d = 0; d < b->n_docs; d++) {
         DocCfg& c = e->cfg[d];
         c.ht_cap = 0;
         c.ht_off = 0;
-        if (!n_cell[d]) continue;
-        std::vector<mte_engine::CellRec>& v = e->cell_recs[d];
+        // a loaded HandleTable (MX_HANDLE records) and cells (MX_CELL / MX_TILE)
+        std::vector<uint32_t> h0;
         for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
             const mte_op& o = b->ops[i];
-            if (o.type != MTE_OP_CELL) continue;
-            if (o.b >= (1u << 28)) return set_err(e, MTE_E_RANGE, "cell index beyond 2^28");
-            v.push_back({o.b, o.seq, o.props < b->n_vals ? o.props : 0u});
-            e->n_cells = std::max<uint64_t>(e->n_cells, (uint64_t)o.b + 1);
+            if (o.type != MTE_OP_NOOP || !(o.flags & MTE_F_MX_MASK)) continue;
+            const uint32_t f = o.flags & MTE_F_MX_MASK;
+            if (f == MTE_F_MX_HANDLE) {
+                if (o.pos1 < 0 || o.pos1 > (1 << 26)) return set_err(e, MTE_E_RANGE, "loaded handle table too long");
+                if (h0.size() <= (size_t)o.pos1) h0.resize((size_t)o.pos1 + 1, 0);
+                h0[(size_t)o.pos1] = (uint32_t)o.a;
+            } else if (f == MTE_F_MX_CELL) {
+                e->mx_init[d].cells.push_back({(uint32_t)o.pos1, (uint32_t)o.a, o.props < b->n_vals ? o.props : 0u});
+            } else if (o.b == 4) {
+                e->mx_init[d].root_len = (uint32_t)o.pos1 + 1;
+            } else {
+                e->mx_init[d].tiles.push_back({(uint32_t)o.pos1, o.b, (uint32_t)o.a});
+            }
         }
-        c.ht_cap = n_cell[d] + 2;
+        if (!n_cell[d] && h0.empty()) continue;
+        if (n_cell[d]) {
+            std::vector<mte_engine::CellRec>& v = e->cell_recs[d];
+            for (uint64_t i = b->doc_op_offsets[d]; i < b->doc_op_offsets[d + 1]; i++) {
+                const mte_op& o = b->ops[i];
+                if (o.type != MTE_OP_CELL) continue;
+                if (o.b >= (1u << 28)) return set_err(e, MTE_E_RANGE, "cell index beyond 2^28");
+                v.push_back({o.b, o.seq, o.props < b->n_vals ? o.props : 0u});
+                e->n_cells = std::max<uint64_t>(e->n_cells, (uint64_t)o.b + 1);
+            }
+        }
+        if (h0.empty()) h0.push_back(1);  // new HandleTable(): [1]
+        // every set allocates at most one handle per vector
+        c.ht_cap = (uint32_t)h0.size() + n_cell[d] + 2;
         c.ht_off = words;
         words += 1 + 2 * (uint64_t)c.ht_cap;
+        init.push_back((uint32_t)h0.size());
+        init.insert(init.end(), h0.begin(), h0.end());
+        init.resize(words, 0u);  // the rest of the handles, and no handle freed yet
+        any = true;
     }
     e->P.cell_pos = e->P.cell_h = e->P.htab = nullptr;
+    e->P.htab0 = nullptr;
+    if (!any) return MTE_OK;
+    if (e->d_htab.n < words) HIP_TRY(e, e->d_htab.alloc(words));
+    if (e->d_htab0.n < words) HIP_TRY(e, e->d_htab0.alloc(words));
+    HIP_TRY(e, hipMemcpyAsync(e->d_htab0.p, init.data(), words * sizeof(uint32_t), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->P.htab = e->d_htab.p;
+    e->P.htab0 = e->d_htab0.p;
     if (!e->n_cells) return MTE_OK;
     if (e->d_cell_pos.n < 2 * e->n_cells) HIP_TRY(e, e->d_cell_pos.alloc(2 * e->n_cells));
     if (e->d_cell_h.n < 2 * e->n_cells) HIP_TRY(e, e->d_cell_h.alloc(2 * e->n_cells));
-    if (e->d_htab.n < words) HIP_TRY(e, e->d_htab.alloc(words));
     // a cell index no document carries keeps both positions undefined
     HIP_TRY(e, hipMemsetAsync(e->d_cell_pos.p, 0xFF, 2 * e->n_cells * sizeof(uint32_t), e->stream));
     HIP_TRY(e, hipMemsetAsync(e->d_cell_h.p, 0, 2 * e->n_cells * sizeof(uint32_t), e->stream));
     e->P.cell_pos = e->d_cell_pos.p;
     e->P.cell_h = e->d_cell_h.p;
-    e->P.htab = e->d_htab.p;
     return MTE_OK;
 }
 
@@ -1034,6 +1081,7 @@ static EmitParams emit_params(mte_engine* e) {
     P.maps = e->P.out_maps;
     P.map_words = e->map_words;
     P.text = e->d_out_text.p;
+    P.esc = e->d_out_esc.p;
     P.key_text = e->d_key_text.p;
     P.key_off = e->d_key_off.p;
     P.key_is_index = e->d_key_is_index.p;
@@ -1951,6 +1999,24 @@ int mte_snapshot_matrix(mte_engine* e, uint32_t rows_doc, uint32_t cols_doc, cha
     // cells: JSON.stringify([cells.snapshot(), pending.snapshot()]); pending stays [undefined] for an
     // observer (it only holds unACKed local writes)
     std::map<uint32_t, CellTile> root;  // keyHi -> level-0 tile
+    uint32_t root_len = 1;
+    // a matrix loaded from a summary starts from its SparseArray2D (SparseArray2D.load keeps every
+    // tile); a loaded cell is cleared when a zamboni of the replay freed its row or col handle
+    auto mi = e->mx_init.find(rows_doc);
+    if (mi != e->mx_init.end()) {
+        root_len = mi->second.root_len;
+        for (const auto& t : mi->second.tiles) {
+            CellTile* x = &root[t[0]];
+            for (uint32_t dd = 0; dd < t[1]; dd++) x = x->at((t[2] >> (16 - 8 * dd)) & 0xFFu);
+        }
+        for (const auto& c : mi->second.cells) {
+            const uint32_t rh = c[0], ch = c[1];
+            const uint32_t hi = morton2x16(rh >> 16, ch >> 16), lo = morton2x16(rh, ch);
+            CellTile* t = root[hi].at(lo >> 24)->at((lo >> 16) & 0xFFu)->at((lo >> 8) & 0xFFu);
+            const bool gone = (rh < freed[0].size() && freed[0][rh]) || (ch < freed[1].size() && freed[1][ch]);
+            t->val[lo & 0xFFu] = gone ? NONE : c[2];
+        }
+    }
     auto it = e->cell_recs.find(rows_doc);
     if (it != e->cell_recs.end() && e->n_cells) {
         std::vector<uint32_t> h(2 * e->n_cells);
@@ -1967,10 +2033,10 @@ int mte_snapshot_matrix(mte_engine* e, uint32_t rows_doc, uint32_t cols_doc, cha
         }
     }
     std::string cells = "[[";
-    if (root.empty()) {
+    if (root.empty() && root_len <= 1) {
         cells += "null";
     } else {
-        const uint32_t top = root.rbegin()->first;
+        const uint32_t top = std::max<uint32_t>(root.empty() ? 0u : root.rbegin()->first, root_len - 1);
         if (top > (1u << 20)) return set_err(e, MTE_E_UNSUPPORTED, "cell handles beyond 2^26");
         for (uint32_t k = 0; k <= top; k++) {
             if (k) cells += ',';
@@ -2895,6 +2961,17 @@ int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* t
 static int load_spec(mte_builder* b, DocBuild& db, const json::Value& seg, mte_op& o, std::u16string* mkid = nullptr,
                      bool* hasId = nullptr) {
     const json::Value* props = nullptr;
+    if (db.perm) {  // PermutationSegment.fromJSONObject (permutationvector.ts:41-44): [length, start]
+        if (seg.kind != json::Value::Array || seg.items.empty() || seg.items[0].kind != json::Value::Number ||
+            seg.items[0].num < 0 || seg.items[0].num > 0x7FFFFFFF)
+            return db.fail(MTE_E_UNSUPPORTED, "not a PermutationSegment spec");
+        const double st = seg.items.size() > 1 && seg.items[1].kind == json::Value::Number ? seg.items[1].num : -2147483648.0;
+        if (st >= 1 && (st > 0x7FFFFFFF || st != (double)(int32_t)st)) return db.fail(MTE_E_UNSUPPORTED, "start handle");
+        o.b = (uint32_t)seg.items[0].num;
+        o.a = st >= 1 ? (int32_t)st : 0;  // a loaded run keeps its handles (no onDelta reset on load)
+        o.flags |= MTE_F_PERM;
+        return MTE_OK;
+    }
     if (seg.kind == json::Value::String) {
         o.a = (int32_t)db.payload.size();
         o.b = (uint32_t)seg.str.size();
@@ -3284,7 +3361,7 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
             o.type = MTE_OP_LOAD_APPEND;
             o.client = (uint8_t)client;
             o.seq = seq;
-            o.flags = (uint16_t)(o.flags & (MTE_F_LOAD_MARKER | MTE_F_LOAD_REMOVED));
+            o.flags = (uint16_t)(o.flags & (MTE_F_LOAD_MARKER | MTE_F_LOAD_REMOVED | MTE_F_PERM));
             if (firstOfCall) o.flags |= MTE_F_APPEND_FIRST;
             if (linked[i]) o.flags |= MTE_F_APPEND_REPEAT;
             else tag_body(i, o);  // a repeat is the same object: mapped already
@@ -3579,25 +3656,10 @@ const char* mte_builder_doc_path(const mte_builder* b, uint32_t doc) {
 
 // SharedMatrix.processCore (matrix.ts:548-560): rows then cols, each PermutationVector fed the
 // messages that target it; a cell op (no target) becomes an MTE_OP_CELL record in both, in message order.
-int mte_builder_add_matrix_log(mte_builder* b, const char* observer_name, const char* text, size_t len) {
-    if (!b || !text) return MTE_E_ARG;
-    json::Value log;
-    try {
-        log = json::parse(text, len);
-    } catch (std::exception& ex) {
-        b->err = ex.what();
-        return MTE_E_PARSE;
-    }
-    if (log.kind != json::Value::Array) {
-        b->err = "matrix log must be a JSON array of messages";
-        return MTE_E_PARSE;
-    }
-    std::vector<std::unique_ptr<DocBuild>> dbs;
-    for (int i = 0; i < 2; i++) {
-        dbs.emplace_back(new DocBuild(observer_name));
-        dbs.back()->perm = true;
-    }
-    uint32_t cells = b->n_cells;
+// SharedMatrix.processCore (matrix.ts:548-560) of a message log into the rows / cols documents: the
+// messages that target a vector go to it; a cell op (no target) becomes an MTE_OP_CELL record in both,
+// in message order.
+static int matrix_messages(mte_builder* b, const json::Value& log, DocBuild* dbs[2], uint32_t& cells) {
     auto fail = [&](int code, const std::string& m) {
         b->err = m;
         return code;
@@ -3654,6 +3716,165 @@ int mte_builder_add_matrix_log(mte_builder* b, const char* observer_name, const 
             db.ops.push_back(o);
         }
         cells++;
+    }
+    return MTE_OK;
+}
+
+int mte_builder_add_matrix_log(mte_builder* b, const char* observer_name, const char* text, size_t len) {
+    if (!b || !text) return MTE_E_ARG;
+    json::Value log;
+    try {
+        log = json::parse(text, len);
+    } catch (std::exception& ex) {
+        b->err = ex.what();
+        return MTE_E_PARSE;
+    }
+    if (log.kind != json::Value::Array) {
+        b->err = "matrix log must be a JSON array of messages";
+        return MTE_E_PARSE;
+    }
+    std::vector<std::unique_ptr<DocBuild>> dbs;
+    for (int i = 0; i < 2; i++) {
+        dbs.emplace_back(new DocBuild(observer_name));
+        dbs.back()->perm = true;
+    }
+    uint32_t cells = b->n_cells;
+    DocBuild* two[2] = {dbs[0].get(), dbs[1].get()};
+    if (int rc = matrix_messages(b, log, two, cells)) return rc;
+    for (int i = 0; i < 2; i++) {
+        dbs[i]->commit(b->hb);
+        b->paths.emplace_back(i ? "cols" : "rows");
+    }
+    b->n_cells = cells;
+    return MTE_OK;
+}
+
+// de-interleave a 32-bit Morton key into its odd (row) and even (col) 16-bit halves
+static void unmorton(uint32_t k, uint32_t* r, uint32_t* c) {
+    uint32_t rr = 0, cc = 0;
+    for (int i = 0; i < 16; i++) {
+        cc |= ((k >> (2 * i)) & 1u) << i;
+        rr |= ((k >> (2 * i + 1)) & 1u) << i;
+    }
+    *r = rr;
+    *c = cc;
+}
+
+// SharedMatrix.loadCore (matrix.ts:528-546) + processCore of the suffix (include/mte.h).
+int mte_builder_add_matrix_from_summary(mte_builder* b, const char* observer_name, const char* summary,
+                                        size_t summary_len, const char* ops, size_t ops_len) {
+    if (!b || !summary) return MTE_E_ARG;
+    json::Value s, log;
+    try {
+        s = json::parse(summary, summary_len);
+        if (ops) log = json::parse(ops, ops_len);
+    } catch (std::exception& ex) {
+        b->err = ex.what();
+        return MTE_E_PARSE;
+    }
+    if (ops && log.kind != json::Value::Array) {
+        b->err = "matrix log must be a JSON array of messages";
+        return MTE_E_PARSE;
+    }
+    auto fail = [&](int code, const std::string& m) {
+        b->err = m;
+        return code;
+    };
+    std::vector<std::unique_ptr<DocBuild>> dbs;
+    const char16_t* paths[2] = {u"rows", u"cols"};
+    for (int i = 0; i < 2; i++) {
+        dbs.emplace_back(new DocBuild(observer_name));
+        DocBuild& db = *dbs.back();
+        db.perm = true;
+        // PermutationVector.load (permutationvector.ts:284-294): the handle table, then the segments
+        const json::Value* e = tree_entry(s, paths[i]);
+        const json::Value* vt = e ? e->get(u"value") : nullptr;
+        if (!vt) return fail(MTE_E_PARSE, "matrix summary without its rows / cols tree");
+        const json::Value* he = tree_entry(*vt, u"handleTable");
+        const json::Value* se = tree_entry(*vt, u"segments");
+        std::string ht;
+        if (!he || !se || !se->get(u"value")) return fail(MTE_E_PARSE, "vector summary entries");
+        if (int rc = blob_text(db, he->get(u"value"), ht, "handleTable blob missing")) return fail(rc, db.err);
+        json::Value hv;
+        try {
+            hv = json::parse(ht.data(), ht.size());
+        } catch (std::exception& ex) {
+            return fail(MTE_E_PARSE, ex.what());
+        }
+        if (hv.kind != json::Value::Array || hv.items.empty()) return fail(MTE_E_PARSE, "handleTable is not an array");
+        if (int rc = add_summary(b, *se->get(u"value"), db)) return fail(rc, db.err);
+        for (size_t h = 0; h < hv.items.size(); h++) {
+            const json::Value& x = hv.items[h];
+            if (x.kind != json::Value::Number || x.num < 0 || x.num > 0x7FFFFFFF) return fail(MTE_E_UNSUPPORTED, "handle value");
+            mte_op o{};
+            o.type = MTE_OP_NOOP;
+            o.flags = MTE_F_MX_HANDLE;
+            o.pos1 = (int32_t)h;
+            o.a = (int32_t)x.num;
+            db.ops.push_back(o);
+        }
+    }
+    // SparseArray2D.load (sparsearray2d.ts:232-235) of [cells, pending][0]: every tile and cell
+    const json::Value* ce = tree_entry(s, u"cells");
+    std::string ct;
+    if (!ce) return fail(MTE_E_PARSE, "cells blob missing");
+    if (int rc = blob_text(*dbs[0], ce->get(u"value"), ct, "cells blob missing")) return fail(rc, dbs[0]->err);
+    json::Value cv;
+    try {
+        cv = json::parse(ct.data(), ct.size());
+    } catch (std::exception& ex) {
+        return fail(MTE_E_PARSE, ex.what());
+    }
+    if (cv.kind != json::Value::Array || cv.items.empty() || cv.items[0].kind != json::Value::Array)
+        return fail(MTE_E_PARSE, "cells blob is not [cells, pending]");
+    DocBuild& rows = *dbs[0];
+    std::function<int(const json::Value&, uint32_t, uint32_t, uint32_t)> tile = [&](const json::Value& a, uint32_t hi,
+                                                                                  uint32_t depth, uint32_t pre) -> int {
+        if (a.kind != json::Value::Array || a.items.size() > 256) return fail(MTE_E_PARSE, "cells tile");
+        mte_op t{};
+        t.type = MTE_OP_NOOP;
+        t.flags = MTE_F_MX_TILE;
+        t.pos1 = (int32_t)hi;
+        t.a = (int32_t)pre;
+        t.b = depth;
+        rows.ops.push_back(t);
+        for (uint32_t i = 0; i < a.items.size(); i++) {
+            const json::Value& x = a.items[i];
+            if (x.kind == json::Value::Null) continue;
+            if (depth < 3) {
+                if (int rc = tile(x, hi, depth + 1, pre | (i << (16 - 8 * depth)))) return rc;
+                continue;
+            }
+            const uint32_t lo = (pre << 8) | i;  // the low key's bytes 0..3
+            uint32_t rh, ch, rl, cl;
+            unmorton(hi, &rh, &ch);
+            unmorton(lo, &rl, &cl);
+            mte_op o{};
+            o.type = MTE_OP_NOOP;
+            o.flags = MTE_F_MX_CELL;
+            o.pos1 = (int32_t)((rh << 16) | rl);
+            o.a = (int32_t)((ch << 16) | cl);
+            o.props = b->in->val(json::stringify(x));
+            rows.ops.push_back(o);
+        }
+        return MTE_OK;
+    };
+    const json::Value& root = cv.items[0];
+    for (uint32_t k = 0; k < root.items.size(); k++)
+        if (root.items[k].kind != json::Value::Null)
+            if (int rc = tile(root.items[k], k, 0, 0)) return rc;
+    if (root.items.size() > 1) {  // the root's length (trailing undefined entries included)
+        mte_op t{};
+        t.type = MTE_OP_NOOP;
+        t.flags = MTE_F_MX_TILE;
+        t.pos1 = (int32_t)root.items.size() - 1;
+        t.b = 4;  // (no tile: only the root's extent)
+        rows.ops.push_back(t);
+    }
+    uint32_t cells = b->n_cells;
+    if (ops) {
+        DocBuild* two[2] = {dbs[0].get(), dbs[1].get()};
+        if (int rc = matrix_messages(b, log, two, cells)) return rc;
     }
     for (int i = 0; i < 2; i++) {
         dbs[i]->commit(b->hb);

@@ -103,7 +103,7 @@ EXPORTS = ["mte_abi_version", "mte_build_info", "mte_create", "mte_destroy", "mt
            "mte_replay", "mte_generate", "mte_generate_ids", "mte_export_batch", "mte_doc_status", "mte_text", "mte_length", "mte_segments",
            "mte_snapshot_v1", "mte_snapshot_legacy", "mte_snapshot_shared_string", "mte_summaries", "mte_rccl_unique_id",
            "mte_rccl_comm_create", "mte_rccl_comm_destroy", "mte_gather_summaries", "mte_gather_summaries_alloc", "mte_free", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
-           "mte_builder_add_matrix_log", "mte_snapshot_matrix",
+           "mte_builder_add_matrix_log", "mte_builder_add_matrix_from_summary", "mte_snapshot_matrix",
            "mte_builder_batch",
            "mte_builder_error", "mte_builder_destroy"]
 
@@ -159,6 +159,7 @@ def lib():
         L.mte_builder_add_doc_from_summary.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, sz]
         L.mte_builder_add_container_log.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_uint32)]
         L.mte_builder_add_matrix_log.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
+        L.mte_builder_add_matrix_from_summary.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, sz]
         L.mte_snapshot_matrix.argtypes = [vp, u32, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.mte_builder_doc_path.argtypes = [vp, ctypes.c_uint32]
         L.mte_builder_doc_path.restype = ctypes.c_char_p
@@ -229,6 +230,20 @@ class Builder:
         rc = lib().mte_builder_add_matrix_log(self._h, observer.encode(), t, len(t))
         if rc:
             raise MteError(f"mte_builder_add_matrix_log: {rc}: {lib().mte_builder_error(self._h).decode()}")
+        n = self.n_docs()
+        return n - 2, n - 1
+
+    def add_matrix_from_summary(self, summary, messages=None, observer="readonly"):
+        """SharedMatrix.loadCore (matrix.ts:528-546) from a summary ITree, then its message suffix:
+        two documents, rows then cols. Returns their indices (rows, cols)."""
+        def enc(x):
+            t = x if isinstance(x, (str, bytes)) else json.dumps(x, separators=(",", ":"), ensure_ascii=False)
+            return t.encode() if isinstance(t, str) else t
+        s = enc(summary)
+        m = enc(messages) if messages is not None else None
+        rc = lib().mte_builder_add_matrix_from_summary(self._h, observer.encode(), s, len(s), m, len(m) if m else 0)
+        if rc:
+            raise MteError(f"mte_builder_add_matrix_from_summary: {rc}: {lib().mte_builder_error(self._h).decode()}")
         n = self.n_docs()
         return n - 2, n - 1
 

@@ -133,6 +133,19 @@ enum {
 #define MTE_F_PERM 0x1000u        /* INSERT: a PermutationSegment of a SharedMatrix row / col vector
                                      (permutationvector.ts:37-127): b = length, no text, handles unallocated */
 #define MTE_F_CELL_COL 0x2000u    /* CELL: the record of the cols vector (else rows) */
+/* SharedMatrix summary state (mte_builder_add_matrix_from_summary), NOOP records (no merge-tree op,
+ * no seq / msn movement) after a vector's load records, read by the host only:
+ *   MX_HANDLE: HandleTable.load (handletable.ts:84-86): handles[pos1] = a (both vectors);
+ *   MX_CELL:   SparseArray2D.load (sparsearray2d.ts:232-235): cell (row handle pos1, col handle a) =
+ *              value id props (the rows document);
+ *   MX_TILE:   a tile the loaded SparseArray2D holds: key hi pos1, depth b (0..3), the first `depth`
+ *              bytes of the low key in a (bits 16..23, 8..15, 0..7) (the rows document).
+ * A LOAD_SEG / LOAD_APPEND with MTE_F_PERM is a loaded PermutationSegment ([length, start]): b =
+ * length, a = its start handle (0 = Handle.unallocated), kept as loaded. */
+#define MTE_F_MX_HANDLE 0x4000u
+#define MTE_F_MX_CELL 0x8000u
+#define MTE_F_MX_TILE 0xC000u
+#define MTE_F_MX_MASK 0xC000u
 #define MTE_F_CATCHUP 0x800u      /* op of a catch-up message the legacy summary rewrites (refSeq != seq - 1,
                                      sequence.ts:603-625): the engine records its delta ranges */
 
@@ -350,6 +363,15 @@ const char* mte_builder_doc_path(const mte_builder* b, uint32_t doc);
  * (processCore's remote branch, matrix.ts:575-601); its row / col must be integers >= 0
  * (MTE_E_UNSUPPORTED otherwise). */
 int mte_builder_add_matrix_log(mte_builder* b, const char* observer_name, const char* json, size_t len);
+/* SharedMatrix.loadCore (matrix.ts:528-546) then processCore of a message suffix: the summary ITree
+ * (snapshotCore, matrix.ts:405-433: "rows" / "cols" PermutationVector trees -- SnapshotV1 "segments"
+ * and the "handleTable" blob, permutationvector.ts:269-294 -- and the "cells" blob [cells, pending])
+ * becomes the rows and the cols document (LOAD records of PermutationSegment runs with their start
+ * handles, the HandleTables and the cells as MTE_F_MX_* records), then `ops` (a JSON array of
+ * messages, may be NULL) as in mte_builder_add_matrix_log. mte_snapshot_matrix of the pair is the
+ * matrix's summary after the suffix. */
+int mte_builder_add_matrix_from_summary(mte_builder* b, const char* observer_name, const char* summary,
+                                        size_t summary_len, const char* ops, size_t ops_len);
 int mte_builder_batch(mte_builder* b, mte_batch* out);   /* view valid until destroy */
 const char* mte_builder_error(const mte_builder* b);
 void mte_builder_destroy(mte_builder* b);

@@ -64,6 +64,7 @@ def lib():
         L.orc_matrix_apply_json.argtypes = [vp, cp, ctypes.c_size_t]
         L.orc_matrix_vector.restype = vp
         L.orc_matrix_vector.argtypes = [vp, i32]
+        L.orc_matrix_load_summary.argtypes = [vp, cp, ctypes.c_size_t]
         L.orc_matrix_snapshot_json.restype = vp
         L.orc_matrix_snapshot_json.argtypes = [vp, u32]
         L.orc_replay_batch.restype = u64
@@ -201,6 +202,11 @@ class OracleMatrix:
     def apply_json(self, text):
         b = text.encode() if isinstance(text, str) else text
         return lib().orc_matrix_apply_json(self._h, b, len(b))
+
+    def load_summary(self, text):
+        """SharedMatrix.loadCore (matrix.ts:528-546) from a summary ITree JSON (a fresh matrix)."""
+        b = text.encode() if isinstance(text, str) else text
+        return lib().orc_matrix_load_summary(self._h, b, len(b))
 
     def snapshot_json(self, chunk=10000):
         """SharedMatrix.snapshotCore (matrix.ts:405-433) ITree JSON."""

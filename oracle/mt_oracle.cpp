@@ -1260,15 +1260,23 @@ class Doc {
     // ---- resume from a summary (SnapshotLoader, snapshotLoader.ts) ----------------------------
     // specToSegment (snapshotLoader.ts:79-111): merge info (hasMergeInfo, snapshotChunks.ts:71-73)
     // carries client / seq / removedSeq / removedClient; a bare spec is universal and NonCollab.
+    // A PermutationSegment keeps its start handle when loaded (PermutationSegment.fromJSONObject,
+    // permutationvector.ts:41-44; loading inserts with no op args, so onDelta's reset, :302-309, does
+    // not run); Handle.unallocated stays unallocated.
+    Segment* loadSegment(const JV& spec) {
+        Segment* s = makeSegment(spec);
+        if (permutation && spec.a.size() > 1 && spec.a[1] && spec.a[1]->t == JV::Num) s->start = (int)spec.a[1]->n;
+        return s;
+    }
     Segment* loadSpec(const JV& spec) {
         JVP json = spec.t == JV::Obj ? spec.o.get(u"json") : nullptr;
         if (!json) {
-            Segment* s = makeSegment(spec);
+            Segment* s = loadSegment(spec);
             s->seq = UniversalSequenceNumber;
             s->clientId = NonCollabClient;
             return s;
         }
-        Segment* s = makeSegment(*json);
+        Segment* s = loadSegment(*json);
         JVP c = spec.o.get(u"client"), sq = spec.o.get(u"seq"), rs = spec.o.get(u"removedSeq"),
             rc = spec.o.get(u"removedClient");
         s->clientId = c && c->t == JV::Str ? getOrAddShortClientId(u16_to_utf8(c->s)) : NonCollabClient;
@@ -2170,6 +2178,65 @@ struct Matrix {
             error = e.what();
         }
     }
+    // SharedMatrix.loadCore (matrix.ts:528-546): each PermutationVector.load (permutationvector.ts:
+    // 284-294: HandleTable.load of the "handleTable" blob, then the merge-tree summary under "segments"),
+    // then SparseArray2D.load of the cells blob's first element (sparsearray2d.ts:232-235:
+    // nullToUndefined, so every tile of the snapshot exists again, emptied where it held null);
+    // `pending` holds only unACKed local writes, none for an observer.
+    void loadTile(std::unique_ptr<Tile>& t, const JV& a, int depth) {
+        t.reset(new Tile());
+        for (size_t i = 0; i < a.a.size() && i < 256; i++) {
+            const JVP& x = a.a[i];
+            if (!x || x->t == JV::Null) continue;
+            if (depth < 3) {
+                if (x->t != JV::Arr) throw EngineError(MTE_DOC_UNSUPPORTED, "cells tile is not an array");
+                loadTile(t->sub[i], *x, depth + 1);
+            } else {
+                t->val[i] = x;
+                t->has[i] = true;
+            }
+        }
+    }
+    void loadSummary(const JV& tree) {
+        try {
+            Doc* vs[2] = {&rows, &cols};
+            const char16_t* paths[2] = {u"rows", u"cols"};
+            for (int i = 0; i < 2; i++) {
+                JVP e = Doc::treeEntry(tree, paths[i]);
+                JVP vt = e && e->t == JV::Obj ? e->o.get(u"value") : nullptr;
+                if (!vt) throw EngineError(MTE_DOC_UNSUPPORTED, "matrix summary without a vector");
+                JVP he = Doc::treeEntry(*vt, u"handleTable");
+                const std::string ht = Doc::blobText(he ? he->o.get(u"value") : nullptr, "handleTable blob missing");
+                JVP hv = parse(ht.data(), ht.size());
+                if (hv->t != JV::Arr || hv->a.empty()) throw EngineError(MTE_DOC_UNSUPPORTED, "handleTable is not an array");
+                vs[i]->handles.clear();
+                for (auto& h : hv->a) vs[i]->handles.push_back(h && h->t == JV::Num ? (int)h->n : 0);
+                JVP se = Doc::treeEntry(*vt, u"segments");
+                JVP st = se && se->t == JV::Obj ? se->o.get(u"value") : nullptr;
+                if (!st) throw EngineError(MTE_DOC_UNSUPPORTED, "vector summary without segments");
+                vs[i]->loadSnapshot(*st);
+                if (vs[i]->status) {
+                    status = vs[i]->status;
+                    error = vs[i]->error;
+                    return;
+                }
+            }
+            JVP ce = Doc::treeEntry(tree, u"cells");
+            const std::string ct = Doc::blobText(ce ? ce->o.get(u"value") : nullptr, "cells blob missing");
+            JVP cv = parse(ct.data(), ct.size());
+            if (cv->t != JV::Arr || cv->a.empty() || !cv->a[0] || cv->a[0]->t != JV::Arr)
+                throw EngineError(MTE_DOC_UNSUPPORTED, "cells blob is not [cells, pending]");
+            const JV& r = *cv->a[0];
+            root.clear();
+            root.resize(std::max<size_t>(1, r.a.size()));
+            rootLen = std::max<size_t>(1, r.a.size());
+            for (size_t k = 0; k < r.a.size(); k++)
+                if (r.a[k] && r.a[k]->t == JV::Arr) loadTile(root[k], *r.a[k], 0);
+        } catch (EngineError& e) {
+            status = e.code;
+            error = e.what();
+        }
+    }
     std::string cellsJson() {  // JSON.stringify([cells.snapshot(), pending.snapshot()])
         std::string o = "[[";
         std::function<void(const Tile*, int)> tile = [&](const Tile* t, int depth) {
@@ -2277,6 +2344,17 @@ int orc_matrix_apply_json(Matrix* m, const char* json, size_t len) {
     return m->status;
 }
 Doc* orc_matrix_vector(Matrix* m, int which) { return which ? &m->cols : &m->rows; }
+// SharedMatrix.loadCore (matrix.ts:528-546) from its summary ITree JSON; the matrix must be fresh
+int orc_matrix_load_summary(Matrix* m, const char* json, size_t len) {
+    try {
+        orc::JVP v = orc::parse(json, len);
+        m->loadSummary(*v);
+    } catch (std::exception& e) {
+        m->status = MTE_DOC_UNSUPPORTED;
+        m->error = e.what();
+    }
+    return m->status;
+}
 char* orc_matrix_snapshot_json(Matrix* m, uint32_t chunk) { return dupstr(m->tree(chunk)); }
 
 // Resume from a summary ITree JSON (SnapshotLoader); the doc must be fresh (observer set).

@@ -10,7 +10,8 @@ export interface DocSummary {
 }
 /** summary: a SnapshotV1 ITree to resume from (SnapshotLoader); messages then are the catch-up suffix. */
 export interface DocLog { observer?: string; messages?: ISequencedDocumentMessage[]; summary?: ITree | string;
-    /** SharedMatrix messages: this entry loads as two documents, the rows then the cols vector */
+    /** SharedMatrix messages: this entry loads as two documents, the rows then the cols vector; with
+     *  `summary` (a SharedMatrix summary ITree, SharedMatrix.loadCore) they are the suffix after it */
     matrix?: ISequencedDocumentMessage[]; }
 
 export declare class BatchedMergeEngine {

@@ -29,7 +29,10 @@ class BatchedMergeEngine {
         const b = addon.createBuilder();
         for (const d of docs) {
             const obs = d.observer === undefined ? "__observer__" : d.observer;
-            if (d.matrix !== undefined) {  // SharedMatrix messages: two documents, rows then cols
+            if (d.matrix !== undefined && d.summary !== undefined) {  // SharedMatrix summary + suffix
+                const s = typeof d.summary === "string" ? d.summary : JSON.stringify(d.summary);
+                addon.builderAddMatrixFromSummary(b, obs, s, JSON.stringify(d.matrix));
+            } else if (d.matrix !== undefined) {  // SharedMatrix messages: two documents, rows then cols
                 addon.builderAddMatrixLog(b, obs, JSON.stringify(d.matrix));
             } else if (d.summary !== undefined) {
                 const s = typeof d.summary === "string" ? d.summary : JSON.stringify(d.summary);
@@ -178,6 +181,7 @@ module.exports = {
     createBuilder: addon.createBuilder, builderAddDoc: addon.builderAddDoc, builderDocCount: addon.builderDocCount,
     builderAddDocFromSummary: addon.builderAddDocFromSummary, builderAddContainerLog: addon.builderAddContainerLog,
     builderAddMatrixLog: addon.builderAddMatrixLog,
+    builderAddMatrixFromSummary: addon.builderAddMatrixFromSummary,
     /** rank 0: the RCCL id (Buffer) to send to every rank; rcclCommDestroy(comm) releases a communicator */
     rcclUniqueId: addon.rcclUniqueId, rcclCommDestroy: addon.rcclCommDestroy,
     /** low level: (engine handle, rank, world, comm) -> Buffer of 32-byte records */

@@ -206,6 +206,30 @@ static napi_value js_builder_add_matrix_log(napi_env env, napi_callback_info inf
     return NULL;
 }
 
+/* builderAddMatrixFromSummary(builder, observerName, summaryJson, messagesJson | null): void — a
+ * SharedMatrix loaded from its summary (loadCore, matrix.ts:528-546) then its message suffix: two
+ * documents, rows then cols */
+static napi_value js_builder_add_matrix_from_summary(napi_env env, napi_callback_info info) {
+    napi_value argv[4];
+    if (!get_args(env, info, 4, argv)) {
+        napi_throw_type_error(env, NULL, "builderAddMatrixFromSummary(builder, observer, summary, messages)");
+        return NULL;
+    }
+    mte_builder* b = (mte_builder*)get_external(env, argv[0]);
+    size_t slen = 0, mlen = 0;
+    napi_valuetype t;
+    char* obs = get_string(env, argv[1], NULL);
+    char* summ = get_string(env, argv[2], &slen);
+    char* msgs = NULL;
+    if (napi_typeof(env, argv[3], &t) == napi_ok && t == napi_string) msgs = get_string(env, argv[3], &mlen);
+    int rc = (b && obs && summ) ? mte_builder_add_matrix_from_summary(b, obs, summ, slen, msgs, mlen) : MTE_E_ARG;
+    free(obs);
+    free(summ);
+    free(msgs);
+    if (rc) return throw_mte(env, "mte_builder_add_matrix_from_summary", rc, b ? mte_builder_error(b) : NULL);
+    return NULL;
+}
+
 /* snapshotMatrix(engine, rowsDoc, colsDoc): string — SharedMatrix.snapshotCore (matrix.ts:405-430) */
 static napi_value js_snapshot_matrix(napi_env env, napi_callback_info info) {
     napi_value argv[3];
@@ -571,6 +595,7 @@ static napi_value init(napi_env env, napi_value exports) {
         {"builderAddDocFromSummary", 0, js_builder_add_doc_from_summary, 0, 0, 0, napi_default, 0},
         {"builderAddContainerLog", 0, js_builder_add_container_log, 0, 0, 0, napi_default, 0},
         {"builderAddMatrixLog", 0, js_builder_add_matrix_log, 0, 0, 0, napi_default, 0},
+        {"builderAddMatrixFromSummary", 0, js_builder_add_matrix_from_summary, 0, 0, 0, napi_default, 0},
         {"snapshotMatrix", 0, js_snapshot_matrix, 0, 0, 0, napi_default, 0},
         {"builderDocCount", 0, js_builder_doc_count, 0, 0, 0, napi_default, 0},
         {"load", 0, js_load, 0, 0, 0, napi_default, 0},

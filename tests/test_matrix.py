@@ -272,3 +272,94 @@ def test_gpu_matrix_cells_match_oracle():
     finally:
         e.close()
     assert recycled > 0  # some handle went back to a free list
+
+
+def matrix_cuts():
+    """(log, cut, summary at the cut): the oracle's SharedMatrix summary of log[:cut] (its vectors'
+    SnapshotV1 with handle runs, their HandleTables with recycled handles, the cells SparseArray2D)."""
+    out = []
+    for seed, total, cuts, kw in ((1, 600, (150, 420), {}), (2, 600, (300, 600), {}),
+                                  (40, 3000, (1200, 2600), {"p_rem": 0.6, "seg_max": 4}),
+                                  (41, 1500, (700,), {"p_set": 0.7})):
+        log = matrix_cell_log(seed, total=total, **kw)
+        for k in cuts:
+            out.append((log, k, oracle_matrix(log[:k]).snapshot_json()))
+    return out
+
+
+def oracle_resumed(summary, suffix):
+    o = OracleMatrix("obs")
+    assert o.load_summary(summary) == 0
+    assert o.apply_json(dumps(suffix)) == 0
+    return o
+
+
+def test_oracle_matrix_resumes_from_summary():
+    """SharedMatrix.loadCore (matrix.ts:528-546) + the message suffix on the oracle: every cell the
+    matrix shows (SharedMatrix.getCell over the vectors' visible handles) equals the full replay's."""
+    from tests.test_matrix_spec import grid
+
+    for log, k, summ in matrix_cuts():
+        full = json.loads(oracle_matrix(log).snapshot_json())
+        got = json.loads(oracle_resumed(summ, log[k:]).snapshot_json())
+        assert grid(got) == grid(full), k
+
+
+def test_builder_matrix_summary_records():
+    """mte_builder_add_matrix_from_summary: PermutationSegment runs load with their start handles
+    (LOAD_SEG, MTE_F_PERM: b = length, a = start, 0 = unallocated), each vector's HandleTable and the
+    rows document's cells / tiles as MTE_F_MX_* records, then the suffix as mte_builder_add_matrix_log
+    writes it."""
+    import numpy as np
+
+    log, k, summ = matrix_cuts()[1]
+    b = mte.Builder()
+    ri, ci = b.add_matrix_from_summary(summ, log[k:], observer="obs")
+    batch = b.batch()
+    ops = mte.batch_ops(batch)
+    offs = np.ctypeslib.as_array(batch.doc_op_offsets, shape=(3,))
+    ents = {e["path"]: e["value"] for e in json.loads(summ)["entries"]}
+    for d, path in ((ri, "rows"), (ci, "cols")):
+        recs = ops[offs[d]:offs[d + 1]]
+        segs = json.loads(ents[path]["entries"][0]["value"]["entries"][0]["value"]["contents"])["segments"]
+        specs = [s["json"] if isinstance(s, dict) else s for s in segs]
+        load = recs[(recs["type"] == 5) | (recs["type"] == 8)]  # LOAD_SEG / LOAD_APPEND
+        assert [(int(r["b"]), int(r["a"])) for r in load[:len(specs)]] == \
+            [(n, 0 if st == UNALLOC else st) for n, st in specs]
+        assert all(f & 0x1000 for f in load["flags"])  # MTE_F_PERM
+        ht = recs[(recs["type"] == 4) & ((recs["flags"] & 0xC000) == 0x4000)]
+        assert list(ht["a"]) == json.loads(ents[path]["entries"][1]["value"]["contents"])
+    rrec = ops[offs[ri]:offs[ri + 1]]
+    cells = rrec[(rrec["type"] == 4) & ((rrec["flags"] & 0xC000) == 0x8000)]
+    root = json.loads(ents["cells"]["contents"])[0]
+
+    def count(x, depth):
+        if x is None:
+            return 0
+        return sum(count(y, depth + 1) for y in x) if depth < 4 else 1
+
+    assert len(cells) == sum(count(t, 0) for t in root)
+
+
+@pytest.mark.gpu
+def test_gpu_matrix_resumes_from_summary():
+    """A SharedMatrix resumed from its summary (the rows / cols PermutationSegment runs with their
+    handles, both HandleTables, the cells) plus the message suffix on the GPU: the matrix summary
+    equals the oracle's resumed one byte for byte, and every cell it shows equals the full replay's."""
+    from tests.test_matrix_spec import grid
+
+    cuts = matrix_cuts()
+    b = mte.Builder()
+    pairs = [b.add_matrix_from_summary(summ, log[k:], observer="obs") for log, k, summ in cuts]
+    e = mte.Engine(0)
+    try:
+        e.load(b.batch())
+        st = e.replay()
+        assert st["failed_docs"] == 0
+        for (log, k, summ), (ri, ci) in zip(cuts, pairs):
+            want = json.loads(oracle_resumed(summ, log[k:]).snapshot_json())
+            got = json.loads(e.snapshot_matrix(ri, ci))
+            assert got == want, k
+            assert grid(got) == grid(json.loads(oracle_matrix(log).snapshot_json())), k
+    finally:
+        e.close()

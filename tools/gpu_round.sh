@@ -2,7 +2,7 @@
 # GPU box: one round of measurements, steps chosen on the command line, results under gpurun_out/<tag>/.
 # Stops at the first step that crashes or hits its time limit (no GPU step runs after a failure).
 # Usage: bash tools/gpu_round.sh <tag> <step>...
-#   suite[:pytest args]   the -m gpu parity suite in one process   -> <tag>/gpu_tests.log
+#   suite[:<-k expr>]     the -m gpu parity suite in one process   -> <tag>/gpu_tests.log
 #   smoke                 __graft_entry__.smoke()                  -> <tag>/smoke.log
 #   lone:<lib>[,<lib>..]  lone 10^6-op document A/B over MTE_LIB variants ("cur" = default build)
 #   bench:<spec>[;<spec>] bench.py lines, spec = config:opt[,opt] (tools/r04_bench_ab.sh)
@@ -14,8 +14,8 @@ mkdir -p gpurun_out/$T
 for step in "$@"; do
   case "$step" in
     suite*)
-      args=${step#suite}; args=${args#:}
-      timeout -k 10 ${SUITE_TO:-900} python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread $args \
+      k=${step#suite}; k=${k#:}  # suite:<pytest -k expression>
+      timeout -k 10 ${SUITE_TO:-900} python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread ${k:+-k "$k"} \
         > gpurun_out/$T/gpu_tests.log 2>&1; rc=$?
       grep -E "FAILED|ERROR" gpurun_out/$T/gpu_tests.log | tail -20; tail -1 gpurun_out/$T/gpu_tests.log
       [ $rc -le 1 ] || exit 1 ;;

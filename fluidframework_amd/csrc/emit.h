@@ -18,7 +18,8 @@ struct EmitParams {
     const u32* maps;           // the property map of every row with props (map_words per row), or null
     u32 map_words;
     const u16* text;           // gathered text of every row
-    const u32* esc;            // per row: its text's JSON byte size + flags (engine_types.hpp ESC_*)
+    u32* esc;                  // per row: its text's JSON byte size + flags (engine_types.hpp ESC_*):
+                               // written by COUNT, read by WRITE
     // property text tables (interned JSON texts of keys and values)
     const char* key_text;
     const u64* key_off;

@@ -447,27 +447,80 @@ struct Doc {
     };
     struct Walk {
         const Doc& D;
+        const bool counting;  // COUNT: the emission words are made (and stored for WRITE) here
         u32 n, base, j, tcarry;
         uint4 bv;          // this lane's row of the batch: vis
         u32 be, bay, btof;  // ... its emission word, aux.y (markers / permutation runs), text offset
         bool open, pend, filled;
         Item run, pe;       // the open run, and a merge-info entry queued behind it
         bool runText, runPerm, runNL, runHI;
-        MTE_DEV explicit Walk(const Doc& d)
-            : D(d), n(d.r.n_segs), base(0), j(64), tcarry(0), open(false), pend(false), filled(false) {}
+        MTE_DEV Walk(const Doc& d, bool count)
+            : D(d), counting(count), n(d.r.n_segs), base(0), j(64), tcarry(0), open(false), pend(false), filled(false) {}
         MTE_DEV void fill() {
-            const u32 k = base + lane_id();
+            const u32 L = lane_id(), k = base + L;
             bv = make_uint4(0, 0, 0, 0);
             be = bay = 0;
+            u32 ax = 0;
             if (k < n) {
                 bv = D.p.vis[D.row0 + k];
-                be = D.p.esc[D.row0 + k];
-                if (bv.w & (F_PERM | F_MARKER)) bay = D.p.aux[D.row0 + k].y;
+                if (counting) {
+                    if (bv.w & (F_PERM | F_MARKER)) {
+                        const uint4 a = D.p.aux[D.row0 + k];
+                        bay = a.y;
+                        ax = a.x;
+                    } else if (D.p.maps) {
+                        ax = D.p.aux[D.row0 + k].x;  // (property-carrying batches only)
+                    }
+                } else {
+                    be = D.p.esc[D.row0 + k];
+                    if (bv.w & (F_PERM | F_MARKER)) bay = D.p.aux[D.row0 + k].y;
+                }
             }
             const u32 tl = (bv.w & (F_PERM | F_MARKER)) ? 0u : bv.x;
             const u32 incl = wave_scan_incl(tl);
             btof = tcarry + incl - tl;
             tcarry += wave_read(incl, 63);
+            if (!counting) return;
+            // the emission word of every row of the batch (esc_unit over its text): short rows one
+            // per lane, rows longer than 32 units by the whole wave, 64 units per step
+            const u16* txt = D.p.text + D.r.text_off;
+            u32 tot = 0, first = 0, last = 0;
+            if (tl && tl <= 32) {
+                const u16* src = txt + btof;
+                u32 prev = 0;
+                first = src[0];
+                for (u32 i = 0; i < tl; i++) {
+                    const u32 c = src[i];
+                    tot += (u32)esc_unit(c, prev);
+                    prev = c;
+                }
+                last = prev;
+            }
+            for (u64 lm = wave_ballot(tl > 32); lm; lm &= lm - 1) {
+                const u32 l = (u32)__builtin_ctzll(lm);
+                const u32 ln = wave_read(tl, l);
+                const u16* src = txt + wave_read(btof, l);
+                u32 sum = 0, carry = 0;
+                for (u32 b0 = 0; b0 < ln; b0 += 64) {
+                    const u32 i = b0 + L;
+                    const u32 c = i < ln ? src[i] : 0u;
+                    u32 pv = __builtin_amdgcn_update_dpp(0u, c, 0x138, 0xf, 0xf, false);  // wave_shr:1
+                    if (L == 0) pv = carry;
+                    const u32 u = i < ln ? (u32)esc_unit(c, pv) : 0u;
+                    sum += wave_read(wave_scan_incl(u), 63);
+                    carry = wave_read(c, ln - 1 - b0 < 63 ? ln - 1 - b0 : 63u);
+                }
+                if (L == l) {
+                    tot = sum;
+                    first = src[0];
+                    last = carry;
+                }
+            }
+            be = (ax ? ESC_PROPS : 0u);
+            if (tl)
+                be |= (tot & ESC_LEN) | (esc_is_lo(first) ? ESC_LO : 0u) | (esc_is_hi(last) ? ESC_HI : 0u) |
+                      (last == (u32)'\n' ? ESC_NL : 0u);
+            if (k < n) D.p.esc[D.row0 + k] = be;
         }
         // the next entry into it; false when the document has no more
         MTE_DEV bool next(Item& it) {
@@ -580,7 +633,7 @@ struct Doc {
     // COUNT (SnapshotV1): byte count and blob count; the chunk table into ent[row0 + c]
     MTE_DEV u64 count_v1(u32& ne, u32& nblobs) const {
         const u32 L = lane_id(), chunk = p.chunk;
-        Walk w(*this);
+        Walk w(*this, true);
         Out o{nullptr, 0};
         u32 nch = 0, cnt = 0, first = 0;
         u64 len = 0, totalLen = 0;
@@ -633,7 +686,7 @@ struct Doc {
     // WRITE (SnapshotV1) from the chunk table COUNT wrote
     MTE_DEV u64 write_v1(u32 ne, u32 nch, char* out, u64* blob_off) const {
         const u32 L = lane_id();
-        Walk w(*this);
+        Walk w(*this, false);
         Out o{out, 0};
         u64 totalLen = 0;
         for (u32 c = 0; c < nch; c++) totalLen += p.ent[row0 + c].z;

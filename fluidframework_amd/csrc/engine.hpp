@@ -2579,30 +2579,20 @@ struct Engine {
                 u32 tat = trun + tincl - bt;
                 for (u32 s = 0; s < c; s++) {
                     uint4 v = VIS()[o.x * 8 + s], a = AUX()[o.x * 8 + s];
-                    u32 esc = a.x ? ESC_PROPS : 0u;  // the row's emission word (ESC_*, engine_types.hpp)
                     if (!(v.w & (F_MARKER | F_PERM))) {  // wave-divergent copy, 8 units in flight per lane
                         const u16* __restrict__ src = text_ptr(a.y);
                         u16* __restrict__ dst = tdst + tat;
-                        u32 tot = 0, prevc = 0, firstc = 0;
                         for (u32 i = 0; i < v.x; i += 8) {
                             u16 t[8];
 #pragma unroll
                             for (u32 j = 0; j < 8; j++) t[j] = i + j < v.x ? src[i + j] : (u16)0;
-                            if (i == 0) firstc = t[0];
 #pragma unroll
                             for (u32 j = 0; j < 8; j++)
-                                if (i + j < v.x) {
-                                    dst[i + j] = t[j];
-                                    tot += (u32)esc_unit(t[j], prevc);
-                                    prevc = t[j];
-                                }
+                                if (i + j < v.x) dst[i + j] = t[j];
                         }
-                        esc |= (tot & ESC_LEN) | (esc_is_lo(firstc) ? ESC_LO : 0u) | (esc_is_hi(prevc) ? ESC_HI : 0u) |
-                               (prevc == (u32)'\n' ? ESC_NL : 0u);
                         a.y = tat;  // offset in the document's text run
                         tat += v.x;
                     }
-                    if (p.out_esc) p.out_esc[at + s] = esc;
                     if (a.x && p.out_maps) {  // the row's property map, indexed by row
                         const uint4* ms = (const uint4*)(maps + (u64)a.x * mw);
                         uint4* md = (uint4*)(p.out_maps + (u64)(at + s) * mw);

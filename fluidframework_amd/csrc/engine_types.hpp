@@ -26,7 +26,7 @@ constexpr u32 MAP_WORDS = 16;  // the narrowest map record: [0] = count, then 7 
                                // (Params::map_words = 1 + 2 * keys, rounded up to 4, <= 128)
 constexpr i32 GRANULARITY = 256;                         // TextSegmentGranularity (mergeTree.ts:1059)
 
-// Per output row, the emission's view of its text (Params::out_esc, written by every engine's finish):
+// Per output row, the emission's view of its text (EmitParams::esc, written by k_emit_count for k_emit_write):
 // the bytes JSON.stringify writes for the row's text alone, quotes excluded (UTF-8, '"' '\\' and control
 // characters escaped, an unpaired surrogate as \uXXXX), and the flags the SnapshotV1 writer needs
 // without reading the text or the aux row: the text starts with a low / ends with a high surrogate (a
@@ -248,7 +248,6 @@ struct Params {
     u32* rows_retry;          // k_rows: documents the row pool could not grow, queued to restart once
                               // (doc + 1 per slot; counters[8] pushed, counters[9] popped), or null
     u32 rows_pool_lim;        // test knob: k_rows pool rows usable per CU (0 = all of the pool)
-    u32* out_esc;             // per output row: JSON byte size of its text + flags (ESC_*), or null
 };
 
 constexpr u32 SOLO_CLK_SLOTS = 64;  // solo workgroups with clock stamps (Params::solo_clk)

@@ -569,7 +569,6 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     P.maps = e->d_maps.p;
     P.map_words = e->map_words;
     P.out_vis = e->d_out_vis.p;
-    P.out_esc = e->d_out_esc.p;
     P.out_aux = e->d_out_aux.p;
     P.out_ovl = e->d_out_ovl.p;
     P.out_cap = out;
@@ -1166,9 +1165,9 @@ static int run_kernel(mte_engine* e, bool gen) {
     // CU for long documents, each on a SIMD of its own with fixed rows (C5: 1 024 x 10^6 ops, 4.4 s
     // per step against 9.8 s on k_lds / k_hbmq), else 12 (three per SIMD on the shared row pool; C2
     // 98 ms against 110 at 8 and 166 on the sixteen LDS / HBM waves per CU; C3 1.34 s against 1.87 at
-    // 8 and 2.15 on k_lds / k_hbmq; a document the pool cannot grow restarts inside the pass). A
-    // batch with solo documents keeps k_lds beside them: its pass is the critical path's anyway, and
-    // k_lds continues a document that outgrows LDS in HBM instead of re-running it from its first op.
+    // 8 and 2.15 on k_lds / k_hbmq; a document the pool cannot grow restarts inside the pass), beside
+    // the solo documents too (C4: the same critical path, 4 046 vs 4 047 ms, but none of the 4 100
+    // documents k_lds continued HBM-resident, whose spill and continuation traffic was 15 GB a pass).
     // Property-carrying batches (FULL only for their properties: no '\n', no relative positions, < 32
     // clients) take the same route on the PROPS row engine.
     uint32_t rows = 0;
@@ -1181,7 +1180,7 @@ static int run_kernel(mte_engine* e, bool gen) {
         // (long documents take 4 waves whatever their count: eight of them, ~120 leaf blocks each,
         // would not fit one CU's 79-row pool and spill to HBM re-runs of 10^5+ ops)
         const bool long_docs = bulk_ops >= 200000ull * (nd - n_solo);
-        rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : long_docs ? 4u : n_solo == 0 ? 12u : 0u;
+        rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : long_docs ? 4u : 12u;
     }
     e->last_rows = rows;
     if (rows) groups = hbm_waves = lds_active = 0;

@@ -1220,34 +1220,6 @@ struct RegEngine {
             simd::st(dbase, i + d0, t, m);
         }
     }
-    // JSON byte size of every lane's unit t after pv (esc_unit, engine_types.hpp)
-    SD static V esc_v(V t, V pv) {
-#ifdef MTE_CPU
-        V r;
-        for (u32 l = 0; l < 64; l++) r.x[l] = (u32)esc_unit(t.x[l], pv.x[l]);
-        return r;
-#else
-        return V{(u32)esc_unit(t.x, pv.x)};
-#endif
-    }
-    // copy_text for finish(), also returning the row's emission word (ESC_*, engine_types.hpp)
-    SD u32 copy_text_esc(u32 dst, u32 src, u32 n, u16* dbase) {
-        const u16* sb = (src & ARENA_BIT) ? arena_cur() : payload;
-        const u32 so = src & ~ARENA_BIT, d0 = dst & ~ARENA_BIT;
-        u32 tot = 0, prevc = 0, first = 0;
-        for (u32 b = 0; b < n; b += 64) {
-            const V i = L() + b;
-            const B m = i < n;
-            const V t = simd::ld(sb, i + so, m);
-            simd::st(dbase, i + d0, t, m);
-            const V pv = simd::sel(L() == 0u, prevc, simd::wave_shr1(t));
-            tot += simd::readlane(simd::scan_incl(simd::sel(m, esc_v(t, pv), 0u)), 63);
-            if (b == 0) first = simd::readlane(t, 0);
-            prevc = simd::readlane(t, n - 1 - b < 63 ? n - 1 - b : 63u);
-        }
-        return (tot & ESC_LEN) | (esc_is_lo(first) ? ESC_LO : 0u) | (esc_is_hi(prevc) ? ESC_HI : 0u) |
-               (prevc == (u32)'\n' ? ESC_NL : 0u);
-    }
     // Semispace compaction of the merge arena: every live arena-resident text, document order.
     SD void arena_gc() {
         fence_arena();
@@ -2150,15 +2122,11 @@ struct RegEngine {
                 simd::st(oa, t4 + 3u, w.sid - 1u, have);
                 simd::st(oo, at * 2u, ovl, have);
                 simd::st(oo, at * 2u + 1u, ovh, have);
-                // text, one segment at a time, 64 units per step, with each row's emission word
-                V esc = simd::splat(0);
-                if constexpr (PROPS) esc = simd::sel(w.props != 0u, simd::splat(ESC_PROPS), 0u);
+                // text, one segment at a time, 64 units per step
                 for (u64 tm = simd::ballot(txt); tm; tm &= tm - 1) {
                     const u32 l = (u32)__builtin_ctzll(tm);
-                    const u32 e = copy_text_esc(simd::readlane(tat, l), simd::readlane(w.toff, l), simd::readlane(w.len, l), tdst);
-                    esc = simd::writelane(esc, l, simd::readlane(esc, l) | e);
+                    copy_text(simd::readlane(tat, l), simd::readlane(w.toff, l), simd::readlane(w.len, l), tdst);
                 }
-                if (p.out_esc) simd::st(p.out_esc, at, esc, have);
                 run += (u32)__builtin_popcountll(simd::ballot(have));
                 trun += simd::readlane(simd::scan_incl(tl), 63);
             }

@@ -159,7 +159,8 @@ def lib():
         L.mte_builder_add_doc_from_summary.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, sz]
         L.mte_builder_add_container_log.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_uint32)]
         L.mte_builder_add_matrix_log.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz]
-        L.mte_builder_add_matrix_from_summary.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, sz]
+        if hasattr(L, "mte_builder_add_matrix_from_summary"):  # (A/B runs load older experiment builds)
+            L.mte_builder_add_matrix_from_summary.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, sz]
         L.mte_snapshot_matrix.argtypes = [vp, u32, u32, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
         L.mte_builder_doc_path.argtypes = [vp, ctypes.c_uint32]
         L.mte_builder_doc_path.restype = ctypes.c_char_p

@@ -106,7 +106,7 @@ def test_wide_row_engine_lone_documents(engine, kind, gid, n_ops, clients, rows)
 
 def test_props_zipf_head_on_rows(engine):
     """The head of a Zipf kind-3 batch runs on k_solo's PROPS row engine (mode 4); the rest of the
-    batch on k_lds beside it; every checksum against the oracle."""
+    batch on k_rows' PROPS engine beside it; every checksum against the oracle."""
     from fluidframework_amd.shard import zipf_op_counts
 
     counts = zipf_op_counts(1024, seed=3, lo=100, hi=100_000)

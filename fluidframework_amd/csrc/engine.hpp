@@ -138,8 +138,8 @@ struct Seg {
 // Synthetic writers' state (generator), resumable across the LDS -> HBM hand-off.
 struct GenState {
     Rng rng;
-    i32 ref[MTE_MAX_CLIENTS];
-    u32 sid_of[MTE_MAX_CLIENTS];
+    i32 ref[GEN_MAX_CLIENTS];
+    u32 sid_of[GEN_MAX_CLIENTS];
     u32 nextShort, pay;
     i32 lastC, lastR, lastPos;
     u64 step;
@@ -194,6 +194,7 @@ struct Engine {
     u32 wave;
     i32 zseq = 0;            // EXT: seq of the op being applied (UNLINK time of freed handles)
     bool continued = false;  // HBM-resident after starting in LDS
+    bool from_rows = false;  // HBM-resident after starting on k_rows' row engine (DocRes mode 6)
     bool capped = false;     // HBM slot smaller than this document's worst case
 
 #define MTE_ARR(T, NAME, MEM, LDSX, SOLOX)     \
@@ -239,6 +240,7 @@ struct Engine {
     u16* payload;
     u16* arena0;
     u64* ovl;
+    u64* ovl2;  // clients 64..127 (documents whose window holds more than 64 clients), else null
     u32* maps;
 
     MTE_DEV Engine(const Params& p_, u32 doc_) : p(p_), doc(doc_) {
@@ -254,6 +256,7 @@ struct Engine {
         payload = p.payload + c.payload_off;
         arena0 = p.arena + c.arena_off;
         ovl = p.ovl + c.ovl_off;
+        ovl2 = (p.ovl2 && c.ovl2_off != OVL2_NONE) ? p.ovl2 + c.ovl2_off : nullptr;
         mw = p.map_words;
         maps = p.maps + c.map_off * mw;
         collab = c.collab != 0;
@@ -465,12 +468,15 @@ struct Engine {
     }
     // C among the overlapping removers (removedClientOverlap, mergeTree.ts:2544-2552): clients
     // 0..31 in the removed slot's aux.z (its arena-capacity word is dead once removed), 32..63 in
-    // the document's HBM mask by segment id.
+    // the document's HBM mask by segment id, 64..127 in its second HBM mask (F_OVLHI: both words
+    // valid).
     MTE_DEV bool ovl_hides(u32 idx, u32 C, u32 meta) const {
         if (C < 32) return (AUX()[idx].z >> C) & 1u;
         if (!(meta & F_OVLHI)) return false;
         const u32 sid = AUX()[idx].w;
-        return sid < seg_cap && ((ovl[sid] >> C) & 1ull);
+        if (sid >= seg_cap) return false;
+        if (C < 64) return (ovl[sid] >> C) & 1ull;
+        return ovl2 && ((ovl2[sid] >> (C - 64)) & 1ull);
     }
     // breakTie for a zero-visible leaf at pos 0: skip tombstones already seen at R (mergeTree.ts:2257-2261)
     MTE_DEV static u32 tie_ok(uint4 q, i32 R, u32 cz) {
@@ -2046,7 +2052,10 @@ struct Engine {
                 left.tcap = rm ? left.tcap : ((left.toff & ARENA_BIT) ? r : 0u);
                 if (left.meta & F_OVLHI) {  // the right piece copies removedClientOverlap (clients >= 32)
                     fence_ovl();
-                    if (L == 0 && left.sid < seg_cap && sid < seg_cap) ovl[sid] = ovl[left.sid];
+                    if (L == 0 && left.sid < seg_cap && sid < seg_cap) {
+                        ovl[sid] = ovl[left.sid];
+                        if (ovl2) ovl2[sid] = ovl2[left.sid];
+                    }
                     st.gdirty = 1;
                 }
                 sync();
@@ -2147,8 +2156,15 @@ struct Engine {
                             if (C < 32) {
                                 AUX()[idx].z = AUX()[idx].z | (1u << C);
                             } else if (sid < seg_cap) {
-                                const u64 old = (q.w & F_OVLHI) ? ovl[sid] : 0ull;
-                                ovl[sid] = old | (1ull << C);
+                                // F_OVLHI's first setting writes every word (stale from an earlier pass)
+                                const bool had = (q.w & F_OVLHI) != 0;
+                                if (C < 64) {
+                                    ovl[sid] = (had ? ovl[sid] : 0ull) | (1ull << C);
+                                    if (ovl2 && !had) ovl2[sid] = 0ull;
+                                } else if (ovl2) {
+                                    ovl2[sid] = (had ? ovl2[sid] : 0ull) | (1ull << (C - 64));
+                                    if (!had) ovl[sid] = 0ull;
+                                }
                                 q.w |= F_OVLHI;
                             }
                             q.w |= F_OVL;
@@ -2608,6 +2624,7 @@ struct Engine {
                     u64 m = (v.w & F_OVL) ? (u64)a.z : 0ull;
                     if ((v.w & F_OVLHI) && a.w < seg_cap) m |= ovl[a.w] & 0xFFFFFFFF00000000ull;
                     p.out_ovl[at + s] = m;
+                    if (p.out_ovl2) p.out_ovl2[at + s] = (ovl2 && (v.w & F_OVLHI) && a.w < seg_cap) ? ovl2[a.w] : 0ull;
                 }
                 run += wave_read(incl, 63);
                 trun += wave_read(tincl, 63);
@@ -2636,7 +2653,7 @@ struct Engine {
             o.text_off = toff;
             o.max_lb = maxlb;
             o.cu_n = ncu;
-            o.mode = SOLO ? 3u : (LDSM ? 0u : (continued ? 2u : 1u));
+            o.mode = SOLO ? 3u : (LDSM ? 0u : (from_rows ? 6u : continued ? 2u : 1u));
         }
     }
 
@@ -2756,7 +2773,7 @@ struct Engine {
         // seeded by the GLOBAL document id, so a document is the same whichever rank generates it
         const u64 sx = 0xF1D0C0DEull ^ (u64)p.docs[doc].gid ^ (p.gen_seed * 0x9E3779B97F4A7C15ull);
         g.rng.seed(sx);
-        for (u32 c = 0; c < MTE_MAX_CLIENTS; c++) {
+        for (u32 c = 0; c < GEN_MAX_CLIENTS; c++) {
             g.ref[c] = 0;
             g.sid_of[c] = 0;
         }
@@ -2771,7 +2788,7 @@ struct Engine {
     // of room before op g.step.
     MTE_DEV bool generate_run(GenState& g) {
         const u32 nc = p.gen_nclients;
-        u32* firstSeen = p.gen_first_seen + (u64)doc * MTE_MAX_CLIENTS;
+        u32* firstSeen = p.gen_first_seen + (u64)doc * GEN_MAX_CLIENTS;
         const u64 op0 = p.docs[doc].op_begin;
         const u64 nops = p.docs[doc].op_end - op0;
         for (; g.step < nops && !st.status; g.step++) {

@@ -125,12 +125,16 @@ static_assert(sizeof(SoloPlan) <= LDS_BYTES, "solo LDS plan exceeds 160 KiB");
 // block ids below MAX_POOL are LDS ids of a document that continued HBM-resident
 constexpr u32 MAX_POOL = SOLO_POOL > POOL_BLOCKS ? SOLO_POOL : POOL_BLOCKS;
 
+constexpr u64 OVL2_NONE = ~0ull;   // DocCfg::ovl2_off of a document whose window holds <= 64 clients
+constexpr u32 GEN_MAX_CLIENTS = 64;  // the synthetic generator's writers (short ids 1..63)
+
 // Host-computed per-document layout.
 struct DocCfg {
     u64 op_begin, op_end;
     u64 payload_off;
     u64 arena_off;     // two semispaces of arena_cap units each
-    u64 ovl_off;       // per segment id: removedClientOverlap mask (u64)
+    u64 ovl_off;       // per segment id: removedClientOverlap mask (u64; clients 32..63 used)
+    u64 ovl2_off;      // ... clients 64..127 (Params::ovl2), OVL2_NONE unless the window exceeds 64 clients
     u64 map_off;
     u64 hb_off;        // byte offset of this doc's HBM-resident state (HBM mode only)
     u64 cu_off;        // first catch-up delta record (Params::cu_rec, 2 x uint4 each) of this doc
@@ -195,11 +199,13 @@ struct Params {
     DocRes* res;
     u16* arena;
     u64* ovl;
+    u64* ovl2;                // removedClientOverlap of clients 64..127 (DocCfg::ovl2_off), or null
     u32* maps;
     unsigned char* hbm;       // HBM-mode per-doc state (DocCfg::hb_off)
     uint4* out_vis;           // final segments, doc order (output pool)
     uint4* out_aux;
     u64* out_ovl;
+    u64* out_ovl2;            // ... clients 64..127 of each final row (null without such documents)
     u64 out_cap;
     u16* out_text;            // final segment texts, one run per document (Engine::finish)
     u32* out_maps;            // property map of each final row with props (MAP_WORDS per row), or null
@@ -224,7 +230,7 @@ struct Params {
     uint4* cu_rec;            // catch-up delta records: (op index in the doc, position, length, kind),
                               // (map after, map before, 0, 0); kind 0 insert, 1 remove, 2 annotate
     // synthetic workload generator
-    u32* gen_first_seen;      // per doc: 64 entries, writer index for each short id (1..)
+    u32* gen_first_seen;      // per doc: GEN_MAX_CLIENTS entries, writer index for each short id (1..)
     u32 gen_kind;
     u32 gen_nclients;
     u64 gen_seed;
@@ -248,7 +254,11 @@ struct Params {
     u32* rows_retry;          // k_rows: documents the row pool could not grow, queued to restart once
                               // (doc + 1 per slot; counters[8] pushed, counters[9] popped), or null
     u32 rows_pool_lim;        // test knob: k_rows pool rows usable per CU (0 = all of the pool)
+    u32* rows_cont;           // k_rows: documents handed to an HBM slot mid-pass, ROWS_CONT_WORDS each
+                              // (doc, slot, op index lo / hi, the HBM engine's St); counters[10] queued,
+                              // counters[11] taken by k_rows_cont
 };
+constexpr u32 ROWS_CONT_WORDS = 32;
 
 constexpr u32 SOLO_CLK_SLOTS = 64;  // solo workgroups with clock stamps (Params::solo_clk)
 

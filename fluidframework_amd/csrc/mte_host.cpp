@@ -265,8 +265,10 @@ struct mte_engine {
     DevBuf<uint32_t> d_out_maps, d_prop_keys, d_prop_vals, d_val_flags, d_val_objidx, d_order, d_list, d_maps, d_counters,
         d_first_seen;
     DevBuf<uint64_t> d_val_objmatch, d_ovl, d_out_ovl, d_prof, d_solo_clk;
+    DevBuf<uint64_t> d_ovl2, d_out_ovl2;  // removedClientOverlap of clients 64..127 (wide windows only)
     DevBuf<uint32_t> d_solo_started;  // k_solo_gate's counter
     DevBuf<uint32_t> d_rows_retry;    // k_rows' restart queue (Params::rows_retry)
+    DevBuf<uint32_t> d_rows_cont;     // k_rows' continuation records (Params::rows_cont), one per slot
     bool solo_gate = true;            // option "solo_gate"
     uint64_t last_solo_cycles = 0, last_solo_ref = 0;  // critical wave: s_memtime / s_memrealtime deltas
     double last_cell_pass_ms = 0;                       // a SharedMatrix batch's first (positions) pass
@@ -320,7 +322,8 @@ struct mte_engine {
     bool ext_cu = false;                 // ... MTE_F_CATCHUP ops: EXT only when a legacy summary is emitted
     bool lean_base = false;              // batch_is_lean, before the catch-up records decide
     uint32_t rows_pool_lim = 0;          // option rows_pool: k_rows pool rows per CU (test knob, 0 = all)
-    bool props_rows_ok = false;          // k_rows may take the batch: no '\n', relative positions or summary loads, < 32 clients
+    bool props_rows_ok = false;          // k_rows may take the batch: no '\n', relative positions, summary loads or local documents
+    bool rows_wide = false;              // ... on its WIDE row engine: a document has writers 32..63
     bool lean_opt = true;                // option "lean" (0 = always the FULL kernels)
     bool last_lean = false;
     uint32_t solo_max = 16;              // at most this many (0 = off)
@@ -371,7 +374,7 @@ struct mte_engine {
     // downloaded final state
     std::vector<uint32_t> h_maps;
     std::vector<uint4> h_out_vis, h_out_aux;
-    std::vector<uint64_t> h_out_ovl;
+    std::vector<uint64_t> h_out_ovl, h_out_ovl2;
     std::vector<uint16_t> h_out_text;
 };
 
@@ -497,7 +500,7 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     const uint32_t nd = (uint32_t)n_ops.size();
     e->cfg.assign(nd, DocCfg{});
     e->n_ops_doc = n_ops;
-    uint64_t op = 0, pay = 0, ar = 0, seg = 0, mp = 0, out = 0;
+    uint64_t op = 0, pay = 0, ar = 0, seg = 0, seg2 = 0, mp = 0, out = 0;
     bool any_props = false;
     for (uint32_t d = 0; d < nd; d++) {
         DocCfg& c = e->cfg[d];
@@ -518,6 +521,14 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
         c.seg_cap = (uint32_t)std::min<uint64_t>(3 * n + 8, 0xFFFFFFF0ull);
         c.ovl_off = seg;
         seg += c.seg_cap;
+        // a window of more than 64 clients (a loaded batch's names; the generator's stay below 64):
+        // removedClientOverlap of clients 64..127 in a second per-segment word
+        const auto& dco = e->hb.doc_client_offsets;
+        c.ovl2_off = OVL2_NONE;
+        if (dco.size() > d + 1 && dco[d + 1] - dco[d] > 64) {
+            c.ovl2_off = seg2;
+            seg2 += c.seg_cap;
+        }
         c.map_cap = (uint32_t)(n_prop_ins[d] + 4 * n_ann[d] + 16);
         c.map_off = mp;
         mp += c.map_cap;
@@ -537,11 +548,13 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     }
     HIP_TRY(e, e->d_arena.fit(ar));
     HIP_TRY(e, e->d_ovl.fit(seg));
+    if (seg2) HIP_TRY(e, e->d_ovl2.fit(seg2));
     HIP_TRY(e, e->d_maps.fit(mp * e->map_words));
     HIP_TRY(e, e->d_out_vis.fit(out));
     HIP_TRY(e, e->d_out_esc.fit(out));
     HIP_TRY(e, e->d_out_aux.fit(out));
     HIP_TRY(e, e->d_out_ovl.fit(out));
+    if (seg2) HIP_TRY(e, e->d_out_ovl2.fit(out));
     if (any_props) HIP_TRY(e, e->d_out_maps.fit(out * e->map_words));  // some document can carry props
     HIP_TRY(e, e->d_counters.fit(16));
     HIP_TRY(e, e->d_rows_retry.fit(nd));
@@ -566,6 +579,8 @@ static int layout_and_alloc(mte_engine* e, const std::vector<uint64_t>& n_ops, c
     P.res = e->d_res.p;
     P.arena = e->d_arena.p;
     P.ovl = e->d_ovl.p;
+    P.ovl2 = seg2 ? e->d_ovl2.p : nullptr;
+    P.out_ovl2 = seg2 ? e->d_out_ovl2.p : nullptr;
     P.maps = e->d_maps.p;
     P.map_words = e->map_words;
     P.out_vis = e->d_out_vis.p;
@@ -684,8 +699,10 @@ static int alloc_slots(mte_engine* e) {
     const uint32_t n = g * LDS_WAVES + h;
     const size_t bytes = (size_t)n * e->P.slot_bytes;
     if (bytes > e->d_spill.n || !e->d_spill.p) HIP_TRY(e, e->d_spill.alloc(bytes));
-    const size_t words = (h + 31) / 32 + 1;
+    const size_t words = (n + 31) / 32 + 1;  // (k_rows may claim any of the n slots: rows_continue)
     if (words > e->d_slot_bits.n || !e->d_slot_bits.p) HIP_TRY(e, e->d_slot_bits.alloc(words));
+    HIP_TRY(e, e->d_rows_cont.fit((size_t)std::max<uint32_t>(n, 1) * ROWS_CONT_WORDS));
+    e->P.rows_cont = e->d_rows_cont.p;
     e->n_slots = n;
     e->P.spill = e->d_spill.p;
     e->P.slot_bits = e->d_slot_bits.p;
@@ -902,7 +919,8 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     e->stage_copy_ms = e->stage_wait_ms = 0;
     const uint32_t nd = b->n_docs;
     std::vector<uint64_t> n_ops(nd), pay(nd), pi(nd), an(nd);
-    std::vector<uint8_t> collab(nd), has_nl(nd, 0), not_lean(nd, 0), doc_ext(nd, 0), doc_cu(nd, 0), not_rows(nd, 0);
+    std::vector<uint8_t> collab(nd), has_nl(nd, 0), not_lean(nd, 0), doc_ext(nd, 0), doc_cu(nd, 0), not_rows(nd, 0),
+        wide(nd, 0);
     std::vector<uint32_t> doc_keys(nd, 0);  // distinct property keys of each document's ops
     std::vector<uint32_t> n_cell(nd, 0);    // SharedMatrix cell records (MTE_OP_CELL)
     // one pass over each document's ops and payload, documents spread over host threads (the scan is
@@ -932,12 +950,17 @@ int mte_load(mte_engine* e, const mte_batch* b) {
             doc_keys[d] = (uint32_t)(std::unique(keys.begin(), keys.end()) - keys.begin());
         }
         collab[d] = e->hb.client(d, 0).empty() ? 0 : 1;  // empty observer name => local, non-collab
-        not_rows[d] = not_rows[d] || has_nl[d] || rel || e->hb.doc_client_offsets[d + 1] - e->hb.doc_client_offsets[d] > 32;
-        not_lean[d] = not_rows[d] || pi[d] || an[d];
+        // writers 32..63: FULL kernels (the lean LDS engine's removers masks are 32 bits), and the
+        // WIDE row engine in k_rows (a second removers word per slot)
+        const uint32_t n_names = e->hb.doc_client_offsets[d + 1] - e->hb.doc_client_offsets[d];
+        wide[d] = n_names > 32;
+        // (clients 64..127: the LDS / HBM engines only, whose overlap masks have a second word)
+        not_rows[d] = not_rows[d] || has_nl[d] || rel || n_names > 64;
+        not_lean[d] = not_rows[d] || wide[d] || pi[d] || an[d];
         // a local, non-collaborative document is the LDS engine's path (lean or not): RegEngine::replay
         // hands it over at op 0, and k_rows has no LDS plan to hand it to
         not_rows[d] = not_rows[d] || !collab[d];
-        // a document with more than MTE_MAX_CLIENTS clients fails alone (MTE_DOC_UNSUPPORTED at its
+        // a document with more than MTE_MAX_CLIENTS clients in a window fails alone (MTE_DOC_UNSUPPORTED at its
         // first op from a client beyond the cap), never the batch
     };
     {
@@ -949,13 +972,14 @@ int mte_load(mte_engine* e, const mte_batch* b) {
         };
         run_pool(nt, work);
     }
-    bool lean = true, ext = false, cu_any = false, rows_ok = true;
+    bool lean = true, ext = false, cu_any = false, rows_ok = true, any_wide = false;
     uint32_t max_keys = 7;
     for (uint32_t d = 0; d < nd; d++) max_keys = std::max(max_keys, std::min<uint32_t>(doc_keys[d], MTE_MAX_PROPS));
     e->map_words = ((1 + 2 * max_keys) + 3) & ~3u;  // 16 for up to 7 keys, 128 for MTE_MAX_PROPS
     for (uint32_t d = 0; d < nd; d++) {
         lean = lean && !not_lean[d];
         rows_ok = rows_ok && !not_rows[d];
+        any_wide = any_wide || wide[d];
         ext = ext || doc_ext[d];
         cu_any = cu_any || doc_cu[d];
     }
@@ -1002,6 +1026,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     // the legacy format (run_kernel decides, snapshot_format may change after the load)
     e->lean_base = lean;
     e->props_rows_ok = rows_ok;
+    e->rows_wide = any_wide;
     e->ext_perm = ext;
     e->ext_cu = cu_any;
     e->lean_ok = lean && !ext;
@@ -1168,8 +1193,8 @@ static int run_kernel(mte_engine* e, bool gen) {
     // 8 and 2.15 on k_lds / k_hbmq; a document the pool cannot grow restarts inside the pass), beside
     // the solo documents too (C4: the same critical path, 4 046 vs 4 047 ms, but none of the 4 100
     // documents k_lds continued HBM-resident, whose spill and continuation traffic was 15 GB a pass).
-    // Property-carrying batches (FULL only for their properties: no '\n', no relative positions, < 32
-    // clients) take the same route on the PROPS row engine.
+    // Property-carrying batches, and batches with writers 32..63 (FULL only for those: no '\n', no
+    // relative positions) take the same route on the PROPS row engine, WIDE for the latter.
     uint32_t rows = 0;
     // (PROPS rows only when properties are what requires FULL: option lean = 0 on a lean batch keeps
     // the FULL LDS kernels, as that diagnostic switch says)
@@ -1180,7 +1205,10 @@ static int run_kernel(mte_engine* e, bool gen) {
         // (long documents take 4 waves whatever their count: eight of them, ~120 leaf blocks each,
         // would not fit one CU's 79-row pool and spill to HBM re-runs of 10^5+ ops)
         const bool long_docs = bulk_ops >= 200000ull * (nd - n_solo);
-        rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : long_docs ? 4u : 12u;
+        // (writers 32..63: documents grow fast -- minSeq trails far behind, zamboni settles little --
+        // so the shared pool at 8 / 12 waves is full most of the time: 4 waves on fixed rows, a
+        // document outgrowing them continuing HBM-resident; tools/wide_probe.py, profiles/r05/r05l)
+        rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : (long_docs || e->rows_wide) ? 4u : 12u;
     }
     e->last_rows = rows;
     if (rows) groups = hbm_waves = lds_active = 0;
@@ -1191,6 +1219,10 @@ static int run_kernel(mte_engine* e, bool gen) {
         while (e->P.n_prio < nd && e->cfg[e->order[e->P.n_prio]].prio) e->P.n_prio++;
     e->P.n_prio = std::max(e->P.n_prio, n_solo);  // k_lds / k_hbmq / k_rows start after the solo documents
     e->P.n_hslots = hbm_waves;
+    if (rows) {  // k_rows alone: its waves continue documents HBM-resident in any free slot
+        e->P.slot_hbm0 = 0;
+        e->P.n_hslots = e->n_slots;
+    }
     // the streams of this pass (an A/B with CU-masked streams, hipExtStreamCreateWithCUMask, that kept
     // the solo workgroups' CUs to themselves measured the C4 pass 8 % SLOWER -- 9.07 s vs 8.38 s, the
     // solo workgroups themselves included -- and hung at teardown: not used)
@@ -1221,7 +1253,10 @@ static int run_kernel(mte_engine* e, bool gen) {
     if (rows) {
         const uint32_t cus = bulk_cus(e, n_solo);
         const uint32_t per = rows >= 12 ? 12u : rows >= 8 ? 8u : 4u;
-        HIP_TRY(e, launch_rows(e->P, per, std::min<uint32_t>(cus, (nd - n_solo + per - 1) / per), full == 1, s_main));
+        HIP_TRY(e, launch_rows(e->P, per, std::min<uint32_t>(cus, (nd - n_solo + per - 1) / per), full == 1,
+                               full == 1 && e->rows_wide, s_main));
+        // documents k_rows handed to HBM slots between two ops continue here (k_rows_cont)
+        HIP_TRY(e, launch_rows_cont(e->P, full, e->P.n_hslots, s_main));
     }
     // k_hbmq: one workgroup (wave) per document; those that find the queue drained exit at once
     if (hbm_waves && !groups) {
@@ -1447,7 +1482,7 @@ int mte_generate(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, 
 
 int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_ops, const uint32_t* ops_per_doc,
                      const uint32_t* doc_ids, uint32_t n_clients, uint64_t seed_base) {
-    if (!e || n_docs == 0 || n_clients == 0 || n_clients >= MTE_MAX_CLIENTS) return MTE_E_ARG;
+    if (!e || n_docs == 0 || n_clients == 0 || n_clients >= GEN_MAX_CLIENTS) return MTE_E_ARG;
     e->map_words = MAP_WORDS;  // the generator's property sets hold at most four keys
     if (kind != 2 && kind != 3 && kind != 5) return set_err(e, MTE_E_ARG, "generator kind must be 2, 3 or 5");
     HIP_TRY(e, hipSetDevice(e->device));
@@ -1479,8 +1514,8 @@ int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_o
     HIP_TRY(e, e->d_ops.alloc(e->hb.doc_op_offsets.back()));
     HIP_TRY(e, e->d_payload.alloc(e->hb.doc_payload_offsets.back()));
     HIP_TRY(e, hipMemsetAsync(e->d_payload.p, 0, e->d_payload.n * sizeof(uint16_t), e->stream));
-    HIP_TRY(e, e->d_first_seen.alloc((size_t)n_docs * MTE_MAX_CLIENTS));
-    HIP_TRY(e, hipMemsetAsync(e->d_first_seen.p, 0xFF, (size_t)n_docs * MTE_MAX_CLIENTS * 4, e->stream));
+    HIP_TRY(e, e->d_first_seen.alloc((size_t)n_docs * GEN_MAX_CLIENTS));
+    HIP_TRY(e, hipMemsetAsync(e->d_first_seen.p, 0xFF, (size_t)n_docs * GEN_MAX_CLIENTS * 4, e->stream));
     if ((rc = upload_props(e))) return rc;
     e->P.ops = e->d_ops.p;
     e->P.payload = e->d_payload.p;
@@ -1494,17 +1529,18 @@ int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_o
     e->emit_tables = false;  // names are known after the generator ran
     // kinds 2 and 5 draw no properties and no '\n'; short ids stay below 1 + n_clients
     e->lean_ok = e->lean_base = kind != 3 && n_clients < 32;
-    e->props_rows_ok = n_clients < 32;
+    e->props_rows_ok = true;
+    e->rows_wide = n_clients >= 32;  // (and then FULL: lean_ok is false)
     e->ext_needed = e->ext_perm = e->ext_cu = false;
     rc = run_kernel(e, true);
     if (rc) return rc;
     // client names: observer + writers in first-appearance (short id) order
-    std::vector<uint32_t> fs((size_t)n_docs * MTE_MAX_CLIENTS);
+    std::vector<uint32_t> fs((size_t)n_docs * GEN_MAX_CLIENTS);
     HIP_TRY(e, hipMemcpy(fs.data(), e->d_first_seen.p, fs.size() * 4, hipMemcpyDeviceToHost));
     for (uint32_t d = 0; d < n_docs; d++) {
         std::vector<std::string> names{"__observer__"};
-        for (uint32_t s = 1; s < MTE_MAX_CLIENTS; s++) {
-            uint32_t w = fs[(size_t)d * MTE_MAX_CLIENTS + s];
+        for (uint32_t s = 1; s < GEN_MAX_CLIENTS; s++) {
+            uint32_t w = fs[(size_t)d * GEN_MAX_CLIENTS + s];
             if (w == 0xFFFFFFFFu) break;
             names.push_back("client-" + std::to_string(w));
         }
@@ -1558,6 +1594,11 @@ static int ensure_download(mte_engine* e) {
     if ((rc = dl(e->h_out_vis, e->d_out_vis, rows))) return rc;
     if ((rc = dl(e->h_out_aux, e->d_out_aux, rows))) return rc;
     if ((rc = dl(e->h_out_ovl, e->d_out_ovl, rows))) return rc;
+    if (e->P.out_ovl2) {
+        if ((rc = dl(e->h_out_ovl2, e->d_out_ovl2, rows))) return rc;
+    } else {
+        e->h_out_ovl2.clear();
+    }
     uint64_t units;
     memcpy(&units, ctr + 6, sizeof units);
     if ((rc = dl(e->h_out_text, e->d_out_text, std::min<uint64_t>(units, e->P.out_text_cap)))) return rc;
@@ -1571,7 +1612,7 @@ struct SegView {
     uint32_t len;
     int32_t seq, client, rseq, rclient;
     bool removed;
-    uint64_t ovl;
+    uint64_t ovl, ovl2;  // removedClientOverlap: clients 0..63, 64..127
     uint32_t props;
     uint32_t reftype;
     const uint16_t* text;
@@ -1601,6 +1642,7 @@ struct DocView {
                 sv.client = c.collab ? (int32_t)(v.w & 0xff) : -1;
                 sv.rclient = c.collab ? (int32_t)((v.w >> 8) & 0xff) : -1;
                 sv.ovl = e->h_out_ovl[i];
+                sv.ovl2 = i < e->h_out_ovl2.size() ? e->h_out_ovl2[i] : 0ull;
                 sv.props = a.x ? (uint32_t)(i + 1) : 0u;
                 // bits 16..31 of a marker's word: its tag; a permutation run's word: its start handle
                 sv.reftype = sv.kind == 1 ? (t.x & 0xFFFFu) : sv.kind == 2 ? t.x : 0;
@@ -1799,8 +1841,8 @@ int mte_segments_json(mte_engine* e, uint32_t doc, char* buf, size_t cap, size_t
         }
         o += ",\"overlap\":[";
         bool first = true;
-        for (int b = 0; b < 64; b++)
-            if ((s.ovl >> b) & 1ull) {
+        for (int b = 0; b < 128; b++)
+            if ((b < 64 ? s.ovl >> b : s.ovl2 >> (b - 64)) & 1ull) {
                 if (!first) o += ",";
                 first = false;
                 std::string nm = v.long_id(b);
@@ -2590,12 +2632,13 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "lean") *value = e->last_lean;
     else if (k == "rows") *value = e->last_rows;  // k_rows waves per CU of the last pass (0: not used)
     else if (k == "cell_pass_us") *value = (int64_t)(e->last_cell_pass_ms * 1000.0);  // SharedMatrix pass 1
-    else if (k == "rows_restart_pushed" || k == "rows_restart_popped") {
+    else if (k == "rows_restart_pushed" || k == "rows_restart_popped" || k == "rows_continued") {
         // k_rows' in-pass restart queue (counters[8] / [9]): documents given back when the row pool
-        // was full, and restarts taken by a wave
-        uint32_t ctr[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        // was full, and restarts taken by a wave; counters[10]: documents that continued HBM-resident
+        // in the pass after outgrowing the row plan (rows_continue, DocRes mode 6)
+        uint32_t ctr[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         if (e->d_counters.p) HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
-        *value = k == "rows_restart_pushed" ? ctr[8] : ctr[9];
+        *value = k == "rows_restart_pushed" ? ctr[8] : k == "rows_restart_popped" ? ctr[9] : ctr[10];
     }
     else if (k == "emit_us") *value = (int64_t)(e->last_emit_ms * 1000.0);  // emission after the replay pass
     else if (k == "out_text") {  // UTF-16 units Engine::finish gathered (counters[6..7])

@@ -63,7 +63,7 @@ MTE_DEV void solo_doc(const Params& p) {
             }
             Engine<true, true, LVL> t(p, d);
             t.bind_lds(0);
-            reg_handoff(r, t);
+            if (!reg_handoff(r, t)) t.st.status = DOC_SPILL;  // (the SoloPlan holds any row-engine state)
             hst = t.st;
             handed = true;
         }
@@ -86,7 +86,7 @@ MTE_DEV void solo_doc(const Params& p) {
             }
             Engine<true, true, LVL> t(p, d);
             t.bind_lds(0);
-            reg_handoff(r, t);
+            if (!reg_handoff(r, t)) t.st.status = DOC_SPILL;  // (the SoloPlan holds any row-engine state)
             hst = t.st;
             handed = true;
         }
@@ -150,25 +150,109 @@ __global__ __launch_bounds__(64 * SOLO_WAVES) __attribute__((amdgpu_waves_per_eu
 // taken as a document grows and given back as it shrinks or ends, so a document at a transient peak
 // borrows what its neighbours do not use. (The table lookup costs a lone wave ~11 %: C5 4.93 s
 // paged against 4.45 s on fixed rows, hence the fixed quarters at 4 waves.) A document the rows
-// cannot hold, or that reaches an op the row engine does not implement, is re-run by the host,
-// HBM-resident, from its first op (DOC_SPILL).
-// LDS geometry of k_rows: 32 B per slot (vis + aux), 36 with the property map ids (PROPS). The pool
-// (8 / 12 waves): vis array, aux array, [props array], row mask. Fixed quarters (4 waves): per wave
-// its rows' vis, aux and [props] arrays.
-template <bool PROPS>
+// cannot hold between two ops, or that reaches an op the row engine does not implement, continues
+// HBM-resident in the pass (rows_continue); one the pool cannot grow in the middle of an op restarts
+// from its first op (the restart queue) or is re-run by the host (DOC_SPILL). WIDE: batches with writers 32..63 (a second removers
+// word per slot, as k_solo's FULL row engine).
+// LDS geometry of k_rows: 32 B per slot (vis + aux), +4 with the property map ids (PROPS), +4 with
+// the removers 32..63 (WIDE). The pool (8 / 12 waves): vis array, aux array, [props array], [rm2
+// array], row mask. Fixed quarters (4 waves): per wave its rows' vis, aux, [props] and [rm2] arrays.
+template <bool PROPS, bool WIDE>
 struct RowsGeom {
-    static constexpr u32 POOL = PROPS ? 71 : 79;
+    static constexpr u32 SLOT = 32 + (PROPS ? 4 : 0) + (WIDE ? 4 : 0);  // LDS bytes per slot
+    static constexpr u32 POOL = (LDS_BYTES - ROWS_POOL_WORDS * 4) / (64 * SLOT);  // 79, 71 or 63 rows
     static constexpr u32 VIS = 0, AUX = POOL * 64 * 16, PRP = 2 * POOL * 64 * 16;
-    static constexpr u32 MASK = PRP + (PROPS ? POOL * 64 * 4 : 0);
+    static constexpr u32 RM2 = PRP + (PROPS ? POOL * 64 * 4 : 0);
+    static constexpr u32 MASK = RM2 + (WIDE ? POOL * 64 * 4 : 0);
     static constexpr u32 LDS = MASK + ROWS_POOL_WORDS * 4;
-    static constexpr u32 FIXED_NR = PROPS ? 17 : 20;
-    static constexpr u32 FIXED_WAVE = FIXED_NR * 64 * (PROPS ? 36 : 32);
+    static constexpr u32 FIXED_NR = LDS_BYTES / 4 / (64 * SLOT);  // 20, 17 or 16 rows per wave
+    static constexpr u32 FIXED_WAVE = FIXED_NR * 64 * SLOT;
     static constexpr u32 FIXED_LDS = 4 * FIXED_WAVE;
     static_assert(LDS <= LDS_BYTES && FIXED_LDS <= LDS_BYTES && POOL <= 32 * ROWS_POOL_WORDS, "k_rows LDS plan");
 };
-template <int RW, bool PROPS>
+// A k_rows document that outgrows the row plan (or reaches an op the row engine does not implement)
+// between two ops continues in the same pass, HBM-resident: its state moves into a free HBM slot
+// (Params::spill, the bitmap slot_bits over n_hslots slots; k_lds / k_hbmq do not run beside k_rows)
+// and is queued (Params::rows_cont); k_rows_cont (mte_kernels.hip), launched right after k_rows,
+// replays the rest of its ops there (DocRes mode 6). Only the handoff is compiled into k_rows: the HBM
+// engine's replay in the same kernel had tripled its spills (C3 1.34 -> 1.61 s). No free slot, a
+// slot too small for the state, or a slot it outgrows later: the host's re-run, as before.
+// A free slot, or NONE when every slot is held: the bitmap is scanned from a per-workgroup start, and
+// a bit lost to another wave's claim moves on to the next free bit of the same word (the word the
+// atomic returned), so a wave gives up only when it saw every word full.
+MTE_DEV u32 try_hslot(const Params& p) {
+    const u32 L = lane_id();
+    const u32 nw = (p.n_hslots + 31) >> 5;
+    const u32 start = (blockIdx.x * 7u) % nw;
+    for (u32 base = 0; base < nw; base += 64) {
+        const u32 w = (start + base + L) % nw;
+        u32 word = 0xFFFFFFFFu;
+        if (base + L < nw) {
+            word = __hip_atomic_load(&p.slot_bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (w == nw - 1 && (p.n_hslots & 31)) word |= ~0u << (p.n_hslots & 31);
+        }
+        u64 m = wave_ballot(word != 0xFFFFFFFFu);
+        while (m) {
+            const u32 l = (u32)__builtin_ctzll(m);
+            const u32 ww = wave_read(w, l);
+            const u32 pad = (ww == nw - 1 && (p.n_hslots & 31)) ? ~0u << (p.n_hslots & 31) : 0u;
+            u32 cur = wave_read(word, l);
+            for (u32 t = 0; t < 32 && cur != 0xFFFFFFFFu; t++) {
+                const u32 bit = (u32)__builtin_ctz(~cur);
+                u32 old = 0;
+                if (L == 0) old = atomicOr(&p.slot_bits[ww], 1u << bit);
+                old = wave_read(old, 0);
+                if (!(old & (1u << bit))) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the previous holder's writes
+                    return ww * 32 + bit;
+                }
+                cur = old | pad | (1u << bit);
+            }
+            m &= m - 1;
+        }
+    }
+    return NONE;
+}
+// Returns 0 when the document was queued for k_rows_cont, else why not (DocRes::spill_why's low byte
+// after the caller's mark): 1 no free slot or queue, 2 the slot cannot hold the state, 3 the rows do
+// not hold the whole state (a PAGED engine that never got its first row)
+template <int LVL, class R>
+MTE_DEV u32 rows_continue(const Params& p, R& r, u32 d, u64 at) {
+    if (!r.rows_whole()) return 3;
+    if (!p.slot_bits || !p.n_hslots || !p.rows_cont) return 1;
+    const u32 slot = try_hslot(p);
+    if (slot == NONE) return 1;
+    Engine<false, false, LVL> h(p, d);
+    h.bind_slot(p.slot_hbm0 + slot);
+    h.reset_stats();
+    if (!reg_handoff(r, h)) {
+        if (lane_id() == 0) atomicAnd(&p.slot_bits[slot >> 5], ~(1u << (slot & 31)));
+        return 2;
+    }
+    u32 k = 0;
+    if (lane_id() == 0) k = atomicAdd(&p.counters[10], 1u);
+    k = wave_read(k, 0);
+    // the record: lanes 0..3 the header, 4.. the replay state (the slot's arrays are written already)
+    u32* rec = p.rows_cont + (u64)k * ROWS_CONT_WORDS;
+    constexpr u32 NS = (u32)(sizeof(St) / 4);
+    static_assert(4 + NS <= ROWS_CONT_WORDS, "rows_cont record");
+    u32 sw[NS];
+    __builtin_memcpy(sw, &h.st, sizeof(St));
+    const u32 L = lane_id();
+    u32 v = L == 0 ? d : L == 1 ? slot : L == 2 ? (u32)at : L == 3 ? (u32)(at >> 32) : 0u;
+#pragma unroll
+    for (u32 q = 0; q < NS; q++)
+        if (L == 4 + q) v = sw[q];
+    if (L < 4 + NS) rec[L] = v;
+    // release: the slot's state and the record before k_rows_cont (another XCD's L2) reads them
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    return 0;
+}
+
+template <int RW, bool PROPS, bool WIDE>
 __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4, RW / 4))) void k_rows(Params p) {
-    typedef RowsGeom<PROPS> G;
+    typedef RowsGeom<PROPS, WIDE> G;
     constexpr bool PAGED = RW > 4;
     const u32 w = wave_first(threadIdx.x >> 6);
     if constexpr (PAGED) {
@@ -184,6 +268,7 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
     const u32 vb = PAGED ? G::VIS : w * G::FIXED_WAVE;
     const u32 ab = PAGED ? G::AUX : vb + G::FIXED_NR * 64u * 16u;
     const u32 pb = PAGED ? G::PRP : vb + G::FIXED_NR * 64u * 32u;
+    const u32 r2b = PAGED ? G::RM2 : pb + (PROPS ? G::FIXED_NR * 64u * 4u : 0u);
     if (blockIdx.x == 0 && threadIdx.x == 0 && p.solo_clk) p.solo_clk[4 * SOLO_CLK_SLOTS] = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         // a document another wave gave back when the pool was full restarts first (once; a second
@@ -225,8 +310,9 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
             }
             d = p.doc_list[i];
         }
-        RegEngine<PAGED ? (int)RG_ROWS : (int)G::FIXED_NR, PAGED, PROPS> r(p, d, vb, ab, 5, G::MASK, pb);
-        if (!r.status) r.replay(p.docs[d].op_begin, p.docs[d].op_end);
+        RegEngine<PAGED ? (int)RG_ROWS : (int)G::FIXED_NR, PAGED, PROPS, WIDE> r(p, d, vb, ab, 5, G::MASK, pb, r2b);
+        u64 at = p.docs[d].op_begin;
+        if (!r.status) at = r.replay(at, p.docs[d].op_end);
         if (r.status == REG_HANDOFF && PAGED && p.rows_retry && r.pool_full && !again) {
             // marked for the host's re-run first (so a document no wave restarts is still replayed),
             // then queued to restart from its first op; a restart that finishes overwrites the mark
@@ -236,7 +322,16 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
                 __hip_atomic_store(p.rows_retry + k, d + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             }
         } else if (r.status == REG_HANDOFF) {
-            r.mark_spilled();
+            // between two ops: continue HBM-resident in this pass (fixed rows, 4 waves: the route of
+            // long and of many-writer documents, which outgrow their rows); inside one, or on the
+            // shared pool (8 / 12 waves: the handoff's code there spilled the row engine's registers,
+            // C3 1.34 -> 1.61 s), the host's re-run
+            u32 why = 5;
+            if constexpr (!PAGED) why = r.midop ? 4u : rows_continue<(PROPS ? 1 : 0)>(p, r, d, at);
+            if (why) {
+                r.mark_spilled();
+                if (lane_id() == 0) p.res[d].spill_why |= why;
+            }
         } else {
             r.finish();
         }
@@ -244,13 +339,15 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
     }
 }
 
-template <bool PROPS>
+template <bool PROPS, bool WIDE>
 static hipError_t launch_rows_t(const Params& p, u32 rw, u32 n_groups, hipStream_t s) {
-    typedef RowsGeom<PROPS> G;
-    const void* k = rw == 12 ? (const void*)k_rows<12, PROPS> : rw == 8 ? (const void*)k_rows<8, PROPS> : (const void*)k_rows<4, PROPS>;
+    typedef RowsGeom<PROPS, WIDE> G;
+    const void* k = rw == 12 ? (const void*)k_rows<12, PROPS, WIDE>
+                  : rw == 8  ? (const void*)k_rows<8, PROPS, WIDE>
+                             : (const void*)k_rows<4, PROPS, WIDE>;
     static const hipError_t attr = [] {
-        hipError_t r = hipFuncSetAttribute((const void*)k_rows<4, PROPS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::FIXED_LDS);
-        for (const void* f : {(const void*)k_rows<8, PROPS>, (const void*)k_rows<12, PROPS>})
+        hipError_t r = hipFuncSetAttribute((const void*)k_rows<4, PROPS, WIDE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::FIXED_LDS);
+        for (const void* f : {(const void*)k_rows<8, PROPS, WIDE>, (const void*)k_rows<12, PROPS, WIDE>})
             if (r == hipSuccess) r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
         return r;
     }();
@@ -258,9 +355,12 @@ static hipError_t launch_rows_t(const Params& p, u32 rw, u32 n_groups, hipStream
     void* args[] = {(void*)&p};
     return hipLaunchKernel(k, dim3(n_groups), dim3(64 * rw), args, (size_t)(rw == 4 ? G::FIXED_LDS : G::LDS), s);
 }
-hipError_t launch_rows(const Params& p, u32 waves_per_cu, u32 n_groups, bool props, hipStream_t s) {
+// WIDE (clients 32..63) only with PROPS: such a batch is a FULL one (the lean LDS kernels keep 32-bit
+// removers masks), whose row engine is the property-carrying one
+hipError_t launch_rows(const Params& p, u32 waves_per_cu, u32 n_groups, bool props, bool wide, hipStream_t s) {
     const u32 rw = waves_per_cu >= 12 ? 12u : waves_per_cu >= 8 ? 8u : 4u;
-    return props ? launch_rows_t<true>(p, rw, n_groups, s) : launch_rows_t<false>(p, rw, n_groups, s);
+    if (wide) return props ? launch_rows_t<true, true>(p, rw, n_groups, s) : hipErrorInvalidValue;
+    return props ? launch_rows_t<true, false>(p, rw, n_groups, s) : launch_rows_t<false, false>(p, rw, n_groups, s);
 }
 
 #define MTE_PICK(K, gen, lvl)                                                                           \

@@ -546,6 +546,11 @@ struct RegEngine {
     SD void release_rows() {
         if constexpr (PAGED) shrink_rows(0);
     }
+    // every row the state uses is held (a PAGED engine whose first row the pool never gave has none)
+    SD bool rows_whole() const {
+        if constexpr (PAGED) return n_rows * 8 >= n_lb;
+        else return true;
+    }
     // Room for leaf blocks [0, nb): PAGED takes pool rows (none left: spill the document, the host
     // re-runs it); otherwise the fixed rows must hold them.
     SD bool ensure_blocks(u32 nb) {
@@ -721,6 +726,7 @@ struct RegEngine {
         heapSize = segNext = arenaTop = arenaSel = 0;
         minSeq = curSeq = heapTop = 0;
         status = 0;
+        midop = false;
         failSeq = -1;
         n_ops = n_msgs = n_gc = 0;
         max_lb = 1;
@@ -734,10 +740,14 @@ struct RegEngine {
     }
 
     SD static V L() { return simd::lanes(); }
+    // a REG_HANDOFF raised INSIDE an op (a pool row or a map record it could not get) leaves the op
+    // half applied: only a restart from op 0 may continue such a document
+    bool midop = false;
     SD void fail(i32 code, i32 seq) {
         if (status == 0) {
             status = code;
             failSeq = seq;
+            midop = code == REG_HANDOFF;
         }
     }
     // Segment ids are 1-based in the rows (an empty slot holds 0), the LDS engine's id + 1: the
@@ -2122,6 +2132,10 @@ struct RegEngine {
                 simd::st(oa, t4 + 3u, w.sid - 1u, have);
                 simd::st(oo, at * 2u, ovl, have);
                 simd::st(oo, at * 2u + 1u, ovh, have);
+                if (p.out_ovl2) {  // clients 64..127: never on the rows (their first op hands over)
+                    simd::st((u32*)p.out_ovl2, at * 2u, simd::splat(0), have);
+                    simd::st((u32*)p.out_ovl2, at * 2u + 1u, simd::splat(0), have);
+                }
                 // text, one segment at a time, 64 units per step
                 for (u64 tm = simd::ballot(txt); tm; tm &= tm - 1) {
                     const u32 l = (u32)__builtin_ctzll(tm);

@@ -1,5 +1,6 @@
 // reg_handoff.hpp — hand a document from the register-resident engine (reg_engine.hpp) to the
-// LDS-resident solo engine (engine.hpp, Engine<true, true, LVL>) between two ops.
+// LDS-resident solo engine (engine.hpp, Engine<true, true, LVL>: k_solo) or to an HBM-resident one
+// (Engine<false, false, LVL> in a wave's HBM slot: k_rows) between two ops.
 //
 // The register engine keeps leaf blocks in document order and the interior levels as child-count
 // vectors; the LDS engine keeps blocks and interior nodes by id with parent pointers and a doc-order
@@ -13,8 +14,10 @@
 
 namespace mte {
 
+// Returns false, writing nothing, when the target's arrays cannot hold the document's state (an HBM
+// slot sized for shorter documents): the caller gives the document to the host's re-run then.
 template <class E, class R>
-MTE_DEV void reg_handoff(R& r, E& e) {
+MTE_DEV bool reg_handoff(R& r, E& e) {
     using simd::V;
     const u32 L = lane_id();
     const u32 nrows = (r.n_lb + 7) >> 3;
@@ -27,6 +30,7 @@ MTE_DEV void reg_handoff(R& r, E& e) {
         base[i] = tot;
         tot += nn[i];
     }
+    if (nrows * 8 > e.blk_cap() || r.n_lb > e.ord_cap() || tot > e.in_cap() || r.heapSize >= e.heap_cap()) return false;
     // leaf block summaries and metadata (parent | needsScour << 30)
     u32 node = 0, left = H > 1 ? simd::readlane(r.LV.get(0), 0) : 0u;
     for (u32 k = 0; k < r.n_lb; k++) {
@@ -85,28 +89,32 @@ MTE_DEV void reg_handoff(R& r, E& e) {
         const u32 hk = r.HK.get(j).x, hs = r.HS.get(j).x;
         if (q >= 1 && q <= r.heapSize) e.HEAP()[q] = make_uint2(hs - 1u, hk);  // ids 1-based in the rows
     }
-    // slots: row rr lane l is block 8*rr + l/8, slot l%8 = the LDS engine's slot index 64*rr + l,
-    // already in place; only the encoding of live segments and needsScour differ
+    // slots: row rr lane l is block 8*rr + l/8, slot l%8 = the LDS engine's slot index 64*rr + l
+    // (for k_solo the same LDS words: each lane reads its slot before it rewrites it); only the
+    // encoding of live segments and needsScour differ
     lds_order();
     for (u32 rr = 0; rr < nrows; rr++) {
-        const uint4 v = e.VIS()[64 * rr + L], a = e.AUX()[64 * rr + L];
+        const auto w = r.ldrow(rr);
+        const uint4 v = make_uint4(w.len.x, w.seq.x, w.rseq.x, w.meta.x), a = make_uint4(w.cap.x, w.toff.x, w.rm.x, w.sid.x);
         const bool live = v.z == RSEQ_LIVE, ov = (v.w & F_OVL) != 0;
         const u32 m2 = (live ? (v.w & ~0xFF00u) : v.w) & ~NS_MASK;
         // aux.z: a live segment's text capacity, a removed one's removedClientOverlap (rm without
         // removedClient) or 0
         u32 ovm = a.z & ~(1u << ((v.w >> 8) & 31u)), m3 = m2;
         if constexpr (R::kWide) {  // removers 32..63: the LDS engine keeps them in its HBM mask by id
-            const u32 rc = (v.w >> 8) & 0xFFu, rm2 = r.RM2P()[64 * rr + L];
+            const u32 rc = (v.w >> 8) & 0xFFu, rm2 = w.rm2.x;
             ovm = a.z & ~(rc < 32 ? 1u << rc : 0u);
             const u32 hi = (!live && ov) ? rm2 & ~(rc >= 32 ? 1u << (rc & 31u) : 0u) : 0u;
             if (v.x && hi && a.w - 1u < e.seg_cap) {
                 e.ovl[a.w - 1u] = (u64)hi << 32;
+                if (e.ovl2) e.ovl2[a.w - 1u] = 0ull;  // (the row engine's writers are below 64)
                 m3 |= F_OVLHI;
             }
         }
+        lds_order();  // (k_solo: the row's reads before the writes over the same words)
         e.VIS()[64 * rr + L] = make_uint4(v.x, v.y, live ? 0u : v.z, m3);
         u32 props = 0;
-        if constexpr (R::kProps) props = v.x ? r.PROPP()[64 * rr + L] : 0u;  // beyond the rows' slots: intact
+        if constexpr (R::kProps) props = v.x ? w.props.x : 0u;
         e.AUX()[64 * rr + L] = make_uint4(props, a.y, live ? a.x : (ov ? ovm : 0u), v.x ? a.w - 1u : 0u);
     }
     // replay state and per-document counters
@@ -144,6 +152,7 @@ MTE_DEV void reg_handoff(R& r, E& e) {
         S[E::ST_CUOP] = 0;
     }
     wave_sync();  // LDS state and the arena text the register engine wrote, before the LDS engine reads
+    return true;
 }
 
 }  // namespace mte

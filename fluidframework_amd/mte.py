@@ -417,7 +417,8 @@ class Engine:
         out = {"spilled": sp.value, "continued": co.value, "lds_ms": a.value, "hbm_ms": b.value,
                "out_rows": rows.value}
         for k in ("lds_groups", "hbm_waves", "hbm_docs", "slot_bytes", "slots", "solo", "solo_us", "solo_lead_us",
-                  "solo_tail_us", "lean", "out_text", "rows", "rows_restart_pushed", "rows_restart_popped"):
+                  "solo_tail_us", "lean", "out_text", "rows", "rows_restart_pushed", "rows_restart_popped",
+                  "rows_continued"):
             out[k] = self.get_info(k)
         return out
 

@@ -47,11 +47,13 @@ enum {
     MTE_DOC_INSERT_FAILED = 1,   /* mergeTree.ts:2210-2216 "MergeTree insert failed" */
     MTE_DOC_SEQ_ORDER = 2,       /* client.ts:469-472,832-834 sequencing asserts */
     MTE_DOC_CAPACITY = 3,        /* engine arena exhausted (sizing bug; never silent) */
-    MTE_DOC_UNSUPPORTED = 4,     /* > 64 clients, > MTE_MAX_PROPS keys on a segment, ... */
+    MTE_DOC_UNSUPPORTED = 4,     /* > 127 writers in one window, > MTE_MAX_PROPS keys on a segment, ... */
     MTE_DOC_NOT_RUN = 5,
 };
 
-#define MTE_MAX_CLIENTS 64       /* short ids 0..63 (observer = 0), overlap kept as a u64 mask */
+#define MTE_MAX_CLIENTS 128      /* short ids 0..127 (observer = 0) in a collaboration window; removedClientOverlap
+                                    kept as masks (clients 64..127: a second per-segment word, only in documents
+                                    whose window holds more than 64 clients) */
 #define MTE_MAX_PROPS 63         /* keys per segment property map on the device; the map records of a
                                     batch are as wide as its widest document needs (its distinct keys) */
 
@@ -237,7 +239,7 @@ typedef struct mte_seg_row {       /* parity dump row (walkAllSegments order, me
     int32_t client;                /* short id (-1 local, -2 non-collab) */
     int32_t removed_seq;           /* INT32_MIN when not removed */
     int32_t removed_client;
-    uint64_t overlap_mask;         /* removedClientOverlap as a short-id set */
+    uint64_t overlap_mask;         /* removedClientOverlap as a short-id set (ids 0..63; mte_segments_json lists all) */
     uint32_t text_off;             /* offset into the text returned by mte_segment_text */
     uint32_t ref_type;             /* marker: refType; permutation run: its start handle (0 = unallocated) */
 } mte_seg_row;

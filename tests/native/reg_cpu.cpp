@@ -131,6 +131,9 @@ uint64_t regcpu_replay_props(const mte_op* ops, uint64_t n_ops, const uint16_t* 
                              const uint32_t* prop_keys, const uint32_t* prop_vals, const uint32_t* val_flags,
                              uint32_t n_vals, uint32_t map_words, uint32_t map_cap, uint32_t* out_maps, uint32_t wide) {
     PropTables t{(const mte_propset*)propsets, n_propsets, prop_keys, prop_vals, val_flags, n_vals, map_words, map_cap, out_maps};
+    if (wide && pool_rows)  // k_rows' WIDE instantiation (batches with writers 32..63), paged
+        return replay_impl<true, true, true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux,
+                                             out_ovl, out_cap, out_text, out_text_cap, res, pool_rows, &t);
     if (wide)  // k_solo's FULL instantiation: clients up to 63
         return replay_impl<false, true, true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux,
                                               out_ovl, out_cap, out_text, out_text_cap, res, 0, &t);

@@ -29,11 +29,12 @@ def _log(n_writers, n=200, window=True):
     return out
 
 
-def test_document_over_64_clients_fails_alone():
-    """A batch with one document of 70 writers all inside the collaboration window: mte_load
-    succeeds, that document reports MTE_DOC_UNSUPPORTED at the first op of its 64th writer (no slot
-    free), the others replay exactly (70 writers whose ops leave the window reuse slots)."""
-    logs = [_log(8), _log(70, window=False), _log(12), _log(70)]
+def test_document_over_127_clients_fails_alone():
+    """A batch with one document of 130 writers all inside the collaboration window: mte_load
+    succeeds, that document reports MTE_DOC_UNSUPPORTED at the first op of its 128th writer (no slot
+    free), the others replay exactly (70 writers at once on slots up to 70; 130 writers whose ops
+    leave the window reuse slots)."""
+    logs = [_log(8), _log(130, window=False), _log(70, window=False), _log(130)]
     b = mte.Builder()
     for lg in logs:
         b.add_doc(lg)
@@ -45,7 +46,7 @@ def test_document_over_64_clients_fails_alone():
         assert st["failed_docs"] == 1
         code, seq = e.status(1)
         assert code == 4  # MTE_DOC_UNSUPPORTED
-        assert seq == 64  # w63 is short id 64 (observer 0): its first message is seq 64
+        assert seq == 128  # w127 is short id 128 (observer 0): its first message is seq 128
         for d in (0, 2, 3):
             compare_doc(e, batch, d)
     finally:

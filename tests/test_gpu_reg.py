@@ -176,6 +176,7 @@ def test_row_engine_markers_and_builder_logs(engine):
 
 
 MODE_BULK_ROWS = 5  # DocRes.mode: k_rows (bulk documents on the row engine)
+MODE_ROWS_CONTINUED = 6  # k_rows, then HBM-resident in the same pass (outgrew the row plan)
 
 
 @pytest.mark.parametrize("waves", [4, 8, 12])
@@ -203,14 +204,21 @@ def test_bulk_rows_kernel_matches_oracle(engine, kind, waves):
         assert modes.count(MODE_BULK_ROWS) >= len(counts) - 16, (modes.count(1), engine.run_info())
         assert modes.count(1) == engine.run_info()["spilled"]
         _check(engine, batch, n_docs=len(counts))
-        # documents that outgrow the rows (reg_lb_limit shrinks them) go back to the host, which
-        # re-runs them HBM-resident from their first op
+        # documents that outgrow the rows between two ops (reg_lb_limit shrinks them): on fixed rows
+        # (4 waves) they continue HBM-resident in the same pass (mode 6, k_rows_cont), none goes
+        # back to the host; on the shared pool the host re-runs them from their first op
         engine.set_option("reg_lb_limit", 24)
         engine.generate(kind, 64, 6000, n_clients=8, seed=31)
         batch = engine.export_batch()
         st = engine.replay()
-        assert st["failed_docs"] == 0
-        assert engine.run_info()["spilled"] > 0
+        info = engine.run_info()
+        modes = [engine.doc_result(d)["mode"] for d in range(64)]
+        if waves == 4:
+            assert st["failed_docs"] == 0 and info["spilled"] == 0 and info["rows_continued"] > 0, info
+            assert set(modes) <= {MODE_BULK_ROWS, MODE_ROWS_CONTINUED, MODE_ROWS, MODE_SOLO_LDS}, sorted(set(modes))
+            assert modes.count(MODE_ROWS_CONTINUED) == info["rows_continued"], (modes, info)
+        else:
+            assert st["failed_docs"] == 0 and info["spilled"] > 0 and info["rows_continued"] == 0, info
         _check(engine, batch, n_docs=64)
     finally:
         engine.set_option("rows_bulk", -1)
@@ -328,3 +336,32 @@ def test_local_documents_keep_the_lds_engine(engine):
     assert st["failed_docs"] == 0 and info["lean"] == 1 and info["solo"] == 0, info
     assert engine.get_info("rows") == 0 and info["spilled"] == 0, info
     assert [engine.text(d) for d in range(96)] == texts
+
+
+@pytest.mark.parametrize("kind,clients", [(2, 40), (3, 48), (2, 63), (3, 63)])
+def test_bulk_rows_wide_batches(engine, kind, clients):
+    """Batches with writers 32..63 (FULL) on k_rows' WIDE engine (a second removers word per slot),
+    auto route: 4 waves per CU on fixed rows. 1 024 documents of 300 ops stay on the rows to the end
+    (mode 5, no continuation, no host re-run); 256 documents of 600 ops outgrow the 16 rows (their
+    leaf blocks pass ~110: minSeq trails 40+ writers, so zamboni settles little) and every one of
+    them continues HBM-resident in the pass (mode 6), none re-run by the host. Every checksum
+    against the oracle."""
+    engine.set_option("rows_bulk", -1)
+    engine.generate(kind, 1024, 300, n_clients=clients, seed=1000)
+    batch = engine.export_batch()
+    st = engine.replay()
+    info = engine.run_info()
+    assert st["failed_docs"] == 0 and info["rows"] == 4 and info["lean"] == 0, info
+    assert info["spilled"] == 0 and info["rows_continued"] == 0, info
+    modes = [engine.doc_result(d)["mode"] for d in range(1024)]
+    assert modes.count(MODE_BULK_ROWS) == 1024, sorted(set(modes))
+    _check(engine, batch, n_docs=1024)
+    engine.generate(kind, 256, 600, n_clients=clients, seed=1000)
+    batch = engine.export_batch()
+    st = engine.replay()
+    info = engine.run_info()
+    assert st["failed_docs"] == 0 and info["rows"] == 4 and info["spilled"] == 0, info
+    modes = [engine.doc_result(d)["mode"] for d in range(256)]
+    assert set(modes) <= {MODE_BULK_ROWS, MODE_ROWS_CONTINUED}, sorted(set(modes))
+    assert modes.count(MODE_ROWS_CONTINUED) == info["rows_continued"] > 0, info
+    _check(engine, batch, n_docs=256)

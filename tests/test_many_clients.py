@@ -1,6 +1,8 @@
 """Unbounded client ids (client.ts:644-668 getOrAddShortClientId never forgets a client; a container
-log gets a new clientId on every reconnect): the builder maps clients to the engine's 64 slots and
-reuses a slot once minSeq has passed every op of its client (mte_host.cpp DocBuild::short_id). CPU:
+log gets a new clientId on every reconnect): the builder maps clients to the engine's 128 slots and
+reuses a slot once minSeq has passed every op of its client (mte_host.cpp DocBuild::short_id); a
+window of more than 64 clients keeps removedClientOverlap of clients 64..127 in a second per-segment
+mask (engine.hpp ovl2). CPU:
 the oracle's record path (slot ids) against its JSON path (real ids, no cap); GPU: the engine against
 the JSON path. Segment tables are not compared: a settled segment's client is immaterial (visibility
 and SnapshotV1 name clients only above minSeq) and after a reuse the slot names its last owner."""
@@ -12,6 +14,7 @@ import pytest
 
 from fluidframework_amd import mte
 from oracle import OracleDoc
+from tests.gpu_helpers import compare_doc
 from tests.oplog import dumps, ins, msg, rem
 from tests.test_container_log import EMPTY_CHUNK, SS, attributes, blob, tree
 
@@ -46,12 +49,34 @@ def reconnect_log(n_msgs=1500, per_client=3, lag=6, seed=0):
 
 
 def concurrent_log(n_writers=70, n=200):
-    """n_writers all inside the collaboration window (msn stays 0): more than the 64 slots at once."""
+    """n_writers all inside the collaboration window (msn stays 0): more than 64 slots at once."""
     out, L = [], 0
     for s in range(1, n + 1):
         w = f"w{(s - 1) % n_writers}"
         out.append(msg(w, s, s - 1, ins(s % (L + 1), f"{s % 10}"), 0))
         L += 1
+    return out
+
+
+def overlap_log(n_writers=100):
+    """Removes that overlap across the whole window: w0 inserts the alphabet; w1..w{n-1}, all at
+    refSeq 1, remove [2, 10) (w1 first, every later one joins removedClientOverlap, ids up to
+    n_writers - 1); then each of them inserts at a position of its own view (the range is gone for
+    it, hidden by its overlap bit) and removes a character next to it; msn stays 0."""
+    out, seq = [], 0
+
+    def m(w, ref, contents):
+        nonlocal seq
+        seq += 1
+        out.append(msg(f"w{w}", seq, ref, contents, 0))
+
+    m(0, 0, ins(0, "abcdefghijklmnopqrstuvwxyz"))
+    for w in range(1, n_writers):
+        m(w, 1, rem(2, 10))
+    for w in range(1, n_writers):
+        m(w, 1, ins(2 + w % 7, f"<{w}>"))
+    for w in range(1, n_writers, 3):
+        m(w, 1, rem(2 + w % 5, 3 + w % 5))
     return out
 
 
@@ -70,8 +95,8 @@ def test_reconnecting_clients_use_windowed_slots(seed):
     b.add_doc(msgs, observer=OBS)
     batch = b.batch()
     ops = mte.batch_ops(batch)
-    assert int(ops["client"].max()) < 64
-    assert batch.doc_client_offsets[1] - batch.doc_client_offsets[0] <= 64
+    assert int(ops["client"].max()) < 128
+    assert batch.doc_client_offsets[1] - batch.doc_client_offsets[0] <= 128
     rec = OracleDoc(OBS)
     rec.apply_batch(ctypes.addressof(batch), 0)
     ref = json_oracle(msgs)
@@ -80,23 +105,41 @@ def test_reconnecting_clients_use_windowed_slots(seed):
     assert rec.snapshot_json() == ref.snapshot_json()
 
 
-def test_more_than_64_concurrent_clients_is_unsupported():
+@pytest.mark.parametrize("log", ["concurrent", "overlap"])
+def test_more_than_64_concurrent_clients(log):
+    """70 writers at once, and 99 removers overlapping on one range: slots up to 99, the record
+    path (slot ids) equals the JSON path (real ids), overlap sets included."""
+    msgs = concurrent_log() if log == "concurrent" else overlap_log()
     b = mte.Builder()
-    b.add_doc(concurrent_log(), observer=OBS)
+    b.add_doc(msgs, observer=OBS)
+    batch = b.batch()
+    assert int(mte.batch_ops(batch)["client"].max()) >= 64
+    rec = OracleDoc(OBS)
+    rec.apply_batch(ctypes.addressof(batch), 0)
+    ref = json_oracle(msgs)
+    assert rec.status()[0] == ref.status()[0] == 0, (rec.status(), ref.status())
+    assert rec.text() == ref.text()
+    assert rec.snapshot_json() == ref.snapshot_json()
+    assert rec.segments_json() == ref.segments_json()
+
+
+def test_more_than_127_concurrent_clients_is_unsupported():
+    b = mte.Builder()
+    b.add_doc(concurrent_log(130, 260), observer=OBS)
     rec = OracleDoc(OBS)
     rec.apply_batch(ctypes.addressof(b.batch()), 0)
-    assert rec.status()[0] == UNSUPPORTED and rec.status()[2] == 64  # w63 (slot 64 does not exist)
+    assert rec.status()[0] == UNSUPPORTED and rec.status()[2] == 128  # w127 (slot 128 does not exist)
 
 
 def test_ref_seq_below_min_seq_after_reuse_is_unsupported():
-    msgs = reconnect_log(n_msgs=300)
+    msgs = reconnect_log(n_msgs=600)  # 200 client ids: slots are reused past the 128th
     bad = dict(msgs[-1])
-    bad.update(sequenceNumber=301, referenceSequenceNumber=100, clientId="late", minimumSequenceNumber=290)
+    bad.update(sequenceNumber=601, referenceSequenceNumber=100, clientId="late", minimumSequenceNumber=590)
     b = mte.Builder()
     b.add_doc(msgs + [bad], observer=OBS)
     rec = OracleDoc(OBS)
     rec.apply_batch(ctypes.addressof(b.batch()), 0)
-    assert rec.status()[0] == UNSUPPORTED and rec.status()[2] == 301
+    assert rec.status()[0] == UNSUPPORTED and rec.status()[2] == 601
 
 
 def container_log_500():
@@ -143,17 +186,42 @@ def test_gpu_windowed_clients_match_json_oracle(engine):
     b = mte.Builder()
     for m in logs:
         b.add_doc(m, observer=OBS)
+    b.add_doc(concurrent_log(130, 260), observer=OBS)
     b.add_doc(concurrent_log(), observer=OBS)
+    b.add_doc(overlap_log(), observer=OBS)
     log, snap, expect = container_log_500()
     b.add_container_log(log, observer=OBS)
     batch = b.batch()
     engine.load(batch)
     engine.replay()
-    refs = [json_oracle(m) for m in logs] + [None, json_oracle(expect, snap)]
+    refs = [json_oracle(m) for m in logs] + [None, json_oracle(concurrent_log()), json_oracle(overlap_log()),
+                                             json_oracle(expect, snap)]
     for d, ref in enumerate(refs):
         if ref is None:
-            assert engine.status(d) == (UNSUPPORTED, 64)
+            assert engine.status(d) == (UNSUPPORTED, 128)
             continue
         assert engine.status(d)[0] == 0
         assert engine.text(d) == ref.text(), d
         assert engine.snapshot_json(d) == ref.snapshot_json(), d
+    # overlap sets of clients 64..127 (the second mask word) against the record-path oracle
+    for d in (len(logs) + 1, len(logs) + 2):
+        compare_doc(engine, batch, d, observer=OBS)
+
+
+@pytest.mark.gpu
+def test_gpu_wide_window_on_the_solo_route(engine):
+    """The overlap log alone (a one-document batch takes k_solo): the FULL row engine replays it until
+    the first op of a client above 63, then hands the document to the LDS engine, whose second
+    overlap word takes clients 64..99; segment table (overlap sets) and snapshot against the oracle."""
+    engine.set_option("solo_min_ops", 1)
+    try:
+        b = mte.Builder()
+        b.add_doc(overlap_log(), observer=OBS)
+        batch = b.batch()
+        engine.load(batch)
+        engine.replay()
+        assert engine.run_info()["solo"] == 1
+        assert engine.doc_result(0)["mode"] == 3, engine.doc_result(0)
+        compare_doc(engine, batch, 0, observer=OBS)
+    finally:
+        engine.set_option("solo_min_ops", 20000)

@@ -229,16 +229,29 @@ def test_wide_engine_matches_oracle(kind, gid, n_ops, clients):
     regcpu.compare_props(ops, pay, wide=True)
 
 
+@pytest.mark.parametrize("kind,gid,n_ops,clients,pool", [(3, 2, 1100, 40, 32), (2, 3, 1100, 48, 32),
+                                                         (3, 4, 1100, 63, 30), (5, 5, 4000, 36, 24)])
+def test_wide_paged_engine_matches_oracle(kind, gid, n_ops, clients, pool):
+    """k_rows' WIDE instantiation (PAGED + PROPS + WIDE: batches with writers 32..63 on the shared
+    row pool; rows taken in a scattered order from a pool of `pool` rows): the second removers word
+    moves with its slots through the pool-row table; segment table and text against the oracle."""
+    ops, pay = regcpu.generated(kind, gid, n_ops, n_clients=clients, seed=1000)
+    assert (ops["client"] >= 32).sum() > 0
+    regcpu.compare_props(ops, pay, pool_rows=pool, wide=True)
+
+
 @pytest.mark.parametrize("seed", range(12))
 def test_row_engine_variants_random_logs(seed):
     """Randomised logs (kind, writers 2-63, length) through every row-engine instantiation the
-    product builds -- lean, lean paged, PROPS, PROPS paged, PROPS + WIDE -- each against the oracle."""
+    product builds -- lean, lean paged, PROPS, PROPS paged, PROPS + WIDE, paged PROPS + WIDE -- each
+    against the oracle."""
     rng = random.Random(seed)
     kind = rng.choice([2, 3, 5])
     clients = rng.choice([2, 3, 8, 16, 31]) if seed % 3 else rng.randint(32, 63)
     n = rng.randint(200, 2500) if clients < 32 else rng.randint(200, 900)
     ops, pay = regcpu.generated(kind, 500 + seed, n, n_clients=clients, seed=seed)
     regcpu.compare_props(ops, pay, wide=True)
+    regcpu.compare_props(ops, pay, pool_rows=32, wide=True)
     if clients >= 32:
         return
     regcpu.compare_props(ops, pay, pool_rows=rng.randint(12, 32))

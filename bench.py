@@ -290,7 +290,7 @@ def run(args):
                        "ops_per_step": total_ops, "clients": args.clients, "parallelism": f"doc-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "replay pass: mte::k_solo + mte::k_lds + mte::k_hbmq (concurrent streams) + SnapshotV1 emission (mte::k_emit_count/k_emit_write, overlapped with k_solo)",
+                         "kernel": "replay pass: mte::k_solo + mte::k_rows (the bulk; k_lds / k_hbmq for batches the rows cannot take) + mte::k_rows_cont (concurrent streams) + SnapshotV1 emission (mte::k_emit_count/k_emit_write, overlapped with k_solo)",
                          "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "extra": {"ops_per_step_rank0": ops_applied, "longest_doc_ops": int(counts.max()),

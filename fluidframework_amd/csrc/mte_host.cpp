@@ -702,7 +702,8 @@ static int alloc_slots(mte_engine* e) {
     const size_t words = (n + 31) / 32 + 1;  // (k_rows may claim any of the n slots: rows_continue)
     if (words > e->d_slot_bits.n || !e->d_slot_bits.p) HIP_TRY(e, e->d_slot_bits.alloc(words));
     HIP_TRY(e, e->d_rows_cont.fit((size_t)std::max<uint32_t>(n, 1) * ROWS_CONT_WORDS));
-    e->P.rows_cont = e->d_rows_cont.p;
+    // (k_rows dumps a document's state into its slot before k_rows_cont converts it in place)
+    e->P.rows_cont = e->P.slot_bytes >= ROWS_DUMP_BYTES ? e->d_rows_cont.p : nullptr;
     e->n_slots = n;
     e->P.spill = e->d_spill.p;
     e->P.slot_bits = e->d_slot_bits.p;
@@ -1256,7 +1257,7 @@ static int run_kernel(mte_engine* e, bool gen) {
         HIP_TRY(e, launch_rows(e->P, per, std::min<uint32_t>(cus, (nd - n_solo + per - 1) / per), full == 1,
                                full == 1 && e->rows_wide, s_main));
         // documents k_rows handed to HBM slots between two ops continue here (k_rows_cont)
-        HIP_TRY(e, launch_rows_cont(e->P, full, e->P.n_hslots, s_main));
+        HIP_TRY(e, launch_rows_cont(e->P, full == 1, full == 1 && e->rows_wide, e->P.n_hslots, s_main));
     }
     // k_hbmq: one workgroup (wave) per document; those that find the queue drained exit at once
     if (hbm_waves && !groups) {

@@ -166,40 +166,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_HBMQ_WPE
     if (L == 0) atomicAnd(&p.slot_bits[slot >> 5], ~(1u << (slot & 31)));
 }
 
-// k_rows documents handed to an HBM slot mid-pass (mte_solo.hip rows_continue): workgroup i replays
-// the rest of queued record i (DocRes mode 6) and gives the slot back. Launched right after k_rows on
-// its stream with one workgroup per slot (every record holds one); those past the queue exit at once.
-template <int LVL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_HBMQ_WPE))) void k_rows_cont(Params p) {
-    const u32 L = lane_id();
-    const u32 i = blockIdx.x;
-    if (i >= wave_first(p.counters[10])) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const u32 w = p.rows_cont[(u64)i * ROWS_CONT_WORDS + (L < ROWS_CONT_WORDS ? L : 0u)];
-    const u32 d = wave_read(w, 0), slot = wave_read(w, 1);
-    const u64 at = (u64)wave_read(w, 2) | ((u64)wave_read(w, 3) << 32);
-    Engine<false, false, LVL> e(p, d);
-    e.bind_slot(p.slot_hbm0 + slot);
-    constexpr u32 NS = (u32)(sizeof(St) / 4);
-    u32 sw[NS];
-#pragma unroll
-    for (u32 q = 0; q < NS; q++) sw[q] = wave_read(w, 4 + q);
-    __builtin_memcpy(&e.st, sw, sizeof(St));
-    e.from_rows = true;
-    e.replay_run(at);
-    if (e.st.status == DOC_SPILL) e.mark_spilled();
-    else e.finish();
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    if (L == 0) atomicAnd(&p.slot_bits[slot >> 5], ~(1u << (slot & 31)));
-}
-hipError_t launch_rows_cont(const Params& p, int full, u32 n_slots, hipStream_t s) {
-    if (!n_slots) return hipSuccess;
-    void* args[] = {(void*)&p};
-    const void* k = full >= 1 ? (const void*)k_rows_cont<1> : (const void*)k_rows_cont<0>;
-    return hipLaunchKernel(k, dim3(n_slots), dim3(64), args, 0, s);
-}
-
 template <bool GEN, int LVL>
 __global__ __launch_bounds__(64) void k_hbm(Params p) {
     const u32 d = p.doc_list[blockIdx.x];

@@ -171,12 +171,15 @@ struct RowsGeom {
     static_assert(LDS <= LDS_BYTES && FIXED_LDS <= LDS_BYTES && POOL <= 32 * ROWS_POOL_WORDS, "k_rows LDS plan");
 };
 // A k_rows document that outgrows the row plan (or reaches an op the row engine does not implement)
-// between two ops continues in the same pass, HBM-resident: its state moves into a free HBM slot
-// (Params::spill, the bitmap slot_bits over n_hslots slots; k_lds / k_hbmq do not run beside k_rows)
-// and is queued (Params::rows_cont); k_rows_cont (mte_kernels.hip), launched right after k_rows,
-// replays the rest of its ops there (DocRes mode 6). Only the handoff is compiled into k_rows: the HBM
-// engine's replay in the same kernel had tripled its spills (C3 1.34 -> 1.61 s). No free slot, a
-// slot too small for the state, or a slot it outgrows later: the host's re-run, as before.
+// between two ops continues in the same pass, HBM-resident: the wave claims a free HBM slot
+// (Params::spill, the bitmap slot_bits over n_hslots slots; k_lds / k_hbmq do not run beside k_rows),
+// dumps the row engine's state into it as it is (rows_dump: every row's fields, the interior levels
+// and heap registers; the scalars in a queue record, Params::rows_cont) and goes on to its next
+// document. k_rows_cont, launched right after k_rows, rebuilds the row engine from the dump in its
+// own LDS, hands it to the HBM engine in the same slot (reg_handoff) and replays the rest of its ops
+// there (DocRes mode 6). k_rows itself holds only the dump (with the HBM engine's replay compiled in,
+// the 12-wave PROPS build spilled 441 VGPRs: C3 1.34 -> 1.61 s), and only in its fixed-row builds.
+// No free slot, a slot too small for the state, or a slot it outgrows later: the host's re-run.
 // A free slot, or NONE when every slot is held: the bitmap is scanned from a per-workgroup start, and
 // a bit lost to another wave's claim moves on to the next free bit of the same word (the word the
 // atomic returned), so a wave gives up only when it saw every word full.
@@ -213,41 +216,162 @@ MTE_DEV u32 try_hslot(const Params& p) {
     }
     return NONE;
 }
+// The dump in a slot: logical row rr's field f (len, seq, rseq, meta, cap, toff, rm, sid, [props],
+// [rm2]) at words ((rr * NF + f) * 64 + lane), then LV, HK and HS (8 registers each) from word
+// RG_ROWS * NF * 64; the record: doc, slot, op index (lo, hi), then the scalars below.
+template <bool PROPS, bool WIDE>
+struct RowsDump {
+    static constexpr u32 NF = 8 + (PROPS ? 1u : 0u) + (WIDE ? 1u : 0u);
+    static constexpr u32 REGS = (u32)RG_ROWS * NF * 64;
+    static constexpr u64 BYTES = (u64)(REGS + 24 * 64) * 4;
+};
+const u64 ROWS_DUMP_BYTES = RowsDump<true, true>::BYTES;  // (mte_kernels.h: the host checks slots against it)
+enum : u32 { RD_NLB = 4, RD_HEIGHT, RD_HEAPSIZE, RD_HEAPTOP, RD_MINSEQ, RD_CURSEQ, RD_SEGNEXT, RD_ARENATOP,
+             RD_ARENASEL, RD_MAPNEXT, RD_NOPS, RD_NMSGS, RD_NGC, RD_MAXLB, RD_END };
+static_assert(RD_END <= ROWS_CONT_WORDS, "rows_cont record");
+
 // Returns 0 when the document was queued for k_rows_cont, else why not (DocRes::spill_why's low byte
-// after the caller's mark): 1 no free slot or queue, 2 the slot cannot hold the state, 3 the rows do
-// not hold the whole state (a PAGED engine that never got its first row)
-template <int LVL, class R>
-MTE_DEV u32 rows_continue(const Params& p, R& r, u32 d, u64 at) {
+// after the caller's mark): 1 no free slot or queue, 3 the rows do not hold the whole state (a PAGED
+// engine that never got its first row)
+template <class R>
+MTE_DEV u32 rows_dump(const Params& p, R& r, u32 d, u64 at) {
+    typedef RowsDump<R::kProps, R::kWide> D;
     if (!r.rows_whole()) return 3;
     if (!p.slot_bits || !p.n_hslots || !p.rows_cont) return 1;
     const u32 slot = try_hslot(p);
     if (slot == NONE) return 1;
-    Engine<false, false, LVL> h(p, d);
-    h.bind_slot(p.slot_hbm0 + slot);
-    h.reset_stats();
-    if (!reg_handoff(r, h)) {
-        if (lane_id() == 0) atomicAnd(&p.slot_bits[slot >> 5], ~(1u << (slot & 31)));
-        return 2;
+    const u32 L = lane_id();
+    u32* base = reinterpret_cast<u32*>(p.spill + (u64)(p.slot_hbm0 + slot) * p.slot_bytes);
+    const u32 nrows = (r.n_lb + 7) >> 3;
+    for (u32 rr = 0; rr < nrows; rr++) {
+        const auto w = r.ldrow(rr);
+        u32* o = base + (u64)rr * D::NF * 64 + L;
+        o[0] = w.len.x;
+        o[64] = w.seq.x;
+        o[128] = w.rseq.x;
+        o[192] = w.meta.x;
+        o[256] = w.cap.x;
+        o[320] = w.toff.x;
+        o[384] = w.rm.x;
+        o[448] = w.sid.x;
+        if constexpr (R::kProps) o[512] = w.props.x;
+        if constexpr (R::kWide) o[64 * (D::NF - 1)] = w.rm2.x;
+    }
+    u32* g = base + D::REGS + L;
+#pragma unroll
+    for (u32 i = 0; i < 8; i++) {
+        g[64 * i] = r.LV.get(i).x;
+        g[64 * (8 + i)] = r.HK.get(i).x;
+        g[64 * (16 + i)] = r.HS.get(i).x;
     }
     u32 k = 0;
-    if (lane_id() == 0) k = atomicAdd(&p.counters[10], 1u);
+    if (L == 0) k = atomicAdd(&p.counters[10], 1u);
     k = wave_read(k, 0);
-    // the record: lanes 0..3 the header, 4.. the replay state (the slot's arrays are written already)
     u32* rec = p.rows_cont + (u64)k * ROWS_CONT_WORDS;
-    constexpr u32 NS = (u32)(sizeof(St) / 4);
-    static_assert(4 + NS <= ROWS_CONT_WORDS, "rows_cont record");
-    u32 sw[NS];
-    __builtin_memcpy(sw, &h.st, sizeof(St));
-    const u32 L = lane_id();
-    u32 v = L == 0 ? d : L == 1 ? slot : L == 2 ? (u32)at : L == 3 ? (u32)(at >> 32) : 0u;
-#pragma unroll
-    for (u32 q = 0; q < NS; q++)
-        if (L == 4 + q) v = sw[q];
-    if (L < 4 + NS) rec[L] = v;
-    // release: the slot's state and the record before k_rows_cont (another XCD's L2) reads them
+    const u32 v = L == 0 ? d : L == 1 ? slot : L == 2 ? (u32)at : L == 3 ? (u32)(at >> 32)
+                : L == RD_NLB ? r.n_lb : L == RD_HEIGHT ? r.height : L == RD_HEAPSIZE ? r.heapSize
+                : L == RD_HEAPTOP ? (u32)r.heapTop : L == RD_MINSEQ ? (u32)r.minSeq : L == RD_CURSEQ ? (u32)r.curSeq
+                : L == RD_SEGNEXT ? r.segNext : L == RD_ARENATOP ? r.arenaTop : L == RD_ARENASEL ? r.arenaSel
+                : L == RD_MAPNEXT ? r.mapNext : L == RD_NOPS ? r.n_ops : L == RD_NMSGS ? r.n_msgs
+                : L == RD_NGC ? r.n_gc : r.max_lb;
+    if (L < RD_END) rec[L] = v;
+    // release: the dump and the record before k_rows_cont (another XCD's L2) reads them
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     return 0;
+}
+
+// k_rows documents dumped into HBM slots mid-pass: workgroup i rebuilds queued record i's row engine
+// in its LDS (the rows at the k_solo layout's offsets, 32 rows), hands it to the HBM engine in the same
+// slot, replays the rest of its ops (DocRes mode 6) and gives the slot back. One workgroup per slot
+// (every record holds one); those past the queue exit at once.
+template <bool PROPS, bool WIDE>
+__global__ __launch_bounds__(64) void k_rows_cont(Params p) {
+    typedef RowsDump<PROPS, WIDE> D;
+    typedef RegEngine<(int)RG_ROWS, false, PROPS, WIDE> R;
+    constexpr int LVL = PROPS ? 1 : 0;
+    const u32 L = lane_id();
+    const u32 i = blockIdx.x;
+    if (i >= wave_first(p.counters[10])) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const u32 w = p.rows_cont[(u64)i * ROWS_CONT_WORDS + (L < ROWS_CONT_WORDS ? L : 0u)];
+    const u32 d = wave_read(w, 0), slot = wave_read(w, 1);
+    const u64 at = (u64)wave_read(w, 2) | ((u64)wave_read(w, 3) << 32);
+    constexpr u32 VB = 0, AB = RG_ROWS * 64 * 16, PB = 2 * RG_ROWS * 64 * 16, R2B = PB + (PROPS ? RG_ROWS * 64 * 4 : 0);
+    R r(p, d, VB, AB, 5, 0, PB, R2B);  // (init: every row zero)
+    r.n_lb = wave_read(w, RD_NLB);
+    r.height = wave_read(w, RD_HEIGHT);
+    r.heapSize = wave_read(w, RD_HEAPSIZE);
+    r.heapTop = (i32)wave_read(w, RD_HEAPTOP);
+    r.minSeq = (i32)wave_read(w, RD_MINSEQ);
+    r.curSeq = (i32)wave_read(w, RD_CURSEQ);
+    r.segNext = wave_read(w, RD_SEGNEXT);
+    r.arenaTop = wave_read(w, RD_ARENATOP);
+    r.arenaSel = wave_read(w, RD_ARENASEL);
+    r.mapNext = wave_read(w, RD_MAPNEXT);
+    r.n_ops = wave_read(w, RD_NOPS);
+    r.n_msgs = wave_read(w, RD_NMSGS);
+    r.n_gc = wave_read(w, RD_NGC);
+    r.max_lb = wave_read(w, RD_MAXLB);
+    r.status = 0;
+    const u32* base = reinterpret_cast<const u32*>(p.spill + (u64)(p.slot_hbm0 + slot) * p.slot_bytes);
+    const u32 nrows = (r.n_lb + 7) >> 3;
+    for (u32 rr = 0; rr < nrows && rr < RG_ROWS; rr++) {
+        const u32* o = base + (u64)rr * D::NF * 64 + L;
+        typename R::Row x;
+        x.len = simd::V{o[0]};
+        x.seq = simd::V{o[64]};
+        x.rseq = simd::V{o[128]};
+        x.meta = simd::V{o[192]};
+        x.cap = simd::V{o[256]};
+        x.toff = simd::V{o[320]};
+        x.rm = simd::V{o[384]};
+        x.sid = simd::V{o[448]};
+        if constexpr (PROPS) x.props = simd::V{o[512]};
+        if constexpr (WIDE) x.rm2 = simd::V{o[64 * (D::NF - 1)]};
+        r.strow(rr, x);
+    }
+    const u32* g = base + D::REGS + L;
+#pragma unroll
+    for (u32 q = 0; q < 8; q++) {
+        r.LV.set(q, simd::V{g[64 * q]});
+        r.HK.set(q, simd::V{g[64 * (8 + q)]});
+        r.HS.set(q, simd::V{g[64 * (16 + q)]});
+    }
+    // every read of the dump done before the handoff writes the HBM engine's arrays over it
+    __builtin_amdgcn_s_waitcnt(0);
+    wave_sync();
+    {
+        Engine<false, false, LVL> h(p, d);
+        h.bind_slot(p.slot_hbm0 + slot);
+        h.reset_stats();
+        if (!reg_handoff(r, h)) {
+            r.mark_spilled();
+            if (L == 0) p.res[d].spill_why |= 2u;
+        } else {
+            h.from_rows = true;
+            h.replay_run(at);
+            if (h.st.status == DOC_SPILL) h.mark_spilled();
+            else h.finish();
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (L == 0) atomicAnd(&p.slot_bits[slot >> 5], ~(1u << (slot & 31)));
+}
+template <bool PROPS, bool WIDE>
+static hipError_t launch_rows_cont_t(const Params& p, u32 n_slots, hipStream_t s) {
+    const void* k = (const void*)k_rows_cont<PROPS, WIDE>;
+    constexpr u32 LDS = RG_ROWS * 64 * (32 + (PROPS ? 4 : 0) + (WIDE ? 4 : 0));
+    static const hipError_t attr = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
+    if (attr != hipSuccess) return attr;
+    void* args[] = {(void*)&p};
+    return hipLaunchKernel(k, dim3(n_slots), dim3(64), args, LDS, s);
+}
+hipError_t launch_rows_cont(const Params& p, bool props, bool wide, u32 n_slots, hipStream_t s) {
+    if (!n_slots || !p.rows_cont) return hipSuccess;
+    if (wide) return props ? launch_rows_cont_t<true, true>(p, n_slots, s) : hipErrorInvalidValue;
+    return props ? launch_rows_cont_t<true, false>(p, n_slots, s) : launch_rows_cont_t<false, false>(p, n_slots, s);
 }
 
 template <int RW, bool PROPS, bool WIDE>
@@ -322,12 +446,12 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
                 __hip_atomic_store(p.rows_retry + k, d + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             }
         } else if (r.status == REG_HANDOFF) {
-            // between two ops: continue HBM-resident in this pass (fixed rows, 4 waves: the route of
-            // long and of many-writer documents, which outgrow their rows); inside one, or on the
-            // shared pool (8 / 12 waves: the handoff's code there spilled the row engine's registers,
-            // C3 1.34 -> 1.61 s), the host's re-run
+            // between two ops on fixed rows (4 waves: the route of long and of many-writer documents,
+            // the ones that outgrow their rows): continue HBM-resident in this pass (rows_dump,
+            // k_rows_cont); inside an op (half applied), or on the shared pool (8 / 12 waves, whose
+            // builds even the dump's code took from 0-16 to 8-90 spilled VGPRs), the host's re-run
             u32 why = 5;
-            if constexpr (!PAGED) why = r.midop ? 4u : rows_continue<(PROPS ? 1 : 0)>(p, r, d, at);
+            if constexpr (!PAGED) why = r.midop ? 4u : rows_dump(p, r, d, at);
             if (why) {
                 r.mark_spilled();
                 if (lane_id() == 0) p.res[d].spill_why |= why;

@@ -211,7 +211,10 @@ struct Params {
     u32* out_maps;            // property map of each final row with props (MAP_WORDS per row), or null
     u64 out_text_cap;
     u32* counters;            // [0] doc queue, [1] output rows, [2] docs re-run by the host,
-                              // [3] unused, [4] docs continued HBM-resident
+                              // [3] unused, [4] docs continued HBM-resident, [5] k_lds critical-path
+                              // queue, [6..7] output text units (u64),
+                              // [8] / [9] k_rows restarts pushed / popped, [10] k_rows documents
+                              // dumped for k_rows_cont (16 words, zeroed before each pass)
     unsigned char* spill;     // per-wave HBM slots (slot_bytes each): LDS waves 0..8G-1 keep theirs for
                               // documents that outgrow the LDS plan, HBM waves use slot_hbm0 + blockIdx
     u64 slot_bytes;

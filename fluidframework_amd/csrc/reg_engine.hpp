@@ -1111,8 +1111,8 @@ struct RegEngine {
     }
     // The same sift-down, lane-parallel while the heap fits positions 1..127 (registers 0 and 1):
     // every node k of register 0 (lane k) picks its child c(k) and whether the moved entry goes
-    // below it (lk > K[c(k)]) at once; the path from the root is then a chain of readlanes of
-    // next(k), and every node on it above the stop node takes its child's entry in one select.
+    // below it (lk > K[c(k)]) at once; the path from the root then follows two ballots of those
+    // decisions, and every node on it above the stop node takes its child's entry in one select.
     SD void pop_fast(u32 m, u32 lk, u32 ls, i32& newTop) {
         const V K0 = HK.get(0), K1 = HK.get(1), S0 = HS.get(0), S1 = HS.get(1);
         const V cl = L() * 2u, cr = cl + 1u;
@@ -1136,24 +1136,17 @@ struct RegEngine {
         const V kc = simd::sel(right, kR, kL);
         const V sc = simd::sel(right, sR, sL);
         const B go = (cl < m + 1u) & simd::slt(kc, (i32)lk);  // the moved entry goes below k
-        const V nxt = simd::sel(go, c, 0u);
         u32 k = 1;
         u64 path = 0;  // nodes of register 0 that take their child's entry
-        // E bit k: node k's parent moves down into k (its chosen, taken child). The path from the
-        // root follows E in scalar registers, two bits per level.
-        const u64 E = simd::ballot(simd::bperm(nxt, L() >> 1) == L()) & ~3ull;
-        while (k < 32u) {
-            const u32 two = (u32)(E >> (2 * k)) & 3u;
-            if (!two) break;
+        // G bit k: node k takes its chosen child's entry (the moved entry goes below k); Rt bit k:
+        // that child is the right one. The path from the root follows them in scalar registers
+        // (one crossbar round trip fewer than gathering each child's parent decision); nodes
+        // 32..63 continue into register 1.
+        const u64 G = simd::ballot(go), Rt = simd::ballot(right);
+        while (k < 64u) {
+            if (!((G >> k) & 1u)) break;
             path |= 1ull << k;
-            k = 2 * k + (two >> 1);
-        }
-        if (k >= 32u && k < 64u) {  // the last level of register 0 may continue into register 1
-            const u32 nk = simd::readlane(nxt, k);
-            if (nk) {
-                path |= 1ull << k;
-                k = nk;
-            }
+            k = 2 * k + (u32)((Rt >> k) & 1u);
         }
         const B mv = simd::ballot_mask(path);
         V N0 = simd::sel(mv, kc, K0), T0 = simd::sel(mv, sc, S0);

@@ -16,7 +16,12 @@ int mte_doc_result(mte_engine* e, uint32_t doc, void* out, size_t sz);
 int mte_run_info(mte_engine* e, uint32_t* spilled, double* lds_ms, double* hbm_ms, uint64_t* out_rows,
                  uint32_t* continued);
 /* Wave plan / routing of the last run by key: "lds_groups", "hbm_waves", "hbm_docs", "continued",
- * "spilled", "slot_bytes", "slots". */
+ * "spilled", "slot_bytes", "slots", "solo", "lean", "rows" (k_rows waves per CU, 0 = not used),
+ * "rows_restart_pushed" / "rows_restart_popped" (k_rows' in-pass restart queue), "rows_continued"
+ * (k_rows documents that continued HBM-resident in the pass, DocRes mode 6), pass timings ("solo_us",
+ * "emit_us", ...). DocRes::spill_why's low byte says why a k_rows document went to the host's re-run:
+ * 1 no free HBM slot, 2 the slot too small for its state, 3 no pool row held, 4 the pool full inside
+ * an op, 5 the shared-pool route (no in-pass continuation). */
 int mte_get_info(mte_engine* e, const char* key, int64_t* value);
 /* Tuning: "force_hbm", "pool_limit", "hbm_waves_per_cu", "slot_budget_mb". */
 int mte_set_option(mte_engine* e, const char* key, int64_t value);

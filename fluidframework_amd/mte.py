@@ -419,7 +419,10 @@ class Engine:
         for k in ("lds_groups", "hbm_waves", "hbm_docs", "slot_bytes", "slots", "solo", "solo_us", "solo_lead_us",
                   "solo_tail_us", "lean", "out_text", "rows", "rows_restart_pushed", "rows_restart_popped",
                   "rows_continued"):
-            out[k] = self.get_info(k)
+            try:
+                out[k] = self.get_info(k)
+            except MteError:  # (a key an older library build does not know)
+                out[k] = -1
         return out
 
     def get_info(self, key):

@@ -171,7 +171,8 @@ struct DocRes {
     u32 out_off;     // first row of this doc's final segments in the output pool
     u32 n_segs;
     u32 max_lb;      // peak leaf-block count
-    u32 mode;        // 0 LDS-resident, 1 HBM-resident, 2 continued HBM-resident, 3 solo LDS-resident
+    u32 mode;        // 0 LDS-resident, 1 HBM-resident (k_hbmq / host re-run), 2 continued HBM-resident,
+                     // 3 solo LDS-resident, 4 solo row engine, 5 k_rows, 6 k_rows then HBM-resident (k_rows_cont)
     u32 spill_why;   // why the LDS pass gave the doc up (engine.hpp St::spillWhy)
     u32 text_off;    // first unit of this doc's gathered final text in the output text pool
     u32 cu_n;        // catch-up delta records written (Engine::cu_record)

@@ -566,7 +566,11 @@ struct Doc {
                         D.match(D.row0 + run.e.x, run.props, D.row0 + row, hasP)) {
                         run.e.y = row;  // clone + append (:197-202)
                         run.e.z += len;
-                        run.tb += (ew & ESC_LEN) - (runHI && (ew & ESC_LO) ? 8u : 0u);
+                        // (a high surrogate ending the run meets a low one starting this row: the two
+                        // 6-byte escapes become one 4-byte UTF-8 pair; in 64 bits, since a row that is
+                        // only that low surrogate adds 6 - 8)
+                        run.tb += (u64)(ew & ESC_LEN);
+                        if (runHI && (ew & ESC_LO)) run.tb -= 8u;
                         runNL = (ew & ESC_NL) != 0;
                         runHI = (ew & ESC_HI) != 0;
                         continue;

@@ -63,3 +63,82 @@ def test_random_routes_match_oracle(engine, seed):
     finally:
         for k, v in DEFAULTS.items():
             engine.set_option(k, v)
+
+
+def random_json_log(seed, n_msgs):
+    """A random sequenced log through the JSON path: 2-100 writers with lagging refSeqs (minSeq
+    trails), text with '\\n' and surrogate pairs now and then, markers with a refType, annotates
+    (rewrite too) with property values incl. null, removes, group ops; every position valid in its
+    writer's view (the oracle's length_at)."""
+    from oracle import OracleDoc
+    from tests.oplog import ann, dumps, group, ins, msg, rem
+
+    rng = random.Random(seed)
+    n_writers = rng.choice([2, 3, 8, 20, 40, 70, 100])
+    names = [f"w{i}" for i in range(n_writers)]
+    d = OracleDoc("obs")
+    order, refs, out, seq = [], {}, [], 0
+    alphabet = "abcdefxyz" + ("\n" if rng.random() < 0.3 else "") + ("\U0001F600" if rng.random() < 0.3 else "")
+    for _ in range(n_msgs):
+        c = rng.choice(names)
+        if c not in order:
+            order.append(c)
+        short = order.index(c) + 1
+        lag = rng.randint(0, 6)
+        refs[c] = max(refs.get(c, 0), seq - lag, 0)
+        ref = refs[c]
+        L = d.length_at(ref, short)
+
+        def one(L):
+            r = rng.random()
+            if L == 0 or r < (0.6 if L < 300 else 0.4):
+                if rng.random() < 0.1:
+                    seg = {"marker": {"refType": rng.choice([0, 1, 2])}}
+                else:
+                    seg = {"text": "".join(rng.choice(alphabet) for _ in range(rng.randint(1, 6)))}
+                    if rng.random() < 0.2:
+                        seg["props"] = {"k": rng.choice([1, "v", None, True])}
+                return ins(rng.randint(0, L), seg), 1
+            a = rng.randint(0, L - 1)
+            b = min(L, a + rng.randint(1, 8))
+            if r < 0.8:
+                return rem(a, b), -(b - a)
+            props = {rng.choice(["bold", "size", "color"]): rng.choice([True, 12, "red", None])}
+            return ann(a, b, props, {"name": "rewrite"} if rng.random() < 0.2 else None), 0
+
+        if L > 4 and rng.random() < 0.08:  # a group of two ops: the second sees the first (same client)
+            o1, d1 = one(L)
+            o2, _ = one(L + d1)
+            contents = group(o1, o2)
+        else:
+            contents, _ = one(L)
+        seq += 1
+        msn = min(refs[x] for x in order) if len(order) == n_writers else 0
+        m = msg(c, seq, ref, contents, msn)
+        d.apply_json(dumps([m]))
+        if d.status()[0] != 0:
+            out.append(None)
+            break
+        out.append(m)
+    return [m for m in out if m is not None]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_json_logs_match_oracle(engine, seed):
+    """Random JSON logs (many writers, markers, properties, rewrite annotates, group ops, '\\n' and
+    surrogate pairs) through the builder: 24 documents per batch on whatever route the batch takes,
+    every status and checksum against the oracle's record path."""
+    rng = random.Random(1000 + seed)
+    b = mte.Builder()
+    for i in range(24):
+        b.add_doc(random_json_log(seed * 100 + i, rng.choice([60, 300, 1200])), observer="obs")
+    batch = b.batch()
+    engine.load(batch)
+    st = engine.replay()
+    info = engine.run_info()
+    print(f"seed {seed}: lean {info['lean']} rows {info['rows']} solo {info['solo']} "
+          f"modes {sorted({engine.doc_result(d)['mode'] for d in range(24)})} failed {st['failed_docs']}")
+    bad, _, _ = compare_batch_checksums(engine, batch, threads=16)
+    if bad:
+        compare_doc(engine, batch, bad[0], observer="obs")
+    assert not bad, bad

@@ -65,7 +65,7 @@ def test_random_routes_match_oracle(engine, seed):
             engine.set_option(k, v)
 
 
-def random_json_log(seed, n_msgs):
+def random_json_log(seed, n_msgs, n_writers=None, newline=None, emoji=None):
     """A random sequenced log through the JSON path: 2-100 writers with lagging refSeqs (minSeq
     trails), text with '\\n' and surrogate pairs now and then, markers with a refType, annotates
     (rewrite too) with property values incl. null, removes, group ops; every position valid in its
@@ -74,11 +74,13 @@ def random_json_log(seed, n_msgs):
     from tests.oplog import ann, dumps, group, ins, msg, rem
 
     rng = random.Random(seed)
-    n_writers = rng.choice([2, 3, 8, 20, 40, 70, 100])
+    n_writers = n_writers or rng.choice([2, 3, 8, 20, 40, 70, 100])
     names = [f"w{i}" for i in range(n_writers)]
     d = OracleDoc("obs")
     order, refs, out, seq = [], {}, [], 0
-    alphabet = "abcdefxyz" + ("\n" if rng.random() < 0.3 else "") + ("\U0001F600" if rng.random() < 0.3 else "")
+    nl = rng.random() < 0.3 if newline is None else newline
+    em = rng.random() < 0.3 if emoji is None else emoji
+    alphabet = "abcdefxyz" + ("\n" if nl else "") + ("\U0001F600" if em else "")
     for _ in range(n_msgs):
         c = rng.choice(names)
         if c not in order:
@@ -123,7 +125,7 @@ def random_json_log(seed, n_msgs):
     return [m for m in out if m is not None]
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(16))
 def test_random_json_logs_match_oracle(engine, seed):
     """Random JSON logs (many writers, markers, properties, rewrite annotates, group ops, '\\n' and
     surrogate pairs) through the builder: 24 documents per batch on whatever route the batch takes,
@@ -142,3 +144,56 @@ def test_random_json_logs_match_oracle(engine, seed):
     if bad:
         compare_doc(engine, batch, bad[0], observer="obs")
     assert not bad, bad
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_json_logs_legacy_format(seed):
+    """The same kind of random JSON logs emitted in the reference's default format (SnapshotLegacy:
+    header, body and the catch-up messages above minSeq, rewritten from their delta records): every
+    document's legacy tree equals the oracle's JSON-path tree byte for byte."""
+    import json as _json
+
+    from oracle import OracleDoc
+    from tests.gpu_helpers import first_diff
+    from tests.oplog import dumps
+
+    rng = random.Random(2000 + seed)
+    logs = [random_json_log(5000 + seed * 100 + i, rng.choice([40, 200, 700])) for i in range(16)]
+    b = mte.Builder()
+    for lg in logs:
+        b.add_doc(lg, observer="obs")
+    e = mte.Engine(0, snapshot_format=1)
+    try:
+        e.load(b.batch())
+        e.replay()
+        for d, lg in enumerate(logs):
+            o = OracleDoc("obs")
+            o.apply_json(dumps(lg))
+            assert o.status()[0] == 0 and e.status(d)[0] == 0, (d, o.status(), e.status(d))
+            want, got = o.snapshot_legacy_json(), e.snapshot_legacy(d)
+            if got != want:
+                i, ga, oa = first_diff(got, want)
+                raise AssertionError(f"doc {d}: legacy tree differs at {i}\n gpu: {ga}\n orc: {oa}")
+            _json.loads(got)
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("seed,writers,newline,emoji", [(0, 3, False, False), (1, 8, True, False),
+                                                        (2, 40, False, True), (3, 100, True, True)])
+def test_random_json_log_on_the_solo_route(engine, seed, writers, newline, emoji):
+    """One long random JSON log alone (k_solo: the FULL row engine to the end, or handing over to the
+    LDS plan -- '\n' in the payload at the start, a client above 63 at its first op): full segment
+    table, text and snapshot against the oracle."""
+    engine.set_option("solo_min_ops", 1)
+    try:
+        b = mte.Builder()
+        b.add_doc(random_json_log(9000 + seed, 6000, writers, newline, emoji), observer="obs")
+        batch = b.batch()
+        engine.load(batch)
+        engine.replay()
+        assert engine.run_info()["solo"] == 1
+        print(f"seed {seed}: mode {engine.doc_result(0)['mode']}")
+        compare_doc(engine, batch, 0, observer="obs")
+    finally:
+        engine.set_option("solo_min_ops", 20000)

@@ -1,0 +1,77 @@
+"""GPU probe: the suite's random generators over many more seeds than the suite runs -- SharedMatrix cell
+logs (tests/test_matrix.py matrix_cell_log), relative-position logs (tests/test_relative_pos.py
+relative_log) and random JSON logs (tests/test_gpu_fuzz.py random_json_log) -- each checked against the
+oracle (segment tables, snapshots, checksums). Prints one line per family; exits 1 on the first
+mismatch, naming it. Usage: python tools/wide_sweep.py [n_seeds]"""
+import ctypes
+import json
+import os
+import random
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fluidframework_amd import mte  # noqa: E402
+from tests.gpu_helpers import compare_batch_checksums, compare_doc  # noqa: E402
+from tests.test_gpu_fuzz import random_json_log  # noqa: E402
+from tests.test_matrix import matrix_cell_log, oracle_matrix  # noqa: E402
+from tests.test_relative_pos import relative_log  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 40
+e = mte.Engine(0)
+bad = 0
+
+# SharedMatrix: vectors' segment tables and snapshots, the matrix summary
+logs = [matrix_cell_log(100 + s, total=random.Random(s).choice([300, 900, 2000])) for s in range(n)]
+b = mte.Builder()
+pairs = [b.add_matrix_log(m, observer="obs") for m in logs]
+e.load(b.batch())
+e.replay()
+for s, (m, (ri, ci)) in enumerate(zip(logs, pairs)):
+    o = oracle_matrix(m)
+    ok = all(e.segments_json(d) == v.segments_json() and e.snapshot_json(d) == v.snapshot_json()
+             for d, v in ((ri, o.rows), (ci, o.cols)))
+    ok = ok and json.loads(e.snapshot_matrix(ri, ci)) == json.loads(o.snapshot_json())
+    if not ok:
+        print(f"matrix seed {100 + s}: MISMATCH", flush=True)
+        bad += 1
+print(f"matrix: {n} logs, {bad} mismatches", flush=True)
+
+# relative positions
+logs = [relative_log(200 + s, n=random.Random(s).choice([200, 600])) for s in range(n)]
+b = mte.Builder()
+for m in logs:
+    b.add_doc(m)
+batch = b.batch()
+e.load(batch)
+e.replay()
+rb = 0
+for d in range(batch.n_docs):
+    try:
+        compare_doc(e, batch, d)
+    except AssertionError as x:
+        print(f"relpos seed {200 + d}: {str(x)[:300]}", flush=True)
+        rb += 1
+print(f"relpos: {n} logs, {rb} mismatches", flush=True)
+bad += rb
+
+# random JSON logs, four batches
+jb = 0
+for k in range(4):
+    rng = random.Random(5000 + k)
+    b = mte.Builder()
+    for i in range(n):
+        b.add_doc(random_json_log(20000 + k * 1000 + i, rng.choice([60, 300, 1500])), observer="obs")
+    batch = b.batch()
+    e.load(batch)
+    e.replay()
+    bb, _, _ = compare_batch_checksums(e, batch, threads=16)
+    for d in bb[:3]:
+        try:
+            compare_doc(e, batch, d, observer="obs")
+        except AssertionError as x:
+            print(f"json batch {k} doc {d}: {str(x)[:300]}", flush=True)
+    jb += len(bb)
+print(f"json: {4 * n} logs, {jb} mismatches", flush=True)
+bad += jb
+e.close()
+sys.exit(1 if bad else 0)

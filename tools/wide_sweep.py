@@ -73,5 +73,28 @@ for k in range(4):
     jb += len(bb)
 print(f"json: {4 * n} logs, {jb} mismatches", flush=True)
 bad += jb
+
+# generated batches under random engine options (tests/test_gpu_fuzz.py draw), seeds past the suite's
+from fluidframework_amd.shard import zipf_op_counts  # noqa: E402
+from tests.test_gpu_fuzz import DEFAULTS, draw  # noqa: E402
+
+gb = 0
+for seed in range(100, 100 + n):
+    kind, clients, n_docs, hi, opts = draw(seed)
+    for k, v in opts.items():
+        e.set_option(k, v)
+    counts = zipf_op_counts(n_docs, seed=seed, lo=20, hi=hi)
+    e.generate(kind, n_docs, 0, n_clients=clients, seed=100 + seed, ops_per_doc=counts)
+    batch = e.export_batch()
+    st = e.replay()
+    bb, _, _ = compare_batch_checksums(e, batch, threads=16)
+    if bb or st["failed_docs"]:
+        print(f"generated seed {seed} {kind} {clients} {n_docs} {hi} {opts}: {len(bb)} mismatches, "
+              f"{st['failed_docs']} failed", flush=True)
+        gb += 1
+    for k, v in DEFAULTS.items():
+        e.set_option(k, v)
+print(f"generated: {n} batches, {gb} with mismatches", flush=True)
+bad += gb
 e.close()
 sys.exit(1 if bad else 0)

@@ -96,5 +96,58 @@ for seed in range(100, 100 + n):
         e.set_option(k, v)
 print(f"generated: {n} batches, {gb} with mismatches", flush=True)
 bad += gb
+
+# resume from a summary of a random prefix (the oracle's SnapshotV1), the rest as catch-up
+from oracle import OracleDoc  # noqa: E402
+from tests.oplog import dumps  # noqa: E402
+
+sb = 0
+rng = random.Random(77)
+cases = []
+for i in range(n):
+    log = random_json_log(40000 + i, rng.choice([80, 400, 1500]))
+    k = rng.randint(1, len(log) - 1)
+    o = OracleDoc("obs")
+    o.apply_json(dumps(log[:k]))
+    cases.append((o.snapshot_json(), log[k:]))
+b = mte.Builder()
+for summ, suffix in cases:
+    b.add_doc_from_summary(summ, suffix, observer="obs")
+batch = b.batch()
+e.load(batch)
+e.replay()
+for d, (summ, suffix) in enumerate(cases):
+    try:
+        compare_doc(e, batch, d, observer="obs")
+        if not e.status(d)[0]:
+            ref = OracleDoc("obs")
+            ref.load_summary(summ)
+            ref.apply_json(dumps(suffix))
+            assert json.loads(e.snapshot_json(d)) == json.loads(ref.snapshot_json()), "snapshot vs JSON-path load"
+    except AssertionError as x:
+        print(f"summary case {d}: {str(x)[:300]}", flush=True)
+        sb += 1
+print(f"summary: {n} resumed logs, {sb} mismatches", flush=True)
+bad += sb
 e.close()
+
+# the legacy format (SnapshotLegacy with catch-up messages)
+lb = 0
+el = mte.Engine(0, snapshot_format=1)
+rng = random.Random(88)
+logs = [random_json_log(50000 + i, rng.choice([40, 200, 700])) for i in range(n)]
+b = mte.Builder()
+for lg in logs:
+    b.add_doc(lg, observer="obs")
+el.load(b.batch())
+el.replay()
+for d, lg in enumerate(logs):
+    o = OracleDoc("obs")
+    o.apply_json(dumps(lg))
+    if o.status()[0] != el.status(d)[0] or (not o.status()[0] and o.snapshot_legacy_json() != el.snapshot_legacy(d)):
+        print(f"legacy doc {d}: MISMATCH", flush=True)
+        lb += 1
+print(f"legacy: {n} logs, {lb} mismatches", flush=True)
+bad += lb
+el.close()
 sys.exit(1 if bad else 0)

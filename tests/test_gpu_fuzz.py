@@ -65,7 +65,7 @@ def test_random_routes_match_oracle(engine, seed):
             engine.set_option(k, v)
 
 
-def random_json_log(seed, n_msgs, n_writers=None, newline=None, emoji=None):
+def random_json_log(seed, n_msgs, n_writers=None, newline=None, emoji=None, text_max=6, extra="", n_keys=3):
     """A random sequenced log through the JSON path: 2-100 writers with lagging refSeqs (minSeq
     trails), text with '\\n' and surrogate pairs now and then, markers with a refType, annotates
     (rewrite too) with property values incl. null, removes, group ops; every position valid in its
@@ -80,7 +80,8 @@ def random_json_log(seed, n_msgs, n_writers=None, newline=None, emoji=None):
     order, refs, out, seq = [], {}, [], 0
     nl = rng.random() < 0.3 if newline is None else newline
     em = rng.random() < 0.3 if emoji is None else emoji
-    alphabet = "abcdefxyz" + ("\n" if nl else "") + ("\U0001F600" if em else "")
+    alphabet = "abcdefxyz" + ("\n" if nl else "") + ("\U0001F600" if em else "") + extra
+    keys = ["bold", "size", "color"] + [f"k{j}" for j in range(max(0, n_keys - 3))]
     for _ in range(n_msgs):
         c = rng.choice(names)
         if c not in order:
@@ -97,7 +98,7 @@ def random_json_log(seed, n_msgs, n_writers=None, newline=None, emoji=None):
                 if rng.random() < 0.1:
                     seg = {"marker": {"refType": rng.choice([0, 1, 2])}}
                 else:
-                    seg = {"text": "".join(rng.choice(alphabet) for _ in range(rng.randint(1, 6)))}
+                    seg = {"text": "".join(rng.choice(alphabet) for _ in range(rng.randint(1, text_max)))}
                     if rng.random() < 0.2:
                         seg["props"] = {"k": rng.choice([1, "v", None, True])}
                 return ins(rng.randint(0, L), seg), 1
@@ -105,7 +106,8 @@ def random_json_log(seed, n_msgs, n_writers=None, newline=None, emoji=None):
             b = min(L, a + rng.randint(1, 8))
             if r < 0.8:
                 return rem(a, b), -(b - a)
-            props = {rng.choice(["bold", "size", "color"]): rng.choice([True, 12, "red", None])}
+            props = {rng.choice(keys): rng.choice([True, 12, "red", None, {"n": [1, "x"]}, 0.5])
+                     for _ in range(rng.randint(1, 3))}
             return ann(a, b, props, {"name": "rewrite"} if rng.random() < 0.2 else None), 0
 
         if L > 4 and rng.random() < 0.08:  # a group of two ops: the second sees the first (same client)

@@ -131,6 +131,30 @@ print(f"summary: {n} resumed logs, {sb} mismatches", flush=True)
 bad += sb
 e.close()
 
+# stress: long texts (runs past the 256-unit granularity), quotes, backslashes, control characters,
+# non-BMP and combining characters, up to 12 property keys (wide map records), object values
+xb = 0
+for k in range(2):
+    rng = random.Random(6000 + k)
+    b = mte.Builder()
+    for i in range(n):
+        b.add_doc(random_json_log(60000 + k * 1000 + i, rng.choice([100, 500]), text_max=rng.choice([20, 400]),
+                                  extra='"\\\x01\t\u00e9\u0301\U0001F680', n_keys=rng.choice([3, 12])), observer="obs")
+    batch = b.batch()
+    e = mte.Engine(0)
+    e.load(batch)
+    e.replay()
+    bb, _, _ = compare_batch_checksums(e, batch, threads=16)
+    for d in bb[:3]:
+        try:
+            compare_doc(e, batch, d, observer="obs")
+        except AssertionError as x:
+            print(f"stress batch {k} doc {d}: {str(x)[:300]}", flush=True)
+    xb += len(bb)
+    e.close()
+print(f"stress: {2 * n} logs, {xb} mismatches", flush=True)
+bad += xb
+
 # the legacy format (SnapshotLegacy with catch-up messages)
 lb = 0
 el = mte.Engine(0, snapshot_format=1)

@@ -155,6 +155,34 @@ for k in range(2):
 print(f"stress: {2 * n} logs, {xb} mismatches", flush=True)
 bad += xb
 
+# JSON logs without '\n' and with at most 63 writers, so the batches take k_rows (PROPS, WIDE when a
+# document has 32+ writers), at the auto route and at 4 / 12 waves
+rb2 = 0
+for k, waves in enumerate((-1, 4, 12, -1)):
+    rng = random.Random(7000 + k)
+    b = mte.Builder()
+    for i in range(n):
+        b.add_doc(random_json_log(70000 + k * 1000 + i, rng.choice([100, 600, 2000]),
+                                  n_writers=rng.choice([3, 8, 20] if k < 3 else [40, 60]), newline=False), observer="obs")
+    batch = b.batch()
+    e = mte.Engine(0)
+    e.set_option("rows_bulk", waves)
+    e.load(batch)
+    e.replay()
+    info = e.run_info()
+    bb, _, _ = compare_batch_checksums(e, batch, threads=16)
+    for d in bb[:3]:
+        try:
+            compare_doc(e, batch, d, observer="obs")
+        except AssertionError as x:
+            print(f"json-rows batch {k} doc {d}: {str(x)[:300]}", flush=True)
+    print(f"json-rows batch {k}: rows {info['rows']} lean {info['lean']} spilled {info['spilled']} "
+          f"continued {info['rows_continued']} mismatches {len(bb)}", flush=True)
+    rb2 += len(bb)
+    e.close()
+print(f"json-rows: {4 * n} logs, {rb2} mismatches", flush=True)
+bad += rb2
+
 # the legacy format (SnapshotLegacy with catch-up messages)
 lb = 0
 el = mte.Engine(0, snapshot_format=1)

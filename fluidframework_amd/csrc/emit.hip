@@ -452,10 +452,13 @@ struct Doc {
         uint4 bv;          // this lane's row of the batch: vis
         u32 be, bay, btof;  // ... its emission word, aux.y (markers / permutation runs), text offset
         bool open, pend, filled;
+        bool sat;           // a row's JSON text size may not fit ESC_LEN (6 bytes a unit at most): COUNT
+                            // gives the walk up and the document takes the entry-table route (emit)
         Item run, pe;       // the open run, and a merge-info entry queued behind it
         bool runText, runPerm, runNL, runHI;
         MTE_DEV Walk(const Doc& d, bool count)
-            : D(d), counting(count), n(d.r.n_segs), base(0), j(64), tcarry(0), open(false), pend(false), filled(false) {}
+            : D(d), counting(count), n(d.r.n_segs), base(0), j(64), tcarry(0), open(false), pend(false), filled(false),
+              sat(false) {}
         MTE_DEV void fill() {
             const u32 L = lane_id(), k = base + L;
             bv = make_uint4(0, 0, 0, 0);
@@ -481,6 +484,10 @@ struct Doc {
             btof = tcarry + incl - tl;
             tcarry += wave_read(incl, 63);
             if (!counting) return;
+            if (wave_ballot(tl > ESC_LEN / 6u)) {
+                sat = true;
+                return;
+            }
             // the emission word of every row of the batch (esc_unit over its text): short rows one
             // per lane, rows longer than 32 units by the whole wave, 64 units per step
             const u16* txt = D.p.text + D.r.text_off;
@@ -536,6 +543,7 @@ struct Doc {
                     filled = true;
                     j = 0;
                     if (base < n) fill();
+                    if (sat) return false;
                 }
                 const u32 row = base + j;
                 if (row >= n) {  // the end: the open run
@@ -634,6 +642,9 @@ struct Doc {
         put(o, "}");
     }
 
+    // n_ent's flag: COUNT found a row too long for the emission words (Walk::sat), so the document's
+    // entries are in ent (build_entries) and WRITE takes emit, which reads the text
+    static constexpr u32 SAT_ROUTE = 0x80000000u;
     // COUNT (SnapshotV1): byte count and blob count; the chunk table into ent[row0 + c]
     MTE_DEV u64 count_v1(u32& ne, u32& nblobs) const {
         const u32 L = lane_id(), chunk = p.chunk;
@@ -644,7 +655,9 @@ struct Doc {
         ne = 0;
         Item it;
         auto close_chunk = [&]() {
-            if (L == 0) p.ent[row0 + nch] = make_uint4(first, cnt, (u32)len, 0u);
+            // (a document with no segments owns no rows: its one empty chunk is not stored, since
+            // row0 is then the next document's first row; write_v1 rebuilds it as (0, 0, 0))
+            if (L == 0 && r.n_segs) p.ent[row0 + nch] = make_uint4(first, cnt, (u32)len, 0u);
             put(o, "{\"version\":\"1\",\"segmentCount\":");
             put_int(o, cnt);
             put(o, ",\"length\":");
@@ -666,6 +679,10 @@ struct Doc {
             cnt++;
             len += it.e.z;
             if (len >= chunk) close_chunk();
+        }
+        if (w.sat) {
+            ne = SAT_ROUTE;
+            return 0;
         }
         if (cnt || nch == 0) close_chunk();
         // the header chunk's metadata
@@ -693,10 +710,11 @@ struct Doc {
         Walk w(*this, false);
         Out o{out, 0};
         u64 totalLen = 0;
-        for (u32 c = 0; c < nch; c++) totalLen += p.ent[row0 + c].z;
+        const bool empty = r.n_segs == 0;  // (COUNT stored no chunk row: one empty chunk)
+        for (u32 c = 0; c < nch && !empty; c++) totalLen += p.ent[row0 + c].z;
         Item it;
         for (u32 c = 0; c < nch; c++) {
-            const uint4 ch = p.ent[row0 + c];
+            const uint4 ch = empty ? make_uint4(0u, 0u, 0u, 0u) : p.ent[row0 + c];
             if (L == 0) blob_off[c] = o.pos;
             put(o, "{\"version\":\"1\",\"segmentCount\":");
             put_int(o, ch.y);
@@ -827,6 +845,13 @@ __global__ __launch_bounds__(64) void k_emit_count(EmitParams p) {
             bytes = doc.emit(ne, nullptr, nullptr, nb);
         } else {
             bytes = doc.count_v1(ne, nb);
+            if (ne == Doc::SAT_ROUTE) {
+                wave_sync();  // (count_v1's chunk rows are overwritten by the entries)
+                ne = doc.build_entries();
+                wave_sync();
+                bytes = doc.emit(ne, nullptr, nullptr, nb);
+                ne |= Doc::SAT_ROUTE;
+            }
         }
     }
     if (lane_id() == 0) {
@@ -844,7 +869,9 @@ __global__ __launch_bounds__(64) void k_emit_write(EmitParams p) {
     Doc doc(p, d);
     if (doc.r.status != 0 || p.size[d] == 0) return;
     u32 nb = 0;
-    if (p.legacy || !p.esc) doc.emit(p.n_ent[d], p.out + p.out_off[d], p.blob_off + p.blob_base[d], nb);
+    const u32 ne = p.n_ent[d];
+    if (p.legacy || !p.esc || (ne & Doc::SAT_ROUTE))
+        doc.emit(ne & ~Doc::SAT_ROUTE, p.out + p.out_off[d], p.blob_off + p.blob_base[d], nb);
     else doc.write_v1(p.n_ent[d], p.nblobs[d], p.out + p.out_off[d], p.blob_off + p.blob_base[d]);
 }
 

@@ -75,3 +75,51 @@ def test_emission_escapes_and_runs():
         assert e.get_info("emit_us") >= 0
     finally:
         e.close()
+
+
+def emptied_log(n, collab=True):
+    """n inserts, then one remove of everything; the MSN reaches the remove's seq, so zamboni
+    detaches every segment and the final table is empty."""
+    out, seq, L = [], 0, 0
+    for i in range(n):
+        seq += 1
+        out.append(msg(f"w{i % 2}" if collab else "local", seq, seq - 1, ins(L, "ab"), seq - 1))
+        L += 2
+    seq += 1
+    out.append(msg("w0" if collab else "local", seq, seq - 1, rem(0, L), seq - 1))
+    for _ in range(2):  # the MSN catches up to the remove (empty removes carry it)
+        seq += 1
+        out.append(msg("w1" if collab else "local", seq, seq - 1, rem(0, 0), seq - 1))
+    return out
+
+
+@pytest.mark.gpu
+def test_empty_documents_beside_full_ones():
+    """a document with no final segments owns no output rows, so its SnapshotV1
+    chunk record must not land on the next document's first row. Empty logs, logs whose every
+    segment zamboni detached, and ordinary documents interleaved; every snapshot byte-equal to the
+    oracle's."""
+    from tests.gpu_helpers import compare_doc
+
+    b = mte.Builder()
+    kinds = []
+    for i in range(48):
+        k = i % 4
+        if k == 0:
+            b.add_doc(json.dumps([]))
+        elif k == 1:
+            b.add_doc(json.dumps(emptied_log(5 + i)))
+        else:
+            b.add_doc(json.dumps(escape_log(True)[: 5 + i % 20]))
+        kinds.append(k)
+    batch = b.batch()
+    e = mte.Engine(0)
+    try:
+        e.load(batch)
+        e.replay()
+        for d in range(len(kinds)):
+            compare_doc(e, batch, d)
+            if kinds[d] < 2:
+                assert json.loads(e.snapshot_json(d)) is not None
+    finally:
+        e.close()

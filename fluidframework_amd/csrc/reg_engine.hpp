@@ -49,6 +49,17 @@ constexpr u32 ROWS_POOL_WORDS = 3;         // k_rows' pool row mask (mte_solo.hi
 constexpr u32 ROWS_WAIT_TRIES = 20000;     // a wave finding the pool full retries this often (s_sleep 8)
 // needsScour (mergeTree.ts:63) in meta bits 24..25 of every slot lane of a block
 constexpr u32 NS_SHIFT = 24, NS_MASK = 3u << NS_SHIFT;
+// critical-path variants (A/B switches): pairwise resolve, the heap's last entry read
+// directly, the split's right piece made by a row shift
+#ifndef MTE_RES2
+#define MTE_RES2 0
+#endif
+#ifndef MTE_HEAP_LAST
+#define MTE_HEAP_LAST 0
+#endif
+#ifndef MTE_SPLIT_SHIFT
+#define MTE_SPLIT_SHIFT 0
+#endif
 static_assert(RG_BLOCKS <= SOLO_POOL, "the rows live in the SoloPlan's slot arrays");
 
 // Phase profile of the row engine (MTE_PROFILE device builds, `make prof`): inclusive s_memtime
@@ -95,6 +106,23 @@ struct RgMark {
     } while (0)
 #define RG_COUNT(slot, n) \
     do {                  \
+    } while (0)
+#endif
+
+// Event statistics of the CPU build (MTE_CPU_STATS, tools/rg_stats.py only): what the critical
+// document's ops do (rows a resolve scans, heap sizes at a pop, scour outcomes), to size the device
+// code paths. Nothing in a device build.
+#if defined(MTE_CPU) && defined(MTE_CPU_STATS)
+enum RgStat : u32 {
+    RS_OPS, RS_RESOLVE, RS_RES_ROWS, RS_RES_NROWS, RS_POP, RS_POP_BIG, RS_POP_HEAP, RS_FIND_ROWS, RS_SCOUR,
+    RS_SCOUR_NOP, RS_SCOUR_SERIAL, RS_SCOUR_COPY, RS_PACK, RS_SPLIT_BLK, RS_MOVE_SLOTS, RS_SPLIT_AT,
+    RS_ZAM_CALLS, RS_ZAM_POPS, RS_LRU_PUSH, RS_RANGE_ROWS, RS_N
+};
+inline u64 g_rg_stats[RS_N + 64];
+#define RG_STAT(i, n) (g_rg_stats[i] += (u64)(n))
+#else
+#define RG_STAT(i, n) \
+    do {              \
     } while (0)
 #endif
 
@@ -859,6 +887,8 @@ struct RegEngine {
         f.row = 0;
         f.carry = 0;
         const u32 nrows = (n_lb + 7) >> 3;
+        RG_STAT(RS_RESOLVE, 1);
+        RG_STAT(RS_RES_NROWS, nrows);
         u32 carry = carry0;
         // Block ends are the lanes 8g+7; blocks past n_lb are empty (rows past the last block stay
         // zero), so their ends never reach pos before a real block's end does.
@@ -885,10 +915,46 @@ struct RegEngine {
                 f.r = (i32)simd::readlane(rr, l);
             }
         };
+        const u32 last = nrows - 1;
+#if MTE_RES2
+        // Two rows per step: their visibility and DPP scans are independent, so they interleave (no
+        // scan waits out its DPP hazards alone) and one branch covers both; the next pair's rows load
+        // while this pair is scanned. Row r+1 past the last row re-reads the last row and is ignored.
+        {
+            Row a = row(r0), b = ldrow(r0 + 1 < last ? r0 + 1 : last);
+            u32 r = r0;
+            for (;;) {
+                const u32 rn = r + 2;
+                const Row a2 = ldrow(rn < last ? rn : last), b2 = ldrow(rn + 1 < last ? rn + 1 : last);
+                RG_COUNT(RP_N_RESOLVE, 2);
+                RG_STAT(RS_RES_ROWS, 2);
+                const V va = vis(a, R, C), vb = vis(b, R, C);
+                const V sa = simd::scan_incl(va), sb = simd::scan_incl(vb);
+                const V ia = sa + carry;
+                const u64 ha = simd::ballot(end & simd::sge(ia, pos));
+                const u32 ca = simd::readlane(ia, 63);  // visible length before row r+1
+                const V ib = sb + ca;
+                const u64 hb = r + 1 < nrows ? simd::ballot(end & simd::sge(ib, pos)) : 0ull;
+                if (ha) {
+                    hit_row(a, r, ha, va, ia);
+                    return f;
+                }
+                if (hb) {
+                    carry = ca;
+                    hit_row(b, r + 1, hb, vb, ib);
+                    return f;
+                }
+                carry = simd::readlane(ib, 63);
+                if (rn >= nrows) return f;
+                r = rn;
+                a = a2;
+                b = b2;
+            }
+        }
+#endif
         // two row buffers, each refilled (unconditionally: the last row again at the end, so the
         // LDS counter wait stays exact) while the other one is scanned; the loop only finds the hit
         // row (no state written in it, so no per-row register copies)
-        const u32 last = nrows - 1;
         Row a = row(r0), b;
         V v, incl;
         u64 hit = 0;
@@ -898,6 +964,7 @@ struct RegEngine {
             b = ldrow(r + 1 < last ? r + 1 : last);
             RG_COUNT(RP_N_RESOLVE, 1);
             v = vis(a, R, C);
+            RG_STAT(RS_RES_ROWS, 1);
             incl = simd::scan_incl(v) + carry;
             hit = simd::ballot(end & simd::sge(incl, pos));
             if (hit) break;
@@ -906,6 +973,7 @@ struct RegEngine {
             a = ldrow(r + 1 < last ? r + 1 : last);
             RG_COUNT(RP_N_RESOLVE, 1);
             v = vis(b, R, C);
+            RG_STAT(RS_RES_ROWS, 1);
             incl = simd::scan_incl(v) + carry;
             hit = simd::ballot(end & simd::sge(incl, pos));
             if (hit) {
@@ -967,6 +1035,7 @@ struct RegEngine {
         if (d == 0) return;
         RG_COUNT(RP_N_MOVE, n_lb - from);
         const u32 n = (n_lb - from) * 8;
+        RG_STAT(RS_MOVE_SLOTS, n);
         if (d > 0) {
             mv_slots((from + (u32)d) * 8, from * 8, n);
         } else {
@@ -1019,6 +1088,7 @@ struct RegEngine {
     SD void split_block(u32 k) {
         RG_PROF(RP_SPLIT);
         RG_COUNT(RP_N_SPLIT_BLK, 1);
+        RG_STAT(RS_SPLIT_BLK, 1);
         if (!ensure_blocks(n_lb + 1)) return;
         shift_blocks(k + 1, 1);
         const u32 r = k >> 3, r2 = (k + 1) >> 3;
@@ -1136,6 +1206,7 @@ struct RegEngine {
             return;
         }
         const u32 n = ++heapSize;
+        RG_STAT(RS_LRU_PUSH, 1);
         if (n == 1) heapTop = key;
         hset(n, sid, (u32)key);
     }
@@ -1222,8 +1293,25 @@ struct RegEngine {
         RG_PROF(RP_HEAP);
         RG_COUNT(RP_N_POP, 1);
         const u32 n = heapSize, m = n - 1;
+        RG_STAT(RS_POP, 1);
+        RG_STAT(RS_POP_BIG, m >= 128u);
+        RG_STAT(RS_POP_HEAP, n);
         const u32 top = hrd<0>(HS, 1);
+#if MTE_HEAP_LAST
+        // the last entry of a heap of < 128 (registers 0 and 1): one select of the register, one
+        // readlane each, instead of the run-time level dispatch of hkey / hsid
+        u32 lk, ls;
+        if (n < 128u) {
+            const bool lo = n < 64u;
+            lk = simd::readlane(lo ? HK.r0 : HK.r1, n & 63u);
+            ls = simd::readlane(lo ? HS.r0 : HS.r1, n & 63u);
+        } else {
+            lk = hkey(n);
+            ls = hsid(n);
+        }
+#else
         const u32 lk = hkey(n), ls = hsid(n);
+#endif
         i32 newTop = (i32)lk;
         if (m >= 1) {
             if (m < 128u) pop_fast(m, lk, ls, newTop);
@@ -1247,6 +1335,7 @@ struct RegEngine {
     SD u32 find_seg(u32 sid) {
         RG_PROF(RP_FIND_SEG);
         const u32 nrows = (n_lb + 7) >> 3;
+        RG_STAT(RS_FIND_ROWS, nrows);
         for (u32 r0 = 0; r0 < nrows; r0 += 8) {  // eight rows' reads in flight per round
             V s8[8];
             for (u32 i = 0; i < 8; i++) s8[i] = ld_sid(r0 + i < nrows ? r0 + i : r0);
@@ -1353,8 +1442,15 @@ struct RegEngine {
                 if (!match_props(simd::readlane(w.props, gb + sb - 1), simd::readlane(w.props, gb + sb))) mJOIN &= ~(1u << sb);
             }
         }
-        if (!mDROP && !mJOIN) return cnt;            // nothing dropped, nothing merged
-        if (mJOIN & group_bits(simd::ballot(w.len > (u32)GRANULARITY), k)) return scour_serial(k, cnt);
+        RG_STAT(RS_SCOUR, 1);
+        if (!mDROP && !mJOIN) {  // nothing dropped, nothing merged
+            RG_STAT(RS_SCOUR_NOP, 1);
+            return cnt;
+        }
+        if (mJOIN & group_bits(simd::ballot(w.len > (u32)GRANULARITY), k)) {
+            RG_STAT(RS_SCOUR_SERIAL, 1);
+            return scour_serial(k, cnt);
+        }
         RG_COUNT(RP_N_SCOUR_CHANGED, 1);
         fence_arena();
         const V sl = L() & 7u;
@@ -1448,6 +1544,7 @@ struct RegEngine {
         const V jinc = simd::scan_incl(jlen);
         const u32 total = simd::readlane(jinc, 63);
         if (!total) return;
+        RG_STAT(RS_SCOUR_COPY, 1);
         const V jstart = jinc - jlen;
         u64 jm = simd::ballot(jlen != 0u);
         u16* ar = arena_cur();
@@ -1626,6 +1723,7 @@ struct RegEngine {
     SD void pack_leaves(u32 pi, u32 m, u32 k0, V cn) {
         RG_PROF(RP_PACK);
         RG_COUNT(RP_N_PACK, 1);
+        RG_STAT(RS_PACK, 1);
         const u32 T = simd::readlane(simd::scan_incl(simd::sel(L() < m, cn, 0u)), 63);
         u32 kk = T / 4;
         if (kk > 7) kk = 7;
@@ -1727,8 +1825,10 @@ struct RegEngine {
     // zamboniSegments (mergeTree.ts:1422-1478): up to 2 heap entries with maxSeq <= minSeq.
     SD void zamboni() {
         RG_PROF(RP_ZAMBONI);
+        RG_STAT(RS_ZAM_CALLS, 1);
         for (int i = 0; i < 2 && !status; i++) {
             if (heapSize == 0 || heapTop > minSeq) break;
+            RG_STAT(RS_ZAM_POPS, 1);
             const u32 sid = heap_pop();
             const u32 k = find_seg(sid);
             if (k == NONE) continue;  // no longer linked
@@ -1760,6 +1860,47 @@ struct RegEngine {
     // right piece copies everything and follows the left one. Returns the insert_slot result.
     SD u32 split_at(const RFound& f) {
         RG_PROF(RP_SPLIT_AT);
+        RG_STAT(RS_SPLIT_AT, 1);
+#if MTE_SPLIT_SHIFT
+        // The right piece made in the row itself: every slot after the split one takes its left
+        // neighbour (so the right piece starts as a copy of the segment), then the two pieces' length,
+        // text offset, capacity and the new id by per-lane selects -- no readlane of the segment's
+        // fields into scalars and back.
+        {
+            if (f.cnt >= 8) {
+                fail(MTE_DOC_CAPACITY, curSeq);
+                return NONE;
+            }
+            const u32 sid = new_sid();
+            if (sid == NONE) return NONE;
+            const u32 r = f.k >> 3, gb = gbase(f.k), sj = (u32)f.slot, rr = (u32)f.r;
+            Row& w = rowref(r);
+            const V sl = L() & 7u;
+            const B mv = in_group(f.k) & (sl > sj);  // (never a group's first lane: no value crosses groups)
+            const B at = L() == gb + sj + 1, lf = L() == gb + sj;
+            auto sh = [&](V& x) MTE_LI { x = simd::sel(mv, simd::row_shr1(x), x); };
+            sh(w.len);
+            sh(w.seq);
+            sh(w.rseq);
+            sh(w.meta);
+            sh(w.toff);
+            sh(w.cap);
+            sh(w.rm);
+            sh(w.sid);
+            if constexpr (PROPS) sh(w.props);  // the right piece shares the map
+            if constexpr (WIDE) sh(w.rm2);
+            // arena text: the capacity is split between the pieces (payload text has none)
+            const B ar = (w.toff & ARENA_BIT) != 0u;
+            w.cap = simd::sel(at, simd::sel(ar, w.cap - rr, 0u), simd::sel(lf, simd::sel(ar, simd::splat(rr), 0u), w.cap));
+            w.len = simd::sel(at, w.len - rr, simd::sel(lf, simd::splat(rr), w.len));
+            w.toff = simd::sel(at, w.toff + rr, w.toff);
+            w.sid = simd::sel(at, sid, w.sid);
+            writeback(r);
+            if (f.cnt + 1 < 8) return f.k;
+            split_block(f.k);
+            return sj + 1 < 4 ? f.k : f.k + 1;
+        }
+#endif
         const u32 r = f.k >> 3, l = gbase(f.k) + (u32)f.slot;
         const Row w = row(r);
         RSeg t;
@@ -1948,6 +2089,7 @@ struct RegEngine {
     // Client.applyMsg for one op record (client.ts:805-836); false => not applied, hand off.
     SD bool apply(const mte_op& op) {
         RG_PROF(RP_APPLY);
+        RG_STAT(RS_OPS, 1);
         const u32 type = op.type;
         const bool ins = type == MTE_OP_INSERT || type == MTE_OP_INSERT_MARKER;
         const bool ann = PROPS && type == MTE_OP_ANNOTATE;

@@ -22,36 +22,6 @@ namespace mte {
 // workgroup each, owning all of a CU's LDS (SoloPlan), at the highest wave priority. The replay
 // latency of the longest document bounds a Zipf batch, so it gets the plan with the
 // most room and no LDS-pool sharing; it continues HBM-resident only if it outgrows even that.
-#ifndef MTE_SOLO_ROWS_ONLY
-#define MTE_SOLO_ROWS_ONLY 0
-#endif
-template <bool GEN, int LVL>
-MTE_DEV void solo_doc(const Params& p);
-// Experiment build (MTE_SOLO_ROWS_ONLY=1): the lean k_solo with the row engine alone -- a document
-// that would hand over is left to the host's re-run -- to see what the LDS engine compiled into the
-// same kernel costs the row engine's register allocation.
-template <bool GEN, int LVL>
-MTE_DEV void solo_doc_rows_only(const Params& p) {
-    const u32 i = blockIdx.x;
-    if (i >= p.n_solo) return;
-    const u32 d = p.doc_list[i];
-    __builtin_amdgcn_s_setprio(3);
-    if (p.solo_started && lane_id() == 0) atomicAdd(p.solo_started, 1u);
-    const u64 c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    RegEngine<> r(p, d);
-    r.replay(p.docs[d].op_begin, p.docs[d].op_end);
-    if (r.status != REG_HANDOFF) r.finish();
-    else r.mark_spilled();
-    const u64 c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    if (p.solo_clk && i < SOLO_CLK_SLOTS && lane_id() == 0) {
-        u64* o = p.solo_clk + 4 * (u64)i;
-        o[0] = c0;
-        o[1] = r0;
-        o[2] = c1;
-        o[3] = r1;
-    }
-    __builtin_amdgcn_s_setprio(0);
-}
 template <bool GEN, int LVL>
 MTE_DEV void solo_doc(const Params& p) {
     const u32 i = blockIdx.x;
@@ -165,10 +135,7 @@ template <bool GEN, int LVL>
 __global__ __launch_bounds__(64 * SOLO_WAVES) __attribute__((amdgpu_waves_per_eu(MTE_SOLO_WPE, MTE_SOLO_WPE))) void k_solo(Params p) {
 #if SOLO_WAVES > 1
     asm volatile("" ::: "v255", "a255");
-    if (wave_first(threadIdx.x >> 6) == 0) {
-        if constexpr (MTE_SOLO_ROWS_ONLY && !GEN && LVL == 0) solo_doc_rows_only<GEN, LVL>(p);
-        else solo_doc<GEN, LVL>(p);
-    }
+    if (wave_first(threadIdx.x >> 6) == 0) solo_doc<GEN, LVL>(p);
     __syncthreads();
 #else
     solo_doc<GEN, LVL>(p);

@@ -49,17 +49,6 @@ constexpr u32 ROWS_POOL_WORDS = 3;         // k_rows' pool row mask (mte_solo.hi
 constexpr u32 ROWS_WAIT_TRIES = 20000;     // a wave finding the pool full retries this often (s_sleep 8)
 // needsScour (mergeTree.ts:63) in meta bits 24..25 of every slot lane of a block
 constexpr u32 NS_SHIFT = 24, NS_MASK = 3u << NS_SHIFT;
-// critical-path variants (A/B switches): pairwise resolve, the heap's last entry read
-// directly, the split's right piece made by a row shift
-#ifndef MTE_RES2
-#define MTE_RES2 0
-#endif
-#ifndef MTE_HEAP_LAST
-#define MTE_HEAP_LAST 0
-#endif
-#ifndef MTE_SPLIT_SHIFT
-#define MTE_SPLIT_SHIFT 0
-#endif
 static_assert(RG_BLOCKS <= SOLO_POOL, "the rows live in the SoloPlan's slot arrays");
 
 // Phase profile of the row engine (MTE_PROFILE device builds, `make prof`): inclusive s_memtime
@@ -916,42 +905,6 @@ struct RegEngine {
             }
         };
         const u32 last = nrows - 1;
-#if MTE_RES2
-        // Two rows per step: their visibility and DPP scans are independent, so they interleave (no
-        // scan waits out its DPP hazards alone) and one branch covers both; the next pair's rows load
-        // while this pair is scanned. Row r+1 past the last row re-reads the last row and is ignored.
-        {
-            Row a = row(r0), b = ldrow(r0 + 1 < last ? r0 + 1 : last);
-            u32 r = r0;
-            for (;;) {
-                const u32 rn = r + 2;
-                const Row a2 = ldrow(rn < last ? rn : last), b2 = ldrow(rn + 1 < last ? rn + 1 : last);
-                RG_COUNT(RP_N_RESOLVE, 2);
-                RG_STAT(RS_RES_ROWS, 2);
-                const V va = vis(a, R, C), vb = vis(b, R, C);
-                const V sa = simd::scan_incl(va), sb = simd::scan_incl(vb);
-                const V ia = sa + carry;
-                const u64 ha = simd::ballot(end & simd::sge(ia, pos));
-                const u32 ca = simd::readlane(ia, 63);  // visible length before row r+1
-                const V ib = sb + ca;
-                const u64 hb = r + 1 < nrows ? simd::ballot(end & simd::sge(ib, pos)) : 0ull;
-                if (ha) {
-                    hit_row(a, r, ha, va, ia);
-                    return f;
-                }
-                if (hb) {
-                    carry = ca;
-                    hit_row(b, r + 1, hb, vb, ib);
-                    return f;
-                }
-                carry = simd::readlane(ib, 63);
-                if (rn >= nrows) return f;
-                r = rn;
-                a = a2;
-                b = b2;
-            }
-        }
-#endif
         // two row buffers, each refilled (unconditionally: the last row again at the end, so the
         // LDS counter wait stays exact) while the other one is scanned; the loop only finds the hit
         // row (no state written in it, so no per-row register copies)
@@ -1296,22 +1249,12 @@ struct RegEngine {
         RG_STAT(RS_POP, 1);
         RG_STAT(RS_POP_BIG, m >= 128u);
         RG_STAT(RS_POP_HEAP, n);
-        const u32 top = hrd<0>(HS, 1);
-#if MTE_HEAP_LAST
-        // the last entry of a heap of < 128 (registers 0 and 1): one select of the register, one
-        // readlane each, instead of the run-time level dispatch of hkey / hsid
-        u32 lk, ls;
-        if (n < 128u) {
-            const bool lo = n < 64u;
-            lk = simd::readlane(lo ? HK.r0 : HK.r1, n & 63u);
-            ls = simd::readlane(lo ? HS.r0 : HS.r1, n & 63u);
-        } else {
-            lk = hkey(n);
-            ls = hsid(n);
-        }
-#else
-        const u32 lk = hkey(n), ls = hsid(n);
+#if defined(MTE_CPU) && defined(MTE_CPU_STATS)
+        if (n > g_rg_stats[RS_N]) g_rg_stats[RS_N] = n;  // the largest heap at a pop
+        if (n_lb > g_rg_stats[RS_N + 1]) g_rg_stats[RS_N + 1] = n_lb;
 #endif
+        const u32 top = hrd<0>(HS, 1);
+        const u32 lk = hkey(n), ls = hsid(n);
         i32 newTop = (i32)lk;
         if (m >= 1) {
             if (m < 128u) pop_fast(m, lk, ls, newTop);
@@ -1861,46 +1804,6 @@ struct RegEngine {
     SD u32 split_at(const RFound& f) {
         RG_PROF(RP_SPLIT_AT);
         RG_STAT(RS_SPLIT_AT, 1);
-#if MTE_SPLIT_SHIFT
-        // The right piece made in the row itself: every slot after the split one takes its left
-        // neighbour (so the right piece starts as a copy of the segment), then the two pieces' length,
-        // text offset, capacity and the new id by per-lane selects -- no readlane of the segment's
-        // fields into scalars and back.
-        {
-            if (f.cnt >= 8) {
-                fail(MTE_DOC_CAPACITY, curSeq);
-                return NONE;
-            }
-            const u32 sid = new_sid();
-            if (sid == NONE) return NONE;
-            const u32 r = f.k >> 3, gb = gbase(f.k), sj = (u32)f.slot, rr = (u32)f.r;
-            Row& w = rowref(r);
-            const V sl = L() & 7u;
-            const B mv = in_group(f.k) & (sl > sj);  // (never a group's first lane: no value crosses groups)
-            const B at = L() == gb + sj + 1, lf = L() == gb + sj;
-            auto sh = [&](V& x) MTE_LI { x = simd::sel(mv, simd::row_shr1(x), x); };
-            sh(w.len);
-            sh(w.seq);
-            sh(w.rseq);
-            sh(w.meta);
-            sh(w.toff);
-            sh(w.cap);
-            sh(w.rm);
-            sh(w.sid);
-            if constexpr (PROPS) sh(w.props);  // the right piece shares the map
-            if constexpr (WIDE) sh(w.rm2);
-            // arena text: the capacity is split between the pieces (payload text has none)
-            const B ar = (w.toff & ARENA_BIT) != 0u;
-            w.cap = simd::sel(at, simd::sel(ar, w.cap - rr, 0u), simd::sel(lf, simd::sel(ar, simd::splat(rr), 0u), w.cap));
-            w.len = simd::sel(at, w.len - rr, simd::sel(lf, simd::splat(rr), w.len));
-            w.toff = simd::sel(at, w.toff + rr, w.toff);
-            w.sid = simd::sel(at, sid, w.sid);
-            writeback(r);
-            if (f.cnt + 1 < 8) return f.k;
-            split_block(f.k);
-            return sj + 1 < 4 ? f.k : f.k + 1;
-        }
-#endif
         const u32 r = f.k >> 3, l = gbase(f.k) + (u32)f.slot;
         const Row w = row(r);
         RSeg t;

@@ -177,7 +177,7 @@ uint32_t regcpu_heap(const int32_t* ops, uint32_t n, uint32_t* popped) {
 #ifdef MTE_CPU_STATS
 // the event statistics of every replay since the last call (tools/rg_stats.py), then cleared
 uint32_t regcpu_stats(uint64_t* out, uint32_t n) {
-    const uint32_t m = n < (uint32_t)RS_N ? n : (uint32_t)RS_N;
+    const uint32_t m = n < (uint32_t)RS_N + 2 ? n : (uint32_t)RS_N + 2;
     for (uint32_t i = 0; i < m; i++) out[i] = g_rg_stats[i];
     memset(g_rg_stats, 0, sizeof g_rg_stats);
     return (uint32_t)RS_N;

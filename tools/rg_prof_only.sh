@@ -10,7 +10,7 @@ declare -A S=([apply]=2 [resolve]=3 [insert_slot]=4 [split]=5 [range]=6 [zamboni
 build() {
   mkdir -p $B/rp_$1
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable \
-    -DMTE_PROFILE -DRG_PROF_ONLY=$2 -c mte_solo.hip -o $B/rp_$1/mte_solo.o
+    -mllvm -amdgpu-sched-strategy=iterative-ilp -DMTE_PROFILE -DRG_PROF_ONLY=$2 -c mte_solo.hip -o $B/rp_$1/mte_solo.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $B/rp_$1/libmte.so $B/prof/mte_kernels.o $B/rp_$1/mte_solo.o $B/emit.o \
     $B/prof/mte_host.o -lpthread
 }

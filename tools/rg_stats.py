@@ -37,16 +37,19 @@ def main():
     ops, pay = regcpu.generated(2, gid, n, n_clients=8, seed=1000)
     at, res, rows, text = regcpu.replay(ops, pay)
     out = (ctypes.c_uint64 * 64)()
-    L.regcpu_stats(out, 64)
+    L.regcpu_stats(out, len(NAMES) + 2)
     st = {k: int(out[i]) for i, k in enumerate(NAMES)}
     o = max(st["ops"], 1)
     per = {k: round(v / o, 4) for k, v in st.items() if k != "ops"}
+    heap_max, lb_max = int(out[len(NAMES)]), int(out[len(NAMES) + 1])
     derived = {
         "rows_per_resolve": round(st["res_rows"] / max(st["resolve"], 1), 3),
         "nrows_at_resolve": round(st["res_nrows"] / max(st["resolve"], 1), 3),
         "heap_at_pop": round(st["pop_heap"] / max(st["pop"], 1), 1),
         "pops_on_serial_sift": round(st["pop_big"] / max(st["pop"], 1), 4),
         "slots_moved_per_split": round(st["move_slots"] / max(st["split_blk"] + st["pack"], 1), 1),
+        "heap_max_at_pop": heap_max,
+        "n_lb_max_at_pop": lb_max,
     }
     print(json.dumps({"doc": f"kind 2 gid {gid}, first {n} ops (CPU build of reg_engine.hpp)", "stop": int(at),
                       "max_lb": int(res["max_lb"]), "n_lb": int(res["n_lb"]), "height": int(res["height"]),

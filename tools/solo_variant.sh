@@ -8,7 +8,7 @@ B=../_build
 V=$1; shift
 make -s -C . >/dev/null
 mkdir -p $B/$V
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable "$@" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable ${SOLOFLAGS--mllvm -amdgpu-sched-strategy=iterative-ilp} "$@" \
   -c mte_solo.hip -o $B/$V/mte_solo.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $B/$V/libmte.so $B/mte_kernels.o $B/$V/mte_solo.o $B/emit.o \
   $B/mte_host.o -lpthread

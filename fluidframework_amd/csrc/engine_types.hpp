@@ -150,6 +150,10 @@ struct DocCfg {
     u32 has_nl;        // payload contains '\n' (TextSegment.canAppend reads last chars only then)
     u32 prio;          // critical-path document (far longer than the batch mean): high wave priority
     u32 gid;           // global document id (summary records; the generator's per-document seed)
+    // incremental replay (option retain, reg_engine.hpp ckpt_*): this pass's checkpoint region in
+    // Params::ck_out (ck_cap words, 0 = none) and, when the loaded log extends the previous pass's, the
+    // previous region in Params::ck_in and the op records it covers (ck_at, 0 = replay from op 0)
+    u64 ck_out_off, ck_cap, ck_in_off, ck_at;
 };
 
 // Per-document results written by the kernel.
@@ -261,8 +265,17 @@ struct Params {
     u32* rows_cont;           // k_rows: documents handed to an HBM slot mid-pass, ROWS_CONT_WORDS each
                               // (doc, slot, op index lo / hi, the HBM engine's St); counters[10] queued,
                               // counters[11] taken by k_rows_cont
+    u32* ck_out;              // option retain: the row engines' checkpoints of this pass (DocCfg::ck_*)
+    const u32* ck_in;         // ... and of the previous pass, the ones this pass continues from
 };
 constexpr u32 ROWS_CONT_WORDS = 32;
+
+// A checkpoint region (option retain, reg_engine.hpp ckpt_save): header, up to CK_MAX_ROWS rows of up
+// to 10 fields, 24 registers, the arena semispace (u16 units) and the map records, in words.
+constexpr u32 CK_MAX_ROWS = 32, CK_HDR_WORDS = 64;
+MTE_HOSTDEV_ u64 ck_region_words(u32 arena_cap, u32 map_cap, u32 map_words) {
+    return CK_HDR_WORDS + (u64)CK_MAX_ROWS * 10 * 64 + 24 * 64 + ((u64)arena_cap + 1) / 2 + (u64)map_cap * map_words;
+}
 
 constexpr u32 SOLO_CLK_SLOTS = 64;  // solo workgroups with clock stamps (Params::solo_clk)
 

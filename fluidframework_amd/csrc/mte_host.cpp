@@ -219,13 +219,19 @@ struct DevBuf {
 
 }  // namespace
 
+struct DocBuild;
 struct mte_builder {
     HostBatch hb;
     std::unique_ptr<Interner> in;
     std::string err;
     std::vector<std::string> paths;  // per document: channel full path (container logs), else ""
     uint32_t n_cells = 0;            // SharedMatrix cell ops so far (MTE_OP_CELL's cell index)
+    // open documents (mte_builder_open_doc): logs still growing, after every committed document;
+    // mte_builder_batch commits copies of them into `view`
+    std::vector<std::unique_ptr<DocBuild>> open;
+    HostBatch view;
     mte_builder() { in.reset(new Interner(&hb)); }
+    ~mte_builder();
 };
 
 struct mte_engine {
@@ -371,6 +377,22 @@ struct mte_engine {
     std::vector<uint8_t> emit_pool_of;  // per document: its pool, 255 = not emitted (failed / emission off)
     bool emit_downloaded = false;
     double last_emit_ms = 0;
+    // incremental replay (option "retain"; reg_engine.hpp ckpt_save / ckpt_resume): the row engines
+    // leave every finished document's state in a checkpoint region; a pass over a batch whose logs
+    // extend the last pass's (ck_match) continues each such document from its checkpoint
+    bool retain = false;
+    DevBuf<uint32_t> d_ck[2];
+    int ck_cur = -1;  // the buffer with the last pass's checkpoints (-1: none)
+    struct CkDoc {
+        uint64_t n_ops = 0, n_pay = 0, off = 0, h_ops = 0, h_pay = 0;
+    };
+    std::vector<CkDoc> ck_prev;        // per document of the last pass: what its checkpoint covers, and where
+    std::vector<CkDoc> ck_load;        // per document of the loaded batch: its whole log's hashes
+    std::vector<uint64_t> ck_match;    // per document of the loaded batch: op records it shares with ck_prev
+    HostBatch ck_tabs;                 // the last pass's property tables (ids must keep their meaning)
+    uint64_t ck_tabs_n = 0;            // their key / value / propset counts, 0 = none kept
+    uint32_t ck_map_words = 0;
+    uint32_t last_resumed_docs = 0, last_resumed_ops = 0, last_ck_offered = 0;
     // downloaded final state
     std::vector<uint32_t> h_maps;
     std::vector<uint4> h_out_vis, h_out_aux;
@@ -909,6 +931,149 @@ static int load_cells(mte_engine* e, const mte_batch* b, const std::vector<uint3
     return MTE_OK;
 }
 
+// ---------------------------------------------------------------- incremental replay (option retain)
+static void ck_forget(mte_engine* e) {
+    e->ck_cur = -1;
+    e->ck_prev.clear();
+    e->ck_load.clear();
+    e->ck_match.clear();
+    e->ck_tabs_n = 0;
+}
+// word-wise hash of a byte range, continuing from h (a prefix's hash continues to the whole log's)
+static uint64_t ck_hash(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, b + i, 8);
+        h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+        h ^= h >> 29;
+    }
+    for (; i < n; i++) h = (h ^ b[i]) * 0x100000001B3ull;
+    return h;
+}
+// payload units one at a time: a prefix's hash continued over the rest is the whole run's hash
+// whatever the prefix's length (a word-wise hash would regroup the units after an odd cut)
+static uint64_t ck_hash_units(uint64_t h, const uint16_t* y, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++) {
+        h = (h ^ y[i]) * 0x100000001B3ull;
+        h ^= h >> 31;
+    }
+    return h;
+}
+// an op record as the engine reads it: MTE_F_CATCHUP marks the ops of the messages still above
+// minSeq at the END of a log (DocBuild::commit), which the row engines never read, so a prefix log
+// and its extension differ there and nowhere else
+static uint64_t ck_hash_ops(uint64_t h, const mte_op* o, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++) {
+        mte_op x = o[i];
+        x.flags &= ~MTE_F_CATCHUP;
+        h = ck_hash(h, &x, sizeof x);
+    }
+    return h;
+}
+static uint64_t ck_tabs_count(const HostBatch& t) {
+    return (uint64_t)t.propsets.size() + t.prop_keys.size() + t.key_offsets.size() + t.val_offsets.size();
+}
+// the loaded tables start with the last pass's: every id the checkpointed map records hold means the
+// same key / value / property set
+static bool ck_tabs_extend(const HostBatch& old, const HostBatch& nw) {
+    auto pre = [](const auto& a, const auto& b) { return a.size() <= b.size() && std::equal(a.begin(), a.end(), b.begin()); };
+    auto pre_ps = [](const std::vector<mte_propset>& a, const std::vector<mte_propset>& b) {
+        if (a.size() > b.size()) return false;
+        for (size_t i = 0; i < a.size(); i++)
+            if (a[i].first != b[i].first || a[i].count != b[i].count) return false;
+        return true;
+    };
+    return pre_ps(old.propsets, nw.propsets) && pre(old.prop_keys, nw.prop_keys) && pre(old.prop_vals, nw.prop_vals) &&
+           pre(old.key_offsets, nw.key_offsets) && pre(old.key_text, nw.key_text) && pre(old.val_offsets, nw.val_offsets) &&
+           pre(old.val_text, nw.val_text);
+}
+// mte_load with retain: which documents of the batch extend the last pass's (ck_match), and the
+// hashes of their whole logs for the next one
+static void ck_match_batch(mte_engine* e, const mte_batch* b) {
+    const uint32_t nd = b->n_docs;
+    e->ck_match.assign(nd, 0);
+    e->ck_load.assign(nd, mte_engine::CkDoc{});
+    const bool same = e->ck_cur >= 0 && e->ck_prev.size() == nd && e->ck_tabs_n &&
+                      e->ck_map_words == e->map_words && ck_tabs_extend(e->ck_tabs, e->hb);
+    for (uint32_t d = 0; d < nd; d++) {
+        const mte_op* o = b->ops + b->doc_op_offsets[d];
+        const uint16_t* y = b->payload + b->doc_payload_offsets[d];
+        const uint64_t n = b->doc_op_offsets[d + 1] - b->doc_op_offsets[d];
+        const uint64_t np = b->doc_payload_offsets[d + 1] - b->doc_payload_offsets[d];
+        mte_engine::CkDoc& c = e->ck_load[d];
+        c.n_ops = n;
+        c.n_pay = np;
+        uint64_t ho = 0xCBF29CE484222325ull, hp = 0xCBF29CE484222325ull, k = 0, kp = 0;
+        if (same) {
+            const mte_engine::CkDoc& q = e->ck_prev[d];
+            if (q.n_ops && q.n_ops <= n && q.n_pay <= np) {
+                ho = ck_hash_ops(ho, o, q.n_ops);
+                hp = ck_hash_units(hp, y, q.n_pay);
+                k = q.n_ops;
+                kp = q.n_pay;
+                if (ho == q.h_ops && hp == q.h_pay) e->ck_match[d] = q.n_ops;
+            }
+        }
+        c.h_ops = ck_hash_ops(ho, o + k, n - k);
+        c.h_pay = ck_hash_units(hp, y + kp, np - kp);
+    }
+}
+// run_kernel with retain: this pass's regions, the previous pass's ones to continue from
+static int ck_begin(mte_engine* e) {
+    const uint32_t nd = (uint32_t)e->cfg.size();
+    const int out = e->ck_cur == 0 ? 1 : 0;
+    uint64_t tot = 0;
+    e->last_ck_offered = 0;
+    for (uint32_t d = 0; d < nd; d++) {
+        DocCfg& c = e->cfg[d];
+        c.ck_out_off = tot;
+        c.ck_cap = ck_region_words(c.arena_cap, c.map_cap, e->map_words);
+        tot += (c.ck_cap + 63) & ~63ull;
+        const bool have = e->ck_cur >= 0 && d < e->ck_match.size() && d < e->ck_prev.size() && e->ck_match[d];
+        c.ck_at = have ? e->ck_match[d] : 0;
+        c.ck_in_off = have ? e->ck_prev[d].off : 0;
+        e->last_ck_offered += have;
+    }
+    HIP_TRY(e, e->d_ck[out].fit(std::max<uint64_t>(tot, 64)));
+    HIP_TRY(e, hipMemsetAsync(e->d_ck[out].p, 0, tot * 4, e->stream));  // every region invalid until saved
+    HIP_TRY(e, hipMemcpyAsync(e->d_cfg.p, e->cfg.data(), nd * sizeof(DocCfg), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(e, hipStreamSynchronize(e->stream));
+    e->P.ck_out = e->d_ck[out].p;
+    e->P.ck_in = e->ck_cur >= 0 ? e->d_ck[e->ck_cur].p : nullptr;
+    return MTE_OK;
+}
+// after the pass: its checkpoints are the ones the next pass continues from (the same batch replayed
+// again continues every document from its end)
+static void ck_end(mte_engine* e, const uint32_t* ctr) {
+    const uint32_t nd = (uint32_t)e->cfg.size();
+    e->ck_cur = e->ck_cur == 0 ? 1 : 0;
+    e->ck_prev.assign(nd, mte_engine::CkDoc{});
+    for (uint32_t d = 0; d < nd; d++) {
+        mte_engine::CkDoc& q = e->ck_prev[d];
+        if (d < e->ck_load.size()) q = e->ck_load[d];
+        q.off = e->cfg[d].ck_out_off;
+        q.n_ops = e->n_ops_doc[d];
+        q.n_pay = e->cfg[d].payload_len;
+    }
+    e->ck_match.assign(nd, 0);
+    for (uint32_t d = 0; d < nd; d++) e->ck_match[d] = e->ck_prev[d].n_ops;
+    e->ck_tabs.propsets = e->hb.propsets;
+    e->ck_tabs.prop_keys = e->hb.prop_keys;
+    e->ck_tabs.prop_vals = e->hb.prop_vals;
+    e->ck_tabs.key_offsets = e->hb.key_offsets;
+    e->ck_tabs.key_text = e->hb.key_text;
+    e->ck_tabs.val_offsets = e->hb.val_offsets;
+    e->ck_tabs.val_text = e->hb.val_text;
+    e->ck_tabs_n = 1 + ck_tabs_count(e->hb);
+    e->ck_map_words = e->map_words;
+    e->last_resumed_docs = ctr[12];
+    e->last_resumed_ops = ctr[13];
+    e->P.ck_out = nullptr;
+    e->P.ck_in = nullptr;
+}
+
 int mte_load(mte_engine* e, const mte_batch* b) {
     if (!e || !b) return MTE_E_ARG;
     HIP_TRY(e, hipSetDevice(e->device));
@@ -1033,6 +1198,8 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     e->lean_ok = lean && !ext;
     e->ext_needed = ext;
     if ((rc = alloc_out_text(e))) return rc;
+    if (e->retain) ck_match_batch(e, b);
+    else ck_forget(e);
     return MTE_OK;
 }
 
@@ -1177,6 +1344,11 @@ static int run_kernel(mte_engine* e, bool gen) {
     e->P.n_list = nd;
     int rc;
     if ((rc = alloc_slots(e))) return rc;  // options may have changed the wave plan
+    // option retain: checkpoints out, and in from the last pass (not for the generator, whose batch
+    // is made in the pass, nor the two passes of a SharedMatrix batch)
+    const bool ck = e->retain && !gen && e->P.cell_mode == 0;
+    e->P.ck_in = e->P.ck_out = nullptr;
+    if (ck && (rc = ck_begin(e))) return rc;
     uint32_t groups, hbm_waves, lds_active;
     const uint32_t n_solo = e->P.n_solo;
     // engine level (engine.hpp): the generator always runs FULL
@@ -1289,7 +1461,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nall * sizeof(DocRes), hipMemcpyDeviceToHost));
     for (uint32_t i = 0; i < nd; i++)
         if (e->res[e->order[i]].status == DOC_SPILL) spill.push_back(e->order[i]);
-    uint32_t ctr[8];
+    uint32_t ctr[16];
     HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
     e->last_continued = ctr[4];
     e->last_hbm_docs = 0;
@@ -1401,10 +1573,14 @@ static int run_kernel(mte_engine* e, bool gen) {
     }
     e->res.resize(nall);
     HIP_TRY(e, hipMemcpy(e->res.data(), e->d_res.p, nall * sizeof(DocRes), hipMemcpyDeviceToHost));
+    if (ck) ck_end(e, ctr);
+    else if (!gen) e->last_resumed_docs = e->last_resumed_ops = 0;
     e->replayed = true;
     e->downloaded = false;
     return MTE_OK;
 }
+
+int mte_retain(mte_engine* e, int on) { return e ? mte_set_option(e, "retain", on) : MTE_E_ARG; }
 
 int mte_replay(mte_engine* e, mte_stats* out) {
     if (!e) return MTE_E_ARG;
@@ -1487,6 +1663,7 @@ int mte_generate_ids(mte_engine* e, uint32_t kind, uint32_t n_docs, uint32_t n_o
     e->map_words = MAP_WORDS;  // the generator's property sets hold at most four keys
     if (kind != 2 && kind != 3 && kind != 5) return set_err(e, MTE_E_ARG, "generator kind must be 2, 3 or 5");
     HIP_TRY(e, hipSetDevice(e->device));
+    ck_forget(e);  // (a new batch: no checkpoint of the last one may be continued)
     e->hb = HostBatch();
     uint32_t nps = build_generator_props(e);
     std::vector<uint64_t> nops(n_docs), pay(n_docs), pi(n_docs), an(n_docs);
@@ -2605,6 +2782,10 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "rows_bulk") e->rows_bulk = value < 0 ? -1 : value == 0 ? 0 : value >= 12 ? 12 : value >= 8 ? 8 : 4;  // lean bulk on k_rows
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
     else if (k == "rows_pool") e->rows_pool_lim = (uint32_t)std::max<int64_t>(0, value);  // k_rows pool rows per CU (0 = all)
+    else if (k == "retain") {  // incremental replay: checkpoints kept for a later pass over extended logs
+        e->retain = value != 0;
+        if (!e->retain) ck_forget(e);
+    }
     else return set_err(e, MTE_E_ARG, "unknown option " + k);
     return MTE_OK;
 }
@@ -2642,6 +2823,9 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
         *value = k == "rows_restart_pushed" ? ctr[8] : k == "rows_restart_popped" ? ctr[9] : ctr[10];
     }
     else if (k == "emit_us") *value = (int64_t)(e->last_emit_ms * 1000.0);  // emission after the replay pass
+    else if (k == "resumed_docs") *value = e->last_resumed_docs;  // option retain: documents continued ...
+    else if (k == "resumed_ops") *value = e->last_resumed_ops;    // ... and the op records they skipped
+    else if (k == "ck_offered") *value = e->last_ck_offered;      // documents whose log extends the last pass's
     else if (k == "out_text") {  // UTF-16 units Engine::finish gathered (counters[6..7])
         uint32_t ctr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (e->d_counters.p) HIP_TRY(e, hipMemcpy(ctr, e->d_counters.p, sizeof ctr, hipMemcpyDeviceToHost));
@@ -2978,8 +3162,16 @@ static int add_messages(mte_builder* b, const json::Value& doc, DocBuild& db) {
     return MTE_OK;
 }
 
+// documents are added before the first open one (mte_builder_open_doc): a batch lists the committed
+// documents, then the open ones
+static int builder_closed(mte_builder* b) {
+    b->err = "documents cannot be added after an open document (mte_builder_open_doc)";
+    return MTE_E_STATE;
+}
+
 int mte_builder_add_doc(mte_builder* b, const char* observer_name, const char* text, size_t len) {
     if (!b || !text) return MTE_E_ARG;
+    if (!b->open.empty()) return builder_closed(b);
     json::Value doc;
     try {
         doc = json::parse(text, len);
@@ -3471,6 +3663,7 @@ static int add_summary(mte_builder* b, const json::Value& summary, DocBuild& db)
 int mte_builder_add_doc_from_summary(mte_builder* b, const char* observer_name, const char* summary,
                                      size_t summary_len, const char* ops, size_t ops_len) {
     if (!b || !summary) return MTE_E_ARG;
+    if (!b->open.empty()) return builder_closed(b);
     DocBuild db(observer_name);
     json::Value s, log;
     try {
@@ -3545,6 +3738,7 @@ static void attach_trees(const json::Value& attach, const std::string& id, std::
 int mte_builder_add_container_log(mte_builder* b, const char* observer_name, const char* text, size_t len,
                                   uint32_t* n_docs) {
     if (!b || !text) return MTE_E_ARG;
+    if (!b->open.empty()) return builder_closed(b);
     if (n_docs) *n_docs = 0;
     json::Value log;
     try {
@@ -3765,6 +3959,7 @@ static int matrix_messages(mte_builder* b, const json::Value& log, DocBuild* dbs
 
 int mte_builder_add_matrix_log(mte_builder* b, const char* observer_name, const char* text, size_t len) {
     if (!b || !text) return MTE_E_ARG;
+    if (!b->open.empty()) return builder_closed(b);
     json::Value log;
     try {
         log = json::parse(text, len);
@@ -3807,6 +4002,7 @@ static void unmorton(uint32_t k, uint32_t* r, uint32_t* c) {
 int mte_builder_add_matrix_from_summary(mte_builder* b, const char* observer_name, const char* summary,
                                         size_t summary_len, const char* ops, size_t ops_len) {
     if (!b || !summary) return MTE_E_ARG;
+    if (!b->open.empty()) return builder_closed(b);
     json::Value s, log;
     try {
         s = json::parse(summary, summary_len);
@@ -3927,9 +4123,54 @@ int mte_builder_add_matrix_from_summary(mte_builder* b, const char* observer_nam
     return MTE_OK;
 }
 
+// An open document (Client.applyMsg one message batch at a time, client.ts:805-836): its log grows
+// by mte_builder_append_messages; every mte_builder_batch sees it as it is then (commit of a copy: the
+// messages above minSeq at the end of the log so far are its catch-up messages).
+int mte_builder_open_doc(mte_builder* b, const char* observer_name, uint32_t* doc) {
+    if (!b || !doc) return MTE_E_ARG;
+    *doc = b->hb.n_docs() + (uint32_t)b->open.size();
+    b->open.emplace_back(new DocBuild(observer_name));
+    b->paths.emplace_back();
+    return MTE_OK;
+}
+int mte_builder_append_messages(mte_builder* b, uint32_t doc, const char* text, size_t len) {
+    if (!b || !text) return MTE_E_ARG;
+    const uint32_t nc = b->hb.n_docs();
+    if (doc < nc || doc - nc >= b->open.size()) {
+        b->err = "not an open document";
+        return MTE_E_ARG;
+    }
+    json::Value msgs;
+    try {
+        msgs = json::parse(text, len);
+    } catch (std::exception& ex) {
+        b->err = ex.what();
+        return MTE_E_PARSE;
+    }
+    DocBuild& db = *b->open[doc - nc];
+    // all or nothing: a message the builder refuses leaves the document as it was
+    DocBuild keep = db;
+    if (int rc = add_messages(b, msgs, db)) {
+        b->err = db.err;
+        db = std::move(keep);
+        return rc;
+    }
+    return MTE_OK;
+}
+mte_builder::~mte_builder() = default;
+
 int mte_builder_batch(mte_builder* b, mte_batch* out) {
     if (!b || !out) return MTE_E_ARG;
-    b->hb.view(out);
+    if (b->open.empty()) {
+        b->hb.view(out);
+        return MTE_OK;
+    }
+    b->view = b->hb;
+    for (auto& d : b->open) {
+        DocBuild c = *d;
+        c.commit(b->view);
+    }
+    b->view.view(out);
     return MTE_OK;
 }
 

@@ -54,8 +54,10 @@ MTE_DEV void solo_doc(const Params& p) {
         // to the LDS plan below only if it outgrows the registers or reaches an op they do not cover
         if (p.reg_solo) {
             RegEngine<> r(p, d);
+            at = r.ckpt_resume(at);  // (option retain: the previous pass's state, if this log extends it)
             at = r.replay(at, p.docs[d].op_end);
             if (r.status != REG_HANDOFF) {
+                r.ckpt_save(at - p.docs[d].op_begin);
                 r.finish();
                 stamp();
                 __builtin_amdgcn_s_setprio(0);
@@ -77,8 +79,10 @@ MTE_DEV void solo_doc(const Params& p) {
             // WIDE: clients 32..63 too (a second removers array after the map ids)
             RegEngine<(int)RG_ROWS, false, true, true> r(p, d, vb, ab, 4, 0, ab + RG_BLOCKS * 8 * 16,
                                                          ab + RG_BLOCKS * 8 * 16 + RG_BLOCKS * 8 * 4);
+            at = r.ckpt_resume(at);
             if (!r.status) at = r.replay(at, p.docs[d].op_end);
             if (r.status != REG_HANDOFF) {
+                r.ckpt_save(at - p.docs[d].op_begin);
                 r.finish();
                 stamp();
                 __builtin_amdgcn_s_setprio(0);
@@ -435,7 +439,7 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
             d = p.doc_list[i];
         }
         RegEngine<PAGED ? (int)RG_ROWS : (int)G::FIXED_NR, PAGED, PROPS, WIDE> r(p, d, vb, ab, 5, G::MASK, pb, r2b);
-        u64 at = p.docs[d].op_begin;
+        u64 at = r.ckpt_resume(p.docs[d].op_begin);
         if (!r.status) at = r.replay(at, p.docs[d].op_end);
         if (r.status == REG_HANDOFF && PAGED && p.rows_retry && r.pool_full && !again) {
             // marked for the host's re-run first (so a document no wave restarts is still replayed),
@@ -457,6 +461,7 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
                 if (lane_id() == 0) p.res[d].spill_why |= why;
             }
         } else {
+            r.ckpt_save(at - p.docs[d].op_begin);
             r.finish();
         }
         r.release_rows();

@@ -2276,6 +2276,171 @@ struct RegEngine {
         }
 #endif
     }
+
+    // ---------------------------------------------------------------- checkpoints (incremental replay)
+    // Client.applyMsg is incremental (client.ts:805-836): a reader interleaves getText with messages.
+    // With Params::ck_out set, a document this engine finishes also leaves its whole replay state in
+    // its checkpoint region (DocCfg::ck_out_off, ck_cap words); a later pass over a log that extends
+    // this one (the host checks the prefix, mte_host.cpp ck_match) starts from that state at op
+    // ck_at instead of op 0. The state is the engine's own: rows, interior levels, heap, scalars, the
+    // live merge-arena semispace and the property maps -- nothing the replay does depends on where it
+    // started, so the continued replay is the full one, op for op.
+    // Region (words): header [0, CK_HDR), rows (NF fields of 64 words each, row by row), LV / HK / HS
+    // (8 registers each), the arena semispace's [0, arenaTop) units, the map records [0, mapNext).
+    static constexpr u32 CK_MAGIC = 0x434B5031u, CK_HDR = CK_HDR_WORDS;
+    static_assert(RG_ROWS <= CK_MAX_ROWS, "checkpoint regions hold the whole row plan");
+    enum : u32 { CK_VALID, CK_AT_LO, CK_AT_HI, CK_FLAGS, CK_NLB, CK_HEIGHT, CK_HEAPSIZE, CK_HEAPTOP, CK_MINSEQ,
+                 CK_CURSEQ, CK_SEGNEXT, CK_ARENATOP, CK_ARENASEL, CK_MAPNEXT, CK_NOPS, CK_NMSGS, CK_NGC, CK_MAXLB,
+                 CK_MW, CK_N };
+    static constexpr u32 CK_NF = 8 + (PROPS ? 1u : 0u) + (WIDE ? 1u : 0u);
+    // words a checkpoint of a document with these capacities can take (the host sizes regions by it)
+    SD static u64 ck_words(u32 arena_cap, u32 map_cap, u32 map_words) { return ck_region_words(arena_cap, map_cap, map_words); }
+    SD void ckpt_save(u64 at) {
+        const DocCfg& c = p.docs[doc];
+        if (!p.ck_out || !c.ck_cap || status || !rows_whole()) return;
+        fence_arena();
+        u32* base = p.ck_out + c.ck_out_off;
+        const u32 nrows = (n_lb + 7) >> 3;
+        const u64 rows_end = CK_HDR + (u64)nrows * CK_NF * 64, regs_end = rows_end + 24 * 64;
+        const u64 ar_end = regs_end + ((u64)arenaTop + 1) / 2;
+        const u64 end = ar_end + (PROPS ? (u64)mapNext * mw : 0);
+        if (end > c.ck_cap) return;  // (the region stays invalid: the next pass replays from op 0)
+        const V Lv = L();
+        for (u32 rr = 0; rr < nrows; rr++) {
+            const Row w = ldrow(rr);
+            u32* o = base + CK_HDR + (u64)rr * CK_NF * 64;
+            simd::st(o, Lv, w.len, simd::mk_all());
+            simd::st(o + 64, Lv, w.seq, simd::mk_all());
+            simd::st(o + 128, Lv, w.rseq, simd::mk_all());
+            simd::st(o + 192, Lv, w.meta, simd::mk_all());
+            simd::st(o + 256, Lv, w.cap, simd::mk_all());
+            simd::st(o + 320, Lv, w.toff, simd::mk_all());
+            simd::st(o + 384, Lv, w.rm, simd::mk_all());
+            simd::st(o + 448, Lv, w.sid, simd::mk_all());
+            if constexpr (PROPS) simd::st(o + 512, Lv, w.props, simd::mk_all());
+            if constexpr (WIDE) simd::st(o + 64 * (CK_NF - 1), Lv, w.rm2, simd::mk_all());
+        }
+        u32* g = base + rows_end;
+#pragma unroll
+        for (u32 i = 0; i < 8; i++) {
+            simd::st(g + 64 * i, Lv, LV.get(i), simd::mk_all());
+            simd::st(g + 64 * (8 + i), Lv, HK.get(i), simd::mk_all());
+            simd::st(g + 64 * (16 + i), Lv, HS.get(i), simd::mk_all());
+        }
+        copy_text(0, ARENA_BIT, arenaTop, reinterpret_cast<u16*>(base + regs_end));
+        if constexpr (PROPS)
+            for (u64 q = 0; q < (u64)mapNext * mw; q += 64) {
+                const V i = Lv + (u32)q;
+                const B m = i < (u32)((u64)mapNext * mw);
+                simd::st(base + ar_end, i, simd::ld(maps, i, m), m);
+            }
+        const u32 flags = (PROPS ? 1u : 0u) | (WIDE ? 2u : 0u);
+        const u32 hv[CK_N] = {0u, (u32)at, (u32)(at >> 32), flags, n_lb, height, heapSize, (u32)heapTop, (u32)minSeq,
+                              (u32)curSeq, segNext, arenaTop, arenaSel, PROPS ? mapNext : 1u, n_ops, n_msgs, n_gc,
+                              max_lb, PROPS ? mw : 0u};
+        V h = simd::splat(0);
+        for (u32 i = 1; i < CK_N; i++) h = simd::sel(Lv == i, hv[i], h);
+        simd::st(base, Lv, h, Lv < (u32)CK_N);
+        // the valid word last, after every other word of the region is out
+        simd::wave_fence();
+        simd::st(base, Lv, simd::splat(CK_MAGIC), Lv == 0u);
+    }
+    // Continue from the checkpoint of the previous pass (DocCfg::ck_at ops in, region ck_in_off of
+    // Params::ck_in): returns the op to go on from, or i0 (state untouched: replay from the start)
+    // when there is none or it does not fit this engine.
+    SD u64 ckpt_resume(u64 i0) {
+        const DocCfg& c = p.docs[doc];
+        if (!p.ck_in || !c.ck_at || status) return i0;
+        const u32* base = p.ck_in + c.ck_in_off;
+        const V Lv = L();
+        const V h = simd::ld(base, Lv, Lv < (u32)CK_N);
+        auto hw = [&](u32 i) MTE_LI { return simd::readlane(h, i); };
+        const u64 at = (u64)hw(CK_AT_LO) | ((u64)hw(CK_AT_HI) << 32);
+        const u32 flags = hw(CK_FLAGS), nlb = hw(CK_NLB);
+        const bool cprops = flags & 1u, cwide = (flags & 2u) != 0;
+        // (a lean checkpoint continues on a PROPS / WIDE engine -- no maps, no high removers -- not the
+        // other way round; a map table narrower than the records written is refused too)
+        if (hw(CK_VALID) != CK_MAGIC || at != c.ck_at || (cprops && !PROPS) || (cwide && !WIDE) || nlb == 0 ||
+            nlb > NBLK || hw(CK_HEIGHT) > RG_LEVELS + 1 || hw(CK_ARENATOP) > arena_cap || hw(CK_SEGNEXT) > seg_cap ||
+            (cprops && (hw(CK_MW) != mw || hw(CK_MAPNEXT) > map_cap)))
+            return i0;
+        const u32 nrows = (nlb + 7) >> 3;
+        if constexpr (PAGED) {
+            if (!grow_rows(nrows)) {  // the pool is full now: k_rows restarts it or the host re-runs it
+                status = REG_HANDOFF;
+                return i0;
+            }
+        }
+        const u32 cnf = 8 + (cprops ? 1u : 0u) + (cwide ? 1u : 0u);
+        for (u32 rr = 0; rr < nrows; rr++) {
+            const u32* o = base + CK_HDR + (u64)rr * cnf * 64;
+            Row w;
+            w.len = simd::ld(o, Lv, simd::mk_all());
+            w.seq = simd::ld(o + 64, Lv, simd::mk_all());
+            w.rseq = simd::ld(o + 128, Lv, simd::mk_all());
+            w.meta = simd::ld(o + 192, Lv, simd::mk_all());
+            w.cap = simd::ld(o + 256, Lv, simd::mk_all());
+            w.toff = simd::ld(o + 320, Lv, simd::mk_all());
+            w.rm = simd::ld(o + 384, Lv, simd::mk_all());
+            w.sid = simd::ld(o + 448, Lv, simd::mk_all());
+            if constexpr (PROPS) w.props = cprops ? simd::ld(o + 512, Lv, simd::mk_all()) : simd::splat(0);
+            if constexpr (WIDE) w.rm2 = cwide ? simd::ld(o + 64 * (cnf - 1), Lv, simd::mk_all()) : simd::splat(0);
+            strow(rr, w);
+        }
+        cr = NONE;
+        const u64 rows_end = CK_HDR + (u64)nrows * cnf * 64, regs_end = rows_end + 24 * 64;
+        const u32* g = base + rows_end;
+#pragma unroll
+        for (u32 i = 0; i < 8; i++) {
+            LV.set(i, simd::ld(g + 64 * i, Lv, simd::mk_all()));
+            HK.set(i, simd::ld(g + 64 * (8 + i), Lv, simd::mk_all()));
+            HS.set(i, simd::ld(g + 64 * (16 + i), Lv, simd::mk_all()));
+        }
+        n_lb = nlb;
+        height = hw(CK_HEIGHT);
+        heapSize = hw(CK_HEAPSIZE);
+        heapTop = (i32)hw(CK_HEAPTOP);
+        minSeq = (i32)hw(CK_MINSEQ);
+        curSeq = (i32)hw(CK_CURSEQ);
+        segNext = hw(CK_SEGNEXT);
+        arenaTop = hw(CK_ARENATOP);
+        arenaSel = hw(CK_ARENASEL) & 1u;
+        n_ops = hw(CK_NOPS);
+        n_msgs = hw(CK_NMSGS);
+        n_gc = hw(CK_NGC);
+        max_lb = hw(CK_MAXLB);
+        // the arena text into this pass's semispace arenaSel (offsets kept: the rows' toff stay valid)
+        {
+            const u16* src = reinterpret_cast<const u16*>(base + regs_end);
+            u16* dst = arena_cur();
+            for (u32 b = 0; b < arenaTop; b += 64) {
+                const V i = Lv + b;
+                const B m = i < arenaTop;
+                simd::st(dst, i, simd::ld(src, i, m), m);
+            }
+        }
+        if constexpr (PROPS) {
+            mapNext = cprops ? hw(CK_MAPNEXT) : 1u;
+            const u32* src = base + regs_end + ((u64)arenaTop + 1) / 2;
+            const u32 nw = cprops ? mapNext * mw : 0u;
+            for (u32 q = 0; q < nw; q += 64) {
+                const V i = Lv + q;
+                const B m = i < nw;
+                simd::st(maps, i, simd::ld(src, i, m), m);
+            }
+        }
+        adirty = true;  // arena and map words written lane-parallel: fence before they are read
+        if (simd::lane0()) {  // counters[12] / [13]: documents and op records resumed this pass
+#ifdef MTE_CPU
+            p.counters[12] += 1;
+            p.counters[13] += (u32)at;
+#else
+            atomicAdd(&p.counters[12], 1u);
+            atomicAdd(&p.counters[13], (u32)at);
+#endif
+        }
+        return i0 + at;
+    }
 };
 
 }  // namespace mte

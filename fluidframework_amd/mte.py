@@ -104,7 +104,7 @@ EXPORTS = ["mte_abi_version", "mte_build_info", "mte_create", "mte_destroy", "mt
            "mte_snapshot_v1", "mte_snapshot_legacy", "mte_snapshot_shared_string", "mte_summaries", "mte_rccl_unique_id",
            "mte_rccl_comm_create", "mte_rccl_comm_destroy", "mte_gather_summaries", "mte_gather_summaries_alloc", "mte_free", "mte_builder_create", "mte_builder_add_doc", "mte_builder_add_doc_from_summary", "mte_builder_add_container_log", "mte_builder_doc_path",
            "mte_builder_add_matrix_log", "mte_builder_add_matrix_from_summary", "mte_snapshot_matrix",
-           "mte_builder_batch",
+           "mte_builder_batch", "mte_builder_open_doc", "mte_builder_append_messages", "mte_retain",
            "mte_builder_error", "mte_builder_destroy"]
 
 _lib = None
@@ -165,6 +165,10 @@ def lib():
         L.mte_builder_doc_path.argtypes = [vp, ctypes.c_uint32]
         L.mte_builder_doc_path.restype = ctypes.c_char_p
         L.mte_builder_batch.argtypes = [vp, ctypes.POINTER(mte_batch)]
+        if hasattr(L, "mte_builder_open_doc"):  # (A/B runs load older experiment builds)
+            L.mte_builder_open_doc.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32)]
+            L.mte_builder_append_messages.argtypes = [vp, ctypes.c_uint32, ctypes.c_char_p, sz]
+            L.mte_retain.argtypes = [vp, ctypes.c_int]
         L.mte_builder_error.argtypes = [vp]
         L.mte_builder_error.restype = ctypes.c_char_p
         L.mte_builder_destroy.argtypes = [vp]
@@ -247,6 +251,24 @@ class Builder:
             raise MteError(f"mte_builder_add_matrix_from_summary: {rc}: {lib().mte_builder_error(self._h).decode()}")
         n = self.n_docs()
         return n - 2, n - 1
+
+    def open_doc(self, observer="__observer__"):
+        """An open document: its log grows with append() (Client.applyMsg, client.ts:805-836); every
+        batch() sees it as it is. No other document may be added after it. Returns its index."""
+        d = ctypes.c_uint32()
+        rc = lib().mte_builder_open_doc(self._h, observer.encode(), ctypes.byref(d))
+        if rc:
+            raise MteError(f"mte_builder_open_doc: {rc}: {lib().mte_builder_error(self._h).decode()}")
+        return d.value
+
+    def append(self, doc, messages):
+        """More sequenced messages onto open document `doc` (all or none of them)."""
+        text = messages if isinstance(messages, (str, bytes)) else json.dumps(messages, separators=(",", ":"),
+                                                                               ensure_ascii=False)
+        b = text.encode() if isinstance(text, str) else text
+        rc = lib().mte_builder_append_messages(self._h, doc, b, len(b))
+        if rc:
+            raise MteError(f"mte_builder_append_messages: {rc}: {lib().mte_builder_error(self._h).decode()}")
 
     def n_docs(self):
         b = mte_batch()
@@ -445,6 +467,11 @@ class Engine:
     def last_kernel_ms(self):
         return lib().mte_last_kernel_ms(self._h)
 
+    def retain(self, on=True):
+        """mte_retain: keep every document's replay state, so a replay of logs that extend the last
+        pass's replays only their new ops (get_info("resumed_docs") / "resumed_ops" say how many)."""
+        self._check(lib().mte_retain(self._h, int(bool(on))), "mte_retain")
+
     def wave_selftest(self, values):
         values = np.ascontiguousarray(values, dtype=np.uint32)
         nw = values.size // 64
@@ -454,33 +481,47 @@ class Engine:
 
 
 class MergeTreeClient:
-    """Client-shaped facade for one document (client.ts:42): applyMsg batches are staged and replayed
-    on the GPU when an output is requested."""
+    """Client-shaped facade for one document (client.ts:42), incremental like Client.applyMsg
+    (client.ts:805-836): messages are parsed onto an open builder document as they come, and a read
+    (getText, getLength, snapshot) after new messages replays on the GPU only the ops since the last
+    read, continuing the document's state from the previous pass (mte_retain). Without new messages
+    a read reuses the last results. A document the row engines cannot hold (summary loads, relative
+    positions, 64+ clients, ...) replays from its first op instead: same results, not incremental."""
 
     def __init__(self, observer="__observer__", device=0):
         self.observer = observer
-        self.msgs = []
+        self._builder = Builder()
+        self._doc = self._builder.open_doc(observer)
+        self._pending = []
         self._engine = None
         self._device = device
         self._dirty = True
+        self.replays = 0  # passes run (a read after new messages runs one)
 
     def applyMsg(self, msg):  # noqa: N802 (reference name)
-        self.msgs.append(msg)
+        self._pending.append(msg)
         self._dirty = True
 
     def _run(self):
         if self._dirty:
-            b = Builder()
-            b.add_doc(self.msgs, observer=self.observer)
+            if self._pending:
+                self._builder.append(self._doc, self._pending)
+                self._pending = []
             if self._engine is None:
                 self._engine = Engine(self._device)
-            self._engine.load(b.batch())
+                self._engine.retain(True)
+            self._engine.load(self._builder.batch())
             self._engine.replay()
+            self.replays += 1
             code, seq = self._engine.status(0)
             if code:
                 raise MteError(f"replay failed at seq {seq}: {DOC_STATUS.get(code, code)}")
             self._dirty = False
         return self._engine
+
+    def resumed_ops(self):
+        """Op records the last read did not replay again (continued from the previous pass)."""
+        return self._run().get_info("resumed_ops")
 
     def getText(self):  # noqa: N802
         return self._run().text(0)

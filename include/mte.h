@@ -260,6 +260,13 @@ int mte_load(mte_engine* e, const mte_batch* batch);
 /* Client.applyMsg for every message of every document (client.ts:805-836), on the GPU.
  * Blocking. Per-doc failures are recorded, never thrown. */
 int mte_replay(mte_engine* e, mte_stats* out);
+/* Incremental replay (Client.applyMsg is incremental, client.ts:805-836): on = 1 keeps each document's
+ * replay state after every mte_replay, so the next mte_load of logs that EXTEND the last pass's (the
+ * same documents, each log the old one plus new messages; the engine checks the prefix) replays only
+ * the new ops of every document the row engines held; any other document replays from op 0. The
+ * results are the full replay's either way. on = 0 drops the kept state. Off by default: a replay
+ * of the same batch again would otherwise only re-read its results. */
+int mte_retain(mte_engine* e, int on);
 
 /* Synthetic workload: generate op logs on the device and leave them loaded, as if
  * by mte_load. kind: 2 = C2 (insert/remove), 3 = C3 (annotate + ties), 5 = C5-style.
@@ -374,6 +381,14 @@ int mte_builder_add_matrix_log(mte_builder* b, const char* observer_name, const 
  * matrix's summary after the suffix. */
 int mte_builder_add_matrix_from_summary(mte_builder* b, const char* observer_name, const char* summary,
                                         size_t summary_len, const char* ops, size_t ops_len);
+/* An open document: Client.applyMsg fed one message batch at a time (client.ts:805-836). *doc = its
+ * index in the batch (after every document added before it; no other document may be added after
+ * it). mte_builder_append_messages parses one more JSON array of messages onto its log (all or none
+ * of them: a refused message leaves the log as it was); each mte_builder_batch sees the log as it is.
+ * With retain on (mte_retain), mte_load + mte_replay of the extended log continue every
+ * document whose log extends the last pass's from that pass's state (replaying only the new ops). */
+int mte_builder_open_doc(mte_builder* b, const char* observer_name, uint32_t* doc);
+int mte_builder_append_messages(mte_builder* b, uint32_t doc, const char* json, size_t len);
 int mte_builder_batch(mte_builder* b, mte_batch* out);   /* view valid until destroy */
 const char* mte_builder_error(const mte_builder* b);
 void mte_builder_destroy(mte_builder* b);

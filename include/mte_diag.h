@@ -21,9 +21,11 @@ int mte_run_info(mte_engine* e, uint32_t* spilled, double* lds_ms, double* hbm_m
  * (k_rows documents that continued HBM-resident in the pass, DocRes mode 6), pass timings ("solo_us",
  * "emit_us", ...). DocRes::spill_why's low byte says why a k_rows document went to the host's re-run:
  * 1 no free HBM slot, 2 the slot too small for its state, 3 no pool row held, 4 the pool full inside
- * an op, 5 the shared-pool route (no in-pass continuation). */
+ * an op, 5 the shared-pool route (no in-pass continuation). "resumed_docs" / "resumed_ops" /
+ * "ck_offered": with mte_retain, documents the last pass continued from a checkpoint, the op records
+ * they did not replay again, and documents whose log extended the previous pass's. */
 int mte_get_info(mte_engine* e, const char* key, int64_t* value);
-/* Tuning: "force_hbm", "pool_limit", "hbm_waves_per_cu", "slot_budget_mb". */
+/* Tuning: "force_hbm", "pool_limit", "hbm_waves_per_cu", "slot_budget_mb"; "retain" = mte_retain. */
 int mte_set_option(mte_engine* e, const char* key, int64_t value);
 /* Phase cycle counters (profiling build only): PROF_SLOTS u64 per document. */
 int mte_profile(mte_engine* e, uint64_t* out, size_t cap);

@@ -44,6 +44,18 @@ class BatchedMergeEngine {
         addon.load(this._engine, b);
         this._docs = addon.builderDocCount(b);
     }
+    _loadBuilder(b) {
+        this._idle();
+        addon.load(this._engine, b);
+        this._docs = addon.builderDocCount(b);
+    }
+    /** mte_retain: keep each document's state after a replay, so replaying logs that extend the last
+     *  pass's replays only their new ops (Client.applyMsg's incremental cost, client.ts:805-836). */
+    retain(on = true) { this._idle(); addon.retain(this._engine, on); }
+    /** op records the last replay did not replay again (continued from the pass before) */
+    resumedOps() { this._idle(); return addon.getInfo(this._engine, "resumed_ops"); }
+    /** mte_get_info: routing and counters of the last pass ("resumed_docs", "rows", "solo", ...) */
+    getInfo(key) { this._idle(); return addon.getInfo(this._engine, key); }
     generate(kind, nDocs, nOps, nClients = 8, seed = 0) {
         this._idle();
         addon.generate(this._engine, kind, nDocs, nOps, nClients, seed);
@@ -107,38 +119,57 @@ function parseSummaries(buf) {
 /**
  * Client-shaped facade for one document (client.ts:42): applyMsg, getText, getLength, snapshot.
  *
- * Batch semantics (documented contract): messages are STAGED by applyMsg/applyMsgs and replayed on
- * the GPU, from the summary (or empty) state, the next time an output is read; reads without new
- * messages reuse that replay. A replay is a kernel launch over the whole log, so read after a batch
- * of messages (a catch-up or summarization step), not after every message: reading after each of n
- * messages replays O(n^2) ops in total. Continuous per-message use belongs to the reference Client.
+ * Incremental like Client.applyMsg (client.ts:805-836): applyMsg stages a message; the next read
+ * parses the staged messages onto the document's open log (builderAppendMessages) and replays on the
+ * GPU only the ops since the previous read, continuing the document's state from that pass (the
+ * engine's retain mode, mte_retain). Reads without new messages reuse the last results. A document
+ * loaded from a summary, or one the row engines cannot hold (relative positions, 64+ clients, ...),
+ * replays from its first op on each read instead: the same results, not incremental.
  */
 class MergeTreeClient {
     constructor(observer = "__observer__", options = {}) {
         this.observer = observer;
         this.options = options;
-        this.messages = [];
+        this.pending = [];
         this.summary = undefined;
+        this.messages = [];       // (summary mode only: the suffix replayed with it)
+        this._builder = addon.createBuilder();
+        this._doc = addon.builderOpenDoc(this._builder, observer);
         this._engine = undefined;
         this._version = 0;        // bumped by every staged change
         this._replayed = -1;      // the version the engine's results belong to
         this._flushing = null;    // pending flush() promise
+        this.replays = 0;
     }
     get _dirty() { return this._version !== this._replayed; }
     /** Client.load / SnapshotLoader (client.ts:944-952): resume from a summary ITree before applyMsg. */
-    load(summary) { this.summary = summary; this.messages = []; this._version++; }
-    applyMsg(msg) { this.messages.push(msg); this._version++; }
+    load(summary) { this.summary = summary; this.messages = []; this.pending = []; this._version++; }
+    applyMsg(msg) { this.pending.push(msg); this._version++; }
     /** Stage a batch of sequenced messages at once (one replay serves them all). */
-    applyMsgs(msgs) { for (const m of msgs) this.messages.push(m); this._version++; }
+    applyMsgs(msgs) { for (const m of msgs) this.pending.push(m); this._version++; }
     _check(version) {
         const [code, seq] = this._engine.docStatus(0);
         if (code === DocStatus.InsertFailed) throw new Error(`MergeTree insert failed at seq ${seq}`);
         if (code !== DocStatus.Ok) throw new Error(`replay failed (status ${code}) at seq ${seq}`);
         this._replayed = version;  // messages staged during an async flush keep the client dirty
+        this.replays++;
     }
     _stage() {
-        if (!this._engine) this._engine = new BatchedMergeEngine(this.options);
-        this._engine.load([{ observer: this.observer, messages: this.messages.slice(), summary: this.summary }]);
+        if (!this._engine) {
+            this._engine = new BatchedMergeEngine(this.options);
+            addon.retain(this._engine._engine, true);
+        }
+        if (this.summary !== undefined) {  // SnapshotLoader + suffix: a whole replay per read
+            for (const m of this.pending) this.messages.push(m);
+            this.pending = [];
+            this._engine.load([{ observer: this.observer, messages: this.messages.slice(), summary: this.summary }]);
+        } else {
+            if (this.pending.length) {
+                addon.builderAppendMessages(this._builder, this._doc, JSON.stringify(this.pending));
+                this.pending = [];
+            }
+            this._engine._loadBuilder(this._builder);
+        }
         return this._version;
     }
     _run() {
@@ -164,6 +195,8 @@ class MergeTreeClient {
         }
         this._check(v);
     }
+    /** op records the last read continued past instead of replaying again */
+    resumedOps() { this._run(); return this._engine.resumedOps(); }
     getText() { return this._run().getText(0); }
     /** Client.getLength (client.ts:1057): markers count 1, unlike getText().length. */
     getLength() { return this._run().getLength(0); }
@@ -179,6 +212,7 @@ module.exports = {
     BatchedMergeEngine, MergeTreeClient, DocStatus,
     abiVersion: addon.abiVersion, buildInfo: addon.buildInfo,
     createBuilder: addon.createBuilder, builderAddDoc: addon.builderAddDoc, builderDocCount: addon.builderDocCount,
+    builderOpenDoc: addon.builderOpenDoc, builderAppendMessages: addon.builderAppendMessages,
     builderAddDocFromSummary: addon.builderAddDocFromSummary, builderAddContainerLog: addon.builderAddContainerLog,
     builderAddMatrixLog: addon.builderAddMatrixLog,
     builderAddMatrixFromSummary: addon.builderAddMatrixFromSummary,

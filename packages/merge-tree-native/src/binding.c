@@ -6,11 +6,13 @@
  */
 #define NAPI_VERSION 8
 #include <node_api.h>
+#include <stdbool.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "../../../include/mte.h"
+#include "../../../include/mte_diag.h"
 
 #define CHECK(env, call)                                                       \
     do {                                                                       \
@@ -248,6 +250,65 @@ static napi_value js_snapshot_matrix(napi_env env, napi_callback_info info) {
     free(buf);
     if (rc) return throw_mte(env, "mte_snapshot_matrix", rc, mte_last_error(e));
     return sv;
+}
+
+/* builderOpenDoc(builder, observerName): number — an open document (its log grows) */
+static napi_value js_builder_open_doc(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) {
+        napi_throw_type_error(env, NULL, "builderOpenDoc(builder, observer)");
+        return NULL;
+    }
+    mte_builder* b = (mte_builder*)get_external(env, argv[0]);
+    char* obs = get_string(env, argv[1], NULL);
+    uint32_t doc = 0;
+    int rc = (b && obs) ? mte_builder_open_doc(b, obs, &doc) : MTE_E_ARG;
+    free(obs);
+    if (rc) return throw_mte(env, "mte_builder_open_doc", rc, b ? mte_builder_error(b) : NULL);
+    return make_u32(env, doc);
+}
+
+/* builderAppendMessages(builder, doc, messagesJson): void — Client.applyMsg of more messages */
+static napi_value js_builder_append_messages(napi_env env, napi_callback_info info) {
+    napi_value argv[3];
+    if (!get_args(env, info, 3, argv)) {
+        napi_throw_type_error(env, NULL, "builderAppendMessages(builder, doc, json)");
+        return NULL;
+    }
+    mte_builder* b = (mte_builder*)get_external(env, argv[0]);
+    uint32_t doc = 0;
+    napi_get_value_uint32(env, argv[1], &doc);
+    size_t len = 0;
+    char* json = get_string(env, argv[2], &len);
+    int rc = (b && json) ? mte_builder_append_messages(b, doc, json, len) : MTE_E_ARG;
+    free(json);
+    if (rc) return throw_mte(env, "mte_builder_append_messages", rc, b ? mte_builder_error(b) : NULL);
+    return NULL;
+}
+
+/* retain(engine, on): void — mte_retain (incremental replay of extended logs) */
+static napi_value js_retain(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    bool on = false;
+    napi_get_value_bool(env, argv[1], &on);
+    int rc = e ? mte_retain(e, on ? 1 : 0) : MTE_E_ARG;
+    if (rc) return throw_mte(env, "mte_retain", rc, e ? mte_last_error(e) : NULL);
+    return NULL;
+}
+
+/* getInfo(engine, key): number — mte_get_info (routing and counters of the last pass) */
+static napi_value js_get_info(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return NULL;
+    mte_engine* e = (mte_engine*)get_external(env, argv[0]);
+    char* key = get_string(env, argv[1], NULL);
+    int64_t v = 0;
+    int rc = (e && key) ? mte_get_info(e, key, &v) : MTE_E_ARG;
+    free(key);
+    if (rc) return throw_mte(env, "mte_get_info", rc, e ? mte_last_error(e) : NULL);
+    return make_f64(env, (double)v);
 }
 
 /* builderDocCount(builder): number */
@@ -598,6 +659,10 @@ static napi_value init(napi_env env, napi_value exports) {
         {"builderAddMatrixFromSummary", 0, js_builder_add_matrix_from_summary, 0, 0, 0, napi_default, 0},
         {"snapshotMatrix", 0, js_snapshot_matrix, 0, 0, 0, napi_default, 0},
         {"builderDocCount", 0, js_builder_doc_count, 0, 0, 0, napi_default, 0},
+        {"builderOpenDoc", 0, js_builder_open_doc, 0, 0, 0, napi_default, 0},
+        {"builderAppendMessages", 0, js_builder_append_messages, 0, 0, 0, napi_default, 0},
+        {"retain", 0, js_retain, 0, 0, 0, napi_default, 0},
+        {"getInfo", 0, js_get_info, 0, 0, 0, napi_default, 0},
         {"load", 0, js_load, 0, 0, 0, napi_default, 0},
         {"generate", 0, js_generate, 0, 0, 0, napi_default, 0},
         {"replay", 0, js_replay, 0, 0, 0, napi_default, 0},

@@ -4,7 +4,8 @@ const assert = require("assert");
 const m = require("..");
 assert.strictEqual(m.abiVersion(), 2);
 assert.ok(/gfx950/.test(m.buildInfo()));
-for (const f of ["BatchedMergeEngine", "MergeTreeClient", "createBuilder", "builderAddDoc", "builderDocCount"]) {
+for (const f of ["BatchedMergeEngine", "MergeTreeClient", "createBuilder", "builderAddDoc", "builderDocCount",
+    "builderOpenDoc", "builderAppendMessages"]) {
     assert.strictEqual(typeof m[f], "function", f);
 }
 const b = m.createBuilder();
@@ -38,4 +39,12 @@ assert.strictEqual(typeof m.BatchedMergeEngine.prototype.rcclCommCreate, "functi
 assert.throws(() => m.gatherSummariesRaw(null, 0, 1, null), /gatherSummaries/);
 assert.throws(() => m.rcclCommCreateRaw(null, Buffer.alloc(128), 0, 2), /rcclCommCreate/);
 assert.throws(() => m.rcclCommCreateRaw(null, Buffer.alloc(3), 0, 2), /rcclCommCreate/);
+// an open document (Client.applyMsg one batch at a time): nothing is added after it
+const ob = m.createBuilder();
+m.builderAddDoc(ob, "__observer__", "[]");
+assert.strictEqual(m.builderOpenDoc(ob, "obs"), 1);
+m.builderAppendMessages(ob, 1, JSON.stringify([msg("a", 1, 0, { pos1: 0, seg: "hi", type: 0 })]));
+assert.throws(() => m.builderAddDoc(ob, "__observer__", "[]"), /mte_builder_add_doc/);
+assert.throws(() => m.builderAppendMessages(ob, 0, "[]"), /mte_builder_append_messages/);
+assert.strictEqual(m.builderDocCount(ob), 2);
 console.log("exports ok");

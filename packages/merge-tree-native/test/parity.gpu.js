@@ -94,5 +94,33 @@ assert.throws(() => e.gatherSummaries(0, 2, null), /communicator/);
     c4.applyMsg(msg("late", 12, 11, { pos1: 11, seg: "!", type: 0 }));  // staged during the flush
     await fl;
     assert.strictEqual(c4.getText(), "hello world!");  // the late message makes the client dirty again
-    console.log(JSON.stringify({ ops: st.ops, checksums: sums.map((s) => s.checksum.toString()), async_ticks: ticks }));
+    // Client.applyMsg interleaved with getText (client.ts:805-836): 10^4 messages of three writers, each
+    // op in the view of every message before it (refSeq = seq - 1), minSeq 16 behind; a read at random
+    // points equals the edited string and replays only the messages since the read before it
+    const ic = new MergeTreeClient("obs");
+    let text = "", prev = 0, reads = 0, rnd = 12345;
+    const rand = (n) => { rnd = (rnd * 1103515245 + 12345) & 0x7fffffff; return rnd % n; };
+    for (let seq = 1; seq <= 10000; seq++) {
+        let c;
+        if (text.length > 0 && rand(10) < 4) {
+            const a = rand(text.length), b = Math.min(text.length, a + 1 + rand(5));
+            c = { pos1: a, pos2: b, type: 1 };
+            text = text.slice(0, a) + text.slice(b);
+        } else {
+            const p = rand(text.length + 1), sg = "abcdef".slice(0, 1 + rand(6));
+            c = { pos1: p, seg: sg, type: 0 };
+            text = text.slice(0, p) + sg + text.slice(p);
+        }
+        ic.applyMsg(msg("w" + rand(3), seq, seq - 1, c, Math.max(0, seq - 16)));
+        if (rand(400) === 0 || seq === 10000) {
+            assert.strictEqual(ic.getText(), text);
+            assert.strictEqual(ic.getLength(), text.length);
+            assert.strictEqual(ic.resumedOps(), reads ? prev : 0);
+            prev = seq;
+            reads++;
+        }
+    }
+    assert.strictEqual(ic.replays, reads);
+    console.log(JSON.stringify({ ops: st.ops, checksums: sums.map((s) => s.checksum.toString()), async_ticks: ticks,
+        interleaved_reads: reads }));
 })().catch((err) => { console.error(err); process.exit(1); });

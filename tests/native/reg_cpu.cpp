@@ -32,7 +32,8 @@ template <bool PAGED, bool PROPS, bool WIDE = false>
 static uint64_t replay_impl(const mte_op* ops, uint64_t n_ops, const uint16_t* payload, uint32_t payload_len,
                             uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
                             uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
-                            DocRes* res, uint32_t pool_rows, const PropTables* pt = nullptr) {
+                            DocRes* res, uint32_t pool_rows, const PropTables* pt = nullptr, uint64_t cut = 0,
+                            uint64_t* ck_resumed = nullptr) {
     std::vector<uint16_t> pay(payload, payload + payload_len + 1);
     std::vector<uint16_t> arena((size_t)arena_cap * 2 + 1, 0);
     DocCfg cfg;
@@ -80,14 +81,40 @@ static uint64_t replay_impl(const mte_op* ops, uint64_t n_ops, const uint16_t* p
     }
     // (the paged engine's pool is its own row arrays here, rows taken in a scattered order)
     typedef RegEngine<(int)RG_ROWS, PAGED, PROPS, WIDE> E;
-    E* ep = new E(p, 0);
-    E& e = *ep;
-    if (PAGED) {
-        e.release_rows();
-        e.pool_rows = pool_rows < RG_ROWS ? pool_rows : RG_ROWS;
-        e.init();
+    auto make = [&]() {
+        E* x = new E(p, 0);
+        if (PAGED) {
+            x->release_rows();
+            x->pool_rows = pool_rows < RG_ROWS ? pool_rows : RG_ROWS;
+            x->init();
+        }
+        return x;
+    };
+    E* ep = make();
+    uint64_t at0 = 0;
+    std::vector<uint32_t> ck;
+    if (cut && cut < n_ops) {
+        // incremental replay (option retain): ops [0, cut) in a first "pass" that checkpoints, then a
+        // fresh engine -- a fresh arena and map table -- continues from the checkpoint
+        cfg.op_end = cut;
+        cfg.ck_cap = E::ck_words(arena_cap, cfg.map_cap, PROPS ? pt->map_words : 0);
+        ck.assign(cfg.ck_cap, 0);
+        p.ck_out = ck.data();
+        const uint64_t a1 = ep->status ? 0 : ep->replay(0, cut);
+        if (ep->status == 0 && a1 == cut) ep->ckpt_save(a1);
+        delete ep;
+        p.ck_out = nullptr;
+        std::fill(arena.begin(), arena.end(), (uint16_t)0);
+        std::fill(maps.begin(), maps.end(), 0u);
+        cfg.op_end = n_ops;
+        cfg.ck_at = cut;
+        p.ck_in = ck.data();
+        ep = make();
+        at0 = ep->ckpt_resume(0);
+        if (ck_resumed) *ck_resumed = at0;
     }
-    const uint64_t at = e.status ? 0 : e.replay(0, n_ops);
+    E& e = *ep;
+    const uint64_t at = e.status ? 0 : e.replay(at0, n_ops);
     if (e.status == REG_HANDOFF) {
         memset(res, 0, sizeof *res);
         res->status = REG_HANDOFF;
@@ -142,6 +169,39 @@ uint64_t regcpu_replay_props(const mte_op* ops, uint64_t n_ops, const uint16_t* 
                                        out_cap, out_text, out_text_cap, res, pool_rows, &t);
     return replay_impl<false, true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
                                     out_cap, out_text, out_text_cap, res, 0, &t);
+}
+
+// Incremental replay: ops [0, cut) checkpointed (reg_engine.hpp ckpt_save), the rest continued on a
+// fresh engine from the checkpoint (ckpt_resume; *resumed = the op it went on from, 0 = it started
+// over). kind: 0 lean, 1 paged, 2 PROPS (3 PROPS paged, +4 WIDE) with the tables of regcpu_replay_props.
+uint64_t regcpu_replay_split(const mte_op* ops, uint64_t n_ops, const uint16_t* payload, uint32_t payload_len,
+                             uint32_t seg_cap, uint32_t arena_cap, uint32_t* out_vis, uint32_t* out_aux,
+                             uint64_t* out_ovl, uint32_t out_cap, uint16_t* out_text, uint64_t out_text_cap,
+                             DocRes* res, uint32_t pool_rows, uint32_t kind, uint64_t cut, uint64_t* resumed,
+                             const uint32_t* propsets, uint32_t n_propsets, const uint32_t* prop_keys,
+                             const uint32_t* prop_vals, const uint32_t* val_flags, uint32_t n_vals, uint32_t map_words,
+                             uint32_t map_cap, uint32_t* out_maps) {
+    PropTables t{(const mte_propset*)propsets, n_propsets, prop_keys, prop_vals, val_flags, n_vals, map_words, map_cap, out_maps};
+    switch (kind) {
+        case 0:
+            return replay_impl<false, false>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
+                                             out_cap, out_text, out_text_cap, res, 0, nullptr, cut, resumed);
+        case 1:
+            return replay_impl<true, false>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
+                                            out_cap, out_text, out_text_cap, res, pool_rows, nullptr, cut, resumed);
+        case 2:
+            return replay_impl<false, true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
+                                            out_cap, out_text, out_text_cap, res, 0, &t, cut, resumed);
+        case 3:
+            return replay_impl<true, true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux, out_ovl,
+                                           out_cap, out_text, out_text_cap, res, pool_rows, &t, cut, resumed);
+        case 6:
+            return replay_impl<false, true, true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux,
+                                                  out_ovl, out_cap, out_text, out_text_cap, res, 0, &t, cut, resumed);
+        default:
+            return replay_impl<true, true, true>(ops, n_ops, payload, payload_len, seg_cap, arena_cap, out_vis, out_aux,
+                                                 out_ovl, out_cap, out_text, out_text_cap, res, pool_rows, &t, cut, resumed);
+    }
 }
 
 uint32_t regcpu_docres_size(void) { return (uint32_t)sizeof(DocRes); }

@@ -39,6 +39,9 @@ def lib():
         L.regcpu_replay_props.restype = u64
         L.regcpu_replay_props.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u32, vp, u64, vp, u32,
                                           vp, u32, vp, vp, vp, u32, u32, u32, vp, u32]
+        L.regcpu_replay_split.restype = u64
+        L.regcpu_replay_split.argtypes = [vp, u64, vp, u32, u32, u32, vp, vp, vp, u32, vp, u64, vp, u32, u32, u64, vp,
+                                          vp, u32, vp, vp, vp, u32, u32, u32, vp]
         L.regcpu_docres_size.restype = u32
         L.regcpu_heap.restype = u32
         L.regcpu_heap.argtypes = [vp, u32, vp]
@@ -137,6 +140,39 @@ def replay_props(ops, pay, gp, pool_rows=0, map_words=16, wide=False):
     r = res[0]
     k = int(r["n_segs"])
     return at, r, (vis[:k], aux[:k], ovl[:k]), text, omaps[:k]
+
+
+def replay_split(ops, pay, cut, kind=0, pool_rows=16, gp=None, map_words=16, arena_cap=None):
+    """Incremental replay on the CPU build (reg_engine.hpp ckpt_save / ckpt_resume): ops [0, cut) then a
+    fresh engine continuing from the checkpoint. kind 0 lean, 1 paged, 2 PROPS, 3 PROPS paged, 6 / 7
+    PROPS + WIDE. Returns (stop index, op the continuation started from, DocRes, rows, text, maps)."""
+    ops = np.ascontiguousarray(ops, dtype=_op_dtype())
+    pay = np.ascontiguousarray(pay, dtype=np.uint16)
+    n = len(ops)
+    seg_cap = 3 * n + 8
+    if arena_cap is None:
+        arena_cap = 6 * len(pay) + 4096
+    cap = seg_cap
+    vis = np.zeros((cap, 4), dtype=np.uint32)
+    aux = np.zeros((cap, 4), dtype=np.uint32)
+    ovl = np.zeros(cap, dtype=np.uint64)
+    text = np.zeros(len(pay) + 16, dtype=np.uint16)
+    res = np.zeros(1, dtype=DOCRES)
+    omaps = np.zeros((cap, map_words), dtype=np.uint32)
+    pay1 = np.concatenate([pay, np.zeros(1, dtype=np.uint16)])
+    resumed = ctypes.c_uint64(0)
+    z = np.zeros(2, dtype=np.uint32)
+    g = gp if gp is not None else None
+    at = lib().regcpu_replay_split(ops.ctypes.data, n, pay1.ctypes.data, len(pay), seg_cap, arena_cap,
+                                   vis.ctypes.data, aux.ctypes.data, ovl.ctypes.data, cap, text.ctypes.data, len(text),
+                                   res.ctypes.data, pool_rows, kind, cut, ctypes.addressof(resumed),
+                                   (g.propsets if g else z).ctypes.data, g.n_propsets if g else 0,
+                                   (g.prop_keys if g else z).ctypes.data, (g.prop_vals if g else z).ctypes.data,
+                                   (g.val_flags if g else z).ctypes.data, len(g.VALS) if g else 0, map_words,
+                                   2 * n + 64, omaps.ctypes.data)
+    r = res[0]
+    k = int(r["n_segs"])
+    return at, int(resumed.value), r, (vis[:k], aux[:k], ovl[:k]), text, omaps[:k]
 
 
 def rows_json(rows, text, names, props=None):

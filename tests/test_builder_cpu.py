@@ -91,3 +91,60 @@ def test_builder_rejects_out_of_scope():
     b = mte.Builder()
     with pytest.raises(mte.MteError):
         b.add_doc([msg("a", 1, 0, {"register": "r", "seg": "q", "type": 0})])
+
+
+def _batch_arrays(b):
+    """(op records with MTE_F_CATCHUP cleared, payload, client names) of a builder's batch."""
+    bt = b.batch()
+    ops = mte.batch_ops(bt).copy()
+    npay = bt.doc_payload_offsets[bt.n_docs]
+    pay = bytes((ctypes.c_uint16 * npay).from_address(ctypes.addressof(bt.payload.contents))) if npay else b""
+    flags = ops["flags"].copy()
+    return ops, flags, pay, [bt.doc_op_offsets[i] for i in range(bt.n_docs + 1)]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_open_document_grows_like_a_whole_log(seed):
+    """mte_builder_open_doc + append_messages in random chunks (Client.applyMsg one batch at a time)
+    make the same batch as add_doc of the whole log: op records, payload, offsets -- at every cut the
+    open document is the log so far (its catch-up flags mark the messages above minSeq at that end)."""
+    msgs = random_log(seed, n=250)
+    whole = mte.Builder()
+    whole.add_doc(msgs, observer="obs")
+    ops_w, fl_w, pay_w, off_w = _batch_arrays(whole)
+    b = mte.Builder()
+    d = b.open_doc("obs")
+    assert d == 0
+    rng = random.Random(seed)
+    i = 0
+    while i < len(msgs):
+        k = rng.randint(1, 40)
+        b.append(d, msgs[i: i + k])
+        i += k
+        pre = mte.Builder()
+        pre.add_doc(msgs[:i], observer="obs")
+        ops_p, fl_p, pay_p, _ = _batch_arrays(pre)
+        ops_o, fl_o, pay_o, _ = _batch_arrays(b)
+        assert (ops_o == ops_p).all() and pay_o == pay_p
+    ops_o, fl_o, pay_o, off_o = _batch_arrays(b)
+    assert (ops_o == ops_w).all() and pay_o == pay_w and off_o == off_w
+
+
+def test_open_document_after_committed_ones_and_refusals():
+    """An open document follows the committed ones; nothing may be added after it; a refused append
+    leaves its log as it was."""
+    b = mte.Builder()
+    b.add_doc(hello_world_log(), observer="obs")
+    d = b.open_doc("obs")
+    assert d == 1
+    with pytest.raises(mte.MteError):
+        b.add_doc(hello_world_log(), observer="obs")
+    b.append(d, hello_world_log())
+    before = _batch_arrays(b)
+    bad = [msg("x", 99, 0, {"pos1": 0, "seg": {"text": "a"}, "type": 0, "register": 1})]
+    with pytest.raises(mte.MteError):
+        b.append(d, bad)
+    after = _batch_arrays(b)
+    assert (before[0] == after[0]).all() and before[2] == after[2] and before[3] == after[3]
+    with pytest.raises(mte.MteError):
+        b.append(0, hello_world_log())  # a committed document is not open

@@ -43,3 +43,4 @@ def test_addon_replay_gpu_matches_oracle():
     ops, cks, st = replay_batch(ctypes.addressof(batch), 0, 8, threads=4)
     assert out["ops"] == ops
     assert [int(c) for c in out["checksums"]] == cks
+    assert out["interleaved_reads"] > 10

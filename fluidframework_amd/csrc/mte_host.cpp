@@ -1383,6 +1383,7 @@ static int run_kernel(mte_engine* e, bool gen) {
         // document outgrowing them continuing HBM-resident; tools/wide_probe.py, profiles/r05/r05l)
         rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : (long_docs || e->rows_wide) ? 4u : 12u;
     }
+    if (ck && rows) rows = 4;  // (the checkpointing k_rows runs 4 waves per CU on fixed rows)
     e->last_rows = rows;
     if (rows) groups = hbm_waves = lds_active = 0;
     e->P.slot_hbm0 = groups * LDS_WAVES;
@@ -1415,7 +1416,7 @@ static int run_kernel(mte_engine* e, bool gen) {
     if (n_solo) {
         HIP_TRY(e, hipStreamWaitEvent(s_solo, e->ev0, 0));
         HIP_TRY(e, hipEventRecord(e->ev_s0, s_solo));
-        HIP_TRY(e, launch_solo(e->P, gen, full, n_solo, s_solo));
+        HIP_TRY(e, launch_solo(e->P, gen, full, n_solo, ck, s_solo));
         HIP_TRY(e, hipEventRecord(e->ev_s1, s_solo));
         HIP_TRY(e, hipEventRecord(e->ev3, s_solo));
         // the bulk starts once the solo workgroups hold their CUs (k_solo_gate)
@@ -1427,7 +1428,7 @@ static int run_kernel(mte_engine* e, bool gen) {
         const uint32_t cus = bulk_cus(e, n_solo);
         const uint32_t per = rows >= 12 ? 12u : rows >= 8 ? 8u : 4u;
         HIP_TRY(e, launch_rows(e->P, per, std::min<uint32_t>(cus, (nd - n_solo + per - 1) / per), full == 1,
-                               full == 1 && e->rows_wide, s_main));
+                               full == 1 && e->rows_wide, ck, s_main));
         // documents k_rows handed to HBM slots between two ops continue here (k_rows_cont)
         HIP_TRY(e, launch_rows_cont(e->P, full == 1, full == 1 && e->rows_wide, e->P.n_hslots, s_main));
     }

@@ -7,11 +7,11 @@
 
 namespace mte {
 hipError_t launch_lds(const Params& p, bool gen, int full, u32 n_groups, hipStream_t s);
-hipError_t launch_solo(const Params& p, bool gen, int full, u32 n_solo, hipStream_t s);
+hipError_t launch_solo(const Params& p, bool gen, int full, u32 n_solo, bool ck, hipStream_t s);
 // wait (one wave, <= 20 ms) until `n_solo` solo workgroups have started: issued on the bulk's stream
 hipError_t launch_solo_gate(const u32* started, u32 n_solo, hipStream_t s);
 // lean replays: the bulk (doc_list[n_prio ..)) on the row engine, waves_per_cu 4 or 8 per CU
-hipError_t launch_rows(const Params& p, u32 waves_per_cu, u32 n_groups, bool props, bool wide, hipStream_t s);
+hipError_t launch_rows(const Params& p, u32 waves_per_cu, u32 n_groups, bool props, bool wide, bool ck, hipStream_t s);
 hipError_t launch_hbmq(const Params& p, bool gen, int full, u32 n_waves, hipStream_t s);
 hipError_t launch_rows_cont(const Params& p, bool props, bool wide, u32 n_slots, hipStream_t s);
 extern const u64 ROWS_DUMP_BYTES;  // a slot must hold k_rows' state dump (mte_solo.hip RowsDump)

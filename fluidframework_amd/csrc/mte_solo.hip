@@ -22,7 +22,11 @@ namespace mte {
 // workgroup each, owning all of a CU's LDS (SoloPlan), at the highest wave priority. The replay
 // latency of the longest document bounds a Zipf batch, so it gets the plan with the
 // most room and no LDS-pool sharing; it continues HBM-resident only if it outgrows even that.
-template <bool GEN, int LVL>
+// CK (option retain): the row engine continues from the previous pass's checkpoint and leaves its
+// own -- separate instantiations, so the kernels of a pass without retain are exactly the ones before
+// (the checkpoint code in the same kernel cost the lone 10^6-op document 1.6 %: 3.885 vs 3.825 us/op
+// on one box, profiles/r06/ck_ab.json)
+template <bool GEN, int LVL, bool CK = false>
 MTE_DEV void solo_doc(const Params& p) {
     const u32 i = blockIdx.x;
     if (i >= p.n_solo) return;
@@ -54,10 +58,10 @@ MTE_DEV void solo_doc(const Params& p) {
         // to the LDS plan below only if it outgrows the registers or reaches an op they do not cover
         if (p.reg_solo) {
             RegEngine<> r(p, d);
-            at = r.ckpt_resume(at);  // (option retain: the previous pass's state, if this log extends it)
+            if constexpr (CK) at = r.ckpt_resume(at);  // the previous pass's state, if this log extends it
             at = r.replay(at, p.docs[d].op_end);
             if (r.status != REG_HANDOFF) {
-                r.ckpt_save(at - p.docs[d].op_begin);
+                if constexpr (CK) r.ckpt_save(at - p.docs[d].op_begin);
                 r.finish();
                 stamp();
                 __builtin_amdgcn_s_setprio(0);
@@ -79,10 +83,10 @@ MTE_DEV void solo_doc(const Params& p) {
             // WIDE: clients 32..63 too (a second removers array after the map ids)
             RegEngine<(int)RG_ROWS, false, true, true> r(p, d, vb, ab, 4, 0, ab + RG_BLOCKS * 8 * 16,
                                                          ab + RG_BLOCKS * 8 * 16 + RG_BLOCKS * 8 * 4);
-            at = r.ckpt_resume(at);
+            if constexpr (CK) at = r.ckpt_resume(at);
             if (!r.status) at = r.replay(at, p.docs[d].op_end);
             if (r.status != REG_HANDOFF) {
-                r.ckpt_save(at - p.docs[d].op_begin);
+                if constexpr (CK) r.ckpt_save(at - p.docs[d].op_begin);
                 r.finish();
                 stamp();
                 __builtin_amdgcn_s_setprio(0);
@@ -135,14 +139,14 @@ MTE_DEV void solo_doc(const Params& p) {
 // AGPRs: the clobbers below make the kernel's allocation the maximum), and all of the CU's LDS: no
 // other wave of the pass can be resident on a critical-path CU. Wave 0 replays the document; the
 // others wait at the barrier (issuing nothing) until it is done.
-template <bool GEN, int LVL>
+template <bool GEN, int LVL, bool CK = false>
 __global__ __launch_bounds__(64 * SOLO_WAVES) __attribute__((amdgpu_waves_per_eu(MTE_SOLO_WPE, MTE_SOLO_WPE))) void k_solo(Params p) {
 #if SOLO_WAVES > 1
     asm volatile("" ::: "v255", "a255");
-    if (wave_first(threadIdx.x >> 6) == 0) solo_doc<GEN, LVL>(p);
+    if (wave_first(threadIdx.x >> 6) == 0) solo_doc<GEN, LVL, CK>(p);
     __syncthreads();
 #else
-    solo_doc<GEN, LVL>(p);
+    solo_doc<GEN, LVL, CK>(p);
 #endif
 }
 
@@ -378,7 +382,9 @@ hipError_t launch_rows_cont(const Params& p, bool props, bool wide, u32 n_slots,
     return props ? launch_rows_cont_t<true, false>(p, n_slots, s) : launch_rows_cont_t<false, false>(p, n_slots, s);
 }
 
-template <int RW, bool PROPS, bool WIDE>
+// CK (option retain, 4 waves only): documents continue from the previous pass's checkpoints and leave
+// their own (reg_engine.hpp ckpt_*)
+template <int RW, bool PROPS, bool WIDE, bool CK = false>
 __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4, RW / 4))) void k_rows(Params p) {
     typedef RowsGeom<PROPS, WIDE> G;
     constexpr bool PAGED = RW > 4;
@@ -439,7 +445,8 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
             d = p.doc_list[i];
         }
         RegEngine<PAGED ? (int)RG_ROWS : (int)G::FIXED_NR, PAGED, PROPS, WIDE> r(p, d, vb, ab, 5, G::MASK, pb, r2b);
-        u64 at = r.ckpt_resume(p.docs[d].op_begin);
+        u64 at = p.docs[d].op_begin;
+        if constexpr (CK) at = r.ckpt_resume(at);
         if (!r.status) at = r.replay(at, p.docs[d].op_end);
         if (r.status == REG_HANDOFF && PAGED && p.rows_retry && r.pool_full && !again) {
             // marked for the host's re-run first (so a document no wave restarts is still replayed),
@@ -461,7 +468,7 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
                 if (lane_id() == 0) p.res[d].spill_why |= why;
             }
         } else {
-            r.ckpt_save(at - p.docs[d].op_begin);
+            if constexpr (CK) r.ckpt_save(at - p.docs[d].op_begin);
             r.finish();
         }
         r.release_rows();
@@ -469,13 +476,17 @@ __global__ __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW / 4,
 }
 
 template <bool PROPS, bool WIDE>
-static hipError_t launch_rows_t(const Params& p, u32 rw, u32 n_groups, hipStream_t s) {
+static hipError_t launch_rows_t(const Params& p, u32 rw, u32 n_groups, bool ck, hipStream_t s) {
     typedef RowsGeom<PROPS, WIDE> G;
-    const void* k = rw == 12 ? (const void*)k_rows<12, PROPS, WIDE>
+    const void* k = ck ? (const void*)k_rows<4, PROPS, WIDE, true>
+                  : rw == 12 ? (const void*)k_rows<12, PROPS, WIDE>
                   : rw == 8  ? (const void*)k_rows<8, PROPS, WIDE>
                              : (const void*)k_rows<4, PROPS, WIDE>;
+    if (ck) rw = 4;
     static const hipError_t attr = [] {
         hipError_t r = hipFuncSetAttribute((const void*)k_rows<4, PROPS, WIDE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::FIXED_LDS);
+        if (r == hipSuccess)
+            r = hipFuncSetAttribute((const void*)k_rows<4, PROPS, WIDE, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::FIXED_LDS);
         for (const void* f : {(const void*)k_rows<8, PROPS, WIDE>, (const void*)k_rows<12, PROPS, WIDE>})
             if (r == hipSuccess) r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
         return r;
@@ -485,27 +496,33 @@ static hipError_t launch_rows_t(const Params& p, u32 rw, u32 n_groups, hipStream
     return hipLaunchKernel(k, dim3(n_groups), dim3(64 * rw), args, (size_t)(rw == 4 ? G::FIXED_LDS : G::LDS), s);
 }
 // WIDE (clients 32..63) only with PROPS: such a batch is a FULL one (the lean LDS kernels keep 32-bit
-// removers masks), whose row engine is the property-carrying one
-hipError_t launch_rows(const Params& p, u32 waves_per_cu, u32 n_groups, bool props, bool wide, hipStream_t s) {
+// removers masks), whose row engine is the property-carrying one. ck (option retain): the checkpointing
+// instantiation, 4 waves per CU on fixed rows.
+hipError_t launch_rows(const Params& p, u32 waves_per_cu, u32 n_groups, bool props, bool wide, bool ck, hipStream_t s) {
     const u32 rw = waves_per_cu >= 12 ? 12u : waves_per_cu >= 8 ? 8u : 4u;
-    if (wide) return props ? launch_rows_t<true, true>(p, rw, n_groups, s) : hipErrorInvalidValue;
-    return props ? launch_rows_t<true, false>(p, rw, n_groups, s) : launch_rows_t<false, false>(p, rw, n_groups, s);
+    if (wide) return props ? launch_rows_t<true, true>(p, rw, n_groups, ck, s) : hipErrorInvalidValue;
+    return props ? launch_rows_t<true, false>(p, rw, n_groups, ck, s) : launch_rows_t<false, false>(p, rw, n_groups, ck, s);
 }
 
 #define MTE_PICK(K, gen, lvl)                                                                           \
     ((gen) ? (const void*)K<true, 1> : (lvl) >= 2 ? (const void*)K<false, 2> : (lvl) == 1 ? (const void*)K<false, 1> \
                                                                                : (const void*)K<false, 0>)
 
-hipError_t launch_solo(const Params& p, bool gen, int full, u32 n_solo, hipStream_t s) {
+hipError_t launch_solo(const Params& p, bool gen, int full, u32 n_solo, bool ck, hipStream_t s) {
     static const hipError_t attr = [] {
         hipError_t r = hipFuncSetAttribute((const void*)k_solo<true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SoloPlan));
-        for (const void* k : {(const void*)k_solo<false, 0>, (const void*)k_solo<false, 1>, (const void*)k_solo<false, 2>})
+        for (const void* k : {(const void*)k_solo<false, 0>, (const void*)k_solo<false, 1>, (const void*)k_solo<false, 2>,
+                              (const void*)k_solo<false, 0, true>, (const void*)k_solo<false, 1, true>})
             if (r == hipSuccess) r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SoloPlan));
         return r;
     }();
     if (attr != hipSuccess) return attr;
     void* args[] = {(void*)&p};
-    return hipLaunchKernel(MTE_PICK(k_solo, gen, full), dim3(n_solo), dim3(64 * SOLO_WAVES), args, sizeof(SoloPlan), s);
+    // (the checkpointing instantiations exist for the row-engine levels only: lean and FULL)
+    const void* k = ck && !gen && full == 0 ? (const void*)k_solo<false, 0, true>
+                  : ck && !gen && full == 1 ? (const void*)k_solo<false, 1, true>
+                                            : MTE_PICK(k_solo, gen, full);
+    return hipLaunchKernel(k, dim3(n_solo), dim3(64 * SOLO_WAVES), args, sizeof(SoloPlan), s);
 }
 
 }  // namespace mte

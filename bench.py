@@ -33,6 +33,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "sequenced ops applied/sec (whole node) + achieved HBM GB/s, 256k docs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# measured on the box (tools/microbench/stream.hip, profiles/r06/stream.txt): float4 streams over 4 GiB
+# buffers, best of 10 launches -- read-only, write-only and copy (read + write bytes)
+HBM_MEASURED_GBS = {"read": 6175.1, "write": 5386.2, "copy": 4679.2, "source": "profiles/r06/stream.txt"}
 OP_RECORD_B, LEAF_BLOCK_B = 32, 512  # SURVEY §8(d) algorithmic bytes per op: 32 + P + 512
 # SURVEY §8(d) configs. docs: per GPU for weak-scaling configs, whole job for strong ones.
 CONFIGS = {
@@ -290,6 +293,7 @@ def run(args):
                        "ops_per_step": total_ops, "clients": args.clients, "parallelism": f"doc-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "measured_peak_gbs": HBM_MEASURED_GBS,
                          "kernel": "replay pass: mte::k_solo + mte::k_rows (the bulk; k_lds / k_hbmq for batches the rows cannot take) + mte::k_rows_cont (concurrent streams) + SnapshotV1 emission (mte::k_emit_count/k_emit_write, overlapped with k_solo)",
                          "kernel_ms": kernel_ms, "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,

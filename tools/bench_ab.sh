@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box: bench.py lines for (config, option) pairs, one JSON line each into gpurun_out/<tag>/.
-# Usage: T=<tag> bash tools/r04_bench_ab.sh "C2:" "C2:rows_bulk=4" "C5:rows_bulk=4" ...
+# Usage: T=<tag> bash tools/bench_ab.sh "C2:" "C2:rows_bulk=4" "C5:rows_bulk=4" ...
 #   (config:opt[,opt...]; an empty opt list = the default engine options)
 set -o pipefail
 T=${T:-bab}

@@ -5,8 +5,9 @@
 #   suite[:<-k expr>]     the -m gpu parity suite in one process   -> <tag>/gpu_tests.log
 #   smoke                 __graft_entry__.smoke()                  -> <tag>/smoke.log
 #   lone:<lib>[,<lib>..]  lone 10^6-op document A/B over MTE_LIB variants ("cur" = default build)
-#   bench:<spec>[;<spec>] bench.py lines, spec = config:opt[,opt] (tools/r04_bench_ab.sh)
+#   bench:<spec>[;<spec>] bench.py lines, spec = config:opt[,opt] (tools/bench_ab.sh)
 #   profile               rocprofv3 kernel trace + FETCH/WRITE passes of the default bench (tools/profile.sh)
+#   pmclone:<ops>:<lib>[,<lib>..]  SQ counter passes of the lone document per library (tools/pmc_lone_ab.sh)
 set -o pipefail
 T=${1:?tag}; shift
 export TMPDIR=/tmp
@@ -25,13 +26,16 @@ for step in "$@"; do
       tail -1 gpurun_out/$T/smoke.log ;;
     lone:*)
       libs=${step#lone:}
-      T=$T bash tools/r04_ab.sh ${libs//,/ } || exit 1 ;;
+      T=$T bash tools/lone_ab.sh ${libs//,/ } || exit 1 ;;
     bench:*)
       specs=${step#bench:}
       IFS=';' read -ra S <<< "$specs"
-      T=$T TO=${BENCH_TO:-600} bash tools/r04_bench_ab.sh "${S[@]}" || exit 1 ;;
+      T=$T TO=${BENCH_TO:-600} bash tools/bench_ab.sh "${S[@]}" || exit 1 ;;
     profile)
       bash tools/profile.sh $T || exit 1 ;;
+    pmclone:*)
+      x=${step#pmclone:}; n=${x%%:*}; libs=${x#*:}
+      bash tools/pmc_lone_ab.sh $T/pmc $n ${libs//,/ } || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU box: SQ / SQC counter passes of the lone-document replay (k_solo<false, 0>) for each library
 # variant (MTE_LIB names, "cur" = default build); prints per-op counts.
-# Usage: bash tools/r04_pmc_ab.sh <tag> <ops> lib...
+# Usage: bash tools/pmc_lone_ab.sh <tag> <ops> lib...
 set -o pipefail
 export TMPDIR=/tmp
 T=$1; N=$2; shift 2

@@ -1,4 +1,4 @@
-"""SQ counters of k_rows (tools/r04_pmc_rows.sh): per op of the C2 batch and per wave-cycle.
+"""SQ counters of k_rows (tools/pmc_rows.sh): per op of the C2 batch and per wave-cycle.
 Usage: python tools/pmc_rows.py [gpurun_out/pmc_rows] -> profiles/r04/pmc_rows_c2.json"""
 import csv
 import glob
@@ -29,7 +29,7 @@ def main(d=os.path.join(ROOT, "gpurun_out", "pmc_rows")):
         derived = {"issue_fraction_per_wave": round(tot.get("SQ_ACTIVE_INST_ANY", 0) / wc, 3),
                    "wait_fraction_per_wave": round(tot.get("SQ_WAIT_ANY", 0) / wc, 3),
                    "instructions_per_op": round(sum(tot.get(k, 0) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM")) / ops, 1)}
-    out = {"config": "C2 (4 096 docs x 10^4 ops), k_rows at 8 waves per CU (two per SIMD)", "source": "tools/r04_pmc_rows.sh",
+    out = {"config": "C2 (4 096 docs x 10^4 ops), k_rows at 8 waves per CU (two per SIMD)", "source": "tools/pmc_rows.sh",
            "k_rows_launches_per_pass": n, "vgpr_count": vgpr, "raw": tot, "per_op": per_op, "derived": derived}
     json.dump(out, open(os.path.join(ROOT, "profiles", "r04", "pmc_rows_c2.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))

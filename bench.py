@@ -51,6 +51,70 @@ CONFIGS = {
 GEN_SEED = 1000  # one seed for every rank: documents differ by global id only
 
 
+def ops_to_messages(ops, pay, lo, hi):
+    """Op records [lo, hi) of a generated document (one message per record: C2 / C5 mixes carry text
+    inserts and removes only) as the ISequencedDocumentMessage JSON the builder ingests."""
+    out = []
+    for o in ops[lo:hi]:
+        t = int(o["type"])
+        if t == 0:
+            a, b = int(o["a"]), int(o["b"])
+            c = {"pos1": int(o["pos1"]), "seg": pay[a:a + b].tobytes().decode("utf-16-le"), "type": 0}
+        else:
+            c = {"pos1": int(o["pos1"]), "pos2": int(o["a"]), "type": 1}
+        out.append({"clientId": f"w{int(o['client'])}", "sequenceNumber": int(o["seq"]),
+                    "referenceSequenceNumber": int(o["ref_seq"]), "minimumSequenceNumber": int(o["msn"]),
+                    "type": "op", "contents": c})
+    return out
+
+
+def catchup_probe(args, n_docs=16, n_ops=20000):
+    """What a summarizer catching up C5-shaped documents meets: each document of
+    a generated C5-mix batch is cut at a random message, its prefix replayed and summarized on the GPU
+    (SnapshotV1, chunk size 10 000: the reference's default), and the summary loaded with the rest of
+    the log (SnapshotLoader + applyMsg). Outcomes by document: loaded, the reference's own "insert
+    failed" (loadBody's never-cleared batch), refused (MTE_DOC_UNSUPPORTED: the aliased re-link),
+    and how many summaries had body chunks. Product path only (the oracle is not used)."""
+    import numpy as np
+
+    from fluidframework_amd import mte
+    rng = np.random.default_rng(7)
+    t0 = time.time()
+    g = mte.Engine(0)
+    g.generate(5, n_docs, n_ops, n_clients=8, seed=GEN_SEED)
+    b = g.export_batch()
+    ops = mte.batch_ops(b).copy()
+    npay = b.doc_payload_offsets[b.n_docs]
+    pay = np.frombuffer(bytes((ctypes.c_uint16 * npay).from_address(ctypes.addressof(b.payload.contents))),
+                        dtype=np.uint16)
+    cuts, logs = [], []
+    pre = mte.Builder()
+    for d in range(n_docs):
+        lo, hi = b.doc_op_offsets[d], b.doc_op_offsets[d + 1]
+        p0 = b.doc_payload_offsets[d]
+        cut = int(rng.integers((hi - lo) // 4, 3 * (hi - lo) // 4))
+        msgs = ops_to_messages(ops, pay[p0:], lo, hi)
+        logs.append(msgs)
+        cuts.append(cut)
+        pre.add_doc(msgs[:cut], observer="__observer__")
+    g.close()
+    e = mte.Engine(0)
+    e.load(pre.batch())
+    e.replay()
+    summaries = [e.snapshot_json(d) for d in range(n_docs)]
+    body = sum(1 for s in summaries if len(json.loads(s)["entries"]) > 1)
+    cu = mte.Builder()
+    for d in range(n_docs):
+        cu.add_doc_from_summary(summaries[d], logs[d][cuts[d]:], observer="__observer__")
+    e.load(cu.batch())
+    e.replay()
+    st = [e.status(d)[0] for d in range(n_docs)]
+    e.close()
+    return {"docs": n_docs, "ops_per_doc": n_ops, "summaries_with_body_chunks": body,
+            "loaded": st.count(0), "insert_failed": st.count(1), "refused": st.count(4),
+            "other": n_docs - st.count(0) - st.count(1) - st.count(4), "seconds": round(time.time() - t0, 2)}
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -60,6 +124,7 @@ def parse(argv=None):
     ap.add_argument("--docs", type=int, default=None)
     ap.add_argument("--ops", type=int, default=None)
     ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--catchup-probe", type=int, default=1, help="0: skip the catch-up outcome probe")
     ap.add_argument("--kind", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--cpu-threads", type=int, default=None, help="default: one per host core available")
@@ -280,6 +345,8 @@ def run(args):
                          f"document ({len(sample)} docs, {c_ops} ops, replay only, longest first) of the same "
                          f"{args.config} batch on {threads} threads, one per usable host core ({why}), in {dt:.2f} s"}
 
+    probe = catchup_probe(args) if rank == 0 and args.catchup_probe else None
+
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "ops/s", "n_gpus": world, "steps": args.steps,
@@ -316,7 +383,8 @@ def run(args):
                       "docs_hbm_waves": info["hbm_docs"], "lds_groups": info["lds_groups"],
                       "hbm_wave_slots": info["hbm_waves"], "rows_waves_per_cu": eng.get_info("rows"),
                       "gen_s": gen_s, "summary_s": snap_host_s,
-                      "snapshot_bytes": snap_bytes, "summaries_gathered": gathered, "oracle_verified_docs": nv},
+                      "snapshot_bytes": snap_bytes, "summaries_gathered": gathered, "oracle_verified_docs": nv,
+                      "catchup_probe": probe},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -21,7 +21,7 @@ out, n, lib = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 tot = collections.defaultdict(float)
 for p in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(p)):
-        if "k_solo<false, 0>" in r["Kernel_Name"]:
+        if "k_solo<false, 0" in r["Kernel_Name"]:
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
 print(lib, {k: round(v / n, 2) for k, v in sorted(tot.items())}, flush=True)
 PY

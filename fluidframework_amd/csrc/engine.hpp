@@ -688,7 +688,9 @@ struct Engine {
     // posFromRelativePos (mergeTree.ts:1943-1966) for the op's RELPOS record (include/mte.h): the
     // marker is found by its builder tag (bits 16..31 of its refType word, aux.y) and
     // getPosition(marker, R, C) (mergeTree.ts:1586-1603) is the visible length before it in document
-    // order. An unmapped tag, or a marker zamboni has dropped, fails the document (unsupported).
+    // order. An unmapped tag fails the document (unsupported). A tagged marker no longer in the tree
+    // was dropped by zamboni, which unlinks it (scourNode: parent = undefined, mergeTree.ts:1317): the
+    // reference's parent walk is then empty, getPosition 0.
     MTE_DEV bool marker_pos(u32 tag, i32 R, u32 C, i32 seq, i32& out) {
         if (tag == 0 || tag > 0xFFFFu) {
             fail(MTE_DOC_UNSUPPORTED, seq);
@@ -709,9 +711,9 @@ struct Engine {
                 break;
             }
         }
-        if (k == NONE) {
-            fail(MTE_DOC_UNSUPPORTED, seq);
-            return false;
+        if (k == NONE) {  // unlinked by zamboni
+            out = 0;
+            return true;
         }
         i32 cum = 0;
         for (u32 base = 0; base < k; base += 64) {
@@ -745,6 +747,12 @@ struct Engine {
         if (rr.a) {
             if (!marker_pos((u32)rr.a, R, C, op.seq, q)) return false;
             op.a = (rr.flags & MTE_F_REL_BEFORE2) ? q - (i32)rr.props : q + 1 + (i32)rr.props;
+        }
+        // a position before 0 (an unlinked marker, "before" with an offset): not modelled (the
+        // reference's walks then run below the tree's start)
+        if ((rr.pos1 && op.pos1 < 0) || (rr.a && op.a < 0)) {
+            fail(MTE_DOC_UNSUPPORTED, op.seq);
+            return false;
         }
         return true;
     }

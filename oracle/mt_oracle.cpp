@@ -974,15 +974,18 @@ class Doc {
         if (i) catchup.erase(catchup.begin(), catchup.begin() + i);
     }
 
-    // posFromRelativePos (mergeTree.ts:1943-1966) -> getPosition (:1586-1603). A marker no longer
-    // linked into the tree (zamboni dropped it; the reference would walk its stale parent chain) and
-    // an unmapped id are unsupported.
+    // posFromRelativePos (mergeTree.ts:1943-1966) -> getPosition (:1586-1603). An unmapped id is
+    // unsupported. A marker zamboni dropped is unlinked (scourNode sets its parent undefined,
+    // mergeTree.ts:1317): getPosition's walk up the parents is empty and gives 0, so the position is
+    // 0 + cachedLength + offset, or 0 - offset before it (client.getPostion.spec.ts:41-57 pins the
+    // unlinking).
     int markerPos(uint32_t tag, int refSeq, int clientId) {
         auto it = tag && tag <= 0xFFFFu ? tagged.find(tag) : tagged.end();
         if (it == tagged.end()) throw EngineError(MTE_DOC_UNSUPPORTED, "relative position: marker id not mapped");
         return getPosition(it->second, refSeq, clientId);
     }
     int getPosition(Node* node, int refSeq, int clientId) {
+        if (!node->parent) return 0;  // unlinked by zamboni
         for (Node* n = node; n != mt.root; n = n->parent) {
             bool linked = false;
             for (int ci = 0; n->parent && ci < n->parent->childCount; ci++) linked |= n->parent->children[ci] == n;
@@ -1015,6 +1018,10 @@ class Doc {
             const int q = markerPos((uint32_t)r.a, op.ref_seq, op.client);
             op.a = (r.flags & MTE_F_REL_BEFORE2) ? q - (int32_t)r.props : q + 1 + (int32_t)r.props;
         }
+        // a position before 0 (an unlinked marker, "before" with an offset) sends the reference's walks
+        // below the tree's start: not modelled
+        if ((r.pos1 && op.pos1 < 0) || (r.a && op.a < 0))
+            throw EngineError(MTE_DOC_UNSUPPORTED, "relative position before the document start");
     }
     void tag(Segment* s, uint32_t word) {
         s->refType = (int)(word & 0xFFFFu);
@@ -1161,9 +1168,14 @@ class Doc {
         // Client.getValidOpRange (client.ts:493-510)
         auto relPositions = [&]() {
             JVP rp1 = op.get(u"relativePos1"), rp2 = op.get(u"relativePos2");
-            if (!op.get(u"pos1") && rp1 && truthy(rp1.get())) pos1 = posFromRelativePos(*rp1, refSeq, clientId);
-            if (type != 0 && !op.get(u"pos2") && rp2 && truthy(rp2.get()))
+            if (!op.get(u"pos1") && rp1 && truthy(rp1.get())) {
+                pos1 = posFromRelativePos(*rp1, refSeq, clientId);
+                if (pos1 < 0) throw EngineError(MTE_DOC_UNSUPPORTED, "relative position before the document start");
+            }
+            if (type != 0 && !op.get(u"pos2") && rp2 && truthy(rp2.get())) {
                 pos2 = posFromRelativePos(*rp2, refSeq, clientId);
+                if (pos2 < 0) throw EngineError(MTE_DOC_UNSUPPORTED, "relative position before the document start");
+            }
         };
         switch (type) {
             case 0: {

@@ -114,6 +114,15 @@ def relative_log(seed, n=300, clients=("a", "b", "c")):
     return msgs
 
 
+def _dropped():
+    """'ZZhe[x]llo', the marker x removed (seq 4) and dropped by zamboni once the msn passes 4, then
+    'kk' inserted in front: 'kkZZhello' with x unlinked."""
+    return [msg("a", 1, 0, ins(0, "hello")),
+            msg("a", 2, 1, ins(2, {"marker": {"refType": 1}, "props": {"markerId": "x"}})),
+            msg("b", 3, 2, ins(0, "ZZ")), msg("a", 4, 3, rem(4, 5), 3), msg("b", 5, 4, ins(0, "k"), 5),
+            msg("a", 6, 5, ins(0, "k"), 5)]
+
+
 def edge_logs():
     """(name, log, expected status, failing seq): the cases the engine reports unsupported."""
     base = [msg("a", 1, 0, ins(0, "hello")),
@@ -133,10 +142,16 @@ def edge_logs():
              # removed but still in the tree (no msn advance): the position is still defined
              ("removed_marker", base + [msg("a", 4, 3, rem(4, 5)),
                                         msg("b", 5, 3, {"relativePos1": rel("x"), "seg": "!", "type": 0})], 0, None),
-             # removed below the msn: zamboni drops it from the tree
-             ("dropped_marker", base + [msg("a", 4, 3, rem(4, 5), 3), msg("b", 5, 4, ins(0, "k"), 5),
-                                        msg("a", 6, 5, ins(0, "k"), 5),
-                                        msg("b", 7, 6, {"relativePos1": rel("x"), "seg": "!", "type": 0}, 6)], UNSUPPORTED, 7),
+             # removed below the msn: zamboni unlinks it (scourNode: parent = undefined, mergeTree.ts:1317),
+             # getPosition's parent walk is empty -> 0, and the position is 0 + 1 + offset (after) or
+             # 0 - offset (before); a position below 0 is not modelled
+             ("dropped_marker", _dropped() + [msg("b", 7, 6, {"relativePos1": rel("x"), "seg": "!", "type": 0}, 6)], 0, None),
+             ("dropped_marker_before", _dropped() + [msg("b", 7, 6, {"relativePos1": rel("x", True), "seg": "!", "type": 0}, 6)],
+              0, None),
+             ("dropped_marker_offset", _dropped() + [msg("b", 7, 6, {"relativePos1": rel("x", False, 3),
+                                                                     "relativePos2": rel("x", False, 5), "type": 1}, 6)], 0, None),
+             ("dropped_marker_below_zero", _dropped() + [msg("b", 7, 6, {"relativePos1": rel("x", True, 1), "seg": "!",
+                                                                         "type": 0}, 6)], UNSUPPORTED, 7),
              ("group_member", base + [msg("b", 4, 3, {"type": 3, "ops": [ins(0, "g"), {"relativePos1": rel("x"), "seg": "!", "type": 0}]})],
               0, None)]
     return cases
@@ -172,6 +187,20 @@ def test_relative_edge_cases(case):
         assert a.status()[2] == z.status()[2] == fseq
     else:
         assert a.snapshot_json() == z.snapshot_json()
+
+
+def test_dropped_marker_positions():
+    """A relative position naming a marker zamboni dropped resolves from 0 (the reference's getPosition
+    of an unlinked segment): after it -> 1 + offset, before it -> 0 - offset."""
+    texts = {}
+    for name, log, code, _ in edge_logs():
+        if name.startswith("dropped") and not code:
+            o = OracleDoc(OBS)
+            o.apply_json(dumps(log))
+            assert o.status()[0] == 0, (name, o.status())
+            texts[name] = o.text()
+    assert texts == {"dropped_marker": "k!kZZhello", "dropped_marker_before": "!kkZZhello",
+                     "dropped_marker_offset": "kkZZllo"}, texts
 
 
 def test_relative_edge_positions():

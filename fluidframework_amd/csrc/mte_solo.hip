@@ -280,7 +280,7 @@ MTE_DEV u32 rows_dump(const Params& p, R& r, u32 d, u64 at) {
                 : L == RD_NLB ? r.n_lb : L == RD_HEIGHT ? r.height : L == RD_HEAPSIZE ? r.heapSize
                 : L == RD_HEAPTOP ? (u32)r.heapTop : L == RD_MINSEQ ? (u32)r.minSeq : L == RD_CURSEQ ? (u32)r.curSeq
                 : L == RD_SEGNEXT ? r.segNext : L == RD_ARENATOP ? r.arenaTop : L == RD_ARENASEL ? r.arenaSel
-                : L == RD_MAPNEXT ? r.mapNext : L == RD_NOPS ? r.n_ops : L == RD_NMSGS ? r.n_msgs
+                : L == RD_MAPNEXT ? r.mapNext : L == RD_NOPS ? r.ops_n() : L == RD_NMSGS ? r.msgs_n()
                 : L == RD_NGC ? r.n_gc : r.max_lb;
     if (L < RD_END) rec[L] = v;
     // release: the dump and the record before k_rows_cont (another XCD's L2) reads them
@@ -317,8 +317,7 @@ __global__ __launch_bounds__(64) void k_rows_cont(Params p) {
     r.arenaTop = wave_read(w, RD_ARENATOP);
     r.arenaSel = wave_read(w, RD_ARENASEL);
     r.mapNext = wave_read(w, RD_MAPNEXT);
-    r.n_ops = wave_read(w, RD_NOPS);
-    r.n_msgs = wave_read(w, RD_NMSGS);
+    r.set_counts(wave_read(w, RD_NOPS), wave_read(w, RD_NMSGS));
     r.n_gc = wave_read(w, RD_NGC);
     r.max_lb = wave_read(w, RD_MAXLB);
     r.status = 0;

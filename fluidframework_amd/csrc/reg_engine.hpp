@@ -213,7 +213,16 @@ struct RegEngine {
     HeapRegs HK, HS;         // heap keys (maxSeq) / segment ids
     u32 n_lb, height, heapSize, segNext, arenaTop, arenaSel;
     i32 minSeq, curSeq, heapTop, status, failSeq;
-    u32 n_ops, n_msgs, n_gc, max_lb;
+    u32 n_gc, max_lb;
+    u32 n_ops, n_msgs;
+    SD u32 ops_n() const { return n_ops; }
+    SD u32 msgs_n() const { return n_msgs; }
+    SD void set_counts(u32 o, u32 m) {
+        n_ops = o;
+        n_msgs = m;
+    }
+    SD void count_op() { n_ops++; }
+    SD void count_msg() { n_msgs++; }
     u32 lb_lim;  // leaf-block limit of room() (Params::reg_lb_limit, read once)
     bool adirty;
 #if defined(MTE_PROFILE) && !defined(MTE_CPU)
@@ -802,7 +811,8 @@ struct RegEngine {
         status = 0;
         midop = false;
         failSeq = -1;
-        n_ops = n_msgs = n_gc = 0;
+        set_counts(0, 0);
+        n_gc = 0;
         max_lb = 1;
         lb_lim = p.reg_lb_limit && p.reg_lb_limit < NBLK ? p.reg_lb_limit : NBLK;
         adirty = false;
@@ -2025,13 +2035,13 @@ struct RegEngine {
                 if (status) return true;
             }
             edited = op_insert(op.pos1, R, C, seq, rec);
-            n_ops++;
+            count_op();
         } else if (type == MTE_OP_REMOVE) {
             edited = op_remove(op.pos1, op.a, R, C, seq);
-            n_ops++;
+            count_op();
         } else if (ann) {
             if constexpr (PROPS) edited = op_annotate(op.pos1, op.a, R, C, seq, op.props, (op.flags & MTE_F_REWRITE) != 0);
-            n_ops++;
+            count_op();
         }
         if (status) return true;
         if (edited) {
@@ -2040,7 +2050,7 @@ struct RegEngine {
         }
         if (status) return true;
         if (op.flags & MTE_F_END_OF_MSG) {
-            n_msgs++;
+            count_msg();
             if (op.seq < curSeq || op.msn > op.seq || op.msn < minSeq) {
                 fail(MTE_DOC_SEQ_ORDER, op.seq);
                 return true;
@@ -2244,8 +2254,8 @@ struct RegEngine {
         if (simd::lane0()) {
             o.status = status;
             o.failing_seq = status ? failSeq : -1;
-            o.ops = n_ops;
-            o.msgs = n_msgs;
+            o.ops = ops_n();
+            o.msgs = msgs_n();
             o.min_seq = minSeq;
             o.cur_seq = curSeq;
             o.height = height;
@@ -2336,7 +2346,7 @@ struct RegEngine {
             }
         const u32 flags = (PROPS ? 1u : 0u) | (WIDE ? 2u : 0u);
         const u32 hv[CK_N] = {0u, (u32)at, (u32)(at >> 32), flags, n_lb, height, heapSize, (u32)heapTop, (u32)minSeq,
-                              (u32)curSeq, segNext, arenaTop, arenaSel, PROPS ? mapNext : 1u, n_ops, n_msgs, n_gc,
+                              (u32)curSeq, segNext, arenaTop, arenaSel, PROPS ? mapNext : 1u, ops_n(), msgs_n(), n_gc,
                               max_lb, PROPS ? mw : 0u};
         V h = simd::splat(0);
         for (u32 i = 1; i < CK_N; i++) h = simd::sel(Lv == i, hv[i], h);
@@ -2405,8 +2415,7 @@ struct RegEngine {
         segNext = hw(CK_SEGNEXT);
         arenaTop = hw(CK_ARENATOP);
         arenaSel = hw(CK_ARENASEL) & 1u;
-        n_ops = hw(CK_NOPS);
-        n_msgs = hw(CK_NMSGS);
+        set_counts(hw(CK_NOPS), hw(CK_NMSGS));
         n_gc = hw(CK_NGC);
         max_lb = hw(CK_MAXLB);
         // the arena text into this pass's semispace arenaSel (offsets kept: the rows' toff stay valid)

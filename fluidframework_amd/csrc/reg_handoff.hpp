@@ -142,8 +142,8 @@ MTE_DEV bool reg_handoff(R& r, E& e) {
     st.gdirty = R::kProps ? 1 : 0;  // map records written lane-parallel by the register engine
     if (L == 0) {
         u32* S = e.STATS();
-        S[ST_OPS] = r.n_ops;
-        S[ST_MSGS] = r.n_msgs;
+        S[ST_OPS] = r.ops_n();
+        S[ST_MSGS] = r.msgs_n();
         S[ST_GC] = r.n_gc;
         S[ST_MAXLB] = r.max_lb;
         S[ST_FAILSEQ] = NONE;

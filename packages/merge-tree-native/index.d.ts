@@ -36,6 +36,13 @@ export declare class BatchedMergeEngine {
     gatherSummaries(rank: number, world: number, comm?: RcclComm | null): DocSummary[];
     /** This rank's RCCL communicator on the engine's device, from rank 0's rcclUniqueId(). */
     rcclCommCreate(id: Buffer, rank: number, world: number): RcclComm;
+    /** mte_retain: keep each document's state, so a load of logs extending the last pass's replays
+     *  only their new ops (Client.applyMsg's incremental cost). */
+    retain(on?: boolean): void;
+    /** op records the last replay continued past instead of replaying (mte_get_info "resumed_ops") */
+    resumedOps(): number;
+    /** mte_get_info: routing and counters of the last pass ("resumed_docs", "rows", "solo", ...) */
+    getInfo(key: string): number;
 }
 
 /** An RCCL communicator handle (released by rcclCommDestroy or when collected). */
@@ -44,8 +51,9 @@ export type RcclComm = { readonly __rcclComm: unique symbol };
 export declare function rcclUniqueId(): Buffer;
 export declare function rcclCommDestroy(comm: RcclComm): void;
 
-/** Client-shaped facade (merge-tree client.ts:42) for one document. Batch semantics: messages are
- *  staged and replayed on the GPU when an output is next read (see index.js). */
+/** Client-shaped facade (merge-tree client.ts:42) for one document, incremental like
+ *  Client.applyMsg (client.ts:805-836): a read after new messages replays only them on the GPU,
+ *  continuing the document's state from the previous read (see index.js). */
 export declare class MergeTreeClient {
     constructor(observer?: string, options?: { device?: number; chunkSize?: number });
     load(summary: ITree | string): void;
@@ -56,6 +64,10 @@ export declare class MergeTreeClient {
     getText(): string;
     getLength(): number;
     snapshot(): ITree;
+    /** op records the last read did not replay again */
+    resumedOps(): number;
+    /** GPU passes run so far (one per read after new messages) */
+    readonly replays: number;
 }
 
 export declare function abiVersion(): number;
@@ -63,4 +75,7 @@ export declare function buildInfo(): string;
 
 /** Low-level builder (the addon's own surface): container logs split per SharedString channel. */
 export declare function createBuilder(): unknown;
+/** An open document (its log grows by builderAppendMessages); returns its index in the batch. */
+export declare function builderOpenDoc(builder: unknown, observer: string): number;
+export declare function builderAppendMessages(builder: unknown, doc: number, messagesJson: string): void;
 export declare function builderAddContainerLog(builder: unknown, observer: string, containerMessagesJson: string): string[];

@@ -166,3 +166,38 @@ def test_retain_off_replays_from_the_start():
     bad, _, _ = compare_batch_checksums(e, bt)
     assert not bad
     e.close()
+
+
+def test_mixed_batch_extended_three_times():
+    """Retain over a batch that mixes routes: short documents, a document with relative positions
+    (FULL kernels; the row engines hand it over, so it never checkpoints), and one long enough for
+    k_solo in every pass. Each of three passes loads longer logs; every checksum equals the oracle's
+    full replay of the logs of that pass."""
+    from tests.test_relative_pos import relative_log
+
+    rng = random.Random(11)
+    logs = [c5_json_log(700 + i, rng.choice([300, 1500])) for i in range(10)]
+    rel = relative_log(3, n=600)
+    ops, pay = regcpu.generated(2, 91, 60_000, n_clients=8, seed=1000)
+    from bench import ops_to_messages
+    long_log = ops_to_messages(ops, pay, 0, len(ops))
+    e = mte.Engine(0)
+    e.retain(True)
+    resumed = []
+    for frac in (0.4, 0.7, 1.0):
+        b = mte.Builder()
+        for l in logs:
+            b.add_doc(l[:max(1, int(len(l) * frac))], observer=OBS)
+        b.add_doc(rel[:max(1, int(len(rel) * frac))], observer=OBS)
+        b.add_doc(long_log[:int(len(long_log) * frac)], observer="__observer__")
+        bt = b.batch()
+        e.load(bt)
+        e.replay()
+        bad, _, _ = compare_batch_checksums(e, bt)
+        assert not bad, (frac, bad)
+        resumed.append(e.get_info("resumed_docs"))
+    # the relative-position document keeps the batch off k_rows (its bulk runs on k_lds, which keeps
+    # no checkpoints: those documents replay from op 0 every pass); the long document (24 000+ ops in
+    # every pass, k_solo's row engine) continues in passes 2 and 3
+    assert resumed == [0, 1, 1], resumed
+    e.close()

@@ -103,8 +103,9 @@ enum {
      *   MTE_REL_UNMAPPED when it was never mapped, was mapped to two markers (blockUpdate re-maps live
      *   markers, :2748-2768, so the winner depends on block-update order), an annotate before the op
      *   set a "markerId" property, or the marker count passed 65535. A document fails
-     *   MTE_DOC_UNSUPPORTED at an op whose marker is unmapped or no longer in the tree (zamboni
-     *   dropped it: the reference would walk its stale parent chain). */
+     *   MTE_DOC_UNSUPPORTED at an op whose marker is unmapped, or whose position comes out below 0.
+     *   A marker zamboni dropped is unlinked (scourNode sets its parent undefined, mergeTree.ts:1317),
+     *   so getPosition gives 0 for it: position 1 + offset after it, 0 - offset before it. */
     MTE_OP_RELPOS = 9,
     /* CELL: a SharedMatrix cell `set` (matrix.ts:560-601) as one of its two PermutationVectors sees it
      *   (both the rows and the cols document carry one, in message order): pos1 = the op's row (rows

@@ -329,6 +329,9 @@ struct mte_engine {
     bool lean_base = false;              // batch_is_lean, before the catch-up records decide
     uint32_t rows_pool_lim = 0;          // option rows_pool: k_rows pool rows per CU (test knob, 0 = all)
     bool props_rows_ok = false;          // k_rows may take the batch: no '\n', relative positions, summary loads or local documents
+    std::vector<uint8_t> doc_not_rows;   // per document: the row engines cannot replay it (hands over at op 0)
+    bool rows_mixed = true;              // option "rows_mixed": a batch with a few such documents still runs its
+                                         // bulk on k_rows (4 waves), those continuing HBM-resident from op 0
     bool rows_wide = false;              // ... on its WIDE row engine: a document has writers 32..63
     bool lean_opt = true;                // option "lean" (0 = always the FULL kernels)
     bool last_lean = false;
@@ -354,6 +357,7 @@ struct mte_engine {
                               // CU; -1 (auto: 4 for long documents, 12 without solo documents), 0: never
     bool xcd_align = true;    // option "xcd_align": bulk grids leave solo CUs free in every XCD (bulk_cus)
     uint32_t last_rows = 0;   // waves per CU of the last pass's k_rows (0: k_lds / k_hbmq)
+    bool last_mixed = false;  // the last pass ran a mixed batch on k_rows (rows_mixed)
     bool emit_opt = true;     // option "emit"
     bool legacy = false;      // snapshot_format 1 (mte_config / option "snapshot_format"): SnapshotLegacy
     bool emitted_legacy = false;  // format of the last emission
@@ -1192,6 +1196,7 @@ int mte_load(mte_engine* e, const mte_batch* b) {
     // the legacy format (run_kernel decides, snapshot_format may change after the load)
     e->lean_base = lean;
     e->props_rows_ok = rows_ok;
+    e->doc_not_rows = not_rows;
     e->rows_wide = any_wide;
     e->ext_perm = ext;
     e->ext_cu = cu_any;
@@ -1371,7 +1376,27 @@ static int run_kernel(mte_engine* e, bool gen) {
     uint32_t rows = 0;
     // (PROPS rows only when properties are what requires FULL: option lean = 0 on a lean batch keeps
     // the FULL LDS kernels, as that diagnostic switch says)
-    const bool props_rows = full == 1 && !e->lean_ok && e->props_rows_ok;
+    bool props_rows = full == 1 && !e->lean_ok && e->props_rows_ok;
+    // A FULL batch with a few documents the row engines cannot replay (summary loads, relative
+    // positions, '\n' in a property-carrying document, local edits, 64+ clients): its bulk still runs
+    // on k_rows' fixed rows, and those documents hand over at op 0 (rows_dump) to continue
+    // HBM-resident in k_rows_cont on the FULL engine -- instead of the whole bulk leaving k_rows for
+    // k_lds / k_hbmq. Only while they are a small share of the bulk and each finds an HBM slot.
+    bool mixed = false;
+    if (!gen && full == 1 && !e->props_rows_ok && e->rows_mixed && e->rows_bulk && !e->force_hbm && nd > n_solo &&
+        e->doc_not_rows.size() == nall) {
+        uint64_t nr_docs = 0, nr_ops = 0, all_ops = 0;
+        for (uint32_t k = n_solo; k < nd; k++) {
+            const uint32_t d = e->order[k];
+            all_ops += e->n_ops_doc[d];
+            if (e->doc_not_rows[d]) {
+                nr_docs++;
+                nr_ops += e->n_ops_doc[d];
+            }
+        }
+        mixed = nr_docs <= e->n_slots && nr_docs <= 4096 && nr_ops * 4 <= all_ops;
+        props_rows = mixed;
+    }
     if (!gen && ((full == 0 && e->props_rows_ok) || props_rows) && e->rows_bulk && !e->force_hbm && nd > n_solo) {
         uint64_t bulk_ops = 0;
         for (uint32_t k = n_solo; k < nd; k++) bulk_ops += e->n_ops_doc[e->order[k]];
@@ -1382,7 +1407,9 @@ static int run_kernel(mte_engine* e, bool gen) {
         // so the shared pool at 8 / 12 waves is full most of the time: 4 waves on fixed rows, a
         // document outgrowing them continuing HBM-resident; tools/wide_probe.py, profiles/r05/r05l)
         rows = e->rows_bulk > 0 ? (uint32_t)e->rows_bulk : (long_docs || e->rows_wide) ? 4u : 12u;
+        if (mixed) rows = 4;  // (the handoff at op 0 needs the fixed rows' state dump)
     }
+    e->last_mixed = rows && mixed;
     if (ck && rows) rows = 4;  // (the checkpointing k_rows runs 4 waves per CU on fixed rows)
     e->last_rows = rows;
     if (rows) groups = hbm_waves = lds_active = 0;
@@ -2783,6 +2810,7 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "rows_bulk") e->rows_bulk = value < 0 ? -1 : value == 0 ? 0 : value >= 12 ? 12 : value >= 8 ? 8 : 4;  // lean bulk on k_rows
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
     else if (k == "rows_pool") e->rows_pool_lim = (uint32_t)std::max<int64_t>(0, value);  // k_rows pool rows per CU (0 = all)
+    else if (k == "rows_mixed") e->rows_mixed = value != 0;
     else if (k == "retain") {  // incremental replay: checkpoints kept for a later pass over extended logs
         e->retain = value != 0;
         if (!e->retain) ck_forget(e);
@@ -2814,6 +2842,7 @@ int mte_get_info(mte_engine* e, const char* key, int64_t* value) {
     else if (k == "solo_tail_us") *value = (int64_t)(e->last_solo_tail_ms * 1000.0);
     else if (k == "lean") *value = e->last_lean;
     else if (k == "rows") *value = e->last_rows;  // k_rows waves per CU of the last pass (0: not used)
+    else if (k == "rows_mixed") *value = e->last_mixed;  // ... with documents handed over at op 0
     else if (k == "cell_pass_us") *value = (int64_t)(e->last_cell_pass_ms * 1000.0);  // SharedMatrix pass 1
     else if (k == "rows_restart_pushed" || k == "rows_restart_popped" || k == "rows_continued") {
         // k_rows' in-pass restart queue (counters[8] / [9]): documents given back when the row pool

@@ -170,8 +170,8 @@ def test_retain_off_replays_from_the_start():
 
 def test_mixed_batch_extended_three_times():
     """Retain over a batch that mixes routes: short documents, a document with relative positions
-    (FULL kernels; the row engines hand it over, so it never checkpoints), and one long enough for
-    k_solo in every pass. Each of three passes loads longer logs; every checksum equals the oracle's
+    (FULL kernels; the row engines hand it over at op 0, so it never checkpoints), and one long enough
+    for k_solo in every pass. Each of three passes loads longer logs; every checksum equals the oracle's
     full replay of the logs of that pass."""
     from tests.test_relative_pos import relative_log
 
@@ -196,8 +196,8 @@ def test_mixed_batch_extended_three_times():
         bad, _, _ = compare_batch_checksums(e, bt)
         assert not bad, (frac, bad)
         resumed.append(e.get_info("resumed_docs"))
-    # the relative-position document keeps the batch off k_rows (its bulk runs on k_lds, which keeps
-    # no checkpoints: those documents replay from op 0 every pass); the long document (24 000+ ops in
-    # every pass, k_solo's row engine) continues in passes 2 and 3
-    assert resumed == [0, 1, 1], resumed
+    # the bulk stays on k_rows (rows_mixed): the ten short documents and the long one (24 000+ ops in
+    # every pass, k_solo's row engine) continue in passes 2 and 3; the relative-position document
+    # hands over at op 0 each pass and replays from its start
+    assert resumed == [0, 11, 11], resumed
     e.close()

@@ -365,3 +365,62 @@ def test_bulk_rows_wide_batches(engine, kind, clients):
     assert set(modes) <= {MODE_BULK_ROWS, MODE_ROWS_CONTINUED}, sorted(set(modes))
     assert modes.count(MODE_ROWS_CONTINUED) == info["rows_continued"] > 0, info
     _check(engine, batch, n_docs=256)
+
+
+def test_mixed_batch_bulk_stays_on_rows():
+    """A FULL batch whose bulk is mostly row-engine documents plus a few the row engines cannot replay
+    -- summaries with a catch-up suffix, relative positions, a property-carrying document with '\\n',
+    a local (non-collaborative) one -- runs its bulk on k_rows' fixed rows (option rows_mixed); those
+    few hand over at op 0 and continue HBM-resident (DocRes mode 6). Every document equals the oracle;
+    with rows_mixed off the same batch takes k_lds / k_hbmq with the same results."""
+    import random as _r
+
+    from tests.catchup import OBS, c5_json_log, catchup_cases
+    from tests.gpu_helpers import compare_batch_checksums, compare_doc
+    from tests.oplog import ins, msg, rem
+    from tests.test_relative_pos import relative_log
+    from tests.test_summary_load import OBS as REL_OBS
+
+    engine = mte.Engine(0)
+
+    rng = _r.Random(5)
+    b = mte.Builder()
+    for i in range(80):
+        b.add_doc(c5_json_log(900 + i, rng.choice([200, 800, 1600])), observer=OBS)
+    special = []
+    for summ, suffix, _ in catchup_cases(3, 800, seed=9):
+        special.append(b.n_docs())
+        b.add_doc_from_summary(summ, suffix, observer=OBS)
+    for s in (1, 2):
+        special.append(b.n_docs())
+        b.add_doc(relative_log(s, n=300), observer=REL_OBS)
+    special.append(b.n_docs())
+    b.add_doc([msg("w1", 1, 0, ins(0, {"text": "a\nb", "props": {"k": 1}})), msg("w2", 2, 1, ins(1, "zz"))],
+              observer=OBS)
+    special.append(b.n_docs())  # local edits (observer "")
+    b.add_doc([msg("local", 0, 0, ins(0, "hello world")), msg("local", 0, 0, rem(2, 5))], observer="")
+    batch = b.batch()
+    observers = [OBS] * 83 + [REL_OBS] * 2 + [OBS, ""]
+    try:
+        results = {}
+        for mixed in (1, 0):
+            engine.set_option("rows_mixed", mixed)
+            engine.load(batch)
+            st = engine.replay()
+            info = engine.run_info()
+            assert engine.get_info("rows_mixed") == mixed and engine.get_info("rows") == (4 if mixed else 0), info
+            bad, _, s = compare_batch_checksums(engine, batch)
+            local = len(observers) - 1  # (the oracle's record path replays sequenced logs only)
+            bad = [d for d in bad if d != local]
+            if bad:
+                compare_doc(engine, batch, bad[0], observer=observers[bad[0]])
+            assert not bad, bad
+            assert engine.status(local)[0] == 0 and engine.text(local) == "he world"
+            if mixed:
+                modes = [engine.doc_result(d)["mode"] for d in special]
+                assert all(m in (6, 1) for m in modes), modes  # continued in the pass (or the host's re-run)
+                assert sum(engine.doc_result(d)["mode"] == 5 for d in range(80)) == 80
+            results[mixed] = (st["failed_docs"], [int(x) for x in s["checksum"]])
+        assert results[1] == results[0]
+    finally:
+        engine.close()

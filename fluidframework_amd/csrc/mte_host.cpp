@@ -1382,8 +1382,10 @@ static int run_kernel(mte_engine* e, bool gen) {
     // on k_rows' fixed rows, and those documents hand over at op 0 (rows_dump) to continue
     // HBM-resident in k_rows_cont on the FULL engine -- instead of the whole bulk leaving k_rows for
     // k_lds / k_hbmq. Only while they are a small share of the bulk and each finds an HBM slot.
+    // (a lean batch's only such documents are local ones: '\n', relative positions, summaries and
+    // 64+ clients make a batch FULL)
     bool mixed = false;
-    if (!gen && full == 1 && !e->props_rows_ok && e->rows_mixed && e->rows_bulk && !e->force_hbm && nd > n_solo &&
+    if (!gen && full <= 1 && !e->props_rows_ok && e->rows_mixed && e->rows_bulk && !e->force_hbm && nd > n_solo &&
         e->doc_not_rows.size() == nall) {
         uint64_t nr_docs = 0, nr_ops = 0, all_ops = 0;
         for (uint32_t k = n_solo; k < nd; k++) {
@@ -1395,9 +1397,9 @@ static int run_kernel(mte_engine* e, bool gen) {
             }
         }
         mixed = nr_docs <= e->n_slots && nr_docs <= 4096 && nr_ops * 4 <= all_ops;
-        props_rows = mixed;
+        if (full == 1) props_rows = mixed;
     }
-    if (!gen && ((full == 0 && e->props_rows_ok) || props_rows) && e->rows_bulk && !e->force_hbm && nd > n_solo) {
+    if (!gen && ((full == 0 && (e->props_rows_ok || mixed)) || props_rows) && e->rows_bulk && !e->force_hbm && nd > n_solo) {
         uint64_t bulk_ops = 0;
         for (uint32_t k = n_solo; k < nd; k++) bulk_ops += e->n_ops_doc[e->order[k]];
         // (long documents take 4 waves whatever their count: eight of them, ~120 leaf blocks each,

@@ -424,3 +424,32 @@ def test_mixed_batch_bulk_stays_on_rows():
         assert results[1] == results[0]
     finally:
         engine.close()
+
+
+def test_lean_batch_with_local_documents_stays_on_rows():
+    """A lean batch (no properties, no '\n') of row-engine documents plus two local (non-collaborative)
+    ones: the bulk stays on k_rows (4 waves), the local documents hand over at op 0 to the lean HBM
+    engine; every collaborative document equals the oracle, the local ones their edited strings."""
+    from tests.catchup import OBS, c5_json_log
+    from tests.gpu_helpers import compare_batch_checksums
+    from tests.oplog import ins, msg, rem
+
+    b = mte.Builder()
+    for i in range(60):
+        b.add_doc(c5_json_log(1200 + i, 600), observer=OBS)
+    b.add_doc([msg("local", 0, 0, ins(0, "hello world")), msg("local", 0, 0, rem(0, 6))], observer="")
+    b.add_doc([msg("local", 0, 0, ins(0, "abc")), msg("local", 0, 0, ins(1, "XY"))], observer="")
+    batch = b.batch()
+    e = mte.Engine(0)
+    try:
+        e.load(batch)
+        st = e.replay()
+        info = e.run_info()
+        assert st["failed_docs"] == 0 and info["lean"] == 1 and e.get_info("rows") == 4, info
+        assert e.get_info("rows_mixed") == 1
+        bad, _, _ = compare_batch_checksums(e, batch)
+        assert [d for d in bad if d < 60] == []
+        assert e.text(60) == "world" and e.text(61) == "aXYbc"
+        assert [e.doc_result(d)["mode"] for d in (60, 61)] == [6, 6]
+    finally:
+        e.close()

@@ -37,6 +37,12 @@ def main():
     build_s = time.time() - t0
     g.close()
     out = {"docs": n_docs, "ops_per_doc": n_ops, "special_docs": 4, "build_s": round(build_s, 1)}
+    if os.environ.get("LEGACY"):  # SnapshotLegacy (the reference's default format): catch-up records
+        e = mte.Engine(0, snapshot_format=1)
+        e.load(b.batch())
+        ms = [round(e.replay()["kernel_ms"], 2) for _ in range(3)]
+        out["legacy"] = {"kernel_ms": ms, "rows": e.get_info("rows"), "run_info": e.run_info()}
+        e.close()
     e = mte.Engine(0)
     for mixed in (1, 0):
         e.set_option("rows_mixed", mixed)

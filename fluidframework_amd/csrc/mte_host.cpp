@@ -330,8 +330,9 @@ struct mte_engine {
     uint32_t rows_pool_lim = 0;          // option rows_pool: k_rows pool rows per CU (test knob, 0 = all)
     bool props_rows_ok = false;          // k_rows may take the batch: no '\n', relative positions, summary loads or local documents
     std::vector<uint8_t> doc_not_rows;   // per document: the row engines cannot replay it (hands over at op 0)
-    bool rows_mixed = true;              // option "rows_mixed": a batch with a few such documents still runs its
-                                         // bulk on k_rows (4 waves), those continuing HBM-resident from op 0
+    int rows_mixed = 1;                  // option "rows_mixed": a batch with a few such documents still runs its
+                                         // bulk on k_rows (4 waves), those continuing HBM-resident from op 0:
+                                         // 1 on retained passes, 2 always, 0 never
     bool rows_wide = false;              // ... on its WIDE row engine: a document has writers 32..63
     bool lean_opt = true;                // option "lean" (0 = always the FULL kernels)
     bool last_lean = false;
@@ -1396,7 +1397,12 @@ static int run_kernel(mte_engine* e, bool gen) {
                 nr_ops += e->n_ops_doc[d];
             }
         }
-        mixed = nr_docs <= e->n_slots && nr_docs <= 4096 && nr_ops * 4 <= all_ops;
+        // Once k_hbmq takes a slot before a document, k_lds / k_hbmq replay such a FULL batch about
+        // as fast as k_rows' 4-wave fixed rows (2 048 x 3 000-op logs: 51 vs 58 ms; 512 x 20 000:
+        // 228 vs 240 ms, profiles/r06/mixed_route.json), so the rows route is taken where it buys
+        // something: a retained pass (its row documents continue from their checkpoints next time)
+        // -- option 2 forces it
+        mixed = nr_docs <= e->n_slots && nr_docs <= 4096 && nr_ops * 4 <= all_ops && (e->rows_mixed >= 2 || ck);
         if (full == 1) props_rows = mixed;
     }
     if (!gen && ((full == 0 && (e->props_rows_ok || mixed)) || props_rows) && e->rows_bulk && !e->force_hbm && nd > n_solo) {
@@ -2812,7 +2818,7 @@ int mte_set_option(mte_engine* e, const char* key, int64_t value) {
     else if (k == "rows_bulk") e->rows_bulk = value < 0 ? -1 : value == 0 ? 0 : value >= 12 ? 12 : value >= 8 ? 8 : 4;  // lean bulk on k_rows
     else if (k == "snapshot_format") e->legacy = value == 1;  // mte_config.snapshot_format
     else if (k == "rows_pool") e->rows_pool_lim = (uint32_t)std::max<int64_t>(0, value);  // k_rows pool rows per CU (0 = all)
-    else if (k == "rows_mixed") e->rows_mixed = value != 0;
+    else if (k == "rows_mixed") e->rows_mixed = (int)std::min<int64_t>(std::max<int64_t>(value, 0), 2);
     else if (k == "retain") {  // incremental replay: checkpoints kept for a later pass over extended logs
         e->retain = value != 0;
         if (!e->retain) ck_forget(e);

@@ -141,12 +141,22 @@ MTE_DEV u32 acquire_hslot(const Params& p) {
 template <bool GEN, int LVL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MTE_HBMQ_WPE))) void k_hbmq(Params p) {
     const u32 L = lane_id();
+    // A slot first, then a document: a wave that claimed a document before it held a slot waited,
+    // with the document, for one of the few slots -- hundreds of the batch's longest documents then
+    // queued behind k_hbmq's slots while the LDS waves ran dry (2 048 x 3 000-op logs: 41 ms to 2.4 s per
+    // pass, now 50-57 ms, profiles/r06/mixed_route.json). A wave that finds the queue drained
+    // before or after taking its slot gives the slot back and exits.
+    if (wave_first(__hip_atomic_load(&p.counters[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + p.n_prio >= p.n_list)
+        return;
+    const u32 slot = acquire_hslot(p);
     u32 i = 0;
     if (L == 0) i = p.n_prio + atomicAdd(&p.counters[0], 1u);
     i = wave_read(i, 0);
-    if (i >= p.n_list) return;
+    if (i >= p.n_list) {
+        if (L == 0) atomicAnd(&p.slot_bits[slot >> 5], ~(1u << (slot & 31)));
+        return;
+    }
     const u32 d = p.doc_list[i];
-    const u32 slot = acquire_hslot(p);
     Engine<false, false, LVL> e(p, d);
     e.bind_slot(p.slot_hbm0 + slot);
     e.reset_stats();

@@ -404,7 +404,7 @@ def test_mixed_batch_bulk_stays_on_rows():
     try:
         results = {}
         for mixed in (1, 0):
-            engine.set_option("rows_mixed", mixed)
+            engine.set_option("rows_mixed", 2 * mixed)  # (2: even for a bulk of short documents)
             engine.load(batch)
             st = engine.replay()
             info = engine.run_info()
@@ -441,6 +441,7 @@ def test_lean_batch_with_local_documents_stays_on_rows():
     b.add_doc([msg("local", 0, 0, ins(0, "abc")), msg("local", 0, 0, ins(1, "XY"))], observer="")
     batch = b.batch()
     e = mte.Engine(0)
+    e.set_option("rows_mixed", 2)  # (2: even for a bulk of short documents)
     try:
         e.load(batch)
         st = e.replay()

@@ -40,19 +40,25 @@ def main():
     if os.environ.get("LEGACY"):  # SnapshotLegacy (the reference's default format): catch-up records
         e = mte.Engine(0, snapshot_format=1)
         e.load(b.batch())
-        ms = [round(e.replay()["kernel_ms"], 2) for _ in range(3)]
-        out["legacy"] = {"kernel_ms": ms, "rows": e.get_info("rows"), "run_info": e.run_info()}
+        ms, infos = [], []
+        for _ in range(int(os.environ.get("REPS", "3"))):
+            ms.append(round(e.replay()["kernel_ms"], 2))
+            ri = e.run_info()
+            infos.append({k: ri[k] for k in ("spilled", "continued", "lds_ms", "hbm_ms", "hbm_docs", "lds_groups", "hbm_waves")})
+        out["legacy"] = {"kernel_ms": ms, "rows": e.get_info("rows"), "per_pass": infos}
         e.close()
     e = mte.Engine(0)
     for mixed in (1, 0):
-        e.set_option("rows_mixed", mixed)
+        e.set_option("rows_mixed", 2 * mixed)  # (2: the rows route even for short documents)
         e.load(b.batch())
-        ms = []
-        for _ in range(3):
+        ms, infos = [], []
+        for _ in range(int(os.environ.get("REPS", "3"))):
             st = e.replay()
             ms.append(round(st["kernel_ms"], 2))
+            ri = e.run_info()
+            infos.append({k: ri[k] for k in ("spilled", "continued", "lds_ms", "hbm_ms", "hbm_docs")})
         out[f"mixed{mixed}"] = {"kernel_ms": ms, "failed": st["failed_docs"], "rows": e.get_info("rows"),
-                                "rows_mixed": e.get_info("rows_mixed"), "run_info": e.run_info()}
+                                "rows_mixed": e.get_info("rows_mixed"), "per_pass": infos}
     print(json.dumps(out), flush=True)
 
 

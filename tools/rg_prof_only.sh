@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")/../fluidframework_amd/csrc"
 B=../_build
 declare -A S=([apply]=2 [resolve]=3 [insert_slot]=4 [split]=5 [range]=6 [zamboni]=7 [scour]=8 [heap]=9 \
-              [find_seg]=10 [pack]=11 [lru]=12 [alloc]=21 [op_ins]=22 [op_rem]=23 [zam_msn]=24 [zam_edit]=25)
+              [find_seg]=10 [pack]=11 [lru]=12 [split_at]=21 [op_ins]=22 [op_rem]=23 [zam_msn]=24 [zam_edit]=25)
 build() {
   mkdir -p $B/rp_$1
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-variable \
